@@ -1,0 +1,48 @@
+// gm_faithful.h -- device state of the FAITHFUL tick (see gm_faithful.hip).
+#pragma once
+#include <stdint.h>
+
+#define F_ENBUFFSIZE 30000  // EmulNet.h:12
+#define F_MAX_NODES 1000    // EmulNet.h:10 (ENsend asserts src <= MAX_NODES)
+#define F_MAX_TIME 3600     // EmulNet.h:11
+
+enum { F_JOINREQ = 0, F_JOINREP = 1, F_LIST = 2 };  // MP1Node.h:30-35
+
+// One EmulNet message (en_msg + payload, EmulNet.h:23-30; MP1Node.cpp:143-149,
+// 246-250, 364-383): destination / source ids, type, the payload entry id
+// (JOINREQ: the joiner; LIST: the gossiped member) and its heartbeat.
+struct FMsg {
+  int32_t to, from, type, subj, hb;
+};
+
+struct FEvent {
+  int32_t t, logger, kind, subject, seq;
+};
+
+struct FState {
+  int n, np, tmax;             // nodes, padded row width (x64), msgcount horizon
+  int gstride;                 // gossip list stride (n + GM_FANOUT)
+  int draw_cap;
+  int drop_pct_now;            // (int)(MSG_DROP_PROB*100) while dropmsg, else -1
+  uint64_t rd_seed;
+  uint32_t *table;             // [n][np] packed (hb | ts<<16), GM_ABSENT
+  int32_t *start;              // [n] (int)(STEP_RATE*i)
+  int32_t *failed, *inited, *ingroup, *hbctr, *started_now;  // [n]
+  FMsg *buf;                   // EmulNet buffer [F_ENBUFFSIZE]
+  int32_t *bufsize;
+  int32_t *holepos;            // [F_ENBUFFSIZE] scratch
+  FMsg *q;                     // this tick's queues, concatenated [F_ENBUFFSIZE]
+  int32_t *q_off, *q_cnt;      // [n]
+  int32_t *scount;             // sends per node this tick
+  int32_t *jcnt, *gcnt, *fcnt; // JOINREPs, gossip targets, fresh entries per node
+  int32_t *jrq;                // [n][n] JOINREP destinations (queue order)
+  int32_t *gossip;             // [n][gstride] gossip target ids
+  int32_t *fcols;              // [n][n] fresh columns ascending
+  int32_t *s1;                 // glibc TYPE_3 state: 31 words + fptr + rptr
+  int32_t *draws;              // [draw_cap]
+  int32_t *sent, *recv;        // [(F_MAX_NODES+1)][tmax]
+  FEvent *ev;
+  unsigned long long *ev_count;
+  int ev_cap;
+  uint32_t *err;
+};

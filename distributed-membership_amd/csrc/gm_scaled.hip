@@ -1,0 +1,225 @@
+// gm_scaled.hip -- SCALED-mode tick: the HBM-bound full-membership hot path.
+//
+// One launch per globaltime tick; one 256-thread workgroup owns one observer
+// row r (MP1Node of node r) and does, in a single streaming pass over the row:
+//   1. merge: max-merge the gossip lists delivered to r this tick
+//      (updatelistCallBack, MP1Node.cpp:259-301). A list is the sender's
+//      post-sweep row of the previous tick reduced to 16-bit heartbeats of its
+//      fresh entries (sendMemberList, MP1Node.cpp:360-395: entries with
+//      t - ts < TFAIL), stored once per sender in a payload plane and read by
+//      each of its <= ~5 receivers ("pull"; no atomics, commutative, order-free);
+//   2. self heartbeat bump (nodeLoopOps, MP1Node.cpp:409-415);
+//   3. failure sweep: age >= TFAIL -> numfailed, age >= TREMOVE -> removed
+//      (MP1Node.cpp:426-444), with join/remove events appended to per-row slots;
+//   4. writes the row back and the row's own payload plane for tick t+1;
+//   5. builds presence / freshness bitmaps of the row in LDS, then one lane runs
+//      the gossip-target draw (mt19937 + Lemire + rank-select, MP1Node.cpp:449-489)
+//      and enqueues r into each target's inbox for the next tick -- the
+//      counting sort by destination that replaces EmulNet's buffer scan.
+// Bytes per live row per tick: 4W read + 4W write (table) + 2W write (payload)
+// + 2W per delivered list (payload reads); nothing else touches HBM at scale.
+#include "gm_device.h"
+#include "gm_scaled.h"
+
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ u16x2 as_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
+__device__ __forceinline__ uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+
+// merge key of one payload word pair: hb+1, NONE (0xFFFF) -> 0
+__device__ __forceinline__ u16x2 key2(uint32_t m) { return as_u16x2(m) + (u16x2)(1); }
+
+__global__ __launch_bounds__(S_THREADS) void gm_s_tick(SState s, int t, int drop_pct) {
+  extern __shared__ __align__(16) unsigned char s_smem[];
+  const int wp = s.wp, nw = wp >> 6;
+  uint64_t *s_pres = (uint64_t *)s_smem;               // [nw] present after the sweep
+  uint64_t *s_fresh = s_pres + nw;                     // [nw] present and t - ts < TFAIL
+  uint32_t *s_pre = (uint32_t *)(s_fresh + nw);        // [nw] exclusive prefix popcounts
+  uint32_t *s_mt = s_pre + nw;                         // [624] mt19937 state
+  int *s_send = (int *)(s_mt + 624);                   // [S_KMAX] senders of this tick's lists
+  int *s_tmp = s_send + S_KMAX;                        // [16] scan scratch
+  int *s_misc = s_tmp + 16;                            // [8]
+
+  const int r = blockIdx.x, tid = threadIdx.x;
+  const int par = t & 1;
+  int32_t *cnt_in = s.inbox_cnt[par];
+  if (tid == 0) {
+    s_misc[0] = cnt_in[r];
+    cnt_in[r] = 0;  // recycled as the append target of tick t+1
+    s_misc[1] = 0;  // event slots used
+  }
+  __syncthreads();
+  const int kin = s_misc[0];
+  int32_t *stat = s.rowstat + (size_t)r * 4;
+  if (s.failed[r]) {  // crashed node: frozen, receives and sends nothing
+    if (tid == 0) {
+      stat[0] = stat[1] = stat[2] = stat[3] = 0;
+      s.ev_cnt[r] = 0;
+    }
+    return;
+  }
+  const int k = kin < S_KMAX ? kin : S_KMAX;
+  if (tid == 0 && kin > S_KMAX) atomicOr(s.err, GM_ERR_INBOX);
+  for (int j = tid; j < k; j += S_THREADS) s_send[j] = s.inbox[par][(size_t)r * S_KMAX + j];
+  __syncthreads();
+
+  uint32_t *trow = s.table + (size_t)r * wp;
+  uint16_t *mout = s.msg[par] + (size_t)r * wp;
+  const uint16_t *min = s.msg[par ^ 1];
+  const int selfc = r - s.c0;  // own column if this shard holds it
+  const uint32_t tt = (uint32_t)t;
+  const int t_send = t - 1;
+  int npres = 0, nfail = 0;
+
+  for (int base = tid * S_COLS_PER_THREAD; base < wp; base += S_COLS_PER_STEP) {
+    const uint4 ta = *(const uint4 *)(trow + base);
+    const uint4 tb = *(const uint4 *)(trow + base + 4);
+    u16x2 k0 = (u16x2)(0), k1 = (u16x2)(0), k2 = (u16x2)(0), k3 = (u16x2)(0);
+    if (drop_pct < 0) {
+      for (int j0 = 0; j0 < k; j0 += 8) {
+        uint4 m[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          if (j0 + u < k) m[u] = *(const uint4 *)(min + (size_t)s_send[j0 + u] * wp + base);
+          else m[u] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          k0 = __builtin_elementwise_max(k0, key2(m[u].x));
+          k1 = __builtin_elementwise_max(k1, key2(m[u].y));
+          k2 = __builtin_elementwise_max(k2, key2(m[u].z));
+          k3 = __builtin_elementwise_max(k3, key2(m[u].w));
+        }
+      }
+    } else {
+      // per-entry drops keyed by (t_send, src, dst, column) -- SCALED regime
+      uint32_t kk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (int j = 0; j < k; j++) {
+        const int snd = s_send[j];
+        const uint4 m = *(const uint4 *)(min + (size_t)snd * wp + base);
+        const uint32_t mw[4] = {m.x, m.y, m.z, m.w};
+        const uint64_t pair = gm_mix64(s.drop_seed ^ ((uint64_t)(uint32_t)t_send << 48) ^
+                                       ((uint64_t)(uint32_t)snd << 24) ^ (uint64_t)(uint32_t)r);
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+          uint32_t hv = (mw[q >> 1] >> (16 * (q & 1))) & 0xFFFFu;
+          uint32_t key = (hv + 1u) & 0xFFFFu;
+          if (key == 0) continue;
+          uint32_t h = (uint32_t)(gm_mix64(pair + (uint64_t)(s.c0 + base + q)) >> 32);
+          if ((int)(h % 100u) < drop_pct) continue;
+          kk[q] = kk[q] > key ? kk[q] : key;
+        }
+      }
+      k0 = (u16x2)((uint16_t)kk[0], (uint16_t)kk[1]);
+      k1 = (u16x2)((uint16_t)kk[2], (uint16_t)kk[3]);
+      k2 = (u16x2)((uint16_t)kk[4], (uint16_t)kk[5]);
+      k3 = (u16x2)((uint16_t)kk[6], (uint16_t)kk[7]);
+    }
+    uint32_t e[8] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y, tb.z, tb.w};
+    const uint32_t keys[4] = {as_u32(k0), as_u32(k1), as_u32(k2), as_u32(k3)};
+    uint32_t out[4] = {0, 0, 0, 0};
+    uint32_t pbits = 0, fbits = 0;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const int c = base + q;
+      uint32_t en = e[q];
+      const uint32_t key = (keys[q >> 1] >> (16 * (q & 1))) & 0xFFFFu;
+      uint32_t ev = 0;
+      if (key) {  // updatelistCallBack: insert, or raise hb and stamp ts = now
+        const uint32_t hb = key - 1u;
+        if (en == GM_ABSENT) { en = gm_pack(hb, tt); ev = S_EV_ADD; }
+        else if (gm_hb(en) < hb) en = gm_pack(hb, tt);
+      }
+      if (c == selfc) {  // updateMyPos + heartbeat++ + myPos->setheartbeat(heartbeat++)
+        if (en == GM_ABSENT) atomicOr(s.err, GM_ERR_SELF);
+        const int hb = s.hbctr[r] + 1;
+        s.hbctr[r] = hb + 1;
+        en = gm_pack((uint32_t)hb, tt);
+      }
+      uint32_t o = GM_NONE16;
+      if (en != GM_ABSENT) {
+        const int age = t - (int)gm_ts(en);
+        if (age >= GM_TFAIL) {
+          nfail++;
+          if (age >= GM_TREMOVE) { en = GM_ABSENT; ev = S_EV_REMOVE; }
+        } else {
+          o = gm_hb(en);
+          fbits |= 1u << q;
+        }
+        if (en != GM_ABSENT) pbits |= 1u << q;
+      }
+      e[q] = en;
+      out[q >> 1] |= o << (16 * (q & 1));
+      if (ev) {
+        const int slot = atomicAdd(&s_misc[1], 1);
+        const uint32_t rec = (ev << 30) | (uint32_t)(s.c0 + c + 1);
+        if (slot < s.evcap) {
+          s.ev_rows[(size_t)r * s.evcap + slot] = rec;
+        } else {
+          const uint32_t sp = atomicAdd(s.ev_spill_cnt, 1u);
+          if (sp < s.ev_spill_cap) s.ev_spill[sp] = ((uint64_t)(uint32_t)r << 32) | rec;
+          else atomicOr(s.err, GM_ERR_EVENTS);
+        }
+      }
+    }
+    npres += __builtin_popcount(pbits);
+    *(uint4 *)(trow + base) = make_uint4(e[0], e[1], e[2], e[3]);
+    *(uint4 *)(trow + base + 4) = make_uint4(e[4], e[5], e[6], e[7]);
+    *(uint4 *)(mout + base) = make_uint4(out[0], out[1], out[2], out[3]);
+    ((uint8_t *)s_pres)[base >> 3] = (uint8_t)pbits;
+    ((uint8_t *)s_fresh)[base >> 3] = (uint8_t)fbits;
+  }
+
+  // row totals and rank-select prefix over the presence bitmap
+  const int size = gm_block_sum(npres, s_tmp);
+  const int numfailed = gm_block_sum(nfail, s_tmp);
+  {
+    const int per = (nw + S_THREADS - 1) / S_THREADS;
+    const int w0 = tid * per, w1 = min(nw, w0 + per);
+    int part = 0;
+    for (int w = w0; w < w1; w++) part += __builtin_popcountll(s_pres[w]);
+    int tot;
+    int acc = gm_block_scan(part, s_tmp, &tot);
+    for (int w = w0; w < w1; w++) {
+      s_pre[w] = (uint32_t)acc;
+      acc += __builtin_popcountll(s_pres[w]);
+    }
+  }
+  __syncthreads();
+
+  if (tid == 0) {
+    // gossip-target draw on the post-sweep list (MP1Node.cpp:449-489); newNodes is
+    // empty in the converged SCALED regime (no JOINREQ traffic)
+    const int numpot = size - 1 - numfailed;
+    int n = 0;
+    int g[GM_FANOUT];
+    if (numpot > 0) {
+      GmLazyMT mt;
+      mt.seed(s_mt, gm_rd_seed(s.rd_seed, t, r + 1));
+      long guard = 0;
+      while (n < GM_FANOUT && n < numpot) {
+        if (++guard > (1l << 22)) { atomicOr(s.err, GM_ERR_DRAWS); break; }
+        const int ix = mt.uniform((uint32_t)size);
+        const int c = gm_rank_select(s_pres, s_pre, nw, (uint32_t)ix);
+        if (c == selfc) continue;                                 // "me"
+        if (!((s_fresh[c >> 6] >> (c & 63)) & 1ull)) continue;    // age >= TFAIL
+        bool dup = false;
+        for (int q = 0; q < n; q++) dup |= g[q] == c;
+        if (!dup) g[n++] = c;
+      }
+    }
+    int32_t *cnt_out = s.inbox_cnt[par ^ 1];
+    for (int q = 0; q < n; q++) {
+      const int dst = s.c0 + g[q];
+      s.targets[(size_t)r * GM_FANOUT + q] = dst;
+      const int slot = atomicAdd(&cnt_out[dst], 1);
+      if (slot < S_KMAX) s.inbox[par ^ 1][(size_t)dst * S_KMAX + slot] = r;
+      else atomicOr(s.err, GM_ERR_INBOX);
+    }
+    stat[0] = k;
+    stat[1] = size;
+    stat[2] = numfailed;
+    stat[3] = n;
+    s.ev_cnt[r] = s_misc[1];
+  }
+}

@@ -1,0 +1,159 @@
+/* gm_abi.h -- C ABI of the MI355X-native gossip-membership simulator (libgm.so).
+ *
+ * The drop-in boundary. The reference's own plugin seam is the
+ * Application <-> MP1Node <-> EmulNet API: the driver calls, per node and per
+ * globaltime tick, MP1Node::recvLoop (-> EmulNet::ENrecv) and MP1Node::nodeStart /
+ * nodeLoop (-> checkMessages, nodeLoopOps, sendMemberList -> EmulNet::ENsend),
+ * then Application::fail pokes Member::bFailed / Params::dropmsg and draws from
+ * rand(). Here the whole per-tick body of Application::mp1Run for ALL nodes is
+ * one call, gm_tick(); fault injection keeps its host-side driver (gm_rand,
+ * gm_set_failed, gm_set_dropmsg); dbg.log / msgcount.log content comes back as
+ * plain records. Plain C types only; no HIP or torch types cross the boundary.
+ *
+ * Reference interface each entry point replaces (file:line in the reference):
+ *   gm_create       Application::Application + EmulNet::EmulNet + ENinit + new MP1Node
+ *                   (Application.cpp:47-70, EmulNet.cpp:12-27,72-77, MP1Node.cpp:25-34),
+ *                   Params::setparams values in gm_config (Params.cpp:19-40)
+ *   gm_tick         Application::mp1Run (Application.cpp:121-164): recvLoop/ENrecv for
+ *                   i ascending, then nodeStart/nodeLoop (checkMessages, updatelistCallBack,
+ *                   joinreqCallBack, nodeLoopOps, sendMemberList, ENsend) for i descending
+ *                   (MP1Node.cpp:47-54,73-163,182-495; EmulNet.cpp:87-177)
+ *   gm_rand         rand() in Application::fail (Application.cpp:182,189) -- the SAME S1
+ *                   stream ENsend draws from (EmulNet.cpp:90)
+ *   gm_set_failed   mp1[i]->getMemberNode()->bFailed = true (Application.cpp:186,194)
+ *   gm_set_dropmsg  par->dropmsg = 0/1 (Application.cpp:178,199)
+ *   gm_drain_events Log::LOG / logNodeAdd / logNodeRemove call sites inside the tick
+ *                   (Log.cpp:44-131; MP1Node.cpp:135,153,295,437; Application.cpp:158)
+ *   gm_msgcount     EmulNet::sent_msgs / recv_msgs as dumped by ENcleanup (EmulNet.cpp:184-220)
+ *   gm_dump_tables  Member::memberList of every node (Member.h:89-122), for parity tests
+ *   gm_destroy      Application::~Application / ENcleanup storage release
+ *
+ * Conventions: every function returns GM_OK (0) or a negative GM_E* code and never
+ * throws; the context owns all device memory; output buffers are caller-owned;
+ * one host thread per context. gm_tick enqueues the tick on the context's HIP
+ * stream and returns (a tick is a BSP round: sends of tick t are consumed in
+ * tick t+1); every read-back function and gm_sync wait for enqueued ticks.
+ */
+#ifndef GM_ABI_H
+#define GM_ABI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GM_ABI_VERSION 1
+
+enum gm_status {
+  GM_OK = 0,
+  GM_EINVAL = -1,     /* bad argument / config */
+  GM_ENOMEM = -2,     /* device or host allocation failed */
+  GM_EDEVICE = -3,    /* HIP runtime error */
+  GM_ERANGE = -4,     /* a bounded resource overflowed (inbox, event ring, draw table) */
+  GM_ESTATE = -5,     /* protocol invariant the fast path relies on was violated */
+  GM_EUNSUPPORTED = -6,
+  GM_ECOMM = -7       /* collective (RCCL) failure */
+};
+
+enum gm_mode {
+  GM_MODE_FAITHFUL = 0, /* the reference: EmulNet cap 30000, per-entry messages, S1 drops */
+  GM_MODE_SCALED = 1    /* build-defined large-N regime: converged start, keyed drops */
+};
+
+enum gm_event_kind {
+  GM_EV_JOINED = 1,        /* "Node a.b.c.d:p joined at time t"   (Log.cpp:116-120) */
+  GM_EV_REMOVED = 2,       /* "Node a.b.c.d:p removed at time t"  (Log.cpp:127-131) */
+  GM_EV_START_GROUP = 3,   /* "Starting up group..."              (MP1Node.cpp:135) */
+  GM_EV_TRY_JOIN = 4,      /* "Trying to join..."                 (MP1Node.cpp:152-153) */
+  GM_EV_TIME_MARK = 5      /* "@@time=t"                          (Application.cpp:156-160) */
+};
+
+typedef struct gm_config {
+  int32_t abi_version;     /* = GM_ABI_VERSION */
+  int32_t mode;            /* enum gm_mode */
+  int32_t n;               /* EN_GPSZ (= MAX_NNB) */
+  int32_t single_failure;  /* SINGLE_FAILURE (host-side fail() uses it; kept for completeness) */
+  int32_t drop_msg;        /* DROP_MSG */
+  double drop_prob;        /* MSG_DROP_PROB (FAITHFUL: drop iff rand()%100 < (int)(p*100)) */
+  uint32_t time_seed;      /* S1: srand(TIME_SEED) */
+  uint64_t rd_seed;        /* S2: per-(tick, id) mt19937 seed contract */
+  /* SCALED only */
+  int32_t drop_pct;        /* per-entry drop percentage */
+  int32_t drop_from;       /* drops apply to sends at ticks in [drop_from, drop_to) */
+  int32_t drop_to;
+  uint64_t drop_seed;
+  /* placement */
+  int32_t device;          /* HIP device ordinal */
+  int32_t shard_rank;      /* column shard of this context (SCALED multi-GPU); 0 */
+  int32_t shard_count;     /* number of column shards; 1 */
+  int32_t reserved[8];
+} gm_config;
+
+/* one log record; `order` sorts records of a drain into reference log order */
+typedef struct gm_event {
+  int32_t t;
+  int32_t logger;          /* node index (id = logger + 1) whose LOG call it is */
+  int32_t kind;            /* enum gm_event_kind */
+  int32_t subject;         /* node id joined/removed; 0 otherwise */
+} gm_event;
+
+typedef struct gm_ctx gm_ctx;
+
+/* Params::setparams equivalent: parse a reference testcase .conf
+ * ("MAX_NNB: %d\nSINGLE_FAILURE: %d\nDROP_MSG: %d\nMSG_DROP_PROB: %lf"). */
+int gm_parse_conf(const char *path, gm_config *cfg);
+
+int gm_create(const gm_config *cfg, gm_ctx **out);
+int gm_destroy(gm_ctx *ctx);
+
+/* Enqueue one Application::mp1Run tick at the context's current globaltime,
+ * then advance globaltime. Returns a latched device error from an earlier tick. */
+int gm_tick(gm_ctx *ctx);
+int gm_sync(gm_ctx *ctx);
+int gm_time(gm_ctx *ctx, int32_t *t);
+
+/* Application::fail hooks (called between ticks, host order preserved) */
+int gm_rand(gm_ctx *ctx, int32_t *out);
+int gm_set_failed(gm_ctx *ctx, const int32_t *idx, int32_t n);
+int gm_set_dropmsg(gm_ctx *ctx, int32_t on);
+
+/* Drain every event produced since the last drain, in reference log order
+ * (ticks ascending; node phase i descending; per node: start line or joins in
+ * dequeue order, then removals by descending id, then @@time). If cap is too
+ * small, *n receives the number pending and GM_ERANGE is returned (nothing drained). */
+int gm_drain_events(gm_ctx *ctx, gm_event *out, size_t cap, size_t *n);
+/* number of events produced in the last tick, per kind (SCALED bench telemetry) */
+int gm_event_counts(gm_ctx *ctx, uint64_t counts[6]);
+
+/* sent/recv message counts per node id 1..n for ticks [0, t): out arrays [n][t] */
+int gm_msgcount(gm_ctx *ctx, int32_t t, int32_t *sent, int32_t *recv);
+
+/* Dense readback of observer row r: hb/ts per subject column (absent -> -1),
+ * columns [c0, c0+len) of this context's shard (c0 relative to the shard start). */
+int gm_read_row(gm_ctx *ctx, int32_t r, int32_t c0, int32_t len, int32_t *hb, int32_t *ts);
+/* node state: inited, inGroup, bFailed, heartbeat counter (4 int32 per node) */
+int gm_read_nodes(gm_ctx *ctx, int32_t *state4);
+/* Render the membership lists of every node in the parity dump format
+ * ("t i inited inGroup bFailed heartbeat n id:hb:ts ...\n" per node). */
+int gm_dump_tables(gm_ctx *ctx, char *buf, size_t cap, size_t *len);
+
+/* SCALED telemetry of the last tick: [0]=delivered gossip lists M, [1]=live nodes,
+ * [2]=max inbox depth, [3]=error flags */
+int gm_tick_stats(gm_ctx *ctx, int64_t stats[4]);
+/* duration (ms) of the last tick's dominant kernel, timed with HIP events on the
+ * context stream (0 when not measured); enable with gm_set_timing(ctx, 1) */
+int gm_set_timing(gm_ctx *ctx, int32_t on);
+int gm_last_kernel_ms(gm_ctx *ctx, float *ms);
+
+/* Crash set of the SCALED fault schedule: `count` node indices, ascending,
+ * chosen by a splitmix64-keyed permutation of [0, n) (host fault injection). */
+int gm_crash_set(int32_t n, int32_t count, uint64_t seed, int32_t *out);
+
+const char *gm_strerror(int code);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GM_ABI_H */

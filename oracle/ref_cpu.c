@@ -1,0 +1,715 @@
+/* ref_cpu.c -- CPU restatement of the reference simulator (the parity oracle).
+ *
+ * TEST INFRASTRUCTURE ONLY; see ref_cpu.h for scope and the list of reference
+ * functions restated. Data structures intentionally follow the reference
+ * (sorted per-node member lists with lower_bound, a flat EmulNet message array
+ * scanned from the end with swap-with-last removal) rather than the dense
+ * SoA table of the HIP product, so the oracle shares no design decision with
+ * the code it checks.
+ */
+#include "ref_cpu.h"
+
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define TFAIL 5            /* MP1Node.h:21 */
+#define TREMOVE 20         /* MP1Node.h:20 */
+#define FANOUT 5           /* MP1Node.cpp:456 maxneighbors */
+#define ENBUFFSIZE 30000   /* EmulNet.h:12 */
+#define MAX_MSG_SIZE 4000  /* Params.cpp:31 */
+#define EN_MSG_HDR 16      /* sizeof(en_msg), EmulNet.h:23-30 */
+#define MAX_TIME 3600      /* EmulNet.h:11 */
+#define MAX_NODES 1000     /* EmulNet.h:10 */
+#define LIST_SIZE 19       /* sizeof(MessageHdr)+6+8+1, MP1Node.cpp:143,364 */
+#define JOINREP_SIZE 4     /* sizeof(MessageHdr), MP1Node.cpp:250 */
+
+enum { JOINREQ = 0, JOINREP = 1, LIST = 2 }; /* MP1Node.h:30-35 */
+
+/* ---------------------------------------------------------------- RNG S1 -- */
+/* glibc TYPE_3 random_r/srandom_r (degree 31, separation 3), restated. */
+void oc_srand(oc_rand *g, uint32_t seed) {
+  if (seed == 0) seed = 1;
+  int32_t word = (int32_t)seed;
+  g->st[0] = word;
+  for (int i = 1; i < 31; i++) {
+    long hi = word / 127773, lo = word % 127773;
+    word = (int32_t)(16807 * lo - 2836 * hi);
+    if (word < 0) word += 2147483647;
+    g->st[i] = word;
+  }
+  g->f = 3;
+  g->r = 0;
+  for (int k = 0; k < 310; k++) (void)oc_rand_next(g);
+}
+
+int32_t oc_rand_next(oc_rand *g) {
+  uint32_t v = (uint32_t)g->st[g->f] + (uint32_t)g->st[g->r];
+  g->st[g->f] = (int32_t)v;
+  g->f = (g->f + 1) % 31;
+  g->r = (g->r + 1) % 31;
+  return (int32_t)(v >> 1);
+}
+
+/* ---------------------------------------------------------------- RNG S2 -- */
+static uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+/* seed contract: one splitmix64 step over RD_SEED ^ (t<<32 | id) */
+uint32_t oc_rd_seed(uint64_t rd_seed, int32_t tick, int32_t id) {
+  uint64_t z = rd_seed ^ (((uint64_t)(uint32_t)tick << 32) | (uint32_t)id);
+  return (uint32_t)mix64(z + 0x9E3779B97F4A7C15ULL);
+}
+
+typedef struct mt { uint32_t x[624]; int i; } mt;
+
+static void mt_seed(mt *m, uint32_t s) {
+  m->x[0] = s;
+  for (int i = 1; i < 624; i++) m->x[i] = 1812433253u * (m->x[i - 1] ^ (m->x[i - 1] >> 30)) + (uint32_t)i;
+  m->i = 624;
+}
+
+static uint32_t mt_next(mt *m) {
+  if (m->i >= 624) {
+    for (int k = 0; k < 624; k++) {
+      uint32_t y = (m->x[k] & 0x80000000u) | (m->x[(k + 1) % 624] & 0x7fffffffu);
+      m->x[k] = m->x[(k + 397) % 624] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    }
+    m->i = 0;
+  }
+  uint32_t y = m->x[m->i++];
+  y ^= y >> 11;
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= y >> 18;
+  return y;
+}
+
+/* libstdc++-11 uniform_int_distribution<int>(0, n-1) over a 32-bit engine: Lemire
+ * (bits/uniform_int_dist.h _S_nd, downscaling branch). */
+static int mt_uniform(mt *m, uint32_t range) {
+  uint64_t prod = (uint64_t)mt_next(m) * range;
+  uint32_t low = (uint32_t)prod;
+  if (low < range) {
+    uint32_t thr = (uint32_t)(-range) % range;
+    while (low < thr) {
+      prod = (uint64_t)mt_next(m) * range;
+      low = (uint32_t)prod;
+    }
+  }
+  return (int)(prod >> 32);
+}
+
+void oc_mt_uniform(uint32_t seed, int n, int k, int32_t *out) {
+  mt m;
+  mt_seed(&m, seed);
+  for (int i = 0; i < k; i++) out[i] = mt_uniform(&m, (uint32_t)n);
+}
+
+/* ------------------------------------------------------------ containers -- */
+typedef struct entry { int32_t id; int16_t port; int64_t hb, ts; } entry; /* MemberListEntry, Member.h:62-81 */
+typedef struct elist { entry *v; int n, cap; } elist;
+typedef struct msg { int32_t size, from, to, type, id; int16_t port; int64_t hb; } msg;
+typedef struct mvec { msg *v; int n, cap; } mvec;
+typedef struct sbuf { char *p; size_t n, cap; } sbuf;
+
+static void el_push(elist *l, entry e) {
+  if (l->n == l->cap) {
+    l->cap = l->cap ? 2 * l->cap : 16;
+    l->v = (entry *)realloc(l->v, sizeof(entry) * (size_t)l->cap);
+  }
+  l->v[l->n++] = e;
+}
+
+static void mv_push(mvec *l, const msg *m) {
+  if (l->n == l->cap) {
+    l->cap = l->cap ? 2 * l->cap : 64;
+    l->v = (msg *)realloc(l->v, sizeof(msg) * (size_t)l->cap);
+  }
+  l->v[l->n++] = *m;
+}
+
+static void sb_put(sbuf *b, const char *s, size_t k) {
+  if (b->n + k + 1 > b->cap) {
+    b->cap = (b->n + k + 1) * 2;
+    b->p = (char *)realloc(b->p, b->cap);
+  }
+  memcpy(b->p + b->n, s, k);
+  b->n += k;
+  b->p[b->n] = 0;
+}
+
+static void sb_printf(sbuf *b, const char *fmt, ...) {
+  char tmp[512];
+  va_list ap;
+  va_start(ap, fmt);
+  int k = vsnprintf(tmp, sizeof tmp, fmt, ap);
+  va_end(ap);
+  sb_put(b, tmp, (size_t)k);
+}
+
+/* MemberCompareLessThan, MP1Node.cpp:13-18 */
+static int ent_less(const entry *a, int32_t id, int16_t port) {
+  return a->id < id || (a->id == id && a->port < port);
+}
+static int ent_cmp(const void *x, const void *y) {
+  const entry *a = (const entry *)x, *b = (const entry *)y;
+  if (a->id != b->id) return a->id < b->id ? -1 : 1;
+  if (a->port != b->port) return a->port < b->port ? -1 : 1;
+  return 0;
+}
+static int lower_bound(const elist *l, int32_t id, int16_t port) {
+  int lo = 0, hi = l->n;
+  while (lo < hi) {
+    int mid = (lo + hi) / 2;
+    if (ent_less(&l->v[mid], id, port)) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+static void el_sort(elist *l) { qsort(l->v, (size_t)l->n, sizeof(entry), ent_cmp); }
+
+/* ------------------------------------------------------------ simulation -- */
+typedef struct node {
+  int32_t id;
+  int inited, in_group, failed;
+  int64_t heartbeat;
+  elist list;
+  int mypos;
+  mvec q;        /* mp1q */
+} node;
+
+typedef struct snap { int32_t *ids, *hbs; int n; } snap; /* SCALED: gossip payload snapshot */
+
+struct oc_ctx {
+  oc_config cfg;
+  int n, t;
+  node *nodes;
+  oc_rand s1;
+  int dropmsg;
+  /* EmulNet */
+  mvec buff;
+  int32_t *sent, *recv; /* [MAX_NODES+1][MAX_TIME] in FAITHFUL */
+  /* Log */
+  sbuf dbg, out, tmp;
+  int log_opened, log_first;
+  /* SCALED network: snapshot + targets of every sender at the previous tick */
+  snap *snaps, *snaps_next;
+  int32_t *tgt, *ntgt, *tgt_next, *ntgt_next;
+  oc_event *ev;
+  size_t nev, evcap;
+  int32_t *crash;
+};
+
+static int is_scaled(const oc_ctx *c) { return c->cfg.mode == OC_SCALED; }
+
+/* Address bytes: int32 id LE + int16 port (Member.h:29-55; EmulNet.cpp:74-75) */
+static void addr_bytes(int32_t id, int16_t port, unsigned char b[6]) {
+  memcpy(b, &id, 4);
+  memcpy(b + 4, &port, 2);
+}
+
+/* strcmp(emsg->to.addr, myaddr->addr) == 0 (EmulNet.cpp:154): C-string compare of the 6 bytes */
+static int addr_streq(int32_t a, int32_t b) {
+  unsigned char x[7], y[7];
+  addr_bytes(a, 0, x);
+  addr_bytes(b, 0, y);
+  x[6] = y[6] = 0;
+  return strcmp((const char *)x, (const char *)y) == 0;
+}
+
+/* "%d.%d.%d.%d:%d" over signed char bytes (Log.cpp:73,118,129) */
+static int fmt_addr(char *dst, int32_t id, int16_t port) {
+  unsigned char b[6];
+  addr_bytes(id, port, b);
+  return sprintf(dst, "%d.%d.%d.%d:%d", (signed char)b[0], (signed char)b[1], (signed char)b[2],
+                 (signed char)b[3], (int)port);
+}
+
+/* Log::LOG (Log.cpp:44-109): first record carries no address prefix; magic "131\n" once. */
+static void log_line(oc_ctx *c, int32_t id, const char *text) {
+  if (is_scaled(c)) return;
+  char pre[64];
+  pre[0] = 0;
+  if (!c->log_opened) {
+    c->log_opened = 1;
+  } else {
+    int k = fmt_addr(pre, id, 0);
+    pre[k] = ' ';
+    pre[k + 1] = 0;
+  }
+  if (!c->log_first) {
+    int magic = 0;
+    const char *m = "CS425";
+    for (int i = 0; m[i]; i++) magic += m[i];
+    sb_printf(&c->dbg, "%x\n", magic);
+    c->log_first = 1;
+  }
+  sb_printf(&c->dbg, "\n %s", pre);
+  sb_printf(&c->dbg, "[%d] ", c->t);
+  sb_put(&c->dbg, text, strlen(text));
+}
+
+static void emit_event(oc_ctx *c, int32_t logger_idx, int kind, int32_t subject) {
+  if (!is_scaled(c)) {
+    char a[48], s[96];
+    fmt_addr(a, subject, 0);
+    sprintf(s, "Node %s %s at time %d", a, kind == OC_EV_ADD ? "joined" : "removed", c->t);
+    log_line(c, c->nodes[logger_idx].id, s);
+    return;
+  }
+  if (c->nev == c->evcap) {
+    c->evcap = c->evcap ? 2 * c->evcap : 1024;
+    c->ev = (oc_event *)realloc(c->ev, sizeof(oc_event) * c->evcap);
+  }
+  oc_event e = {c->t, logger_idx, kind, subject};
+  c->ev[c->nev++] = e;
+}
+
+/* EmulNet::ENsend (EmulNet.cpp:87-118) */
+static int en_send(oc_ctx *c, int32_t from, int32_t to, int type, int32_t id, int16_t port, int64_t hb, int size) {
+  int draw = oc_rand_next(&c->s1) % 100;
+  if (c->buff.n >= ENBUFFSIZE || size + EN_MSG_HDR >= MAX_MSG_SIZE ||
+      (c->dropmsg && draw < (int)(c->cfg.drop_prob * 100)))
+    return 0;
+  msg m = {size, from, to, type, id, port, hb};
+  mv_push(&c->buff, &m);
+  c->sent[(size_t)from * MAX_TIME + (size_t)c->t]++;
+  return size;
+}
+
+/* EmulNet::ENrecv (EmulNet.cpp:144-177): scan from the end, swap-with-last removal */
+static void en_recv(oc_ctx *c, node *nd) {
+  for (int i = c->buff.n - 1; i >= 0; i--) {
+    if (addr_streq(c->buff.v[i].to, nd->id)) {
+      msg m = c->buff.v[i];
+      c->buff.v[i] = c->buff.v[c->buff.n - 1];
+      c->buff.n--;
+      mv_push(&nd->q, &m);
+      c->recv[(size_t)nd->id * MAX_TIME + (size_t)c->t]++;
+    }
+  }
+}
+
+/* MP1Node::updateMyPos (MP1Node.cpp:308-322), including the `&&` quirk at :316 */
+static void update_my_pos(oc_ctx *c, node *nd) {
+  int p = lower_bound(&nd->list, nd->id, 0);
+  if (p == nd->list.n || (nd->list.v[p].id != nd->id && nd->list.v[p].port != 0)) {
+    entry e = {nd->id, 0, nd->heartbeat, c->t};
+    el_push(&nd->list, e);
+    el_sort(&nd->list);
+    p = lower_bound(&nd->list, nd->id, 0);
+  }
+  nd->mypos = p;
+}
+
+/* MP1Node::updatelistCallBack (MP1Node.cpp:259-301): returns 1 when inserted */
+static int update_list(oc_ctx *c, int idx, int32_t id, int16_t port, int64_t hb) {
+  node *nd = &c->nodes[idx];
+  int p = lower_bound(&nd->list, id, port);
+  if (p < nd->list.n && nd->list.v[p].id == id && nd->list.v[p].port == port) {
+    if (nd->list.v[p].hb < hb) {
+      nd->list.v[p].hb = hb;
+      nd->list.v[p].ts = c->t;
+    }
+    return 0;
+  }
+  entry e = {id, port, hb, c->t};
+  el_push(&nd->list, e);
+  emit_event(c, idx, OC_EV_ADD, id);
+  el_sort(&nd->list);
+  return 1;
+}
+
+/* MP1Node::sendMemberList (MP1Node.cpp:360-395) */
+static void send_member_list(oc_ctx *c, node *nd, int32_t to) {
+  for (int k = 0; k < nd->list.n; k++) {
+    entry *e = &nd->list.v[k];
+    if (c->t - e->ts >= TFAIL) continue;
+    en_send(c, nd->id, to, LIST, e->id, e->port, e->hb, LIST_SIZE);
+  }
+}
+
+/* MP1Node::nodeLoopOps (MP1Node.cpp:404-495) */
+static void node_loop_ops(oc_ctx *c, int idx, const entry *new_nodes, int n_new) {
+  node *nd = &c->nodes[idx];
+  int64_t now = c->t;
+  update_my_pos(c, nd);
+  nd->heartbeat++;
+  nd->list.v[nd->mypos].hb = nd->heartbeat++;
+  nd->list.v[nd->mypos].ts = now;
+  entry me = nd->list.v[nd->mypos];
+  int len = nd->list.n, numfailed = 0;
+  for (int i = len - 1; i >= 0; --i) {
+    int64_t diff = now - nd->list.v[i].ts;
+    if (diff >= TFAIL) {
+      numfailed++;
+      if (diff >= TREMOVE) {
+        int cur = nd->list.n;
+        emit_event(c, idx, OC_EV_REMOVE, nd->list.v[i].id);
+        entry tmp = nd->list.v[i];
+        nd->list.v[i] = nd->list.v[cur - 1];
+        nd->list.v[cur - 1] = tmp;
+        nd->list.n--;
+      }
+    }
+  }
+  el_sort(&nd->list);
+  nd->mypos = lower_bound(&nd->list, me.id, me.port);
+
+  mt m;
+  mt_seed(&m, oc_rd_seed(c->cfg.rd_seed, c->t, nd->id));
+  uint32_t range = (uint32_t)nd->list.n; /* dist(0, size-1) */
+  entry *gossip = (entry *)malloc(sizeof(entry) * (size_t)(n_new + FANOUT));
+  int n = 0;
+  for (int k = 0; k < n_new; k++) gossip[n++] = new_nodes[k];
+  int32_t myid = nd->list.v[nd->mypos].id;
+  int16_t myport = nd->list.v[nd->mypos].port;
+  int numpot = nd->list.n - 1 - numfailed;
+  int skipfailed = numpot > 0;
+  while (n < FANOUT && n < numpot) {
+    int ix = mt_uniform(&m, range);
+    entry *e = &nd->list.v[ix];
+    if (e->id != myid || e->port != myport) {
+      if (skipfailed && (now - e->ts >= TFAIL)) continue;
+      int found = 0;
+      for (int k = 0; k < n; k++)
+        if (gossip[k].id == e->id && gossip[k].port == e->port) { found = 1; break; }
+      if (!found) gossip[n++] = *e;
+    }
+  }
+  if (!is_scaled(c)) {
+    for (int k = 0; k < n; k++) send_member_list(c, nd, gossip[k].id);
+    free(gossip);
+    return;
+  }
+  /* SCALED: one payload snapshot per sender (its fresh entries now), shared by every target */
+  snap *s = &c->snaps_next[idx];
+  s->n = 0;
+  for (int k = 0; k < nd->list.n; k++) {
+    entry *e = &nd->list.v[k];
+    if (now - e->ts >= TFAIL) continue;
+    s->ids[s->n] = e->id;
+    s->hbs[s->n] = (int32_t)e->hb;
+    s->n++;
+  }
+  c->ntgt_next[idx] = n;
+  for (int k = 0; k < n; k++) c->tgt_next[(size_t)idx * FANOUT + k] = gossip[k].id - 1;
+  free(gossip);
+}
+
+/* MP1Node::nodeLoop + checkMessages + recvCallBack + joinreqCallBack (MP1Node.cpp:182-353) */
+static void node_loop(oc_ctx *c, int idx) {
+  node *nd = &c->nodes[idx];
+  if (nd->failed) return;
+  entry *newn = NULL;
+  int n_new = 0, cap_new = 0;
+  for (int k = 0; k < nd->q.n; k++) {
+    msg *m = &nd->q.v[k];
+    if (m->type == JOINREQ) {
+      if (update_list(c, idx, m->id, m->port, m->hb)) {
+        if (n_new == cap_new) {
+          cap_new = cap_new ? 2 * cap_new : 8;
+          newn = (entry *)realloc(newn, sizeof(entry) * (size_t)cap_new);
+        }
+        entry e = {m->id, m->port, m->hb, c->t};
+        newn[n_new++] = e;
+      }
+      en_send(c, nd->id, m->id, JOINREP, 0, 0, 0, JOINREP_SIZE);
+    } else if (m->type == JOINREP) {
+      nd->in_group = 1;
+    } else if (m->type == LIST) {
+      update_list(c, idx, m->id, m->port, m->hb);
+    }
+  }
+  nd->q.n = 0;
+  if (nd->in_group) node_loop_ops(c, idx, newn, n_new);
+  free(newn);
+}
+
+/* MP1Node::nodeStart -> initThisNode + introduceSelfToGroup (MP1Node.cpp:73-163) */
+static void node_start(oc_ctx *c, int idx) {
+  node *nd = &c->nodes[idx];
+  nd->failed = 0;
+  nd->inited = 1;
+  nd->in_group = 0;
+  nd->heartbeat = 0;
+  nd->list.n = 0;
+  if (nd->id == 1) { /* getJoinAddress() = 1:0 (MP1Node.cpp:511-519) */
+    log_line(c, nd->id, "Starting up group...");
+    update_my_pos(c, nd);
+    nd->in_group = 1;
+  } else {
+    log_line(c, nd->id, "Trying to join...");
+    en_send(c, nd->id, 1, JOINREQ, nd->id, 0, nd->heartbeat, LIST_SIZE);
+  }
+}
+
+/* SCALED recv: every gossip list sent to this node at t-1, senders ascending,
+ * entries ascending id, per-entry keyed drops. */
+static void scaled_recv(oc_ctx *c, int idx) {
+  for (int s = 0; s < c->n; s++) {
+    for (int k = 0; k < c->ntgt[s]; k++) {
+      if (c->tgt[(size_t)s * FANOUT + k] != idx) continue;
+      snap *p = &c->snaps[s];
+      int t_send = c->t - 1;
+      int dropping = c->cfg.drop_pct > 0 && t_send >= c->cfg.drop_from && t_send < c->cfg.drop_to;
+      uint64_t pair = mix64(c->cfg.drop_seed ^ ((uint64_t)(uint32_t)t_send << 48) ^ ((uint64_t)s << 24) ^ (uint64_t)idx);
+      for (int e = 0; e < p->n; e++) {
+        if (dropping) {
+          uint32_t h = (uint32_t)(mix64(pair + (uint64_t)(p->ids[e] - 1)) >> 32);
+          if ((int)(h % 100u) < c->cfg.drop_pct) continue;
+        }
+        update_list(c, idx, p->ids[e], 0, p->hbs[e]);
+      }
+    }
+  }
+}
+
+static int ev_canon(const void *x, const void *y) {
+  const oc_event *a = (const oc_event *)x, *b = (const oc_event *)y;
+  if (a->logger != b->logger) return a->logger > b->logger ? -1 : 1; /* node phase: i descending */
+  if (a->kind != b->kind) return a->kind < b->kind ? -1 : 1;         /* ADDs then REMOVEs */
+  if (a->kind == OC_EV_ADD) return a->subject < b->subject ? -1 : (a->subject > b->subject);
+  return a->subject > b->subject ? -1 : (a->subject < b->subject);
+}
+
+/* Application::mp1Run (Application.cpp:121-164) */
+static void mp1_run(oc_ctx *c) {
+  int t = c->t;
+  if (!is_scaled(c)) {
+    for (int i = 0; i < c->n; i++)
+      if (t > (int)(0.25 * i) && !c->nodes[i].failed) en_recv(c, &c->nodes[i]);
+    for (int i = c->n - 1; i >= 0; i--) {
+      if (t == (int)(0.25 * i)) {
+        node_start(c, i);
+        sb_printf(&c->out, "%d-th introduced node is assigned with the address: %d:0\n", i, c->nodes[i].id);
+      } else if (t > (int)(0.25 * i) && !c->nodes[i].failed) {
+        node_loop(c, i);
+        if (i == 0 && t % 500 == 0) {
+          char s[64];
+          sprintf(s, "@@time=%d", t);
+          log_line(c, c->nodes[0].id, s);
+        }
+      }
+    }
+    return;
+  }
+  c->nev = 0;
+  for (int i = c->n - 1; i >= 0; i--) {
+    if (c->nodes[i].failed) continue;
+    scaled_recv(c, i);
+    node_loop(c, i);
+  }
+  qsort(c->ev, c->nev, sizeof(oc_event), ev_canon);
+  snap *ts = c->snaps; c->snaps = c->snaps_next; c->snaps_next = ts;
+  int32_t *tt = c->tgt; c->tgt = c->tgt_next; c->tgt_next = tt;
+  tt = c->ntgt; c->ntgt = c->ntgt_next; c->ntgt_next = tt;
+  memset(c->ntgt_next, 0, sizeof(int32_t) * (size_t)c->n);
+}
+
+/* Application::fail (Application.cpp:173-202) */
+static void app_fail(oc_ctx *c) {
+  int t = c->t;
+  if (is_scaled(c)) {
+    if (t == c->cfg.crash_tick)
+      for (int k = 0; k < c->cfg.crash_count; k++) c->nodes[c->crash[k]].failed = 1;
+    return;
+  }
+  char s[64];
+  if (c->cfg.drop_msg && t == 50) c->dropmsg = 1;
+  if (c->cfg.single_failure && t == 100) {
+    int removed = oc_rand_next(&c->s1) % c->n;
+    sprintf(s, "Node failed at time=%d", t);
+    log_line(c, c->nodes[removed].id, s);
+    c->nodes[removed].failed = 1;
+  } else if (t == 100) {
+    int removed = oc_rand_next(&c->s1) % c->n / 2;
+    for (int i = removed; i < removed + c->n / 2; i++) {
+      sprintf(s, "Node failed at time = %d", t);
+      log_line(c, c->nodes[i].id, s);
+      c->nodes[i].failed = 1;
+    }
+  }
+  if (c->cfg.drop_msg && t == 300) c->dropmsg = 0;
+}
+
+typedef struct ck { uint64_t key; int32_t idx; } ck;
+static int ck_cmp(const void *x, const void *y) {
+  const ck *a = (const ck *)x, *b = (const ck *)y;
+  if (a->key != b->key) return a->key < b->key ? -1 : 1;
+  return a->idx - b->idx;
+}
+static int i32_cmp(const void *x, const void *y) { return *(const int32_t *)x - *(const int32_t *)y; }
+
+int oc_crash_set(int n, int count, uint64_t seed, int32_t *out) {
+  if (count < 0 || count > n) return -1;
+  ck *k = (ck *)malloc(sizeof(ck) * (size_t)n);
+  for (int i = 0; i < n; i++) {
+    k[i].key = mix64(seed + 0x9E3779B97F4A7C15ULL * (uint64_t)(i + 1));
+    k[i].idx = i;
+  }
+  qsort(k, (size_t)n, sizeof(ck), ck_cmp);
+  for (int i = 0; i < count; i++) out[i] = k[i].idx;
+  qsort(out, (size_t)count, sizeof(int32_t), i32_cmp);
+  free(k);
+  return 0;
+}
+
+oc_ctx *oc_create(const oc_config *cfg) {
+  if (cfg->n <= 0) return NULL;
+  if (cfg->mode == OC_FAITHFUL && cfg->n > MAX_NODES) return NULL; /* EmulNet.cpp:108 assert */
+  oc_ctx *c = (oc_ctx *)calloc(1, sizeof(oc_ctx));
+  c->cfg = *cfg;
+  c->n = cfg->n;
+  c->nodes = (node *)calloc((size_t)c->n, sizeof(node));
+  for (int i = 0; i < c->n; i++) c->nodes[i].id = i + 1; /* ENinit: ids from 1 (EmulNet.cpp:74) */
+  if (cfg->mode == OC_FAITHFUL) {
+    c->sent = (int32_t *)calloc((size_t)(MAX_NODES + 1) * MAX_TIME, sizeof(int32_t));
+    c->recv = (int32_t *)calloc((size_t)(MAX_NODES + 1) * MAX_TIME, sizeof(int32_t));
+    for (int i = 0; i < c->n; i++) log_line(c, c->nodes[i].id, "APP"); /* Application.cpp:66 */
+    oc_srand(&c->s1, cfg->time_seed); /* srand(time(NULL)), Application.cpp:50 and :96 */
+    c->t = 0;
+  } else {
+    for (int i = 0; i < c->n; i++) {
+      node *nd = &c->nodes[i];
+      nd->inited = nd->in_group = 1;
+      nd->list.v = (entry *)malloc(sizeof(entry) * (size_t)c->n);
+      nd->list.cap = nd->list.n = c->n;
+      for (int j = 0; j < c->n; j++) {
+        entry e = {j + 1, 0, 0, 0};
+        nd->list.v[j] = e;
+      }
+    }
+    c->snaps = (snap *)calloc((size_t)c->n, sizeof(snap));
+    c->snaps_next = (snap *)calloc((size_t)c->n, sizeof(snap));
+    for (int i = 0; i < c->n; i++) {
+      c->snaps[i].ids = (int32_t *)malloc(sizeof(int32_t) * (size_t)c->n);
+      c->snaps[i].hbs = (int32_t *)malloc(sizeof(int32_t) * (size_t)c->n);
+      c->snaps_next[i].ids = (int32_t *)malloc(sizeof(int32_t) * (size_t)c->n);
+      c->snaps_next[i].hbs = (int32_t *)malloc(sizeof(int32_t) * (size_t)c->n);
+    }
+    c->tgt = (int32_t *)calloc((size_t)c->n * FANOUT, sizeof(int32_t));
+    c->tgt_next = (int32_t *)calloc((size_t)c->n * FANOUT, sizeof(int32_t));
+    c->ntgt = (int32_t *)calloc((size_t)c->n, sizeof(int32_t));
+    c->ntgt_next = (int32_t *)calloc((size_t)c->n, sizeof(int32_t));
+    c->crash = (int32_t *)calloc((size_t)(cfg->crash_count > 0 ? cfg->crash_count : 1), sizeof(int32_t));
+    if (cfg->crash_count > 0 && oc_crash_set(c->n, cfg->crash_count, cfg->crash_seed, c->crash)) {
+      oc_destroy(c);
+      return NULL;
+    }
+    c->t = 1; /* converged state is "as of tick 0" */
+  }
+  return c;
+}
+
+void oc_destroy(oc_ctx *c) {
+  if (!c) return;
+  for (int i = 0; i < c->n; i++) {
+    free(c->nodes[i].list.v);
+    free(c->nodes[i].q.v);
+    if (c->snaps) { free(c->snaps[i].ids); free(c->snaps[i].hbs); }
+    if (c->snaps_next) { free(c->snaps_next[i].ids); free(c->snaps_next[i].hbs); }
+  }
+  free(c->snaps); free(c->snaps_next);
+  free(c->tgt); free(c->tgt_next); free(c->ntgt); free(c->ntgt_next);
+  free(c->crash); free(c->ev);
+  free(c->nodes);
+  free(c->buff.v);
+  free(c->sent);
+  free(c->recv);
+  free(c->dbg.p); free(c->out.p); free(c->tmp.p);
+  free(c);
+}
+
+int oc_tick(oc_ctx *c) {
+  if (!is_scaled(c) && c->t >= MAX_TIME) return -1; /* EmulNet.cpp:109 assert */
+  mp1_run(c);
+  app_fail(c);
+  c->t++;
+  return 0;
+}
+
+int oc_time(const oc_ctx *c) { return c->t; }
+
+const char *oc_dbg_log(oc_ctx *c, size_t *len) {
+  *len = c->dbg.n;
+  return c->dbg.p ? c->dbg.p : "";
+}
+
+const char *oc_stdout(oc_ctx *c, size_t *len) {
+  *len = c->out.n;
+  return c->out.p ? c->out.p : "";
+}
+
+/* EmulNet::ENcleanup (EmulNet.cpp:184-220), incl. the node-67 special case */
+const char *oc_msgcount(oc_ctx *c, size_t *len) {
+  c->tmp.n = 0;
+  if (is_scaled(c)) { *len = 0; return ""; }
+  for (int i = 1; i <= c->n; i++) {
+    sb_printf(&c->tmp, "node %3d ", i);
+    unsigned st = 0, rt = 0;
+    for (int j = 0; j < c->t; j++) {
+      int s = c->sent[(size_t)i * MAX_TIME + j], r = c->recv[(size_t)i * MAX_TIME + j];
+      st += (unsigned)s;
+      rt += (unsigned)r;
+      if (i != 67) {
+        sb_printf(&c->tmp, " (%4d, %4d)", s, r);
+        if (j % 10 == 9) sb_printf(&c->tmp, "\n         ");
+      } else {
+        sb_printf(&c->tmp, "special %4d %4d %4d\n", j, s, r);
+      }
+    }
+    sb_printf(&c->tmp, "\n");
+    sb_printf(&c->tmp, "node %3d sent_total %6u  recv_total %6u\n\n", i, st, rt);
+  }
+  *len = c->tmp.n;
+  return c->tmp.p;
+}
+
+/* state of the tick just finished, in oracle/shim/dump_main.cpp's line format */
+const char *oc_dump(oc_ctx *c, size_t *len) {
+  c->tmp.n = 0;
+  int t = c->t - 1;
+  for (int i = 0; i < c->n; i++) {
+    node *nd = &c->nodes[i];
+    sb_printf(&c->tmp, "%d %d %d %d %d %ld %d", t, i, nd->inited, nd->in_group, nd->failed, (long)nd->heartbeat,
+              nd->list.n);
+    for (int k = 0; k < nd->list.n; k++)
+      sb_printf(&c->tmp, " %d:%ld:%ld", nd->list.v[k].id, (long)nd->list.v[k].hb, (long)nd->list.v[k].ts);
+    sb_put(&c->tmp, "\n", 1);
+  }
+  *len = c->tmp.n;
+  return c->tmp.p ? c->tmp.p : "";
+}
+
+size_t oc_events(oc_ctx *c, const oc_event **ev) {
+  *ev = c->ev;
+  return c->nev;
+}
+
+int oc_row(oc_ctx *c, int r, int32_t *hb, int32_t *ts) {
+  if (r < 0 || r >= c->n) return -1;
+  for (int j = 0; j < c->n; j++) hb[j] = ts[j] = -1;
+  node *nd = &c->nodes[r];
+  for (int k = 0; k < nd->list.n; k++) {
+    int j = nd->list.v[k].id - 1;
+    if (j < 0 || j >= c->n) continue;
+    hb[j] = (int32_t)nd->list.v[k].hb;
+    ts[j] = (int32_t)nd->list.v[k].ts;
+  }
+  return 0;
+}
+
+int oc_node(oc_ctx *c, int r, int32_t *st) {
+  if (r < 0 || r >= c->n) return -1;
+  node *nd = &c->nodes[r];
+  st[0] = nd->inited;
+  st[1] = nd->in_group;
+  st[2] = nd->failed;
+  st[3] = (int32_t)nd->heartbeat;
+  return 0;
+}
