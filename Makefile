@@ -1,0 +1,37 @@
+# Top-level build. `make` produces the in-tree HIP library and the
+# reference-shaped ./Application (so the reference's grader flow
+# `make && ./Application testcases/X.conf` runs against this build).
+#   distributed-membership_amd/lib/libgm.so   hand-written HIP (gfx950) + C ABI
+#   ./Application                             host C++ driver (Application/Params/Log surface)
+#   oracle/build/*                            CPU restatement (test infrastructure)
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+PKG := distributed-membership_amd
+CSRC := $(PKG)/csrc
+HIPFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Iinclude -I$(CSRC) -Wall -Wno-unused-result
+LIB := $(PKG)/lib/libgm.so
+KOBJS := $(PKG)/build/gm_faithful.o $(PKG)/build/gm_scaled.o $(PKG)/build/gm_host.o
+HDRS := include/gm_abi.h $(CSRC)/gm_device.h $(CSRC)/gm_faithful.h $(CSRC)/gm_scaled.h
+
+all: $(LIB) Application oracle
+
+$(PKG)/build/%.o: $(CSRC)/%.hip $(HDRS)
+	@mkdir -p $(PKG)/build
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(LIB): $(KOBJS)
+	@mkdir -p $(PKG)/lib
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(KOBJS)
+
+Application: $(PKG)/app/Application.cpp $(PKG)/app/Log.cpp $(PKG)/app/Application.h $(PKG)/app/Log.h $(LIB)
+	g++ -O2 -std=c++17 -Wall -Iinclude -I$(PKG)/app -o $@ $(PKG)/app/Application.cpp $(PKG)/app/Log.cpp \
+	    -L$(PKG)/lib -lgm -Wl,-rpath,'$$ORIGIN/$(PKG)/lib'
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -rf $(PKG)/build $(PKG)/lib Application dbg.log stats.log msgcount.log
+	$(MAKE) -C oracle clean
+
+.PHONY: all oracle clean

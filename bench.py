@@ -1,0 +1,151 @@
+#!/usr/bin/env python3
+"""Headline benchmark: simulated node-ticks/s (+ achieved HBM GB/s) of the
+SCALED full-membership tick at N = 65,536 (BASELINE.json metric, SURVEY.md
+§8(d) scenario S-A).
+
+A "step" is one globaltime tick of the whole cluster (Application::mp1Run for
+all N nodes: merge delivered gossip lists, heartbeat bump, TFAIL/TREMOVE sweep,
+gossip-target draw, delivery to next tick's inboxes), state resident in HBM.
+
+Scenario S-A: converged start (every observer holds every subject), fanout 5,
+TFAIL 5, TREMOVE 20, RD_SEED 7, 1% of the nodes (655) crash at the end of tick
+10 (splitmix64-keyed crash set, seed 42), no drops. A fixed 25-tick prologue
+(T_warm of S-A) brings the cluster to steady state with the crash's removals
+still ahead; then W warmup ticks, then exactly K timed ticks.
+
+Multi-GPU (--gpus N via torch.distributed.run): the N x N table is sharded by
+subject column across ranks (weak scaling: the cluster grows with the rank
+count so each GPU keeps ~N^2 cells); see DESIGN.md §Multi-GPU.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "distributed-membership_amd"))
+
+PEAK_HBM_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--n", type=int, default=65536)
+    p.add_argument("--prologue", type=int, default=25)
+    p.add_argument("--crash-tick", type=int, default=10)
+    p.add_argument("--crash-frac", type=float, default=0.01)
+    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--no-cpu", action="store_true")
+    return p.parse_args()
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl")
+        dist = tdist
+
+    from membership import GM_MODE_SCALED, Simulator, crash_set
+
+    n = a.n
+    if world > 1:
+        raise SystemExit("multi-GPU sharded bench: see bench_shard (not built yet)")
+    ncrash = int(round(n * a.crash_frac))
+    sim = Simulator(n, GM_MODE_SCALED, rd_seed=7, device=local)
+    crash = crash_set(n, ncrash, 42)
+    while sim.time <= a.prologue:
+        t = sim.time
+        sim.tick()
+        if t == a.crash_tick:
+            sim.set_failed(crash)
+    for _ in range(a.warmup):
+        sim.tick()
+    sim.sync()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    barrier()
+    sim.sync()
+    sim.set_timing(1)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        sim.tick()
+    sim.sync()
+    t1 = time.perf_counter()
+    barrier()
+    elapsed = t1 - t0
+    if dist is not None:
+        import torch
+        x = torch.tensor([elapsed], device="cuda")
+        dist.all_reduce(x, op=dist.ReduceOp.MAX)
+        elapsed = float(x.item())
+    kernel_ms = sim.last_kernel_ms()
+    st = sim.tick_stats()
+    assert st["err"] == 0, st
+
+    n_live, m_lists = st["live"], st["lists"]
+    W = n
+    # algorithmic HBM bytes of one tick in this layout:
+    # per live row 4W read + 4W write (packed table) + 2W write (payload plane),
+    # plus 2W per delivered gossip list (payload read)
+    b_alg = (10 * n_live + 2 * m_lists) * W
+    # the survey's int32 (hb, ts) formulation of the same work
+    b_survey = 16 * n_live * n + 8 * m_lists * n
+    achieved = b_alg / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else None
+    traffic = None
+    tpath = os.path.join(REPO, "profiles", f"traffic_n{n}.json")
+    if os.path.exists(tpath):
+        with open(tpath) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
+
+    value = n * a.steps / elapsed
+    out = {
+        "metric": "simulated node-ticks/sec + achieved HBM GB/s at N=65,536 full-membership",
+        "value": value,
+        "unit": "node-ticks/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": elapsed / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u16",
+        "data": "synthetic (converged full-membership table, seeded crash set)",
+        "config": {"workload": "S-A: SCALED full membership, 1% crash at tick 10, fanout 5, TFAIL 5, TREMOVE 20",
+                   "n": n, "prologue_ticks": a.prologue, "crashed": ncrash, "live": n_live,
+                   "lists_per_tick": m_lists, "parallelism": f"column-shard x{world}" if world > 1 else "single GPU"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+                     "frac": (achieved / PEAK_HBM_GBPS) if achieved else None, "traffic": traffic,
+                     "kernel": "gm_s_tick", "kernel_ms": kernel_ms, "alg_bytes_per_launch": b_alg,
+                     "survey_int32_bytes_per_launch": b_survey},
+    }
+    if rank == 0 and world == 1 and not a.no_cpu:
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        import oracle_py  # the oracle is the CPU baseline here, never the measured path
+        nodes, secs = oracle_py.bench_sample(n, lists=5, min_seconds=a.cpu_seconds)
+        out["cpu_baseline"] = {"value": nodes / secs, "unit": "node-ticks/s", "cores": 1, "kind": "port",
+                               "sample": f"{nodes} node-ticks of the N={n} SCALED workload on one host core "
+                                         f"({secs:.1f} s): per node-tick 5 gossip lists x {n} entries merged via "
+                                         "updatelistCallBack + nodeLoopOps sweep/sort/draw (oracle/ref_cpu.c)"}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

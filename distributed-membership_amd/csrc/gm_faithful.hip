@@ -7,9 +7,9 @@
 //               order; for each it matches the buffer in parallel, emits the
 //               matches in descending buffer index (the order the reference's
 //               backward scan dequeues them) and applies the swap-with-last
-//               compaction in closed form: holes below the new size, taken
-//               from the top, are filled by the surviving tail elements, taken
-//               from the top.
+//               compaction in closed form: the i-th hole from the top is
+//               filled from position B-i, following the chain through holes
+//               that were themselves refilled earlier in the scan.
 //   gm_f_node   node phase: nodeStart / nodeLoop for every node in parallel
 //               (one workgroup per node; MP1Node.cpp:73-163,182-495). The
 //               queue merge is commutative on the table (max heartbeat); the
@@ -22,6 +22,7 @@
 //               consumes the next glibc rand() draw of the S1 stream; the
 //               30000 cap is a prefix count over the not-drop-drawn sends.
 #include "gm_device.h"
+#include "gm_abi.h"
 #include "gm_faithful.h"
 
 #define F_RECV_THREADS 1024
@@ -58,32 +59,39 @@ __global__ __launch_bounds__(F_RECV_THREADS) void gm_f_recv(FState s, int t) {
     int before = gm_block_scan(c, s_tmp, &k);  // matches at index < lo
     if (k == 0) continue;
     const int Bn = B - k;
-    // matches below the new size (holes) = k - matches at index >= Bn
-    int cin = 0;
-    for (int j = lo; j < hi; j++) cin += (j >= Bn) && f_strkey(buf[j].to) == me;
-    int ktop;
-    (void)gm_block_scan(cin, s_tmp, &ktop);
-    const int mlow = k - ktop;
-    // deliver in descending buffer index; record hole slots
+    // deliver in descending buffer index; tag the matches that sit in the
+    // vacated tail [Bn, B) with their 1-based descending rank
     int r = before;
     for (int j = lo; j < hi; j++) {
       if (f_strkey(buf[j].to) == me) {
         s.q[qbase + (k - 1 - r)] = buf[j];
-        if (j < Bn) s.holepos[mlow - 1 - r] = j;  // hr(j) = mlow-1-rank_asc(j)
+        r++;
+      }
+    }
+    for (int j = max(lo, Bn); j < hi; j++) s.holepos[j - Bn] = 0;
+    __syncthreads();
+    r = before;
+    for (int j = lo; j < hi; j++) {
+      if (f_strkey(buf[j].to) == me) {
+        if (j >= Bn) s.holepos[j - Bn] = k - r;
         r++;
       }
     }
     __syncthreads();
-    // move surviving tail elements into the holes, both taken from the top
-    // (sources sit at >= Bn, holes below Bn: no overlap)
+    // swap-with-last, closed form: the i-th hole (descending) receives what sits
+    // at position B-i when it is processed; if B-i is itself an earlier hole h_m,
+    // that is what h_m received from B-m -- follow the chain to an original element
     r = before;
     for (int j = lo; j < hi; j++) {
-      bool m = f_strkey(buf[j].to) == me;
-      if (!m && j >= Bn) {
-        int sr = (B - 1 - j) - (k - r);  // non-matched elements above j
-        buf[s.holepos[sr]] = buf[j];
+      if (f_strkey(buf[j].to) == me) {
+        if (j < Bn) {
+          int x = B - (k - r);
+          int guard = 0;
+          while (s.holepos[x - Bn] > 0 && ++guard <= k) x = B - s.holepos[x - Bn];
+          buf[j] = buf[x];  // x >= Bn: never overwritten in this pass
+        }
+        r++;
       }
-      r += m;
     }
     __syncthreads();
     if (threadIdx.x == 0) {

@@ -1,0 +1,605 @@
+// gm_host.cpp -- libgm: the C ABI of include/gm_abi.h on top of the HIP kernels.
+//
+// Owns the per-context device state, launches one tick per gm_tick on the
+// context stream, and turns device event records into reference log order.
+// Compiled by hipcc for gfx950 together with gm_faithful.hip / gm_scaled.hip.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "gm_abi.h"
+#include "gm_device.h"
+#include "gm_faithful.h"
+#include "gm_scaled.h"
+
+__global__ void gm_f_recv(FState s, int t);
+__global__ void gm_f_node(FState s, int t);
+__global__ void gm_f_send(FState s, int t);
+__global__ void gm_s_tick(SState s, int t, int drop_pct);
+
+#define GM_T_LIMIT 32766  // packed 16-bit hb/ts stay exact: hb <= 2t+1 < 0xFFFF
+
+struct gm_ctx {
+  gm_config cfg;
+  hipStream_t stream = nullptr;
+  int t = 0;
+  int n = 0;
+  int dropmsg = 0;
+  int latched = GM_OK;
+  bool timing = false;
+  int timed_ticks = 0;  // ticks in the current timing window
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  std::vector<void *> allocs;
+  std::vector<int32_t> failed_h;
+  // FAITHFUL
+  FState f{};
+  size_t f_smem = 0;
+  std::vector<gm_event> pending;
+  // SCALED
+  SState s{};
+  size_t s_smem = 0;
+  uint64_t ev_counts[6] = {0, 0, 0, 0, 0, 0};
+};
+
+static thread_local char g_errbuf[256];
+
+#define HIPCHECK(x)                                                                   \
+  do {                                                                                \
+    hipError_t e_ = (x);                                                              \
+    if (e_ != hipSuccess) {                                                           \
+      snprintf(g_errbuf, sizeof g_errbuf, "%s:%d %s", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      return GM_EDEVICE;                                                              \
+    }                                                                                 \
+  } while (0)
+
+template <class T>
+static int dalloc(gm_ctx *c, T **p, size_t count) {
+  void *q = nullptr;
+  size_t bytes = sizeof(T) * (count ? count : 1);
+  if (hipMalloc(&q, bytes) != hipSuccess) {
+    snprintf(g_errbuf, sizeof g_errbuf, "hipMalloc(%zu) failed", bytes);
+    return GM_ENOMEM;
+  }
+  c->allocs.push_back(q);
+  *p = (T *)q;
+  return GM_OK;
+}
+
+#define TRY(x)              \
+  do {                      \
+    int r_ = (x);           \
+    if (r_ != GM_OK) return r_; \
+  } while (0)
+
+extern "C" const char *gm_strerror(int code) {
+  switch (code) {
+    case GM_OK: return "ok";
+    case GM_EINVAL: return "invalid argument";
+    case GM_ENOMEM: return g_errbuf[0] ? g_errbuf : "out of memory";
+    case GM_EDEVICE: return g_errbuf[0] ? g_errbuf : "HIP runtime error";
+    case GM_ERANGE: return "bounded resource overflowed";
+    case GM_ESTATE: return "protocol invariant violated";
+    case GM_EUNSUPPORTED: return "unsupported configuration";
+    case GM_ECOMM: return "collective failure";
+    default: return "unknown error";
+  }
+}
+
+// Params::setparams (Params.cpp:19-40): same fscanf key sequence
+extern "C" int gm_parse_conf(const char *path, gm_config *cfg) {
+  if (!path || !cfg) return GM_EINVAL;
+  FILE *fp = fopen(path, "r");
+  if (!fp) return GM_EINVAL;
+  int n = 0, single = 0, drop = 0;
+  double prob = 0;
+  if (fscanf(fp, "MAX_NNB: %d", &n) != 1) n = 0;
+  if (fscanf(fp, "\nSINGLE_FAILURE: %d", &single) != 1) single = 0;
+  if (fscanf(fp, "\nDROP_MSG: %d", &drop) != 1) drop = 0;
+  if (fscanf(fp, "\nMSG_DROP_PROB: %lf", &prob) != 1) prob = 0;
+  fclose(fp);
+  cfg->n = n;
+  cfg->single_failure = single;
+  cfg->drop_msg = drop;
+  cfg->drop_prob = prob;
+  return n > 0 ? GM_OK : GM_EINVAL;
+}
+
+// glibc srandom_r (TYPE_3) seeding of the S1 stream; the draws themselves are
+// stepped on the device (gm_f_send) and by gm_rand.
+static void s1_seed(uint32_t seed, int32_t st[33]) {
+  if (seed == 0) seed = 1;
+  int32_t word = (int32_t)seed;
+  st[0] = word;
+  for (int i = 1; i < 31; i++) {
+    long hi = word / 127773, lo = word % 127773;
+    word = (int32_t)(16807 * lo - 2836 * hi);
+    if (word < 0) word += 2147483647;
+    st[i] = word;
+  }
+  int f = 3, r = 0;
+  for (int k = 0; k < 310; k++) {
+    st[f] = (int32_t)((uint32_t)st[f] + (uint32_t)st[r]);
+    f = (f + 1) % 31;
+    r = (r + 1) % 31;
+  }
+  st[31] = f;
+  st[32] = r;
+}
+
+static int create_faithful(gm_ctx *c) {
+  const int n = c->n;
+  if (n > F_MAX_NODES) return GM_EUNSUPPORTED;  // EmulNet.cpp:108 assert(src <= MAX_NODES)
+  FState &f = c->f;
+  f.n = n;
+  f.np = (n + 63) / 64 * 64;
+  f.tmax = F_MAX_TIME;
+  f.gstride = n + GM_FANOUT;
+  f.draw_cap = 5 * n * n + 2 * n + 1024;
+  f.rd_seed = c->cfg.rd_seed;
+  f.ev_cap = std::max(4096, 4 * n * n + 64 * n);
+  TRY(dalloc(c, &f.table, (size_t)n * f.np));
+  TRY(dalloc(c, &f.start, n));
+  TRY(dalloc(c, &f.failed, n));
+  TRY(dalloc(c, &f.inited, n));
+  TRY(dalloc(c, &f.ingroup, n));
+  TRY(dalloc(c, &f.hbctr, n));
+  TRY(dalloc(c, &f.started_now, n));
+  TRY(dalloc(c, &f.buf, F_ENBUFFSIZE));
+  TRY(dalloc(c, &f.bufsize, 1));
+  TRY(dalloc(c, &f.holepos, F_ENBUFFSIZE));
+  TRY(dalloc(c, &f.q, F_ENBUFFSIZE));
+  TRY(dalloc(c, &f.q_off, n));
+  TRY(dalloc(c, &f.q_cnt, n));
+  TRY(dalloc(c, &f.scount, n));
+  TRY(dalloc(c, &f.jcnt, n));
+  TRY(dalloc(c, &f.gcnt, n));
+  TRY(dalloc(c, &f.fcnt, n));
+  TRY(dalloc(c, &f.jrq, (size_t)n * n));
+  TRY(dalloc(c, &f.gossip, (size_t)n * f.gstride));
+  TRY(dalloc(c, &f.fcols, (size_t)n * n));
+  TRY(dalloc(c, &f.s1, 33));
+  TRY(dalloc(c, &f.draws, f.draw_cap));
+  TRY(dalloc(c, &f.sent, (size_t)(F_MAX_NODES + 1) * f.tmax));
+  TRY(dalloc(c, &f.recv, (size_t)(F_MAX_NODES + 1) * f.tmax));
+  TRY(dalloc(c, &f.ev, f.ev_cap));
+  TRY(dalloc(c, &f.ev_count, 1));
+  TRY(dalloc(c, &f.err, 1));
+  HIPCHECK(hipMemset(f.table, 0xFF, sizeof(uint32_t) * (size_t)n * f.np));
+  std::vector<int32_t> start(n);
+  for (int i = 0; i < n; i++) start[i] = (int)(0.25 * i);  // (int)(STEP_RATE*i), Application.cpp:143
+  HIPCHECK(hipMemcpy(f.start, start.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice));
+  for (int32_t *p : {f.failed, f.inited, f.ingroup, f.hbctr, f.started_now, f.q_off, f.q_cnt,
+                     f.scount, f.jcnt, f.gcnt, f.fcnt})
+    HIPCHECK(hipMemset(p, 0, sizeof(int32_t) * (size_t)n));
+  HIPCHECK(hipMemset(f.sent, 0, sizeof(int32_t) * (size_t)(F_MAX_NODES + 1) * f.tmax));
+  HIPCHECK(hipMemset(f.recv, 0, sizeof(int32_t) * (size_t)(F_MAX_NODES + 1) * f.tmax));
+  HIPCHECK(hipMemset(f.bufsize, 0, sizeof(int32_t)));
+  HIPCHECK(hipMemset(f.ev_count, 0, sizeof(unsigned long long)));
+  HIPCHECK(hipMemset(f.err, 0, sizeof(uint32_t)));
+  int32_t st[33];
+  s1_seed(c->cfg.time_seed, st);  // srand(time(NULL)) at Application.cpp:50 and :96
+  HIPCHECK(hipMemcpy(f.s1, st, sizeof st, hipMemcpyHostToDevice));
+  const int nw = f.np / 64;
+  c->f_smem = (size_t)f.np * 8 + (size_t)nw * 8 * 3 + (size_t)nw * 4 + 624 * 4 + 48 * 4;
+  return GM_OK;
+}
+
+static int create_scaled(gm_ctx *c) {
+  const int n = c->n;
+  const int G = c->cfg.shard_count > 0 ? c->cfg.shard_count : 1;
+  const int rank = c->cfg.shard_rank;
+  if (G != 1 || rank != 0) return GM_EUNSUPPORTED;  // column sharding: see gm_shard (multi-GPU)
+  SState &s = c->s;
+  s.n = n;
+  s.c0 = 0;
+  s.w = n;
+  s.wp = (n + S_ROW_ALIGN - 1) / S_ROW_ALIGN * S_ROW_ALIGN;
+  s.evcap = std::min(s.wp, 1024);
+  s.ev_spill_cap = 1u << 24;
+  s.rd_seed = c->cfg.rd_seed;
+  s.drop_seed = c->cfg.drop_seed;
+  const size_t cells = (size_t)n * s.wp;
+  TRY(dalloc(c, &s.table, cells));
+  TRY(dalloc(c, &s.msg[0], cells));
+  TRY(dalloc(c, &s.msg[1], cells));
+  for (int p = 0; p < 2; p++) {
+    TRY(dalloc(c, &s.inbox_cnt[p], n));
+    TRY(dalloc(c, &s.inbox[p], (size_t)n * S_KMAX));
+  }
+  TRY(dalloc(c, &s.hbctr, n));
+  TRY(dalloc(c, &s.failed, n));
+  TRY(dalloc(c, &s.ev_rows, (size_t)n * s.evcap));
+  TRY(dalloc(c, &s.ev_cnt, n));
+  TRY(dalloc(c, &s.ev_spill, s.ev_spill_cap));
+  TRY(dalloc(c, &s.ev_spill_cnt, 1));
+  TRY(dalloc(c, &s.rowstat, (size_t)n * 4));
+  TRY(dalloc(c, &s.targets, (size_t)n * GM_FANOUT));
+  TRY(dalloc(c, &s.err, 1));
+  // converged start: every observer holds every subject at {hb 0, ts 0}; padding absent
+  HIPCHECK(hipMemset(s.table, 0, sizeof(uint32_t) * cells));
+  if (s.wp > s.w)
+    HIPCHECK(hipMemset2D(s.table + s.w, sizeof(uint32_t) * s.wp, 0xFF, sizeof(uint32_t) * (s.wp - s.w), n));
+  HIPCHECK(hipMemset(s.msg[0], 0xFF, sizeof(uint16_t) * cells));
+  HIPCHECK(hipMemset(s.msg[1], 0xFF, sizeof(uint16_t) * cells));
+  for (int p = 0; p < 2; p++) HIPCHECK(hipMemset(s.inbox_cnt[p], 0, sizeof(int32_t) * n));
+  HIPCHECK(hipMemset(s.hbctr, 0, sizeof(int32_t) * n));
+  HIPCHECK(hipMemset(s.failed, 0, sizeof(int32_t) * n));
+  HIPCHECK(hipMemset(s.ev_cnt, 0, sizeof(int32_t) * n));
+  HIPCHECK(hipMemset(s.ev_spill_cnt, 0, sizeof(uint32_t)));
+  HIPCHECK(hipMemset(s.rowstat, 0, sizeof(int32_t) * n * 4));
+  HIPCHECK(hipMemset(s.err, 0, sizeof(uint32_t)));
+  const int nw = s.wp / 64;
+  c->s_smem = (size_t)nw * 8 * 2 + (size_t)nw * 4 + 624 * 4 + (S_KMAX + 16 + 8) * 4;
+  c->t = 1;  // the converged table is the state "as of tick 0"
+  return GM_OK;
+}
+
+extern "C" int gm_create(const gm_config *cfg, gm_ctx **out) {
+  if (!cfg || !out) return GM_EINVAL;
+  *out = nullptr;
+  if (cfg->abi_version != GM_ABI_VERSION) return GM_EINVAL;
+  if (cfg->n <= 0 || (cfg->mode != GM_MODE_FAITHFUL && cfg->mode != GM_MODE_SCALED)) return GM_EINVAL;
+  g_errbuf[0] = 0;
+  gm_ctx *c = new gm_ctx();
+  c->cfg = *cfg;
+  c->n = cfg->n;
+  c->failed_h.assign(cfg->n, 0);
+  int rc = GM_OK;
+  if (hipSetDevice(cfg->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&c->e0) != hipSuccess || hipEventCreate(&c->e1) != hipSuccess) {
+    snprintf(g_errbuf, sizeof g_errbuf, "HIP device %d unavailable", cfg->device);
+    rc = GM_EDEVICE;
+  }
+  if (rc == GM_OK) rc = cfg->mode == GM_MODE_FAITHFUL ? create_faithful(c) : create_scaled(c);
+  if (rc != GM_OK) {
+    gm_destroy(c);
+    return rc;
+  }
+  *out = c;
+  return GM_OK;
+}
+
+extern "C" int gm_destroy(gm_ctx *c) {
+  if (!c) return GM_EINVAL;
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (void *p : c->allocs) (void)hipFree(p);
+  if (c->e0) (void)hipEventDestroy(c->e0);
+  if (c->e1) (void)hipEventDestroy(c->e1);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  return GM_OK;
+}
+
+static int check_err(gm_ctx *c) {
+  uint32_t *errp = c->cfg.mode == GM_MODE_FAITHFUL ? c->f.err : c->s.err;
+  uint32_t e = 0;
+  HIPCHECK(hipMemcpyAsync(&e, errp, sizeof e, hipMemcpyDeviceToHost, c->stream));
+  HIPCHECK(hipStreamSynchronize(c->stream));
+  if (e) {
+    snprintf(g_errbuf, sizeof g_errbuf, "device error flags 0x%x", e);
+    c->latched = (e & (GM_ERR_SELF | GM_ERR_BUFFER)) ? GM_ESTATE : GM_ERANGE;
+  }
+  return c->latched;
+}
+
+static bool ev_order(const FEvent &a, const FEvent &b) {
+  if (a.t != b.t) return a.t < b.t;
+  if (a.logger != b.logger) return a.logger > b.logger;  // node phase: i descending
+  return a.seq < b.seq;
+}
+
+static int tick_faithful(gm_ctx *c) {
+  if (c->t >= F_MAX_TIME) return GM_ERANGE;  // EmulNet.cpp:109 assert(time < MAX_TIME)
+  FState st = c->f;
+  st.drop_pct_now = c->dropmsg ? (int)(c->cfg.drop_prob * 100) : -1;  // EmulNet.cpp:92
+  hipLaunchKernelGGL(gm_f_recv, dim3(1), dim3(1024), 0, c->stream, st, c->t);
+  hipLaunchKernelGGL(gm_f_node, dim3(c->n), dim3(256), c->f_smem, c->stream, st, c->t);
+  hipLaunchKernelGGL(gm_f_send, dim3(1), dim3(1024), 0, c->stream, st, c->t);
+  HIPCHECK(hipGetLastError());
+  unsigned long long nev = 0;
+  HIPCHECK(hipMemcpyAsync(&nev, c->f.ev_count, sizeof nev, hipMemcpyDeviceToHost, c->stream));
+  HIPCHECK(hipStreamSynchronize(c->stream));
+  if (nev > (unsigned long long)c->f.ev_cap) {
+    c->latched = GM_ERANGE;
+    return c->latched;
+  }
+  if (nev) {
+    std::vector<FEvent> ev(nev);
+    HIPCHECK(hipMemcpyAsync(ev.data(), c->f.ev, sizeof(FEvent) * nev, hipMemcpyDeviceToHost, c->stream));
+    HIPCHECK(hipMemsetAsync(c->f.ev_count, 0, sizeof(unsigned long long), c->stream));
+    HIPCHECK(hipStreamSynchronize(c->stream));
+    std::sort(ev.begin(), ev.end(), ev_order);
+    for (const FEvent &e : ev) c->pending.push_back(gm_event{e.t, e.logger, e.kind, e.subject});
+  }
+  return check_err(c);
+}
+
+static int tick_scaled(gm_ctx *c) {
+  if (c->t > GM_T_LIMIT) return GM_ERANGE;
+  const int t_send = c->t - 1;
+  const bool drop = c->cfg.drop_pct > 0 && t_send >= c->cfg.drop_from && t_send < c->cfg.drop_to;
+  if (c->timing && c->timed_ticks == 0) HIPCHECK(hipEventRecord(c->e0, c->stream));
+  hipLaunchKernelGGL(gm_s_tick, dim3(c->n), dim3(S_THREADS), c->s_smem, c->stream, c->s, c->t,
+                     drop ? c->cfg.drop_pct : -1);
+  if (c->timing) {
+    HIPCHECK(hipEventRecord(c->e1, c->stream));
+    c->timed_ticks++;
+  }
+  HIPCHECK(hipGetLastError());
+  return GM_OK;
+}
+
+extern "C" int gm_tick(gm_ctx *c) {
+  if (!c) return GM_EINVAL;
+  if (c->latched != GM_OK) return c->latched;
+  int rc = c->cfg.mode == GM_MODE_FAITHFUL ? tick_faithful(c) : tick_scaled(c);
+  if (rc == GM_OK) c->t++;
+  return rc;
+}
+
+extern "C" int gm_sync(gm_ctx *c) {
+  if (!c) return GM_EINVAL;
+  HIPCHECK(hipStreamSynchronize(c->stream));
+  return check_err(c);
+}
+
+extern "C" int gm_time(gm_ctx *c, int32_t *t) {
+  if (!c || !t) return GM_EINVAL;
+  *t = c->t;
+  return GM_OK;
+}
+
+extern "C" int gm_rand(gm_ctx *c, int32_t *out) {
+  if (!c || !out) return GM_EINVAL;
+  if (c->cfg.mode != GM_MODE_FAITHFUL) return GM_EUNSUPPORTED;
+  int32_t st[33];
+  HIPCHECK(hipMemcpyAsync(st, c->f.s1, sizeof st, hipMemcpyDeviceToHost, c->stream));
+  HIPCHECK(hipStreamSynchronize(c->stream));
+  int f = st[31], r = st[32];
+  uint32_t v = (uint32_t)st[f] + (uint32_t)st[r];
+  st[f] = (int32_t)v;
+  st[31] = (f + 1) % 31;
+  st[32] = (r + 1) % 31;
+  HIPCHECK(hipMemcpy(c->f.s1, st, sizeof st, hipMemcpyHostToDevice));
+  *out = (int32_t)(v >> 1);
+  return GM_OK;
+}
+
+extern "C" int gm_set_failed(gm_ctx *c, const int32_t *idx, int32_t n) {
+  if (!c || (n > 0 && !idx)) return GM_EINVAL;
+  for (int k = 0; k < n; k++) {
+    if (idx[k] < 0 || idx[k] >= c->n) return GM_EINVAL;
+    c->failed_h[idx[k]] = 1;
+  }
+  int32_t *dst = c->cfg.mode == GM_MODE_FAITHFUL ? c->f.failed : c->s.failed;
+  HIPCHECK(hipStreamSynchronize(c->stream));
+  HIPCHECK(hipMemcpy(dst, c->failed_h.data(), sizeof(int32_t) * c->n, hipMemcpyHostToDevice));
+  return GM_OK;
+}
+
+extern "C" int gm_set_dropmsg(gm_ctx *c, int32_t on) {
+  if (!c) return GM_EINVAL;
+  c->dropmsg = on ? 1 : 0;
+  return GM_OK;
+}
+
+static int drain_scaled(gm_ctx *c, std::vector<gm_event> &out) {
+  const SState &s = c->s;
+  std::vector<int32_t> cnt(c->n);
+  uint32_t nsp = 0;
+  HIPCHECK(hipMemcpyAsync(cnt.data(), s.ev_cnt, sizeof(int32_t) * c->n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHECK(hipMemcpyAsync(&nsp, s.ev_spill_cnt, sizeof nsp, hipMemcpyDeviceToHost, c->stream));
+  HIPCHECK(hipStreamSynchronize(c->stream));
+  const int t = c->t - 1;
+  std::vector<uint32_t> row(s.evcap);
+  for (int r = 0; r < c->n; r++) {
+    int k = std::min(cnt[r], s.evcap);
+    if (k <= 0) continue;
+    HIPCHECK(hipMemcpy(row.data(), s.ev_rows + (size_t)r * s.evcap, sizeof(uint32_t) * k, hipMemcpyDeviceToHost));
+    for (int q = 0; q < k; q++)
+      out.push_back(gm_event{t, r, (int)(row[q] >> 30) == (int)S_EV_ADD ? GM_EV_JOINED : GM_EV_REMOVED,
+                             (int32_t)(row[q] & 0x3FFFFFFFu)});
+  }
+  nsp = std::min(nsp, s.ev_spill_cap);
+  if (nsp) {
+    std::vector<uint64_t> sp(nsp);
+    HIPCHECK(hipMemcpy(sp.data(), s.ev_spill, sizeof(uint64_t) * nsp, hipMemcpyDeviceToHost));
+    for (uint64_t v : sp) {
+      uint32_t rec = (uint32_t)v;
+      out.push_back(gm_event{t, (int32_t)(v >> 32), (int)(rec >> 30) == (int)S_EV_ADD ? GM_EV_JOINED : GM_EV_REMOVED,
+                             (int32_t)(rec & 0x3FFFFFFFu)});
+    }
+    HIPCHECK(hipMemset(s.ev_spill_cnt, 0, sizeof(uint32_t)));
+  }
+  // canonical SCALED order: loggers descending; joins ascending id, then removals descending id
+  std::sort(out.begin(), out.end(), [](const gm_event &a, const gm_event &b) {
+    if (a.logger != b.logger) return a.logger > b.logger;
+    if (a.kind != b.kind) return a.kind < b.kind;
+    return a.kind == GM_EV_JOINED ? a.subject < b.subject : a.subject > b.subject;
+  });
+  return GM_OK;
+}
+
+extern "C" int gm_drain_events(gm_ctx *c, gm_event *out, size_t cap, size_t *n) {
+  if (!c || !n) return GM_EINVAL;
+  if (c->cfg.mode == GM_MODE_SCALED) {
+    c->pending.clear();
+    TRY(drain_scaled(c, c->pending));
+  }
+  *n = c->pending.size();
+  if (c->pending.size() > cap) return GM_ERANGE;
+  if (!c->pending.empty()) memcpy(out, c->pending.data(), sizeof(gm_event) * c->pending.size());
+  c->pending.clear();
+  return GM_OK;
+}
+
+extern "C" int gm_event_counts(gm_ctx *c, uint64_t counts[6]) {
+  if (!c || !counts) return GM_EINVAL;
+  for (int k = 0; k < 6; k++) counts[k] = 0;
+  if (c->cfg.mode == GM_MODE_SCALED) {
+    std::vector<int32_t> cnt(c->n);
+    uint32_t nsp = 0;
+    HIPCHECK(hipMemcpyAsync(cnt.data(), c->s.ev_cnt, sizeof(int32_t) * c->n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHECK(hipMemcpyAsync(&nsp, c->s.ev_spill_cnt, sizeof nsp, hipMemcpyDeviceToHost, c->stream));
+    HIPCHECK(hipStreamSynchronize(c->stream));
+    uint64_t tot = nsp;
+    for (int32_t v : cnt) tot += (uint64_t)std::min(v, c->s.evcap);
+    counts[0] = tot;  // join+remove records of the last tick (per-kind split needs a drain)
+  } else {
+    for (const gm_event &e : c->pending) counts[e.kind]++;
+  }
+  return GM_OK;
+}
+
+extern "C" int gm_msgcount(gm_ctx *c, int32_t t, int32_t *sent, int32_t *recv) {
+  if (!c || !sent || !recv || t < 0) return GM_EINVAL;
+  if (c->cfg.mode != GM_MODE_FAITHFUL) return GM_EUNSUPPORTED;
+  if (t > c->f.tmax) return GM_EINVAL;
+  HIPCHECK(hipStreamSynchronize(c->stream));
+  std::vector<int32_t> hs((size_t)(F_MAX_NODES + 1) * c->f.tmax), hr(hs.size());
+  HIPCHECK(hipMemcpy(hs.data(), c->f.sent, sizeof(int32_t) * hs.size(), hipMemcpyDeviceToHost));
+  HIPCHECK(hipMemcpy(hr.data(), c->f.recv, sizeof(int32_t) * hr.size(), hipMemcpyDeviceToHost));
+  for (int i = 0; i < c->n; i++)
+    for (int j = 0; j < t; j++) {
+      sent[(size_t)i * t + j] = hs[(size_t)(i + 1) * c->f.tmax + j];
+      recv[(size_t)i * t + j] = hr[(size_t)(i + 1) * c->f.tmax + j];
+    }
+  return GM_OK;
+}
+
+static int read_table_row(gm_ctx *c, int r, std::vector<uint32_t> &row, int &w) {
+  const bool fm = c->cfg.mode == GM_MODE_FAITHFUL;
+  const int stride = fm ? c->f.np : c->s.wp;
+  w = fm ? c->n : c->s.w;
+  row.resize(w);
+  const uint32_t *base = (fm ? c->f.table : c->s.table) + (size_t)r * stride;
+  HIPCHECK(hipMemcpy(row.data(), base, sizeof(uint32_t) * w, hipMemcpyDeviceToHost));
+  return GM_OK;
+}
+
+extern "C" int gm_read_row(gm_ctx *c, int32_t r, int32_t c0, int32_t len, int32_t *hb, int32_t *ts) {
+  if (!c || !hb || !ts || r < 0 || r >= c->n || c0 < 0 || len < 0) return GM_EINVAL;
+  HIPCHECK(hipStreamSynchronize(c->stream));
+  std::vector<uint32_t> row;
+  int w;
+  TRY(read_table_row(c, r, row, w));
+  if (c0 + len > w) return GM_EINVAL;
+  for (int j = 0; j < len; j++) {
+    uint32_t e = row[c0 + j];
+    hb[j] = e == GM_ABSENT ? -1 : (int32_t)(e & 0xFFFF);
+    ts[j] = e == GM_ABSENT ? -1 : (int32_t)(e >> 16);
+  }
+  return GM_OK;
+}
+
+extern "C" int gm_read_nodes(gm_ctx *c, int32_t *st4) {
+  if (!c || !st4) return GM_EINVAL;
+  HIPCHECK(hipStreamSynchronize(c->stream));
+  const int n = c->n;
+  std::vector<int32_t> a(n), b(n), f(n), h(n);
+  if (c->cfg.mode == GM_MODE_FAITHFUL) {
+    HIPCHECK(hipMemcpy(a.data(), c->f.inited, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(b.data(), c->f.ingroup, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(f.data(), c->f.failed, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(h.data(), c->f.hbctr, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+  } else {
+    std::fill(a.begin(), a.end(), 1);
+    std::fill(b.begin(), b.end(), 1);
+    HIPCHECK(hipMemcpy(f.data(), c->s.failed, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(h.data(), c->s.hbctr, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+  }
+  for (int i = 0; i < n; i++) {
+    st4[4 * i] = a[i];
+    st4[4 * i + 1] = b[i];
+    st4[4 * i + 2] = f[i];
+    st4[4 * i + 3] = h[i];
+  }
+  return GM_OK;
+}
+
+extern "C" int gm_dump_tables(gm_ctx *c, char *buf, size_t cap, size_t *len) {
+  if (!c || !len) return GM_EINVAL;
+  std::vector<int32_t> st(4 * (size_t)c->n);
+  TRY(gm_read_nodes(c, st.data()));
+  std::string out;
+  char tmp[96];
+  const int t = c->t - 1;
+  std::vector<uint32_t> row;
+  for (int i = 0; i < c->n; i++) {
+    int w;
+    TRY(read_table_row(c, i, row, w));
+    int cnt = 0;
+    for (int j = 0; j < w; j++) cnt += row[j] != GM_ABSENT;
+    snprintf(tmp, sizeof tmp, "%d %d %d %d %d %d %d", t, i, st[4 * i], st[4 * i + 1], st[4 * i + 2], st[4 * i + 3], cnt);
+    out += tmp;
+    for (int j = 0; j < w; j++) {
+      if (row[j] == GM_ABSENT) continue;
+      snprintf(tmp, sizeof tmp, " %d:%u:%u", j + 1, row[j] & 0xFFFFu, row[j] >> 16);
+      out += tmp;
+    }
+    out += "\n";
+  }
+  *len = out.size();
+  if (!buf || cap < out.size()) return GM_ERANGE;
+  memcpy(buf, out.data(), out.size());
+  return GM_OK;
+}
+
+extern "C" int gm_tick_stats(gm_ctx *c, int64_t stats[4]) {
+  if (!c || !stats) return GM_EINVAL;
+  if (c->cfg.mode != GM_MODE_SCALED) return GM_EUNSUPPORTED;
+  std::vector<int32_t> rs((size_t)c->n * 4);
+  uint32_t e = 0;
+  HIPCHECK(hipMemcpyAsync(rs.data(), c->s.rowstat, sizeof(int32_t) * rs.size(), hipMemcpyDeviceToHost, c->stream));
+  HIPCHECK(hipMemcpyAsync(&e, c->s.err, sizeof e, hipMemcpyDeviceToHost, c->stream));
+  HIPCHECK(hipStreamSynchronize(c->stream));
+  int64_t m = 0, live = 0, mx = 0;
+  for (int r = 0; r < c->n; r++) {
+    m += rs[4 * r];
+    mx = std::max<int64_t>(mx, rs[4 * r]);
+    live += c->failed_h[r] ? 0 : 1;
+  }
+  stats[0] = m;
+  stats[1] = live;
+  stats[2] = mx;
+  stats[3] = e;
+  return GM_OK;
+}
+
+extern "C" int gm_set_timing(gm_ctx *c, int32_t on) {
+  if (!c) return GM_EINVAL;
+  c->timing = on != 0;
+  c->timed_ticks = 0;  // (re)opens the timing window at the next tick
+  return GM_OK;
+}
+
+extern "C" int gm_last_kernel_ms(gm_ctx *c, float *ms) {
+  if (!c || !ms) return GM_EINVAL;
+  *ms = 0.f;
+  if (!c->timing || c->cfg.mode != GM_MODE_SCALED || c->timed_ticks == 0) return GM_OK;
+  HIPCHECK(hipEventSynchronize(c->e1));
+  HIPCHECK(hipEventElapsedTime(ms, c->e0, c->e1));
+  *ms /= (float)c->timed_ticks;
+  return GM_OK;
+}
+
+static uint64_t mix64h(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+extern "C" int gm_crash_set(int32_t n, int32_t count, uint64_t seed, int32_t *out) {
+  if (n <= 0 || count < 0 || count > n || (count && !out)) return GM_EINVAL;
+  std::vector<std::pair<uint64_t, int32_t>> k(n);
+  for (int i = 0; i < n; i++) k[i] = {mix64h(seed + 0x9E3779B97F4A7C15ULL * (uint64_t)(i + 1)), i};
+  std::partial_sort(k.begin(), k.begin() + count, k.end());
+  for (int i = 0; i < count; i++) out[i] = k[i].second;
+  std::sort(out, out + count);
+  return GM_OK;
+}

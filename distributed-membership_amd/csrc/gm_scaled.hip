@@ -65,7 +65,7 @@ __global__ __launch_bounds__(S_THREADS) void gm_s_tick(SState s, int t, int drop
 
   uint32_t *trow = s.table + (size_t)r * wp;
   uint16_t *mout = s.msg[par] + (size_t)r * wp;
-  const uint16_t *min = s.msg[par ^ 1];
+  const uint16_t *mprev = s.msg[par ^ 1];
   const int selfc = r - s.c0;  // own column if this shard holds it
   const uint32_t tt = (uint32_t)t;
   const int t_send = t - 1;
@@ -80,7 +80,7 @@ __global__ __launch_bounds__(S_THREADS) void gm_s_tick(SState s, int t, int drop
         uint4 m[8];
 #pragma unroll
         for (int u = 0; u < 8; u++) {
-          if (j0 + u < k) m[u] = *(const uint4 *)(min + (size_t)s_send[j0 + u] * wp + base);
+          if (j0 + u < k) m[u] = *(const uint4 *)(mprev + (size_t)s_send[j0 + u] * wp + base);
           else m[u] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
         }
 #pragma unroll
@@ -96,7 +96,7 @@ __global__ __launch_bounds__(S_THREADS) void gm_s_tick(SState s, int t, int drop
       uint32_t kk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
       for (int j = 0; j < k; j++) {
         const int snd = s_send[j];
-        const uint4 m = *(const uint4 *)(min + (size_t)snd * wp + base);
+        const uint4 m = *(const uint4 *)(mprev + (size_t)snd * wp + base);
         const uint32_t mw[4] = {m.x, m.y, m.z, m.w};
         const uint64_t pair = gm_mix64(s.drop_seed ^ ((uint64_t)(uint32_t)t_send << 48) ^
                                        ((uint64_t)(uint32_t)snd << 24) ^ (uint64_t)(uint32_t)r);
@@ -110,10 +110,10 @@ __global__ __launch_bounds__(S_THREADS) void gm_s_tick(SState s, int t, int drop
           kk[q] = kk[q] > key ? kk[q] : key;
         }
       }
-      k0 = (u16x2)((uint16_t)kk[0], (uint16_t)kk[1]);
-      k1 = (u16x2)((uint16_t)kk[2], (uint16_t)kk[3]);
-      k2 = (u16x2)((uint16_t)kk[4], (uint16_t)kk[5]);
-      k3 = (u16x2)((uint16_t)kk[6], (uint16_t)kk[7]);
+      k0 = as_u16x2(kk[0] | (kk[1] << 16));
+      k1 = as_u16x2(kk[2] | (kk[3] << 16));
+      k2 = as_u16x2(kk[4] | (kk[5] << 16));
+      k3 = as_u16x2(kk[6] | (kk[7] << 16));
     }
     uint32_t e[8] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y, tb.z, tb.w};
     const uint32_t keys[4] = {as_u32(k0), as_u32(k1), as_u32(k2), as_u32(k3)};

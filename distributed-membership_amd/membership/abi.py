@@ -1,0 +1,212 @@
+"""ctypes binding of include/gm_abi.h (libgm.so)."""
+import ctypes
+import os
+
+import numpy as np
+
+GM_ABI_VERSION = 1
+GM_MODE_FAITHFUL, GM_MODE_SCALED = 0, 1
+GM_EV_JOINED, GM_EV_REMOVED, GM_EV_START_GROUP, GM_EV_TRY_JOIN, GM_EV_TIME_MARK = 1, 2, 3, 4, 5
+GM_OK, GM_ERANGE = 0, -4
+
+_PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def lib_path():
+    return os.environ.get("GM_LIBRARY", os.path.join(_PKG, "lib", "libgm.so"))
+
+
+class GmConfig(ctypes.Structure):
+    _fields_ = [("abi_version", ctypes.c_int32), ("mode", ctypes.c_int32), ("n", ctypes.c_int32),
+                ("single_failure", ctypes.c_int32), ("drop_msg", ctypes.c_int32), ("drop_prob", ctypes.c_double),
+                ("time_seed", ctypes.c_uint32), ("rd_seed", ctypes.c_uint64),
+                ("drop_pct", ctypes.c_int32), ("drop_from", ctypes.c_int32), ("drop_to", ctypes.c_int32),
+                ("drop_seed", ctypes.c_uint64),
+                ("device", ctypes.c_int32), ("shard_rank", ctypes.c_int32), ("shard_count", ctypes.c_int32),
+                ("reserved", ctypes.c_int32 * 8)]
+
+
+class GmEvent(ctypes.Structure):
+    _fields_ = [("t", ctypes.c_int32), ("logger", ctypes.c_int32), ("kind", ctypes.c_int32),
+                ("subject", ctypes.c_int32)]
+
+
+EXPORTS = ["gm_parse_conf", "gm_create", "gm_destroy", "gm_tick", "gm_sync", "gm_time", "gm_rand", "gm_set_failed",
+           "gm_set_dropmsg", "gm_drain_events", "gm_event_counts", "gm_msgcount", "gm_read_row", "gm_read_nodes",
+           "gm_dump_tables", "gm_tick_stats", "gm_set_timing", "gm_last_kernel_ms", "gm_crash_set", "gm_strerror"]
+
+_lib = None
+
+
+class GmError(RuntimeError):
+    def __init__(self, code, what):
+        self.code = code
+        super().__init__(f"{what}: {load_library().gm_strerror(code).decode()} ({code})")
+
+
+def load_library():
+    """Load libgm.so (built in-tree by `make` / __graft_entry__.build()); raises if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = lib_path()
+    if not os.path.exists(path):
+        raise FileNotFoundError(f"libgm.so not built: {path} (run `make` at the repo root)")
+    lib = ctypes.CDLL(path)
+    P = ctypes.POINTER
+    i32, u64, sz = ctypes.c_int32, ctypes.c_uint64, ctypes.c_size_t
+    sig = {
+        "gm_parse_conf": [ctypes.c_char_p, P(GmConfig)],
+        "gm_create": [P(GmConfig), P(ctypes.c_void_p)],
+        "gm_destroy": [ctypes.c_void_p], "gm_tick": [ctypes.c_void_p], "gm_sync": [ctypes.c_void_p],
+        "gm_time": [ctypes.c_void_p, P(i32)], "gm_rand": [ctypes.c_void_p, P(i32)],
+        "gm_set_failed": [ctypes.c_void_p, P(i32), i32], "gm_set_dropmsg": [ctypes.c_void_p, i32],
+        "gm_drain_events": [ctypes.c_void_p, P(GmEvent), sz, P(sz)],
+        "gm_event_counts": [ctypes.c_void_p, P(u64)],
+        "gm_msgcount": [ctypes.c_void_p, i32, P(i32), P(i32)],
+        "gm_read_row": [ctypes.c_void_p, i32, i32, i32, P(i32), P(i32)],
+        "gm_read_nodes": [ctypes.c_void_p, P(i32)],
+        "gm_dump_tables": [ctypes.c_void_p, ctypes.c_char_p, sz, P(sz)],
+        "gm_tick_stats": [ctypes.c_void_p, P(ctypes.c_int64)],
+        "gm_set_timing": [ctypes.c_void_p, i32], "gm_last_kernel_ms": [ctypes.c_void_p, P(ctypes.c_float)],
+        "gm_crash_set": [i32, i32, u64, P(i32)],
+    }
+    for name, args in sig.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = ctypes.c_int
+    lib.gm_strerror.argtypes = [ctypes.c_int]
+    lib.gm_strerror.restype = ctypes.c_char_p
+    _lib = lib
+    return lib
+
+
+def _ptr(a, ct=ctypes.c_int32):
+    return a.ctypes.data_as(ctypes.POINTER(ct))
+
+
+def crash_set(n, count, seed):
+    lib = load_library()
+    out = np.zeros(max(count, 1), dtype=np.int32)
+    rc = lib.gm_crash_set(n, count, seed, _ptr(out))
+    if rc:
+        raise GmError(rc, "gm_crash_set")
+    return out[:count]
+
+
+class Simulator:
+    """One libgm context: the whole cluster's MP1Node/EmulNet state on one GPU (or shard)."""
+
+    def __init__(self, n, mode=GM_MODE_FAITHFUL, single_failure=1, drop_msg=0, drop_prob=0.1, time_seed=0,
+                 rd_seed=0, drop_pct=0, drop_from=0, drop_to=0, drop_seed=0, device=0, shard_rank=0, shard_count=1):
+        self.lib = load_library()
+        cfg = GmConfig()
+        cfg.abi_version = GM_ABI_VERSION
+        cfg.mode, cfg.n = mode, n
+        cfg.single_failure, cfg.drop_msg, cfg.drop_prob = single_failure, drop_msg, drop_prob
+        cfg.time_seed, cfg.rd_seed = time_seed & 0xFFFFFFFF, rd_seed
+        cfg.drop_pct, cfg.drop_from, cfg.drop_to, cfg.drop_seed = drop_pct, drop_from, drop_to, drop_seed
+        cfg.device, cfg.shard_rank, cfg.shard_count = device, shard_rank, shard_count
+        self.cfg = cfg
+        self.n = n
+        self.mode = mode
+        h = ctypes.c_void_p()
+        self._call("gm_create", ctypes.byref(cfg), ctypes.byref(h))
+        self.h = h
+
+    def _call(self, name, *args):
+        rc = getattr(self.lib, name)(*args)
+        if rc != GM_OK:
+            raise GmError(rc, name)
+        return rc
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.gm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def tick(self):
+        self._call("gm_tick", self.h)
+
+    def sync(self):
+        self._call("gm_sync", self.h)
+
+    @property
+    def time(self):
+        t = ctypes.c_int32()
+        self._call("gm_time", self.h, ctypes.byref(t))
+        return t.value
+
+    def rand(self):
+        v = ctypes.c_int32()
+        self._call("gm_rand", self.h, ctypes.byref(v))
+        return v.value
+
+    def set_failed(self, idx):
+        a = np.ascontiguousarray(np.asarray(idx, dtype=np.int32))
+        self._call("gm_set_failed", self.h, _ptr(a), len(a))
+
+    def set_dropmsg(self, on):
+        self._call("gm_set_dropmsg", self.h, 1 if on else 0)
+
+    def drain_events(self):
+        n = ctypes.c_size_t()
+        rc = self.lib.gm_drain_events(self.h, None, 0, ctypes.byref(n))
+        if rc == GM_OK:
+            return []
+        if rc != GM_ERANGE:
+            raise GmError(rc, "gm_drain_events")
+        buf = (GmEvent * n.value)()
+        self._call("gm_drain_events", self.h, buf, n.value, ctypes.byref(n))
+        return [(e.t, e.logger, e.kind, e.subject) for e in buf[:n.value]]
+
+    def event_total(self):
+        c = (ctypes.c_uint64 * 6)()
+        self._call("gm_event_counts", self.h, c)
+        return int(c[0])
+
+    def msgcount(self, t):
+        sent = np.zeros((self.n, t), dtype=np.int32)
+        recv = np.zeros((self.n, t), dtype=np.int32)
+        self._call("gm_msgcount", self.h, t, _ptr(sent), _ptr(recv))
+        return sent, recv
+
+    def read_row(self, r, c0=0, length=None):
+        length = self.n if length is None else length
+        hb = np.zeros(length, dtype=np.int32)
+        ts = np.zeros(length, dtype=np.int32)
+        self._call("gm_read_row", self.h, r, c0, length, _ptr(hb), _ptr(ts))
+        return hb, ts
+
+    def read_nodes(self):
+        st = np.zeros((self.n, 4), dtype=np.int32)
+        self._call("gm_read_nodes", self.h, _ptr(st))
+        return st
+
+    def dump_tables(self):
+        n = ctypes.c_size_t()
+        rc = self.lib.gm_dump_tables(self.h, None, 0, ctypes.byref(n))
+        if rc not in (GM_OK, GM_ERANGE):
+            raise GmError(rc, "gm_dump_tables")
+        buf = ctypes.create_string_buffer(n.value + 1)
+        self._call("gm_dump_tables", self.h, buf, n.value + 1, ctypes.byref(n))
+        return buf.raw[:n.value]
+
+    def tick_stats(self):
+        s = (ctypes.c_int64 * 4)()
+        self._call("gm_tick_stats", self.h, s)
+        return {"lists": int(s[0]), "live": int(s[1]), "max_inbox": int(s[2]), "err": int(s[3])}
+
+    def set_timing(self, on):
+        self._call("gm_set_timing", self.h, 1 if on else 0)
+
+    def last_kernel_ms(self):
+        v = ctypes.c_float()
+        self._call("gm_last_kernel_ms", self.h, ctypes.byref(v))
+        return float(v.value)

@@ -142,8 +142,10 @@ int gm_dump_tables(gm_ctx *ctx, char *buf, size_t cap, size_t *len);
 /* SCALED telemetry of the last tick: [0]=delivered gossip lists M, [1]=live nodes,
  * [2]=max inbox depth, [3]=error flags */
 int gm_tick_stats(gm_ctx *ctx, int64_t stats[4]);
-/* duration (ms) of the last tick's dominant kernel, timed with HIP events on the
- * context stream (0 when not measured); enable with gm_set_timing(ctx, 1) */
+/* Mean per-tick duration (ms) of the tick kernel over the timing window, measured
+ * with HIP events recorded on the context stream before the window's first
+ * kernel and after its last. gm_set_timing(ctx, 1) opens a new window at the
+ * next tick; 0 when nothing was timed. */
 int gm_set_timing(gm_ctx *ctx, int32_t on);
 int gm_last_kernel_ms(gm_ctx *ctx, float *ms);
 

@@ -1,3 +1,4 @@
+#define _POSIX_C_SOURCE 199309L
 /* ref_cpu.c -- CPU restatement of the reference simulator (the parity oracle).
  *
  * TEST INFRASTRUCTURE ONLY; see ref_cpu.h for scope and the list of reference
@@ -13,6 +14,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #define TFAIL 5            /* MP1Node.h:21 */
 #define TREMOVE 20         /* MP1Node.h:20 */
@@ -711,5 +713,84 @@ int oc_node(oc_ctx *c, int r, int32_t *st) {
   st[1] = nd->in_group;
   st[2] = nd->failed;
   st[3] = (int32_t)nd->heartbeat;
+  return 0;
+}
+
+/* CPU baseline sample (bench.py cpu_baseline leg): time `nodes` node-ticks of the
+ * SCALED full-membership workload at cluster size n through the same restated
+ * code paths (updatelistCallBack per delivered entry, nodeLoopOps sweep + sort +
+ * gossip draw), without materialising the other n - nodes member lists. Each
+ * sampled observer holds all n subjects (converged regime) and receives `lists`
+ * gossip lists of n fresh entries. Stops after min_seconds or max_nodes. */
+int oc_bench_sample(int n, int lists, int max_nodes, double min_seconds, int *out_nodes, double *out_seconds) {
+  if (n < 8 || lists < 0 || max_nodes <= 0) return -1;
+  oc_config cfg = {0};
+  cfg.mode = OC_SCALED;
+  cfg.n = n;
+  cfg.rd_seed = 7;
+  oc_ctx *c = (oc_ctx *)calloc(1, sizeof(oc_ctx));
+  c->cfg = cfg;
+  c->n = n;
+  c->t = 40;
+  c->nodes = (node *)calloc((size_t)n, sizeof(node));
+  for (int i = 0; i < n; i++) c->nodes[i].id = i + 1;
+  c->snaps_next = (snap *)calloc((size_t)n, sizeof(snap));
+  c->tgt_next = (int32_t *)calloc((size_t)n * FANOUT, sizeof(int32_t));
+  c->ntgt_next = (int32_t *)calloc((size_t)n, sizeof(int32_t));
+  /* sender payloads: every subject fresh, heartbeat a little ahead of the observer's */
+  snap *pay = (snap *)calloc((size_t)(lists > 0 ? lists : 1), sizeof(snap));
+  uint64_t z = 12345;
+  for (int k = 0; k < lists; k++) {
+    pay[k].ids = (int32_t *)malloc(sizeof(int32_t) * (size_t)n);
+    pay[k].hbs = (int32_t *)malloc(sizeof(int32_t) * (size_t)n);
+    pay[k].n = n;
+    for (int j = 0; j < n; j++) {
+      z = mix64(z + 1);
+      pay[k].ids[j] = j + 1;
+      pay[k].hbs[j] = 70 + (int32_t)(z % 4);
+    }
+  }
+  struct timespec t0, t1;
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  int done = 0;
+  double el = 0;
+  while (done < max_nodes) {
+    int r = (int)(mix64((uint64_t)done * 7919 + 1) % (uint64_t)n);
+    node *nd = &c->nodes[r];
+    nd->inited = nd->in_group = 1;
+    nd->heartbeat = 2 * c->t;
+    nd->list.v = (entry *)malloc(sizeof(entry) * (size_t)n);
+    nd->list.cap = nd->list.n = n;
+    for (int j = 0; j < n; j++) {
+      entry e = {j + 1, 0, 70, c->t - 1 - (j % 3)};
+      nd->list.v[j] = e;
+    }
+    c->snaps_next[r].ids = (int32_t *)malloc(sizeof(int32_t) * (size_t)n);
+    c->snaps_next[r].hbs = (int32_t *)malloc(sizeof(int32_t) * (size_t)n);
+    /* the measured node-tick: merge every delivered list, then nodeLoopOps */
+    for (int k = 0; k < lists; k++)
+      for (int e = 0; e < pay[k].n; e++) update_list(c, r, pay[k].ids[e], 0, pay[k].hbs[e]);
+    node_loop(c, r);
+    free(nd->list.v);
+    nd->list.v = NULL;
+    nd->list.n = nd->list.cap = 0;
+    free(c->snaps_next[r].ids);
+    free(c->snaps_next[r].hbs);
+    c->snaps_next[r].ids = c->snaps_next[r].hbs = NULL;
+    done++;
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    el = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+    if (el >= min_seconds) break;
+  }
+  *out_nodes = done;
+  *out_seconds = el;
+  for (int k = 0; k < lists; k++) { free(pay[k].ids); free(pay[k].hbs); }
+  free(pay);
+  free(c->snaps_next);
+  free(c->tgt_next);
+  free(c->ntgt_next);
+  free(c->ev);
+  free(c->nodes);
+  free(c);
   return 0;
 }

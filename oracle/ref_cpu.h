@@ -77,6 +77,9 @@ int oc_node(oc_ctx *c, int r, int32_t *state4);
 /* the crash set the SCALED driver uses (host fault injection) */
 int oc_crash_set(int n, int count, uint64_t seed, int32_t *out);
 
+/* CPU-baseline sample: time node-ticks of the SCALED workload at size n (see ref_cpu.c) */
+int oc_bench_sample(int n, int lists, int max_nodes, double min_seconds, int *out_nodes, double *out_seconds);
+
 /* RNG restatements, exported for the known-answer tests */
 typedef struct oc_rand { int32_t st[31]; int f, r; } oc_rand;
 void oc_srand(oc_rand *g, uint32_t seed);

@@ -1,0 +1,165 @@
+"""ctypes binding of the oracle (oracle/ref_cpu.h) -- TEST INFRASTRUCTURE ONLY."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(REPO, "oracle")
+LIB = os.path.join(ORACLE_DIR, "build", "liboracle.so")
+CLI = os.path.join(ORACLE_DIR, "build", "ref_cpu")
+OC_FAITHFUL, OC_SCALED = 0, 1
+
+
+class OcConfig(ctypes.Structure):
+    _fields_ = [("mode", ctypes.c_int), ("n", ctypes.c_int), ("single_failure", ctypes.c_int),
+                ("drop_msg", ctypes.c_int), ("drop_prob", ctypes.c_double), ("time_seed", ctypes.c_uint32),
+                ("rd_seed", ctypes.c_uint64), ("crash_tick", ctypes.c_int), ("crash_count", ctypes.c_int),
+                ("crash_seed", ctypes.c_uint64), ("drop_pct", ctypes.c_int), ("drop_from", ctypes.c_int),
+                ("drop_to", ctypes.c_int), ("drop_seed", ctypes.c_uint64)]
+
+
+class OcEvent(ctypes.Structure):
+    _fields_ = [("t", ctypes.c_int32), ("logger", ctypes.c_int32), ("kind", ctypes.c_int32),
+                ("subject", ctypes.c_int32)]
+
+
+_lib = None
+
+
+def ensure_built():
+    if not (os.path.exists(LIB) and os.path.exists(CLI)):
+        subprocess.run(["make", "-C", ORACLE_DIR], check=True, capture_output=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        ensure_built()
+        L = ctypes.CDLL(LIB)
+        P = ctypes.POINTER
+        L.oc_create.argtypes = [P(OcConfig)]
+        L.oc_create.restype = ctypes.c_void_p
+        L.oc_destroy.argtypes = [ctypes.c_void_p]
+        L.oc_tick.argtypes = [ctypes.c_void_p]
+        L.oc_time.argtypes = [ctypes.c_void_p]
+        for f in ("oc_dbg_log", "oc_stdout", "oc_msgcount", "oc_dump"):
+            getattr(L, f).argtypes = [ctypes.c_void_p, P(ctypes.c_size_t)]
+            getattr(L, f).restype = ctypes.c_void_p
+        L.oc_events.argtypes = [ctypes.c_void_p, P(P(OcEvent))]
+        L.oc_events.restype = ctypes.c_size_t
+        L.oc_row.argtypes = [ctypes.c_void_p, ctypes.c_int, P(ctypes.c_int32), P(ctypes.c_int32)]
+        L.oc_node.argtypes = [ctypes.c_void_p, ctypes.c_int, P(ctypes.c_int32)]
+        L.oc_crash_set.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint64, P(ctypes.c_int32)]
+        L.oc_srand.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+        L.oc_rand_next.argtypes = [ctypes.c_void_p]
+        L.oc_rand_next.restype = ctypes.c_int32
+        L.oc_rd_seed.argtypes = [ctypes.c_uint64, ctypes.c_int32, ctypes.c_int32]
+        L.oc_rd_seed.restype = ctypes.c_uint32
+        L.oc_mt_uniform.argtypes = [ctypes.c_uint32, ctypes.c_int, ctypes.c_int, P(ctypes.c_int32)]
+        _lib = L
+    return _lib
+
+
+def _i32p(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+
+
+class Oracle:
+    def __init__(self, n, mode=OC_FAITHFUL, single_failure=1, drop_msg=0, drop_prob=0.1, time_seed=0, rd_seed=0,
+                 crash_tick=-1, crash_count=0, crash_seed=0, drop_pct=0, drop_from=0, drop_to=0, drop_seed=0):
+        self.L = lib()
+        cfg = OcConfig(mode, n, single_failure, drop_msg, drop_prob, time_seed & 0xFFFFFFFF, rd_seed, crash_tick,
+                       crash_count, crash_seed, drop_pct, drop_from, drop_to, drop_seed)
+        self.h = self.L.oc_create(ctypes.byref(cfg))
+        if not self.h:
+            raise ValueError("oc_create failed")
+        self.n = n
+
+    def close(self):
+        if self.h:
+            self.L.oc_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def tick(self):
+        if self.L.oc_tick(self.h):
+            raise RuntimeError("oc_tick")
+
+    @property
+    def time(self):
+        return self.L.oc_time(self.h)
+
+    def _buf(self, fn):
+        n = ctypes.c_size_t()
+        p = getattr(self.L, fn)(self.h, ctypes.byref(n))
+        return ctypes.string_at(p, n.value) if n.value else b""
+
+    def dump(self):
+        return self._buf("oc_dump")
+
+    def dbg(self):
+        return self._buf("oc_dbg_log")
+
+    def events(self):
+        p = ctypes.POINTER(OcEvent)()
+        n = self.L.oc_events(self.h, ctypes.byref(p))
+        return [(p[k].t, p[k].logger, p[k].kind, p[k].subject) for k in range(n)]
+
+    def row(self, r):
+        hb = np.zeros(self.n, dtype=np.int32)
+        ts = np.zeros(self.n, dtype=np.int32)
+        self.L.oc_row(self.h, r, _i32p(hb), _i32p(ts))
+        return hb, ts
+
+    def node(self, r):
+        st = np.zeros(4, dtype=np.int32)
+        self.L.oc_node(self.h, r, _i32p(st))
+        return st
+
+
+def crash_set(n, count, seed):
+    out = np.zeros(max(count, 1), dtype=np.int32)
+    lib().oc_crash_set(n, count, seed, _i32p(out))
+    return out[:count]
+
+
+def glibc_rand(seed, k):
+    L = lib()
+    st = ctypes.create_string_buffer(256)
+    L.oc_srand(st, seed)
+    return np.array([L.oc_rand_next(st) for _ in range(k)], dtype=np.int32)
+
+
+def mt_uniform(seed, n, k):
+    out = np.zeros(k, dtype=np.int32)
+    lib().oc_mt_uniform(seed, n, k, _i32p(out))
+    return out
+
+
+def run_cli(conf_text, time_seed, rd_seed, workdir, dump=False):
+    """Run the oracle's ./Application-shaped CLI; returns (dbg, msgcount, stdout, dump)."""
+    ensure_built()
+    cpath = os.path.join(workdir, "case.conf")
+    with open(cpath, "w") as f:
+        f.write(conf_text)
+    env = dict(os.environ, TIME_SEED=str(time_seed), RD_SEED=str(rd_seed))
+    if dump:
+        env["DUMP_FILE"] = os.path.join(workdir, "tables.txt")
+    p = subprocess.run([CLI, cpath], cwd=workdir, env=env, capture_output=True, check=True)
+    rd = lambda name: open(os.path.join(workdir, name), "rb").read()  # noqa: E731
+    return rd("dbg.log"), rd("msgcount.log"), p.stdout, (rd("tables.txt") if dump else None)
+
+
+def bench_sample(n, lists=5, max_nodes=1000000, min_seconds=10.0):
+    """Time node-ticks of the SCALED workload on one host core (bench cpu_baseline leg)."""
+    L = lib()
+    L.oc_bench_sample.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double,
+                                  ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_double)]
+    nodes, secs = ctypes.c_int(), ctypes.c_double()
+    if L.oc_bench_sample(n, lists, max_nodes, min_seconds, ctypes.byref(nodes), ctypes.byref(secs)):
+        raise RuntimeError("oc_bench_sample")
+    return nodes.value, secs.value

@@ -1,0 +1,79 @@
+"""SCALED parity: the HBM-bound HIP tick against the oracle's SCALED restatement.
+
+Per tick: the full membership tables (dump digest), node state and the join /
+remove event set, with a crash set and keyed message drops; then size-
+independent invariants at a larger N that the oracle cannot finish quickly."""
+import numpy as np
+import pytest
+
+import oracle_py
+from golden_util import digest64
+from membership import GM_EV_JOINED, GM_EV_REMOVED, GM_MODE_SCALED, Simulator, crash_set
+
+pytestmark = pytest.mark.gpu
+
+
+def run_pair(n, ticks, crash_tick, crash_count, drop_pct=0, drop_from=0, drop_to=0, rd_seed=7, seed=42):
+    ora = oracle_py.Oracle(n, oracle_py.OC_SCALED, rd_seed=rd_seed, crash_tick=crash_tick, crash_count=crash_count,
+                           crash_seed=seed, drop_pct=drop_pct, drop_from=drop_from, drop_to=drop_to, drop_seed=seed)
+    sim = Simulator(n, GM_MODE_SCALED, rd_seed=rd_seed, drop_pct=drop_pct, drop_from=drop_from, drop_to=drop_to,
+                    drop_seed=seed)
+    crash = crash_set(n, crash_count, seed)
+    assert np.array_equal(crash, oracle_py.crash_set(n, crash_count, seed))
+    kinds = {GM_EV_JOINED: 1, GM_EV_REMOVED: 2}
+    for _ in range(ticks):
+        t = sim.time
+        assert ora.time == t
+        ora.tick()
+        sim.tick()
+        if t == crash_tick:
+            sim.set_failed(crash)
+        ev_g = [(e[0], e[1], kinds[e[2]], e[3]) for e in sim.drain_events()]
+        assert ev_g == ora.events(), f"events differ at tick {t}"
+        assert digest64(sim.dump_tables()) == digest64(ora.dump()), f"tables differ at tick {t}"
+    st = sim.tick_stats()
+    assert st["err"] == 0
+    return sim, ora
+
+
+@pytest.mark.parametrize("n", [64, 300, 1024])
+def test_scaled_matches_oracle(n):
+    run_pair(n, 40, crash_tick=8, crash_count=max(1, n // 50))
+
+
+@pytest.mark.parametrize("n", [128, 513])
+def test_scaled_with_drops_matches_oracle(n):
+    run_pair(n, 45, crash_tick=10, crash_count=3, drop_pct=20, drop_from=5, drop_to=30)
+
+
+def test_scaled_heavy_drop_false_removals_match():
+    # 60% loss makes entries go stale and get removed/re-added: exercises ADD events
+    sim, ora = run_pair(96, 60, crash_tick=-1, crash_count=0, drop_pct=60, drop_from=2, drop_to=60)
+
+
+def test_scaled_invariants_large():
+    n, crash_tick, ncrash = 8192, 10, 82
+    sim = Simulator(n, GM_MODE_SCALED, rd_seed=7)
+    crash = crash_set(n, ncrash, 42)
+    crashed = np.zeros(n, bool)
+    crashed[crash] = True
+    removed = 0
+    for _ in range(45):
+        t = sim.time
+        sim.tick()
+        if t == crash_tick:
+            sim.set_failed(crash)
+        ev = sim.drain_events()
+        for (_, logger, kind, subject) in ev:
+            assert kind == GM_EV_REMOVED and crashed[subject - 1] and not crashed[logger]
+        removed += len(ev)
+    assert removed == (n - ncrash) * ncrash  # every live observer removed every crashed node, nothing else
+    st = sim.tick_stats()
+    assert st["err"] == 0 and st["live"] == n - ncrash
+    for r in [0, 1, 4095, n - 1]:
+        if crashed[r]:
+            continue
+        hb, ts = sim.read_row(r)
+        assert np.all(hb[crashed] == -1)
+        assert np.all(hb[~crashed] >= 0)
+        assert np.all(sim.time - 1 - ts[~crashed] < 5)
