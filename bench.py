@@ -29,6 +29,30 @@ sys.path.insert(0, os.path.join(REPO, "distributed-membership_amd"))
 PEAK_HBM_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 
 
+class Roctx:
+    """roctxProfilerPause/Resume around the timed region, so that
+    `rocprofv3 --selected-regions --kernel-trace --stats -- python3 bench.py`
+    traces exactly the K timed ticks (no-ops when not profiling)."""
+
+    def __init__(self):
+        import ctypes
+        self.lib = None
+        for name in ("librocprofiler-sdk-roctx.so.1", "libroctx64.so"):
+            try:
+                self.lib = ctypes.CDLL(name)
+                break
+            except OSError:
+                continue
+
+    def pause(self):
+        if self.lib is not None:
+            self.lib.roctxProfilerPause(0)
+
+    def resume(self):
+        if self.lib is not None:
+            self.lib.roctxProfilerResume(0)
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -45,6 +69,8 @@ def parse():
 
 def main():
     a = parse()
+    rtx = Roctx()
+    rtx.pause()
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -80,11 +106,13 @@ def main():
     barrier()
     sim.sync()
     sim.set_timing(1)
+    rtx.resume()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         sim.tick()
     sim.sync()
     t1 = time.perf_counter()
+    rtx.pause()
     barrier()
     elapsed = t1 - t0
     if dist is not None:

@@ -1,0 +1,43 @@
+#!/usr/bin/env python3
+"""Turn rocprofv3 FETCH_SIZE / WRITE_SIZE passes into per-launch HBM bytes of the
+tick kernel (profiles/traffic_n<N>.json, read by bench.py as roofline.traffic).
+
+Corrections per MI355X_MICROARCH.md §HBM (gfx950): FETCH_SIZE (KiB) reports half
+the bytes of a wide (16 B/lane) coalesced streaming read -> x2; WRITE_SIZE (KiB)
+is exact for 16 B/lane stores. Steady-state launches only: the median of the last
+`--last` dispatches (the prologue's converged-start transient is excluded)."""
+import argparse
+import csv
+import json
+import statistics
+
+
+def per_launch(path, counter, kernel, last):
+    rows = [r for r in csv.DictReader(open(path)) if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter]
+    vals = [float(r["Counter_Value"]) for r in rows][-last:]
+    return statistics.median(vals), len(rows)
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--fetch", required=True)
+    p.add_argument("--write", required=True)
+    p.add_argument("--n", type=int, default=65536)
+    p.add_argument("--kernel", default="gm_s_tick")
+    p.add_argument("--last", type=int, default=6)
+    p.add_argument("--out", required=True)
+    a = p.parse_args()
+    f, nf = per_launch(a.fetch, "FETCH_SIZE", a.kernel, a.last)
+    w, nw = per_launch(a.write, "WRITE_SIZE", a.kernel, a.last)
+    fetch_b = f * 1024 * 2  # gfx950: FETCH_SIZE counts half of 16 B/lane streaming reads
+    write_b = w * 1024
+    out = {"kernel": a.kernel, "n": a.n, "fetch_size_kib_raw": f, "write_size_kib_raw": w,
+           "fetch_bytes_corrected": fetch_b, "write_bytes": write_b, "hbm_bytes_per_launch": fetch_b + write_b,
+           "launches_seen": [nf, nw], "note": "FETCH_SIZE x2 (gfx950 16B/lane streaming-read correction)"}
+    with open(a.out, "w") as fh:
+        json.dump(out, fh, indent=1)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

@@ -76,4 +76,4 @@ def test_scaled_invariants_large():
         hb, ts = sim.read_row(r)
         assert np.all(hb[crashed] == -1)
         assert np.all(hb[~crashed] >= 0)
-        assert np.all(sim.time - 1 - ts[~crashed] < 5)
+        assert np.all(sim.time - 1 - ts[~crashed] < 20)  # present => younger than TREMOVE
