@@ -21,7 +21,7 @@ $(PKG)/build/%.o: $(CSRC)/%.hip $(HDRS)
 
 $(LIB): $(KOBJS)
 	@mkdir -p $(PKG)/lib
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(KOBJS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(KOBJS) -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
 Application: $(PKG)/app/Application.cpp $(PKG)/app/Log.cpp $(PKG)/app/Application.h $(PKG)/app/Log.h $(LIB)
 	g++ -O2 -std=c++17 -Wall -Iinclude -I$(PKG)/app -o $@ $(PKG)/app/Application.cpp $(PKG)/app/Log.cpp \

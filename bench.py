@@ -13,9 +13,13 @@ TFAIL 5, TREMOVE 20, RD_SEED 7, 1% of the nodes (655) crash at the end of tick
 (T_warm of S-A) brings the cluster to steady state with the crash's removals
 still ahead; then W warmup ticks, then exactly K timed ticks.
 
-Multi-GPU (--gpus N via torch.distributed.run): the N x N table is sharded by
-subject column across ranks (weak scaling: the cluster grows with the rank
-count so each GPU keeps ~N^2 cells); see DESIGN.md §Multi-GPU.
+Multi-GPU (--gpus G via torch.distributed.run, one rank per GPU): the same
+N = 65,536 cluster with its N x N table sharded by subject column, rank g
+owning N/G columns of every row ("strong" scaling: total work fixed). libgm
+runs the per-tick exchange (all-gather of per-row counts, MAX-allreduce of
+resolved gossip draws) with RCCL on its own stream; torch.distributed is only
+the CPU (gloo) rendezvous that hands every rank the RCCL unique id, plus the
+barrier / max-over-ranks timing. See DESIGN.md §Multi-GPU.
 """
 import argparse
 import json
@@ -76,19 +80,21 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if world > 1:
-        import torch
+        # CPU-only process group: rendezvous, barrier and max-over-ranks timing.
+        # The GPU (and RCCL over xGMI) is driven by libgm alone.
         import torch.distributed as tdist
-        torch.cuda.set_device(local)
-        tdist.init_process_group("nccl")
+        tdist.init_process_group("gloo")
         dist = tdist
 
     from membership import GM_MODE_SCALED, Simulator, crash_set
+    from membership.sharded import distributed_shard
 
     n = a.n
-    if world > 1:
-        raise SystemExit("multi-GPU sharded bench: see bench_shard (not built yet)")
     ncrash = int(round(n * a.crash_frac))
-    sim = Simulator(n, GM_MODE_SCALED, rd_seed=7, device=local)
+    if world > 1:
+        sim = distributed_shard(n, rank, world, local, rd_seed=7)
+    else:
+        sim = Simulator(n, GM_MODE_SCALED, rd_seed=7, device=local)
     crash = crash_set(n, ncrash, 42)
     while sim.time <= a.prologue:
         t = sim.time
@@ -117,7 +123,7 @@ def main():
     elapsed = t1 - t0
     if dist is not None:
         import torch
-        x = torch.tensor([elapsed], device="cuda")
+        x = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(x, op=dist.ReduceOp.MAX)
         elapsed = float(x.item())
     kernel_ms = sim.last_kernel_ms()
@@ -125,17 +131,18 @@ def main():
     assert st["err"] == 0, st
 
     n_live, m_lists = st["live"], st["lists"]
-    W = n
+    W = sim.shard_layout()[1] if world > 1 else n  # this rank's subject columns
     # algorithmic HBM bytes of one tick in this layout:
     # per live row 4W read + 4W write (packed table) + 2W write (payload plane),
     # plus 2W per delivered gossip list (payload read)
     b_alg = (10 * n_live + 2 * m_lists) * W
     # the survey's int32 (hb, ts) formulation of the same work
-    b_survey = 16 * n_live * n + 8 * m_lists * n
+    b_survey = 16 * n_live * W + 8 * m_lists * W
     achieved = b_alg / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else None
     traffic = None
+    tpath_ok = world == 1
     tpath = os.path.join(REPO, "profiles", f"traffic_n{n}.json")
-    if os.path.exists(tpath):
+    if tpath_ok and os.path.exists(tpath):
         with open(tpath) as f:
             traffic = json.load(f).get("hbm_bytes_per_launch")
 
@@ -149,7 +156,7 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": elapsed / a.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "u16",
         "data": "synthetic (converged full-membership table, seeded crash set)",
@@ -158,8 +165,9 @@ def main():
                    "lists_per_tick": m_lists, "parallelism": f"column-shard x{world}" if world > 1 else "single GPU"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                      "frac": (achieved / PEAK_HBM_GBPS) if achieved else None, "traffic": traffic,
-                     "kernel": "gm_s_tick", "kernel_ms": kernel_ms, "alg_bytes_per_launch": b_alg,
-                     "survey_int32_bytes_per_launch": b_survey},
+                     "kernel": "gm_s_tick_shard" if world > 1 else "gm_s_tick", "kernel_ms": kernel_ms,
+                     "alg_bytes_per_launch": b_alg, "survey_int32_bytes_per_launch": b_survey,
+                     "columns_per_gpu": W},
     }
     if rank == 0 and world == 1 and not a.no_cpu:
         sys.path.insert(0, os.path.join(REPO, "tests"))

@@ -49,24 +49,29 @@ __device__ __forceinline__ uint32_t gm_rd_seed(uint64_t rd_seed, int32_t tick, i
 // workgroup, driven by a single lane). Twisting word k just before output k and
 // storing it back is exactly the standard block twist, because word k's twist
 // reads x[k+1] (old) and x[(k+397)%624] (old for k<227, already-new for k>=227).
+// `stride` lets the 624 words live strided in global memory ([624][rows],
+// coalesced across the rows of a launch) for generators that outlive a kernel.
 struct GmLazyMT {
-  uint32_t *x;     // 624 words of LDS
+  uint32_t *x;     // 624 words (LDS, or global with a row stride)
+  int stride;      // distance between consecutive state words
   int k;           // next output index within the current 624-block
   int ninit;       // init words computed so far (first block only)
   bool first;      // still in the first block (init words possibly incomplete)
 
-  __device__ void seed(uint32_t *lds, uint32_t s) {
-    x = lds;
+  __device__ void seed(uint32_t *base, uint32_t s, int stride_ = 1) {
+    x = base;
+    stride = stride_;
     x[0] = s;
     ninit = 1;
     k = 0;
     first = true;
   }
+  __device__ __forceinline__ uint32_t &w(int i) { return x[(size_t)i * stride]; }
   __device__ __forceinline__ void init_to(int upto) {  // make init words [0, upto] valid
-    uint32_t v = x[ninit - 1];
+    uint32_t v = w(ninit - 1);
     for (int i = ninit; i <= upto; i++) {
       v = 1812433253u * (v ^ (v >> 30)) + (uint32_t)i;
-      x[i] = v;
+      w(i) = v;
     }
     if (upto + 1 > ninit) ninit = upto + 1;
   }
@@ -77,9 +82,9 @@ struct GmLazyMT {
       if (k + 1 > need) need = k + 1 < 624 ? k + 1 : 623;
       if (need >= ninit) init_to(need);
     }
-    uint32_t y = (x[k] & 0x80000000u) | (x[k + 1 < 624 ? k + 1 : 0] & 0x7fffffffu);
-    uint32_t v = x[k + 397 < 624 ? k + 397 : k - 227] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
-    x[k] = v;
+    uint32_t y = (w(k) & 0x80000000u) | (w(k + 1 < 624 ? k + 1 : 0) & 0x7fffffffu);
+    uint32_t v = w(k + 397 < 624 ? k + 397 : k - 227) ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    w(k) = v;
     k++;
     v ^= v >> 11;
     v ^= (v << 7) & 0x9d2c5680u;

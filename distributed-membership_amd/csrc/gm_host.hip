@@ -4,6 +4,7 @@
 // context stream, and turns device event records into reference log order.
 // Compiled by hipcc for gfx950 together with gm_faithful.hip / gm_scaled.hip.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cstdio>
@@ -21,12 +22,19 @@ __global__ void gm_f_recv(FState s, int t);
 __global__ void gm_f_node(FState s, int t);
 __global__ void gm_f_send(FState s, int t);
 __global__ void gm_s_tick(SState s, int t, int drop_pct);
+__global__ void gm_s_tick_shard(SState s, int t, int drop_pct);
+__global__ void gm_s_draw(SState s, int t, int round, int D);
+__global__ void gm_s_accept(SState s, int t, int D);
 
 #define GM_T_LIMIT 32766  // packed 16-bit hb/ts stay exact: hb <= 2t+1 < 0xFFFF
 
 struct gm_ctx {
   gm_config cfg;
   hipStream_t stream = nullptr;
+  int dmax = 0;                      // status exchange depth (sharded)
+  ncclComm_t comm = nullptr;         // RCCL communicator across column shards
+  hipEvent_t k0 = nullptr, k1 = nullptr;  // per-tick merge-kernel events (sharded)
+  double kernel_ms_sum = 0;
   int t = 0;
   int n = 0;
   int dropmsg = 0;
@@ -193,11 +201,14 @@ static int create_scaled(gm_ctx *c) {
   const int n = c->n;
   const int G = c->cfg.shard_count > 0 ? c->cfg.shard_count : 1;
   const int rank = c->cfg.shard_rank;
-  if (G != 1 || rank != 0) return GM_EUNSUPPORTED;  // column sharding: see gm_shard (multi-GPU)
+  if (rank < 0 || rank >= G || G > n) return GM_EINVAL;
   SState &s = c->s;
   s.n = n;
-  s.c0 = 0;
-  s.w = n;
+  s.shard_rank = rank;
+  s.shard_count = G;
+  // contiguous, balanced subject-column ranges
+  s.c0 = (int)((int64_t)n * rank / G);
+  s.w = (int)((int64_t)n * (rank + 1) / G) - s.c0;
   s.wp = (n + S_ROW_ALIGN - 1) / S_ROW_ALIGN * S_ROW_ALIGN;
   s.evcap = std::min(s.wp, 1024);
   s.ev_spill_cap = 1u << 24;
@@ -234,6 +245,21 @@ static int create_scaled(gm_ctx *c) {
   HIPCHECK(hipMemset(s.rowstat, 0, sizeof(int32_t) * n * 4));
   HIPCHECK(hipMemset(s.err, 0, sizeof(uint32_t)));
   const int nw = s.wp / 64;
+  if (G > 1) {
+    TRY(dalloc(c, &s.gpres, (size_t)n * nw));
+    TRY(dalloc(c, &s.gfresh, (size_t)n * nw));
+    TRY(dalloc(c, &s.gpre, (size_t)n * nw));
+    TRY(dalloc(c, &s.mt, (size_t)624 * n));
+    TRY(dalloc(c, &s.mtk, (size_t)n * 3));
+    TRY(dalloc(c, &s.acc, (size_t)n * 8));
+    TRY(dalloc(c, &s.pending, n));
+    TRY(dalloc(c, &s.npending, 1));
+    c->dmax = 64;
+    TRY(dalloc(c, &s.xcnt, (size_t)G * n * 2));
+    TRY(dalloc(c, &s.status, (size_t)n * c->dmax));
+    HIPCHECK(hipMemset(s.pending, 0, sizeof(int32_t) * n));
+    HIPCHECK(hipMemset(s.xcnt, 0, sizeof(int32_t) * (size_t)G * n * 2));
+  }
   c->s_smem = (size_t)nw * 8 * 2 + (size_t)nw * 4 + 624 * 4 + (S_KMAX + 16 + 8) * 4;
   c->t = 1;  // the converged table is the state "as of tick 0"
   return GM_OK;
@@ -251,7 +277,8 @@ extern "C" int gm_create(const gm_config *cfg, gm_ctx **out) {
   c->failed_h.assign(cfg->n, 0);
   int rc = GM_OK;
   if (hipSetDevice(cfg->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreate(&c->e0) != hipSuccess || hipEventCreate(&c->e1) != hipSuccess) {
+      hipEventCreate(&c->e0) != hipSuccess || hipEventCreate(&c->e1) != hipSuccess ||
+      hipEventCreate(&c->k0) != hipSuccess || hipEventCreate(&c->k1) != hipSuccess) {
     snprintf(g_errbuf, sizeof g_errbuf, "HIP device %d unavailable", cfg->device);
     rc = GM_EDEVICE;
   }
@@ -267,9 +294,10 @@ extern "C" int gm_create(const gm_config *cfg, gm_ctx **out) {
 extern "C" int gm_destroy(gm_ctx *c) {
   if (!c) return GM_EINVAL;
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->comm) (void)ncclCommDestroy(c->comm);
   for (void *p : c->allocs) (void)hipFree(p);
-  if (c->e0) (void)hipEventDestroy(c->e0);
-  if (c->e1) (void)hipEventDestroy(c->e1);
+  for (hipEvent_t e : {c->e0, c->e1, c->k0, c->k1})
+    if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return GM_OK;
@@ -319,8 +347,11 @@ static int tick_faithful(gm_ctx *c) {
   return check_err(c);
 }
 
+static int tick_sharded(gm_ctx *c);
+
 static int tick_scaled(gm_ctx *c) {
   if (c->t > GM_T_LIMIT) return GM_ERANGE;
+  if (c->s.shard_count > 1) return tick_sharded(c);
   const int t_send = c->t - 1;
   const bool drop = c->cfg.drop_pct > 0 && t_send >= c->cfg.drop_from && t_send < c->cfg.drop_to;
   if (c->timing && c->timed_ticks == 0) HIPCHECK(hipEventRecord(c->e0, c->stream));
@@ -475,7 +506,7 @@ extern "C" int gm_msgcount(gm_ctx *c, int32_t t, int32_t *sent, int32_t *recv) {
 static int read_table_row(gm_ctx *c, int r, std::vector<uint32_t> &row, int &w) {
   const bool fm = c->cfg.mode == GM_MODE_FAITHFUL;
   const int stride = fm ? c->f.np : c->s.wp;
-  w = fm ? c->n : c->s.w;
+  w = fm ? c->n : c->s.w;  // this context's columns
   row.resize(w);
   const uint32_t *base = (fm ? c->f.table : c->s.table) + (size_t)r * stride;
   HIPCHECK(hipMemcpy(row.data(), base, sizeof(uint32_t) * w, hipMemcpyDeviceToHost));
@@ -534,12 +565,13 @@ extern "C" int gm_dump_tables(gm_ctx *c, char *buf, size_t cap, size_t *len) {
     int w;
     TRY(read_table_row(c, i, row, w));
     int cnt = 0;
+    const int c0 = c->cfg.mode == GM_MODE_FAITHFUL ? 0 : c->s.c0;
     for (int j = 0; j < w; j++) cnt += row[j] != GM_ABSENT;
     snprintf(tmp, sizeof tmp, "%d %d %d %d %d %d %d", t, i, st[4 * i], st[4 * i + 1], st[4 * i + 2], st[4 * i + 3], cnt);
     out += tmp;
     for (int j = 0; j < w; j++) {
       if (row[j] == GM_ABSENT) continue;
-      snprintf(tmp, sizeof tmp, " %d:%u:%u", j + 1, row[j] & 0xFFFFu, row[j] >> 16);
+      snprintf(tmp, sizeof tmp, " %d:%u:%u", c0 + j + 1, row[j] & 0xFFFFu, row[j] >> 16);
       out += tmp;
     }
     out += "\n";
@@ -575,6 +607,7 @@ extern "C" int gm_set_timing(gm_ctx *c, int32_t on) {
   if (!c) return GM_EINVAL;
   c->timing = on != 0;
   c->timed_ticks = 0;  // (re)opens the timing window at the next tick
+  c->kernel_ms_sum = 0;
   return GM_OK;
 }
 
@@ -582,6 +615,10 @@ extern "C" int gm_last_kernel_ms(gm_ctx *c, float *ms) {
   if (!c || !ms) return GM_EINVAL;
   *ms = 0.f;
   if (!c->timing || c->cfg.mode != GM_MODE_SCALED || c->timed_ticks == 0) return GM_OK;
+  if (c->s.shard_count > 1) {  // per-tick merge-kernel events, summed at each tick end
+    *ms = (float)(c->kernel_ms_sum / c->timed_ticks);
+    return GM_OK;
+  }
   HIPCHECK(hipEventSynchronize(c->e1));
   HIPCHECK(hipEventElapsedTime(ms, c->e0, c->e1));
   *ms /= (float)c->timed_ticks;
@@ -601,5 +638,155 @@ extern "C" int gm_crash_set(int32_t n, int32_t count, uint64_t seed, int32_t *ou
   std::partial_sort(k.begin(), k.begin() + count, k.end());
   for (int i = 0; i < count; i++) out[i] = k[i].second;
   std::sort(out, out + count);
+  return GM_OK;
+}
+
+// ------------------------------------------------------------ column shards
+// A tick of a column shard: merge/sweep own columns, all-gather per-row counts,
+// then rounds of {draw, MAX-allreduce of resolved draws, accept} until every row
+// has its targets. Collectives are RCCL on the context stream (gm_comm_init),
+// or in-process between contexts of one device (gm_shard_loopback, tests).
+
+#define NCCLCHECK(x)                                                                 \
+  do {                                                                               \
+    ncclResult_t r_ = (x);                                                           \
+    if (r_ != ncclSuccess) {                                                         \
+      snprintf(g_errbuf, sizeof g_errbuf, "%s:%d RCCL %s", __FILE__, __LINE__, ncclGetErrorString(r_)); \
+      return GM_ECOMM;                                                               \
+    }                                                                                \
+  } while (0)
+
+#define GM_D_FIRST 16  // draws per row in the first round (steady state needs ~5-6)
+#define GM_D_MORE 64   // draws per row in later rounds (transients with many stale entries)
+
+extern "C" int gm_comm_unique_id(uint8_t *out128) {
+  if (!out128) return GM_EINVAL;
+  ncclUniqueId id;
+  NCCLCHECK(ncclGetUniqueId(&id));
+  memcpy(out128, &id, sizeof id);
+  return GM_OK;
+}
+
+extern "C" int gm_comm_init(gm_ctx *c, const uint8_t *id128, int32_t nranks, int32_t rank) {
+  if (!c || !id128 || c->cfg.mode != GM_MODE_SCALED || c->s.shard_count != nranks || c->s.shard_rank != rank)
+    return GM_EINVAL;
+  if (c->comm) return GM_OK;
+  ncclUniqueId id;
+  memcpy(&id, id128, sizeof id);
+  HIPCHECK(hipSetDevice(c->cfg.device));
+  NCCLCHECK(ncclCommInitRank(&c->comm, nranks, id, rank));
+  return GM_OK;
+}
+
+extern "C" int gm_shard_layout(gm_ctx *c, int32_t *c0, int32_t *w) {
+  if (!c || !c0 || !w || c->cfg.mode != GM_MODE_SCALED) return GM_EINVAL;
+  *c0 = c->s.c0;
+  *w = c->s.w;
+  return GM_OK;
+}
+
+static int shard_ready(gm_ctx *c) {
+  if (!c || c->cfg.mode != GM_MODE_SCALED || c->s.shard_count < 2) return GM_EINVAL;
+  if (c->latched != GM_OK) return c->latched;
+  if (c->t > GM_T_LIMIT) return GM_ERANGE;
+  return GM_OK;
+}
+
+extern "C" int gm_shard_merge(gm_ctx *c) {
+  TRY(shard_ready(c));
+  const int t_send = c->t - 1;
+  const bool drop = c->cfg.drop_pct > 0 && t_send >= c->cfg.drop_from && t_send < c->cfg.drop_to;
+  if (c->timing) HIPCHECK(hipEventRecord(c->k0, c->stream));
+  hipLaunchKernelGGL(gm_s_tick_shard, dim3(c->n), dim3(S_THREADS), c->s_smem, c->stream, c->s, c->t,
+                     drop ? c->cfg.drop_pct : -1);
+  if (c->timing) HIPCHECK(hipEventRecord(c->k1, c->stream));
+  HIPCHECK(hipGetLastError());
+  return GM_OK;
+}
+
+extern "C" int gm_shard_draw(gm_ctx *c, int32_t round, int32_t D) {
+  TRY(shard_ready(c));
+  if (D <= 0 || D > c->dmax || round < 0) return GM_EINVAL;
+  hipLaunchKernelGGL(gm_s_draw, dim3((c->n + 255) / 256), dim3(256), 0, c->stream, c->s, c->t, round, D);
+  HIPCHECK(hipGetLastError());
+  return GM_OK;
+}
+
+extern "C" int gm_shard_accept(gm_ctx *c, int32_t D, int32_t *npending) {
+  TRY(shard_ready(c));
+  if (D <= 0 || D > c->dmax || !npending) return GM_EINVAL;
+  HIPCHECK(hipMemsetAsync(c->s.npending, 0, sizeof(int32_t), c->stream));
+  hipLaunchKernelGGL(gm_s_accept, dim3((c->n + 255) / 256), dim3(256), 0, c->stream, c->s, c->t, D);
+  HIPCHECK(hipGetLastError());
+  HIPCHECK(hipMemcpyAsync(npending, c->s.npending, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  HIPCHECK(hipStreamSynchronize(c->stream));
+  return GM_OK;
+}
+
+extern "C" int gm_shard_end_tick(gm_ctx *c) {
+  TRY(shard_ready(c));
+  if (c->timing) {
+    float ms = 0;
+    HIPCHECK(hipEventSynchronize(c->k1));
+    HIPCHECK(hipEventElapsedTime(&ms, c->k0, c->k1));
+    c->kernel_ms_sum += ms;
+    c->timed_ticks++;
+  }
+  c->t++;
+  return GM_OK;
+}
+
+__global__ void gm_max_into(int32_t *dst, const int32_t *src, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    dst[i] = max(dst[i], src[i]);
+}
+
+// In-process collectives between the G shard contexts of one device:
+// what = 0 all-gathers xcnt, what = 1 MAX-allreduces status[0, n*D).
+extern "C" int gm_shard_loopback(gm_ctx **ctxs, int32_t G, int32_t what, int32_t D) {
+  if (!ctxs || G < 2) return GM_EINVAL;
+  for (int g = 0; g < G; g++) {
+    TRY(shard_ready(ctxs[g]));
+    if (ctxs[g]->s.shard_count != G || ctxs[g]->s.shard_rank != g || ctxs[g]->n != ctxs[0]->n) return GM_EINVAL;
+    HIPCHECK(hipStreamSynchronize(ctxs[g]->stream));
+  }
+  const size_t n = (size_t)ctxs[0]->n;
+  hipStream_t st = ctxs[0]->stream;
+  if (what == 0) {
+    for (int dst = 0; dst < G; dst++)
+      for (int src = 0; src < G; src++)
+        if (src != dst)
+          HIPCHECK(hipMemcpyAsync(ctxs[dst]->s.xcnt + (size_t)src * n * 2, ctxs[src]->s.xcnt + (size_t)src * n * 2,
+                                  sizeof(int32_t) * n * 2, hipMemcpyDeviceToDevice, st));
+  } else {
+    if (D <= 0 || D > ctxs[0]->dmax) return GM_EINVAL;
+    const size_t cnt = n * (size_t)D;
+    for (int g = 1; g < G; g++)
+      hipLaunchKernelGGL(gm_max_into, dim3(256), dim3(256), 0, st, ctxs[0]->s.status, ctxs[g]->s.status, cnt);
+    for (int g = 1; g < G; g++)
+      HIPCHECK(hipMemcpyAsync(ctxs[g]->s.status, ctxs[0]->s.status, sizeof(int32_t) * cnt, hipMemcpyDeviceToDevice, st));
+  }
+  HIPCHECK(hipGetLastError());
+  HIPCHECK(hipStreamSynchronize(st));
+  return GM_OK;
+}
+
+static int tick_sharded(gm_ctx *c) {
+  if (!c->comm) return GM_EUNSUPPORTED;  // multi-GPU ticks need gm_comm_init (or the phase API + loopback)
+  const size_t n = (size_t)c->n;
+  TRY(gm_shard_merge(c));
+  NCCLCHECK(ncclAllGather(c->s.xcnt + (size_t)c->s.shard_rank * n * 2, c->s.xcnt, n * 2, ncclInt32, c->comm, c->stream));
+  int round = 0, D = GM_D_FIRST;
+  for (;;) {
+    TRY(gm_shard_draw(c, round, D));
+    NCCLCHECK(ncclAllReduce(c->s.status, c->s.status, n * D, ncclInt32, ncclMax, c->comm, c->stream));
+    int32_t pend = 0;
+    TRY(gm_shard_accept(c, D, &pend));
+    if (pend == 0) break;
+    round++;
+    D = GM_D_MORE;
+  }
+  c->t--;  // gm_tick advances globaltime
+  TRY(gm_shard_end_tick(c));
   return GM_OK;
 }

@@ -32,4 +32,15 @@ struct SState {
   int32_t *rowstat;        // [n][4]: lists delivered, present, numfailed, targets chosen
   int32_t *targets;        // [n][GM_FANOUT]
   uint32_t *err;
+  // ---- column-sharded mode (shard_count > 1; see gm_s_draw / gm_s_accept)
+  int shard_rank, shard_count;
+  uint64_t *gpres, *gfresh;  // [n][wp/64] post-sweep presence / freshness of this shard's columns
+  uint32_t *gpre;            // [n][wp/64] exclusive prefix popcounts of gpres
+  int32_t *xcnt;             // bound exchange buffer [shard_count][n][2]: (present, numfailed) per shard
+  int32_t *status;           // bound exchange buffer [n][D]: resolved draws, MAX-allreduced
+  uint32_t *mt;              // [624][n] per-row mt19937 state, strided
+  int32_t *mtk;              // [n][3]: k, ninit, first of each row's generator
+  int32_t *acc;              // [n][8]: targets so far, g[5], numpot, size
+  int32_t *pending;          // [n] rows still drawing
+  int32_t *npending;         // rows still drawing after the last accept round
 };

@@ -29,7 +29,8 @@ __device__ __forceinline__ uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(
 // merge key of one payload word pair: hb+1, NONE (0xFFFF) -> 0
 __device__ __forceinline__ u16x2 key2(uint32_t m) { return as_u16x2(m) + (u16x2)(1); }
 
-__global__ __launch_bounds__(S_THREADS) void gm_s_tick(SState s, int t, int drop_pct) {
+template <bool SHARDED>
+__device__ __forceinline__ void gm_s_tick_body(SState &s, int t, int drop_pct) {
   extern __shared__ __align__(16) unsigned char s_smem[];
   const int wp = s.wp, nw = wp >> 6;
   uint64_t *s_pres = (uint64_t *)s_smem;               // [nw] present after the sweep
@@ -55,6 +56,10 @@ __global__ __launch_bounds__(S_THREADS) void gm_s_tick(SState s, int t, int drop
     if (tid == 0) {
       stat[0] = stat[1] = stat[2] = stat[3] = 0;
       s.ev_cnt[r] = 0;
+      if (SHARDED) {
+        int32_t *x = s.xcnt + ((size_t)s.shard_rank * s.n + r) * 2;
+        x[0] = x[1] = 0;
+      }
     }
     return;
   }
@@ -66,7 +71,7 @@ __global__ __launch_bounds__(S_THREADS) void gm_s_tick(SState s, int t, int drop
   uint32_t *trow = s.table + (size_t)r * wp;
   uint16_t *mout = s.msg[par] + (size_t)r * wp;
   const uint16_t *mprev = s.msg[par ^ 1];
-  const int selfc = r - s.c0;  // own column if this shard holds it
+  const int selfc = (r >= s.c0 && r < s.c0 + s.w) ? r - s.c0 : -1;  // own column, if in this shard
   const uint32_t tt = (uint32_t)t;
   const int t_send = t - 1;
   int npres = 0, nfail = 0;
@@ -187,6 +192,27 @@ __global__ __launch_bounds__(S_THREADS) void gm_s_tick(SState s, int t, int drop
   }
   __syncthreads();
 
+  if (SHARDED) {
+    // publish this shard's slice of the row: counts for the all-gather, bitmaps
+    // and prefix for draw resolution (gm_s_draw); the draw itself needs the
+    // whole row and runs after the exchange
+    uint64_t *gp = s.gpres + (size_t)r * nw, *gf = s.gfresh + (size_t)r * nw;
+    uint32_t *gq = s.gpre + (size_t)r * nw;
+    for (int w = tid; w < nw; w += S_THREADS) {
+      gp[w] = s_pres[w];
+      gf[w] = s_fresh[w];
+      gq[w] = s_pre[w];
+    }
+    if (tid == 0) {
+      int32_t *x = s.xcnt + ((size_t)s.shard_rank * s.n + r) * 2;
+      x[0] = size;
+      x[1] = numfailed;
+      stat[0] = k;
+      s.ev_cnt[r] = s_misc[1];
+    }
+    return;
+  }
+
   if (tid == 0) {
     // gossip-target draw on the post-sweep list (MP1Node.cpp:449-489); newNodes is
     // empty in the converged SCALED regime (no JOINREQ traffic)
@@ -222,4 +248,124 @@ __global__ __launch_bounds__(S_THREADS) void gm_s_tick(SState s, int t, int drop
     stat[3] = n;
     s.ev_cnt[r] = s_misc[1];
   }
+}
+
+__global__ __launch_bounds__(S_THREADS) void gm_s_tick(SState s, int t, int drop_pct) {
+  gm_s_tick_body<false>(s, t, drop_pct);
+}
+
+// Column-sharded phase A: merge + sweep of this shard's columns for every row.
+__global__ __launch_bounds__(S_THREADS) void gm_s_tick_shard(SState s, int t, int drop_pct) {
+  gm_s_tick_body<true>(s, t, drop_pct);
+}
+
+// Column-sharded phase B: each rank replays every live row's S2 stream (the
+// same mt19937 + Lemire sequence on every rank), and resolves the draws whose
+// rank lands in its own columns: status = (global column << 1) | fresh, else -1.
+// round 0 seeds the generators and the acceptance state from the all-gathered
+// per-shard (present, numfailed) counts.
+__global__ __launch_bounds__(256) void gm_s_draw(SState s, int t, int round, int D) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= s.n) return;
+  const int G = s.shard_count, nw = s.wp >> 6;
+  int32_t *acc = s.acc + (size_t)r * 8;
+  int32_t *mtk = s.mtk + (size_t)r * 3;
+  if (round == 0) {
+    int size = 0, nf = 0;
+    for (int g = 0; g < G; g++) {
+      size += s.xcnt[((size_t)g * s.n + r) * 2];
+      nf += s.xcnt[((size_t)g * s.n + r) * 2 + 1];
+    }
+    const int numpot = size - 1 - nf;
+    const bool live = !s.failed[r];
+    acc[0] = 0;
+    acc[6] = numpot;
+    acc[7] = size;
+    s.pending[r] = live && numpot > 0;
+    int32_t *stat = s.rowstat + (size_t)r * 4;
+    if (!live) stat[0] = 0;
+    stat[1] = live ? size : 0;
+    stat[2] = live ? nf : 0;
+    stat[3] = 0;
+    if (!s.pending[r]) return;
+    GmLazyMT mt;
+    mt.seed(s.mt + r, gm_rd_seed(s.rd_seed, t, r + 1), s.n);
+    mtk[0] = mt.k;
+    mtk[1] = mt.ninit;
+    mtk[2] = 1;
+  }
+  if (!s.pending[r]) return;
+  GmLazyMT mt;
+  mt.x = s.mt + r;
+  mt.stride = s.n;
+  mt.k = mtk[0];
+  mt.ninit = mtk[1];
+  mt.first = mtk[2] != 0;
+  const uint32_t size = (uint32_t)acc[7];
+  int32_t *st = s.status + (size_t)r * D;
+  for (int d = 0; d < D; d++) {
+    const uint32_t ix = (uint32_t)mt.uniform(size);
+    // which shard holds the ix-th present entry of row r (shards in column order)
+    uint32_t pre = 0;
+    int owner = G - 1;
+    for (int g = 0; g < G; g++) {
+      const uint32_t c = (uint32_t)s.xcnt[((size_t)g * s.n + r) * 2];
+      if (ix < pre + c) { owner = g; break; }
+      pre += c;
+    }
+    int32_t v = -1;
+    if (owner == s.shard_rank) {
+      const int cl = gm_rank_select(s.gpres + (size_t)r * nw, s.gpre + (size_t)r * nw, nw, ix - pre);
+      const int fresh = (int)((s.gfresh[(size_t)r * nw + (cl >> 6)] >> (cl & 63)) & 1ull);
+      v = ((s.c0 + cl) << 1) | fresh;
+    }
+    st[d] = v;
+  }
+  mtk[0] = mt.k;
+  mtk[1] = mt.ninit;
+  mtk[2] = mt.first ? 1 : 0;
+}
+
+// Column-sharded phase C: with every draw resolved (MAX-allreduced status), run
+// the acceptance loop of MP1Node.cpp:466-489 (skip me, skip stale, skip
+// duplicates) identically on every rank; finished rows enqueue themselves into
+// their targets' inboxes for the next tick.
+__global__ __launch_bounds__(256) void gm_s_accept(SState s, int t, int D) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= s.n || !s.pending[r]) return;
+  int32_t *acc = s.acc + (size_t)r * 8;
+  int n = acc[0];
+  const int numpot = acc[6];
+  int g[GM_FANOUT];
+  for (int q = 0; q < n; q++) g[q] = acc[1 + q];
+  const int32_t *st = s.status + (size_t)r * D;
+  bool done = false;
+  for (int d = 0; d < D && !done; d++) {
+    const int32_t v = st[d];
+    if (v < 0) { atomicOr(s.err, GM_ERR_DRAWS); done = true; break; }
+    const int c = v >> 1;
+    if (c == r) continue;        // "me"
+    if (!(v & 1)) continue;      // age >= TFAIL (skipfailed: numpot > 0 here)
+    bool dup = false;
+    for (int q = 0; q < n; q++) dup |= g[q] == c;
+    if (!dup) g[n++] = c;
+    done = n >= GM_FANOUT || n >= numpot;
+  }
+  for (int q = 0; q < n; q++) acc[1 + q] = g[q];
+  acc[0] = n;
+  if (!done) {
+    atomicAdd(s.npending, 1);
+    return;
+  }
+  s.pending[r] = 0;
+  const int par = t & 1;
+  int32_t *cnt_out = s.inbox_cnt[par ^ 1];
+  for (int q = 0; q < n; q++) {
+    const int dst = g[q];
+    s.targets[(size_t)r * GM_FANOUT + q] = dst;
+    const int slot = atomicAdd(&cnt_out[dst], 1);
+    if (slot < S_KMAX) s.inbox[par ^ 1][(size_t)dst * S_KMAX + slot] = r;
+    else atomicOr(s.err, GM_ERR_INBOX);
+  }
+  s.rowstat[(size_t)r * 4 + 3] = n;
 }

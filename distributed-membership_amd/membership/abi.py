@@ -33,7 +33,9 @@ class GmEvent(ctypes.Structure):
 
 EXPORTS = ["gm_parse_conf", "gm_create", "gm_destroy", "gm_tick", "gm_sync", "gm_time", "gm_rand", "gm_set_failed",
            "gm_set_dropmsg", "gm_drain_events", "gm_event_counts", "gm_msgcount", "gm_read_row", "gm_read_nodes",
-           "gm_dump_tables", "gm_tick_stats", "gm_set_timing", "gm_last_kernel_ms", "gm_crash_set", "gm_strerror"]
+           "gm_dump_tables", "gm_tick_stats", "gm_set_timing", "gm_last_kernel_ms", "gm_crash_set", "gm_strerror",
+           "gm_comm_unique_id", "gm_comm_init", "gm_shard_layout", "gm_shard_merge", "gm_shard_draw",
+           "gm_shard_accept", "gm_shard_end_tick", "gm_shard_loopback"]
 
 _lib = None
 
@@ -70,6 +72,12 @@ def load_library():
         "gm_tick_stats": [ctypes.c_void_p, P(ctypes.c_int64)],
         "gm_set_timing": [ctypes.c_void_p, i32], "gm_last_kernel_ms": [ctypes.c_void_p, P(ctypes.c_float)],
         "gm_crash_set": [i32, i32, u64, P(i32)],
+        "gm_comm_unique_id": [ctypes.c_char_p],
+        "gm_comm_init": [ctypes.c_void_p, ctypes.c_char_p, i32, i32],
+        "gm_shard_layout": [ctypes.c_void_p, P(i32), P(i32)],
+        "gm_shard_loopback": [P(ctypes.c_void_p), i32, i32, i32],
+        "gm_shard_merge": [ctypes.c_void_p], "gm_shard_draw": [ctypes.c_void_p, i32, i32],
+        "gm_shard_accept": [ctypes.c_void_p, i32, P(i32)], "gm_shard_end_tick": [ctypes.c_void_p],
     }
     for name, args in sig.items():
         fn = getattr(lib, name)
@@ -210,3 +218,42 @@ class Simulator:
         v = ctypes.c_float()
         self._call("gm_last_kernel_ms", self.h, ctypes.byref(v))
         return float(v.value)
+
+    # ---- column shards (SCALED multi-GPU; see membership.sharded)
+    def comm_init(self, uid, nranks, rank):
+        self._call("gm_comm_init", self.h, uid, nranks, rank)
+
+    def shard_layout(self):
+        c0, w = ctypes.c_int32(), ctypes.c_int32()
+        self._call("gm_shard_layout", self.h, ctypes.byref(c0), ctypes.byref(w))
+        return c0.value, w.value
+
+    def shard_merge(self):
+        self._call("gm_shard_merge", self.h)
+
+    def shard_draw(self, rnd, d):
+        self._call("gm_shard_draw", self.h, rnd, d)
+
+    def shard_accept(self, d):
+        v = ctypes.c_int32()
+        self._call("gm_shard_accept", self.h, d, ctypes.byref(v))
+        return v.value
+
+    def shard_end_tick(self):
+        self._call("gm_shard_end_tick", self.h)
+
+
+def comm_unique_id():
+    """ncclGetUniqueId (RCCL) as 128 bytes, to broadcast to every rank."""
+    buf = ctypes.create_string_buffer(128)
+    rc = load_library().gm_comm_unique_id(buf)
+    if rc:
+        raise GmError(rc, "gm_comm_unique_id")
+    return buf.raw
+
+
+def shard_loopback(sims, what, d=0):
+    arr = (ctypes.c_void_p * len(sims))(*[s.h for s in sims])
+    rc = load_library().gm_shard_loopback(arr, len(sims), what, d)
+    if rc:
+        raise GmError(rc, "gm_shard_loopback")

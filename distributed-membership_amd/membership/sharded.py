@@ -1,0 +1,70 @@
+"""Column-sharded SCALED ticks: multi-GPU (one rank per GPU, RCCL inside libgm)
+or several shards of one device (in-process loopback collectives).
+
+The N x N membership table is split by SUBJECT column: rank g owns columns
+[c0_g, c0_g + w_g) of every observer row. The merge + sweep of a delivered
+gossip list touches only local columns, so no gossip payload ever crosses a
+GPU boundary. What does cross is the gossip-target draw of MP1Node.cpp:449-489,
+which indexes the whole post-sweep row ("memberlist[ix]"). Per tick:
+
+  1. every rank merges/sweeps its columns             (gm_shard_merge)
+  2. all-gather of per-row (present, numfailed)       int32[G][N][2]
+  3. every rank replays every row's S2 stream and resolves the draws landing
+     in its columns                                   (gm_shard_draw)
+  4. MAX-allreduce of the resolved draws              int32[N][D]
+  5. every rank runs the acceptance loop identically  (gm_shard_accept);
+     rows that ran out of draws repeat 3-5 with more draws
+after which every rank holds identical inboxes for the next tick. With RCCL
+attached (gm_comm_init) gm_tick runs all of this natively; loopback_tick
+drives the same phases for G contexts living on one device.
+"""
+import os
+
+from .abi import GM_MODE_SCALED, Simulator, comm_unique_id, shard_loopback
+
+D_FIRST = 16  # must match GM_D_FIRST in gm_host.hip
+D_MORE = 64   # must match GM_D_MORE
+
+
+def loopback_tick(sims):
+    """One tick of G in-process shard contexts (one device); returns the draw rounds used."""
+    for s in sims:
+        s.shard_merge()
+    shard_loopback(sims, 0)
+    rnd, d = 0, D_FIRST
+    while True:
+        for s in sims:
+            s.shard_draw(rnd, d)
+        shard_loopback(sims, 1, d)
+        pend = [s.shard_accept(d) for s in sims]
+        if any(p != pend[0] for p in pend):
+            raise RuntimeError(f"shards disagree on pending rows: {pend}")
+        if pend[0] == 0:
+            break
+        rnd, d = rnd + 1, D_MORE
+    for s in sims:
+        s.shard_end_tick()
+    return rnd + 1
+
+
+def rendezvous_uid(rank, world):
+    """Share an RCCL unique id over the CPU (gloo) process group torchrun set up."""
+    import torch.distributed as dist
+    obj = [comm_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    return obj[0]
+
+
+def distributed_shard(n, rank, world, local_rank, **kw):
+    """This rank's column shard of an n-node cluster, with RCCL attached.
+
+    Expects torch.distributed initialised with the gloo backend (CPU only: the
+    GPU is driven by libgm alone, so torch never initialises HIP here)."""
+    sim = Simulator(n, GM_MODE_SCALED, shard_rank=rank, shard_count=world, device=local_rank, **kw)
+    sim.comm_init(rendezvous_uid(rank, world), world, rank)
+    return sim
+
+
+def env_ranks():
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+            int(os.environ.get("LOCAL_RANK", "0")))

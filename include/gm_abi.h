@@ -149,6 +149,24 @@ int gm_tick_stats(gm_ctx *ctx, int64_t stats[4]);
 int gm_set_timing(gm_ctx *ctx, int32_t on);
 int gm_last_kernel_ms(gm_ctx *ctx, float *ms);
 
+/* ---- SCALED column sharding (multi-GPU). A context with shard_count = G > 1
+ * owns subject columns [c0, c0 + w) of every observer row (one context per GPU).
+ * Once RCCL is attached (gm_comm_init, same unique id on every rank), gm_tick
+ * runs the sharded tick: merge/sweep own columns -> ncclAllGather of per-row
+ * (present, numfailed) -> rounds of {draw + resolve own-column draws ->
+ * ncclAllReduce(MAX) of resolved draws -> acceptance} until every row has its
+ * gossip targets. No gossip payload crosses GPUs. The phase functions expose
+ * the same steps for G contexts on one device (gm_shard_loopback collectives). */
+int gm_comm_unique_id(uint8_t *out128);   /* ncclGetUniqueId, on one rank */
+int gm_comm_init(gm_ctx *ctx, const uint8_t *id128, int32_t nranks, int32_t rank);
+int gm_shard_layout(gm_ctx *ctx, int32_t *c0, int32_t *w);
+int gm_shard_merge(gm_ctx *ctx);
+int gm_shard_draw(gm_ctx *ctx, int32_t round, int32_t D);
+int gm_shard_accept(gm_ctx *ctx, int32_t D, int32_t *npending);
+int gm_shard_end_tick(gm_ctx *ctx);
+/* what = 0: all-gather the per-row counts; what = 1: MAX-allreduce the first n*D draws */
+int gm_shard_loopback(gm_ctx **ctxs, int32_t G, int32_t what, int32_t D);
+
 /* Crash set of the SCALED fault schedule: `count` node indices, ascending,
  * chosen by a splitmix64-keyed permutation of [0, n) (host fault injection). */
 int gm_crash_set(int32_t n, int32_t count, uint64_t seed, int32_t *out);

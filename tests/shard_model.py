@@ -1,0 +1,140 @@
+"""A numpy model of the column-sharded SCALED tick (membership/sharded.py,
+gm_s_tick_shard / gm_s_draw / gm_s_accept) -- TEST INFRASTRUCTURE.
+
+Each instance owns subject columns [c0, c0+w) of every row and talks to the
+other shards only through the two collectives of the protocol (all-gather of
+per-row (present, numfailed), MAX-allreduce of resolved draws), supplied as
+callables -- torch.distributed gloo in the multi-process CPU test. The S2
+stream comes from the oracle's mt19937 + Lemire restatement."""
+import numpy as np
+
+import oracle_py
+
+TFAIL, TREMOVE, FANOUT = 5, 20, 5
+M64 = (1 << 64) - 1
+
+
+def mix64(z):
+    z &= M64
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M64
+    return z ^ (z >> 31)
+
+
+class ShardModel:
+    def __init__(self, n, rank, world, rd_seed=7, drop_pct=0, drop_from=0, drop_to=0, drop_seed=0):
+        self.n, self.rank, self.world = n, rank, world
+        self.c0 = n * rank // world
+        self.w = n * (rank + 1) // world - self.c0
+        self.hb = np.zeros((n, self.w), np.int64)
+        self.ts = np.zeros((n, self.w), np.int64)         # converged start: all present at {0, 0}
+        self.pay = np.full((n, self.w), -1, np.int64)     # payload plane of the previous tick
+        self.inbox = [[] for _ in range(n)]
+        self.hbctr = np.zeros(n, np.int64)
+        self.failed = np.zeros(n, bool)
+        self.rd_seed, self.drop = rd_seed, (drop_pct, drop_from, drop_to, drop_seed)
+        self.t = 1
+        self.events = []
+
+    def _dropped(self, t_send, s, r, col):
+        pct, lo, hi, seed = self.drop
+        if pct <= 0 or not (lo <= t_send < hi):
+            return False
+        pair = mix64(seed ^ (t_send << 48) ^ (s << 24) ^ r)
+        return ((mix64(pair + col) >> 32) % 100) < pct
+
+    def tick(self, all_gather, all_reduce_max):
+        n, t, w, c0 = self.n, self.t, self.w, self.c0
+        present = self.ts >= 0
+        new_pay = np.full((n, w), -1, np.int64)
+        counts = np.zeros((n, 2), np.int64)
+        fresh = np.zeros((n, w), bool)
+        self.events = []
+        for r in range(n):
+            if self.failed[r]:
+                continue
+            key = np.full(w, -1, np.int64)
+            for s in self.inbox[r]:
+                for j in range(w):
+                    v = self.pay[s, j]
+                    if v >= 0 and not self._dropped(t - 1, s, r, c0 + j):
+                        key[j] = max(key[j], v)
+            for j in range(w):
+                if key[j] >= 0:
+                    if not present[r, j]:
+                        self.hb[r, j], self.ts[r, j] = key[j], t
+                        present[r, j] = True
+                        self.events.append((t, r, 1, c0 + j + 1))
+                    elif key[j] > self.hb[r, j]:
+                        self.hb[r, j], self.ts[r, j] = key[j], t
+            if c0 <= r < c0 + w:
+                self.hbctr[r] += 1
+                self.hb[r, r - c0], self.ts[r, r - c0] = self.hbctr[r], t
+                self.hbctr[r] += 1
+            nf = 0
+            for j in range(w):
+                if not present[r, j]:
+                    continue
+                age = t - self.ts[r, j]
+                if age >= TFAIL:
+                    nf += 1
+                    if age >= TREMOVE:
+                        present[r, j] = False
+                        self.ts[r, j] = self.hb[r, j] = -1
+                        self.events.append((t, r, 2, c0 + j + 1))
+                        continue
+                else:
+                    fresh[r, j] = True
+                    new_pay[r, j] = self.hb[r, j]
+            counts[r] = (present[r].sum(), nf)
+        allc = all_gather(counts)                       # [world][n][2]
+        size = allc[:, :, 0].sum(0)
+        numpot = size - 1 - allc[:, :, 1].sum(0)
+        cols = [np.nonzero(present[r])[0] for r in range(n)]
+        drawn = {r: 0 for r in range(n) if not self.failed[r] and numpot[r] > 0}
+        acc = {r: [] for r in drawn}
+        targets = {r: [] for r in range(n)}
+        d = 16
+        while drawn:
+            status = np.full((n, d), -1, np.int64)
+            for r in drawn:
+                ix = oracle_py.mt_uniform(oracle_py.lib().oc_rd_seed(self.rd_seed, t, r + 1), int(size[r]),
+                                          drawn[r] + d)[drawn[r]:]
+                for k, x in enumerate(ix):
+                    pre = 0
+                    for g in range(self.world):
+                        if x < pre + allc[g, r, 0]:
+                            break
+                        pre += allc[g, r, 0]
+                    if g == self.rank:
+                        j = cols[r][x - pre]
+                        status[r, k] = ((c0 + j) << 1) | int(fresh[r, j])
+            status = all_reduce_max(status)
+            done = []
+            for r in drawn:
+                for k in range(d):
+                    v = int(status[r, k])
+                    assert v >= 0
+                    c = v >> 1
+                    if c == r or not (v & 1) or c in acc[r]:
+                        continue
+                    acc[r].append(c)
+                    if len(acc[r]) >= FANOUT or len(acc[r]) >= numpot[r]:
+                        break
+                drawn[r] += d
+                if len(acc[r]) >= FANOUT or len(acc[r]) >= numpot[r]:
+                    done.append(r)
+            for r in done:
+                targets[r] = acc.pop(r)
+                del drawn[r]
+            d = 64
+        self.inbox = [[] for _ in range(n)]
+        for r in range(n):
+            for c in targets[r]:
+                self.inbox[c].append(r)
+        self.pay = new_pay
+        self.t += 1
+
+    def row(self, r):
+        hb = np.where(self.ts[r] >= 0, self.hb[r], -1)
+        return hb, self.ts[r].copy()

@@ -1,0 +1,53 @@
+"""Column-sharded SCALED ticks (the multi-GPU path) on one GPU: G shard contexts
+in one process exchange through the in-process loopback collectives and must
+reproduce the single-context fused kernel -- tables, node state and events --
+tick for tick (crash set, keyed drops, converged-start transient included)."""
+import numpy as np
+import pytest
+
+from membership import GM_MODE_SCALED, Simulator, crash_set
+from membership.sharded import loopback_tick
+
+pytestmark = pytest.mark.gpu
+
+
+def merge_dumps(dumps, owners):
+    """Combine per-shard dumps (same rows, disjoint column ranges) into one dump."""
+    per = [d.decode().splitlines() for d in dumps]
+    out = []
+    for i, lines in enumerate(zip(*per)):
+        toks = [ln.split(" ") for ln in lines]
+        head = toks[owners[i]][:6]
+        n = sum(int(t[6]) for t in toks)
+        ents = [e for t in toks for e in t[7:]]
+        out.append(" ".join(head + [str(n)] + ents))
+    return ("\n".join(out) + "\n").encode()
+
+
+@pytest.mark.parametrize("n,world,drop", [(256, 2, 0), (600, 3, 0), (512, 2, 25), (1100, 4, 10)])
+def test_shards_match_fused_kernel(n, world, drop):
+    kw = dict(rd_seed=7, drop_pct=drop, drop_from=3, drop_to=25, drop_seed=42)
+    ref = Simulator(n, GM_MODE_SCALED, **kw)
+    shards = [Simulator(n, GM_MODE_SCALED, shard_rank=g, shard_count=world, **kw) for g in range(world)]
+    owners = np.zeros(n, dtype=int)
+    for g, s in enumerate(shards):
+        c0, w = s.shard_layout()
+        owners[c0:c0 + w] = g
+    crash = crash_set(n, max(2, n // 64), 42)
+    for _ in range(36):
+        t = ref.time
+        ref.tick()
+        loopback_tick(shards)
+        if t == 6:
+            ref.set_failed(crash)
+            for s in shards:
+                s.set_failed(crash)
+        assert all(s.time == ref.time for s in shards)
+        ev = sorted(e for s in shards for e in s.drain_events())
+        assert ev == sorted(ref.drain_events()), f"events differ at tick {t}"
+        got = merge_dumps([s.dump_tables() for s in shards], owners)
+        assert got == ref.dump_tables(), f"tables differ at tick {t}"
+    for s in shards:
+        st = s.tick_stats()
+        assert st["err"] == 0
+        assert st["lists"] == ref.tick_stats()["lists"]
