@@ -13,7 +13,7 @@ from membership import GM_EV_JOINED, GM_EV_REMOVED, GM_MODE_SCALED, Simulator, c
 pytestmark = pytest.mark.gpu
 
 
-def run_pair(n, ticks, crash_tick, crash_count, drop_pct=0, drop_from=0, drop_to=0, rd_seed=7, seed=42):
+def run_pair(n, ticks, crash_tick, crash_count, drop_pct=0, drop_from=0, drop_to=0, rd_seed=7, seed=42, seen=None):
     ora = oracle_py.Oracle(n, oracle_py.OC_SCALED, rd_seed=rd_seed, crash_tick=crash_tick, crash_count=crash_count,
                            crash_seed=seed, drop_pct=drop_pct, drop_from=drop_from, drop_to=drop_to, drop_seed=seed)
     sim = Simulator(n, GM_MODE_SCALED, rd_seed=rd_seed, drop_pct=drop_pct, drop_from=drop_from, drop_to=drop_to,
@@ -30,6 +30,9 @@ def run_pair(n, ticks, crash_tick, crash_count, drop_pct=0, drop_from=0, drop_to
             sim.set_failed(crash)
         ev_g = [(e[0], e[1], kinds[e[2]], e[3]) for e in sim.drain_events()]
         assert ev_g == ora.events(), f"events differ at tick {t}"
+        if seen is not None:
+            for e in ev_g:
+                seen[e[2]] = seen.get(e[2], 0) + 1
         assert digest64(sim.dump_tables()) == digest64(ora.dump()), f"tables differ at tick {t}"
     st = sim.tick_stats()
     assert st["err"] == 0
@@ -47,8 +50,10 @@ def test_scaled_with_drops_matches_oracle(n):
 
 
 def test_scaled_heavy_drop_false_removals_match():
-    # 60% loss makes entries go stale and get removed/re-added: exercises ADD events
-    sim, ora = run_pair(96, 60, crash_tick=-1, crash_count=0, drop_pct=60, drop_from=2, drop_to=60)
+    # heavy loss makes entries go stale, get removed and re-join: exercises ADD events
+    seen = {}
+    run_pair(96, 60, crash_tick=-1, crash_count=0, drop_pct=85, drop_from=2, drop_to=60, seen=seen)
+    assert seen.get(1, 0) > 0 and seen.get(2, 0) > 0, seen
 
 
 def test_scaled_invariants_large():
