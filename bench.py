@@ -7,11 +7,13 @@ A "step" is one globaltime tick of the whole cluster (Application::mp1Run for
 all N nodes: merge delivered gossip lists, heartbeat bump, TFAIL/TREMOVE sweep,
 gossip-target draw, delivery to next tick's inboxes), state resident in HBM.
 
-Scenario S-A: converged start (every observer holds every subject), fanout 5,
+Scenario S-A: converged start (every observer holds every subject; the warm
+variant of gm_abi.h init_mode 1 at t0 = 8, i.e. entries 0-3 ticks old as if the
+cluster had been gossiping, so there is no mass-staleness transient), fanout 5,
 TFAIL 5, TREMOVE 20, RD_SEED 7, 1% of the nodes (655) crash at the end of tick
-10 (splitmix64-keyed crash set, seed 42), no drops. A fixed 25-tick prologue
-(T_warm of S-A) brings the cluster to steady state with the crash's removals
-still ahead; then W warmup ticks, then exactly K timed ticks.
+10 (splitmix64-keyed crash set, seed 42), no drops. The prologue runs to tick
+25 (T_warm of S-A); then W warmup ticks, then exactly K timed ticks, which
+contain the crashed nodes' TREMOVE removals (~42 M events).
 
 Multi-GPU (--gpus G via torch.distributed.run, one rank per GPU): the same
 N = 65,536 cluster with its N x N table sharded by subject column, rank g
@@ -62,8 +64,9 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--n", type=int, default=65536)
+    p.add_argument("--cluster", type=int, default=65536, help="N, simulated nodes")
     p.add_argument("--prologue", type=int, default=25)
+    p.add_argument("--t0", type=int, default=8, help="warm converged start at tick t0 (0: cold start)")
     p.add_argument("--crash-tick", type=int, default=10)
     p.add_argument("--crash-frac", type=float, default=0.01)
     p.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -78,6 +81,14 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if "GM_DEVICE_OVERRIDE" in os.environ:  # diagnostics only: pin every rank to one device
+        local = int(os.environ["GM_DEVICE_OVERRIDE"])
+    # libgm first: it binds the system ROCm HIP runtime and RCCL it was built
+    # against before torch (CPU-only here) brings its own copies into the process
+    from membership import GM_MODE_SCALED, Simulator, crash_set, load_library
+    from membership.sharded import distributed_shard
+    load_library()
+
     dist = None
     if world > 1:
         # CPU-only process group: rendezvous, barrier and max-over-ranks timing.
@@ -86,15 +97,13 @@ def main():
         tdist.init_process_group("gloo")
         dist = tdist
 
-    from membership import GM_MODE_SCALED, Simulator, crash_set
-    from membership.sharded import distributed_shard
-
-    n = a.n
+    n = a.cluster
     ncrash = int(round(n * a.crash_frac))
+    init = dict(init_mode=1 if a.t0 > 0 else 0, init_t0=a.t0, init_seed=11)
     if world > 1:
-        sim = distributed_shard(n, rank, world, local, rd_seed=7)
+        sim = distributed_shard(n, rank, world, local, rd_seed=7, **init)
     else:
-        sim = Simulator(n, GM_MODE_SCALED, rd_seed=7, device=local)
+        sim = Simulator(n, GM_MODE_SCALED, rd_seed=7, device=local, **init)
     crash = crash_set(n, ncrash, 42)
     while sim.time <= a.prologue:
         t = sim.time
@@ -161,11 +170,11 @@ def main():
         "dtype": "u16",
         "data": "synthetic (converged full-membership table, seeded crash set)",
         "config": {"workload": "S-A: SCALED full membership, 1% crash at tick 10, fanout 5, TFAIL 5, TREMOVE 20",
-                   "n": n, "prologue_ticks": a.prologue, "crashed": ncrash, "live": n_live,
+                   "n": n, "start": f"warm t0={a.t0}" if a.t0 > 0 else "cold", "prologue_to_tick": a.prologue, "crashed": ncrash, "live": n_live,
                    "lists_per_tick": m_lists, "parallelism": f"column-shard x{world}" if world > 1 else "single GPU"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                      "frac": (achieved / PEAK_HBM_GBPS) if achieved else None, "traffic": traffic,
-                     "kernel": "gm_s_tick_shard" if world > 1 else "gm_s_tick", "kernel_ms": kernel_ms,
+                     "kernel": "gm_s_tick_shard" if world > 1 else "gm_s_tick_nt", "kernel_ms": kernel_ms,
                      "alg_bytes_per_launch": b_alg, "survey_int32_bytes_per_launch": b_survey,
                      "columns_per_gpu": W},
     }

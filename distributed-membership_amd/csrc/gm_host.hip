@@ -22,9 +22,11 @@ __global__ void gm_f_recv(FState s, int t);
 __global__ void gm_f_node(FState s, int t);
 __global__ void gm_f_send(FState s, int t);
 __global__ void gm_s_tick(SState s, int t, int drop_pct);
+__global__ void gm_s_tick_nt(SState s, int t, int drop_pct);
 __global__ void gm_s_tick_shard(SState s, int t, int drop_pct);
 __global__ void gm_s_draw(SState s, int t, int round, int D);
 __global__ void gm_s_accept(SState s, int t, int D);
+__global__ void gm_s_init(SState s, int warm, int t0, uint64_t seed);
 
 #define GM_T_LIMIT 32766  // packed 16-bit hb/ts stay exact: hb <= 2t+1 < 0xFFFF
 
@@ -35,6 +37,7 @@ struct gm_ctx {
   ncclComm_t comm = nullptr;         // RCCL communicator across column shards
   hipEvent_t k0 = nullptr, k1 = nullptr;  // per-tick merge-kernel events (sharded)
   double kernel_ms_sum = 0;
+  bool nt = true;                    // non-temporal table streams (env GM_NT=0 to disable)
   int t = 0;
   int n = 0;
   int dropmsg = 0;
@@ -93,7 +96,7 @@ extern "C" const char *gm_strerror(int code) {
     case GM_ERANGE: return "bounded resource overflowed";
     case GM_ESTATE: return "protocol invariant violated";
     case GM_EUNSUPPORTED: return "unsupported configuration";
-    case GM_ECOMM: return "collective failure";
+    case GM_ECOMM: return g_errbuf[0] ? g_errbuf : "collective failure";
     default: return "unknown error";
   }
 }
@@ -216,8 +219,19 @@ static int create_scaled(gm_ctx *c) {
   s.drop_seed = c->cfg.drop_seed;
   const size_t cells = (size_t)n * s.wp;
   TRY(dalloc(c, &s.table, cells));
-  TRY(dalloc(c, &s.msg[0], cells));
-  TRY(dalloc(c, &s.msg[1], cells));
+  // both parities of a row's payload sit next to each other (one allocation), so
+  // even and odd ticks see the same address pattern (env GM_MSG_SEPARATE=1: two planes)
+  const bool sep = getenv("GM_MSG_SEPARATE") && atoi(getenv("GM_MSG_SEPARATE"));
+  c->nt = !(getenv("GM_NT") && !atoi(getenv("GM_NT")));  // default on (A/B: +1 %)
+  if (sep) {
+    TRY(dalloc(c, &s.msg[0], cells));
+    TRY(dalloc(c, &s.msg[1], cells));
+    s.mstride = s.wp;
+  } else {
+    TRY(dalloc(c, &s.msg[0], 2 * cells));
+    s.msg[1] = s.msg[0] + s.wp;
+    s.mstride = 2 * (size_t)s.wp;
+  }
   for (int p = 0; p < 2; p++) {
     TRY(dalloc(c, &s.inbox_cnt[p], n));
     TRY(dalloc(c, &s.inbox[p], (size_t)n * S_KMAX));
@@ -231,15 +245,21 @@ static int create_scaled(gm_ctx *c) {
   TRY(dalloc(c, &s.rowstat, (size_t)n * 4));
   TRY(dalloc(c, &s.targets, (size_t)n * GM_FANOUT));
   TRY(dalloc(c, &s.err, 1));
-  // converged start: every observer holds every subject at {hb 0, ts 0}; padding absent
-  HIPCHECK(hipMemset(s.table, 0, sizeof(uint32_t) * cells));
-  if (s.wp > s.w)
-    HIPCHECK(hipMemset2D(s.table + s.w, sizeof(uint32_t) * s.wp, 0xFF, sizeof(uint32_t) * (s.wp - s.w), n));
-  HIPCHECK(hipMemset(s.msg[0], 0xFF, sizeof(uint16_t) * cells));
-  HIPCHECK(hipMemset(s.msg[1], 0xFF, sizeof(uint16_t) * cells));
+  // converged start (cold or warm, gm_config.init_mode); padding columns absent
+  const bool warm = c->cfg.init_mode == 1;
+  const int t0 = warm ? c->cfg.init_t0 : 0;
+  if (c->cfg.init_mode < 0 || c->cfg.init_mode > 1 || (warm && (t0 < 5 || t0 > GM_T_LIMIT / 2))) return GM_EINVAL;
+  if (sep) {
+    HIPCHECK(hipMemset(s.msg[0], 0xFF, sizeof(uint16_t) * cells));
+    HIPCHECK(hipMemset(s.msg[1], 0xFF, sizeof(uint16_t) * cells));
+  } else {
+    HIPCHECK(hipMemset(s.msg[0], 0xFF, sizeof(uint16_t) * 2 * cells));
+  }
   for (int p = 0; p < 2; p++) HIPCHECK(hipMemset(s.inbox_cnt[p], 0, sizeof(int32_t) * n));
-  HIPCHECK(hipMemset(s.hbctr, 0, sizeof(int32_t) * n));
   HIPCHECK(hipMemset(s.failed, 0, sizeof(int32_t) * n));
+  hipLaunchKernelGGL(gm_s_init, dim3(n), dim3(256), 0, c->stream, s, warm ? 1 : 0, t0, c->cfg.init_seed);
+  HIPCHECK(hipGetLastError());
+  HIPCHECK(hipStreamSynchronize(c->stream));
   HIPCHECK(hipMemset(s.ev_cnt, 0, sizeof(int32_t) * n));
   HIPCHECK(hipMemset(s.ev_spill_cnt, 0, sizeof(uint32_t)));
   HIPCHECK(hipMemset(s.rowstat, 0, sizeof(int32_t) * n * 4));
@@ -261,7 +281,7 @@ static int create_scaled(gm_ctx *c) {
     HIPCHECK(hipMemset(s.xcnt, 0, sizeof(int32_t) * (size_t)G * n * 2));
   }
   c->s_smem = (size_t)nw * 8 * 2 + (size_t)nw * 4 + 624 * 4 + (S_KMAX + 16 + 8) * 4;
-  c->t = 1;  // the converged table is the state "as of tick 0"
+  c->t = t0 + 1;  // the converged table is the state "as of tick t0"
   return GM_OK;
 }
 
@@ -355,8 +375,8 @@ static int tick_scaled(gm_ctx *c) {
   const int t_send = c->t - 1;
   const bool drop = c->cfg.drop_pct > 0 && t_send >= c->cfg.drop_from && t_send < c->cfg.drop_to;
   if (c->timing && c->timed_ticks == 0) HIPCHECK(hipEventRecord(c->e0, c->stream));
-  hipLaunchKernelGGL(gm_s_tick, dim3(c->n), dim3(S_THREADS), c->s_smem, c->stream, c->s, c->t,
-                     drop ? c->cfg.drop_pct : -1);
+  hipLaunchKernelGGL(c->nt ? gm_s_tick_nt : gm_s_tick, dim3(c->n), dim3(S_THREADS), c->s_smem, c->stream, c->s,
+                     c->t, drop ? c->cfg.drop_pct : -1);
   if (c->timing) {
     HIPCHECK(hipEventRecord(c->e1, c->stream));
     c->timed_ticks++;

@@ -20,7 +20,8 @@ struct SState {
   uint32_t ev_spill_cap;
   uint64_t rd_seed, drop_seed;
   uint32_t *table;         // [n][wp] packed {hb | ts<<16}, GM_ABSENT
-  uint16_t *msg[2];        // [n][wp] gossip payload planes, indexed by tick parity
+  uint16_t *msg[2];        // gossip payload planes, indexed by tick parity; row r at msg[p] + r*mstride
+  size_t mstride;          // row stride of the payload planes (2*wp: both parities of a row adjacent)
   int32_t *inbox_cnt[2];   // [n] lists queued for each receiver, by delivery-tick parity
   int32_t *inbox[2];       // [n][S_KMAX] sender rows
   int32_t *hbctr;          // [n] MP1Node heartbeat counter (Member::heartbeat)

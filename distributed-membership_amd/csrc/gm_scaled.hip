@@ -29,7 +29,22 @@ __device__ __forceinline__ uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(
 // merge key of one payload word pair: hb+1, NONE (0xFFFF) -> 0
 __device__ __forceinline__ u16x2 key2(uint32_t m) { return as_u16x2(m) + (u16x2)(1); }
 
-template <bool SHARDED>
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// 16-byte row-stream accesses, optionally non-temporal (A/B variant)
+template <bool NT>
+__device__ __forceinline__ uint4 ld(const uint4 *p) {
+  u32x4 v = NT ? __builtin_nontemporal_load((const u32x4 *)p) : *(const u32x4 *)p;
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+template <bool NT>
+__device__ __forceinline__ void st(uint4 *p, uint4 v) {
+  u32x4 w = {v.x, v.y, v.z, v.w};
+  if (NT) __builtin_nontemporal_store(w, (u32x4 *)p);
+  else *(u32x4 *)p = w;
+}
+
+template <bool SHARDED, bool NT>
 __device__ __forceinline__ void gm_s_tick_body(SState &s, int t, int drop_pct) {
   extern __shared__ __align__(16) unsigned char s_smem[];
   const int wp = s.wp, nw = wp >> 6;
@@ -69,23 +84,24 @@ __device__ __forceinline__ void gm_s_tick_body(SState &s, int t, int drop_pct) {
   __syncthreads();
 
   uint32_t *trow = s.table + (size_t)r * wp;
-  uint16_t *mout = s.msg[par] + (size_t)r * wp;
+  uint16_t *mout = s.msg[par] + (size_t)r * s.mstride;
   const uint16_t *mprev = s.msg[par ^ 1];
+  const size_t ms = s.mstride;
   const int selfc = (r >= s.c0 && r < s.c0 + s.w) ? r - s.c0 : -1;  // own column, if in this shard
   const uint32_t tt = (uint32_t)t;
   const int t_send = t - 1;
   int npres = 0, nfail = 0;
 
   for (int base = tid * S_COLS_PER_THREAD; base < wp; base += S_COLS_PER_STEP) {
-    const uint4 ta = *(const uint4 *)(trow + base);
-    const uint4 tb = *(const uint4 *)(trow + base + 4);
+    const uint4 ta = ld<NT>((const uint4 *)(trow + base));
+    const uint4 tb = ld<NT>((const uint4 *)(trow + base + 4));
     u16x2 k0 = (u16x2)(0), k1 = (u16x2)(0), k2 = (u16x2)(0), k3 = (u16x2)(0);
     if (drop_pct < 0) {
       for (int j0 = 0; j0 < k; j0 += 8) {
         uint4 m[8];
 #pragma unroll
         for (int u = 0; u < 8; u++) {
-          if (j0 + u < k) m[u] = *(const uint4 *)(mprev + (size_t)s_send[j0 + u] * wp + base);
+          if (j0 + u < k) m[u] = *(const uint4 *)(mprev + (size_t)s_send[j0 + u] * ms + base);
           else m[u] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
         }
 #pragma unroll
@@ -101,7 +117,7 @@ __device__ __forceinline__ void gm_s_tick_body(SState &s, int t, int drop_pct) {
       uint32_t kk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
       for (int j = 0; j < k; j++) {
         const int snd = s_send[j];
-        const uint4 m = *(const uint4 *)(mprev + (size_t)snd * wp + base);
+        const uint4 m = *(const uint4 *)(mprev + (size_t)snd * ms + base);
         const uint32_t mw[4] = {m.x, m.y, m.z, m.w};
         const uint64_t pair = gm_mix64(s.drop_seed ^ ((uint64_t)(uint32_t)t_send << 48) ^
                                        ((uint64_t)(uint32_t)snd << 24) ^ (uint64_t)(uint32_t)r);
@@ -168,9 +184,9 @@ __device__ __forceinline__ void gm_s_tick_body(SState &s, int t, int drop_pct) {
       }
     }
     npres += __builtin_popcount(pbits);
-    *(uint4 *)(trow + base) = make_uint4(e[0], e[1], e[2], e[3]);
-    *(uint4 *)(trow + base + 4) = make_uint4(e[4], e[5], e[6], e[7]);
-    *(uint4 *)(mout + base) = make_uint4(out[0], out[1], out[2], out[3]);
+    st<NT>((uint4 *)(trow + base), make_uint4(e[0], e[1], e[2], e[3]));
+    st<NT>((uint4 *)(trow + base + 4), make_uint4(e[4], e[5], e[6], e[7]));
+    st<NT>((uint4 *)(mout + base), make_uint4(out[0], out[1], out[2], out[3]));
     ((uint8_t *)s_pres)[base >> 3] = (uint8_t)pbits;
     ((uint8_t *)s_fresh)[base >> 3] = (uint8_t)fbits;
   }
@@ -251,12 +267,16 @@ __device__ __forceinline__ void gm_s_tick_body(SState &s, int t, int drop_pct) {
 }
 
 __global__ __launch_bounds__(S_THREADS) void gm_s_tick(SState s, int t, int drop_pct) {
-  gm_s_tick_body<false>(s, t, drop_pct);
+  gm_s_tick_body<false, false>(s, t, drop_pct);
+}
+// same, with non-temporal table / payload-write streams (default; GM_NT=0 selects gm_s_tick)
+__global__ __launch_bounds__(S_THREADS) void gm_s_tick_nt(SState s, int t, int drop_pct) {
+  gm_s_tick_body<false, true>(s, t, drop_pct);
 }
 
 // Column-sharded phase A: merge + sweep of this shard's columns for every row.
 __global__ __launch_bounds__(S_THREADS) void gm_s_tick_shard(SState s, int t, int drop_pct) {
-  gm_s_tick_body<true>(s, t, drop_pct);
+  gm_s_tick_body<true, false>(s, t, drop_pct);
 }
 
 // Column-sharded phase B: each rank replays every live row's S2 stream (the
@@ -368,4 +388,27 @@ __global__ __launch_bounds__(256) void gm_s_accept(SState s, int t, int D) {
     else atomicOr(s.err, GM_ERR_INBOX);
   }
   s.rowstat[(size_t)r * 4 + 3] = n;
+}
+
+// SCALED initial state (gm_config.init_mode): every observer holds every subject.
+// Cold: {hb 0, ts 0}. Warm at t0: own entry {2*t0-1, t0}; others {2*(t0-1-a)-1,
+// t0-a}, a = splitmix64(seed ^ r<<32 ^ c) % 4 -- values as if the cluster had been
+// gossiping, so the first ticks carry no mass-staleness transient. Padding absent.
+__global__ void gm_s_init(SState s, int warm, int t0, uint64_t seed) {
+  const int r = blockIdx.x;
+  uint32_t *row = s.table + (size_t)r * s.wp;
+  for (int j = threadIdx.x; j < s.wp; j += blockDim.x) {
+    uint32_t e = GM_ABSENT;
+    if (j < s.w) {
+      const int c = s.c0 + j;
+      if (!warm) e = gm_pack(0, 0);
+      else if (c == r) e = gm_pack((uint32_t)(2 * t0 - 1), (uint32_t)t0);
+      else {
+        const int a = (int)((gm_mix64(seed ^ ((uint64_t)(uint32_t)r << 32) ^ (uint64_t)(uint32_t)c) >> 40) % 4);
+        e = gm_pack((uint32_t)(2 * (t0 - 1 - a) - 1), (uint32_t)(t0 - a));
+      }
+    }
+    row[j] = e;
+  }
+  if (threadIdx.x == 0) s.hbctr[r] = warm ? 2 * t0 : 0;
 }

@@ -88,7 +88,14 @@ typedef struct gm_config {
   int32_t device;          /* HIP device ordinal */
   int32_t shard_rank;      /* column shard of this context (SCALED multi-GPU); 0 */
   int32_t shard_count;     /* number of column shards; 1 */
-  int32_t reserved[8];
+  /* SCALED initial state: 0 = cold converged start (every cell {hb 0, ts 0},
+   * first tick 1); 1 = warm converged start at t0: own entry {2*t0-1, t0},
+   * others {2*(t0-1-a)-1, t0-a} with a = splitmix64(init_seed, r, c) % 4,
+   * heartbeat counters 2*t0, first tick t0+1 (no mass-staleness transient) */
+  int32_t init_mode;
+  int32_t init_t0;
+  uint64_t init_seed;
+  int32_t reserved[4];
 } gm_config;
 
 /* one log record; `order` sorts records of a drain into reference log order */

@@ -563,6 +563,7 @@ int oc_crash_set(int n, int count, uint64_t seed, int32_t *out) {
 
 oc_ctx *oc_create(const oc_config *cfg) {
   if (cfg->n <= 0) return NULL;
+  if (cfg->mode == OC_SCALED && cfg->init_mode == 1 && cfg->init_t0 < 5) return NULL; /* hb >= 0 needs t0 >= 5 */
   if (cfg->mode == OC_FAITHFUL && cfg->n > MAX_NODES) return NULL; /* EmulNet.cpp:108 assert */
   oc_ctx *c = (oc_ctx *)calloc(1, sizeof(oc_ctx));
   c->cfg = *cfg;
@@ -576,13 +577,24 @@ oc_ctx *oc_create(const oc_config *cfg) {
     oc_srand(&c->s1, cfg->time_seed); /* srand(time(NULL)), Application.cpp:50 and :96 */
     c->t = 0;
   } else {
+    const int warm = cfg->init_mode == 1;
+    const int t0 = warm ? cfg->init_t0 : 0;
     for (int i = 0; i < c->n; i++) {
       node *nd = &c->nodes[i];
       nd->inited = nd->in_group = 1;
+      nd->heartbeat = warm ? 2 * t0 : 0;
       nd->list.v = (entry *)malloc(sizeof(entry) * (size_t)c->n);
       nd->list.cap = nd->list.n = c->n;
       for (int j = 0; j < c->n; j++) {
         entry e = {j + 1, 0, 0, 0};
+        if (warm && j == i) {
+          e.hb = 2 * t0 - 1;
+          e.ts = t0;
+        } else if (warm) {
+          int a = (int)((mix64(cfg->init_seed ^ ((uint64_t)(uint32_t)i << 32) ^ (uint64_t)(uint32_t)j) >> 40) % 4);
+          e.hb = 2 * (t0 - 1 - a) - 1;
+          e.ts = t0 - a;
+        }
         nd->list.v[j] = e;
       }
     }
@@ -603,7 +615,7 @@ oc_ctx *oc_create(const oc_config *cfg) {
       oc_destroy(c);
       return NULL;
     }
-    c->t = 1; /* converged state is "as of tick 0" */
+    c->t = t0 + 1; /* converged state is "as of tick t0" */
   }
   return c;
 }

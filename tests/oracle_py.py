@@ -17,7 +17,8 @@ class OcConfig(ctypes.Structure):
                 ("drop_msg", ctypes.c_int), ("drop_prob", ctypes.c_double), ("time_seed", ctypes.c_uint32),
                 ("rd_seed", ctypes.c_uint64), ("crash_tick", ctypes.c_int), ("crash_count", ctypes.c_int),
                 ("crash_seed", ctypes.c_uint64), ("drop_pct", ctypes.c_int), ("drop_from", ctypes.c_int),
-                ("drop_to", ctypes.c_int), ("drop_seed", ctypes.c_uint64)]
+                ("drop_to", ctypes.c_int), ("drop_seed", ctypes.c_uint64), ("init_mode", ctypes.c_int),
+                ("init_t0", ctypes.c_int), ("init_seed", ctypes.c_uint64)]
 
 
 class OcEvent(ctypes.Structure):
@@ -68,10 +69,11 @@ def _i32p(a):
 
 class Oracle:
     def __init__(self, n, mode=OC_FAITHFUL, single_failure=1, drop_msg=0, drop_prob=0.1, time_seed=0, rd_seed=0,
-                 crash_tick=-1, crash_count=0, crash_seed=0, drop_pct=0, drop_from=0, drop_to=0, drop_seed=0):
+                 crash_tick=-1, crash_count=0, crash_seed=0, drop_pct=0, drop_from=0, drop_to=0, drop_seed=0,
+                 init_mode=0, init_t0=0, init_seed=0):
         self.L = lib()
         cfg = OcConfig(mode, n, single_failure, drop_msg, drop_prob, time_seed & 0xFFFFFFFF, rd_seed, crash_tick,
-                       crash_count, crash_seed, drop_pct, drop_from, drop_to, drop_seed)
+                       crash_count, crash_seed, drop_pct, drop_from, drop_to, drop_seed, init_mode, init_t0, init_seed)
         self.h = self.L.oc_create(ctypes.byref(cfg))
         if not self.h:
             raise ValueError("oc_create failed")

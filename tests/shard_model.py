@@ -22,18 +22,29 @@ def mix64(z):
 
 
 class ShardModel:
-    def __init__(self, n, rank, world, rd_seed=7, drop_pct=0, drop_from=0, drop_to=0, drop_seed=0):
+    def __init__(self, n, rank, world, rd_seed=7, drop_pct=0, drop_from=0, drop_to=0, drop_seed=0,
+                 init_mode=0, init_t0=0, init_seed=0):
         self.n, self.rank, self.world = n, rank, world
         self.c0 = n * rank // world
         self.w = n * (rank + 1) // world - self.c0
         self.hb = np.zeros((n, self.w), np.int64)
-        self.ts = np.zeros((n, self.w), np.int64)         # converged start: all present at {0, 0}
+        self.ts = np.zeros((n, self.w), np.int64)         # cold converged start: all present at {0, 0}
+        t0 = init_t0 if init_mode == 1 else 0
+        if init_mode == 1:                                 # warm converged start (gm_abi.h init_mode)
+            for r in range(n):
+                for j in range(self.w):
+                    c = self.c0 + j
+                    if c == r:
+                        self.hb[r, j], self.ts[r, j] = 2 * t0 - 1, t0
+                    else:
+                        a = (mix64(init_seed ^ (r << 32) ^ c) >> 40) % 4
+                        self.hb[r, j], self.ts[r, j] = 2 * (t0 - 1 - a) - 1, t0 - a
         self.pay = np.full((n, self.w), -1, np.int64)     # payload plane of the previous tick
         self.inbox = [[] for _ in range(n)]
-        self.hbctr = np.zeros(n, np.int64)
+        self.hbctr = np.full(n, 2 * t0, np.int64)
         self.failed = np.zeros(n, bool)
         self.rd_seed, self.drop = rd_seed, (drop_pct, drop_from, drop_to, drop_seed)
-        self.t = 1
+        self.t = t0 + 1
         self.events = []
 
     def _dropped(self, t_send, s, r, col):

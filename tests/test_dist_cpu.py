@@ -50,7 +50,7 @@ def _protocol_worker(rank, world, port, n, ticks, q):
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             return t.numpy()
 
-        drop = dict(drop_pct=30, drop_from=4, drop_to=18, drop_seed=42)
+        drop = dict(drop_pct=30, drop_from=4, drop_to=18, drop_seed=42, init_mode=1, init_t0=5, init_seed=9)
         m = ShardModel(n, rank, world, rd_seed=7, **drop)
         ora = oracle_py.Oracle(n, oracle_py.OC_SCALED, rd_seed=7, crash_tick=6, crash_count=3, crash_seed=42, **drop)
         crash = oracle_py.crash_set(n, 3, 42)

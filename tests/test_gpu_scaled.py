@@ -13,11 +13,14 @@ from membership import GM_EV_JOINED, GM_EV_REMOVED, GM_MODE_SCALED, Simulator, c
 pytestmark = pytest.mark.gpu
 
 
-def run_pair(n, ticks, crash_tick, crash_count, drop_pct=0, drop_from=0, drop_to=0, rd_seed=7, seed=42, seen=None):
+def run_pair(n, ticks, crash_tick, crash_count, drop_pct=0, drop_from=0, drop_to=0, rd_seed=7, seed=42, seen=None,
+             init_mode=0, init_t0=0):
+    init = dict(init_mode=init_mode, init_t0=init_t0, init_seed=seed + 1)
     ora = oracle_py.Oracle(n, oracle_py.OC_SCALED, rd_seed=rd_seed, crash_tick=crash_tick, crash_count=crash_count,
-                           crash_seed=seed, drop_pct=drop_pct, drop_from=drop_from, drop_to=drop_to, drop_seed=seed)
+                           crash_seed=seed, drop_pct=drop_pct, drop_from=drop_from, drop_to=drop_to, drop_seed=seed,
+                           **init)
     sim = Simulator(n, GM_MODE_SCALED, rd_seed=rd_seed, drop_pct=drop_pct, drop_from=drop_from, drop_to=drop_to,
-                    drop_seed=seed)
+                    drop_seed=seed, **init)
     crash = crash_set(n, crash_count, seed)
     assert np.array_equal(crash, oracle_py.crash_set(n, crash_count, seed))
     kinds = {GM_EV_JOINED: 1, GM_EV_REMOVED: 2}
@@ -44,6 +47,11 @@ def test_scaled_matches_oracle(n):
     run_pair(n, 40, crash_tick=8, crash_count=max(1, n // 50))
 
 
+@pytest.mark.parametrize("n", [200, 777])
+def test_scaled_warm_start_matches_oracle(n):
+    run_pair(n, 36, crash_tick=10, crash_count=max(1, n // 100), init_mode=1, init_t0=8)
+
+
 @pytest.mark.parametrize("n", [128, 513])
 def test_scaled_with_drops_matches_oracle(n):
     run_pair(n, 45, crash_tick=10, crash_count=3, drop_pct=20, drop_from=5, drop_to=30)
@@ -56,14 +64,15 @@ def test_scaled_heavy_drop_false_removals_match():
     assert seen.get(1, 0) > 0 and seen.get(2, 0) > 0, seen
 
 
-def test_scaled_invariants_large():
+@pytest.mark.parametrize("warm", [0, 1])
+def test_scaled_invariants_large(warm):
     n, crash_tick, ncrash = 8192, 10, 82
-    sim = Simulator(n, GM_MODE_SCALED, rd_seed=7)
+    sim = Simulator(n, GM_MODE_SCALED, rd_seed=7, init_mode=warm, init_t0=8 if warm else 0, init_seed=3)
     crash = crash_set(n, ncrash, 42)
     crashed = np.zeros(n, bool)
     crashed[crash] = True
     removed = 0
-    for _ in range(45):
+    while sim.time <= 45:
         t = sim.time
         sim.tick()
         if t == crash_tick:

@@ -24,9 +24,10 @@ def merge_dumps(dumps, owners):
     return ("\n".join(out) + "\n").encode()
 
 
-@pytest.mark.parametrize("n,world,drop", [(256, 2, 0), (600, 3, 0), (512, 2, 25), (1100, 4, 10)])
-def test_shards_match_fused_kernel(n, world, drop):
-    kw = dict(rd_seed=7, drop_pct=drop, drop_from=3, drop_to=25, drop_seed=42)
+@pytest.mark.parametrize("n,world,drop,warm", [(256, 2, 0, 0), (600, 3, 0, 1), (512, 2, 25, 0), (1100, 4, 10, 1)])
+def test_shards_match_fused_kernel(n, world, drop, warm):
+    kw = dict(rd_seed=7, drop_pct=drop, drop_from=3, drop_to=25, drop_seed=42, init_mode=warm,
+              init_t0=6 if warm else 0, init_seed=5)
     ref = Simulator(n, GM_MODE_SCALED, **kw)
     shards = [Simulator(n, GM_MODE_SCALED, shard_rank=g, shard_count=world, **kw) for g in range(world)]
     owners = np.zeros(n, dtype=int)
@@ -38,7 +39,7 @@ def test_shards_match_fused_kernel(n, world, drop):
         t = ref.time
         ref.tick()
         loopback_tick(shards)
-        if t == 6:
+        if t == 8:
             ref.set_failed(crash)
             for s in shards:
                 s.set_failed(crash)
