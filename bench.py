@@ -174,7 +174,7 @@ def main():
                    "lists_per_tick": m_lists, "parallelism": f"column-shard x{world}" if world > 1 else "single GPU"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                      "frac": (achieved / PEAK_HBM_GBPS) if achieved else None, "traffic": traffic,
-                     "kernel": "gm_s_tick_shard" if world > 1 else "gm_s_tick_nt", "kernel_ms": kernel_ms,
+                     "kernel": "gm_s_band", "kernel_ms": kernel_ms,
                      "alg_bytes_per_launch": b_alg, "survey_int32_bytes_per_launch": b_survey,
                      "columns_per_gpu": W},
     }

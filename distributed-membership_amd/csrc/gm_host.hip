@@ -21,12 +21,11 @@
 __global__ void gm_f_recv(FState s, int t);
 __global__ void gm_f_node(FState s, int t);
 __global__ void gm_f_send(FState s, int t);
-__global__ void gm_s_tick(SState s, int t, int drop_pct);
-__global__ void gm_s_tick_nt(SState s, int t, int drop_pct);
-__global__ void gm_s_tick_shard(SState s, int t, int drop_pct);
-__global__ void gm_s_draw(SState s, int t, int round, int D);
-__global__ void gm_s_accept(SState s, int t, int D);
-__global__ void gm_s_init(SState s, int warm, int t0, uint64_t seed);
+hipError_t gm_launch_tick(const SState &s, int t, int drop_pct, bool nt, hipStream_t st, hipEvent_t k0, hipEvent_t k1,
+                          bool pick);
+hipError_t gm_launch_draw(const SState &s, int t, int round, int D, hipStream_t st);
+hipError_t gm_launch_accept(const SState &s, int t, int D, hipStream_t st);
+hipError_t gm_launch_init(const SState &s, int warm, int t0, uint64_t seed, hipStream_t st);
 
 #define GM_T_LIMIT 32766  // packed 16-bit hb/ts stay exact: hb <= 2t+1 < 0xFFFF
 
@@ -35,7 +34,8 @@ struct gm_ctx {
   hipStream_t stream = nullptr;
   int dmax = 0;                      // status exchange depth (sharded)
   ncclComm_t comm = nullptr;         // RCCL communicator across column shards
-  hipEvent_t k0 = nullptr, k1 = nullptr;  // per-tick merge-kernel events (sharded)
+  hipEvent_t k0 = nullptr, k1 = nullptr;  // per-tick band-kernel events (sharded)
+  std::vector<hipEvent_t> tev;            // per-tick band-kernel event pairs (single context)
   double kernel_ms_sum = 0;
   bool nt = true;                    // non-temporal table streams (env GM_NT=0 to disable)
   int t = 0;
@@ -44,6 +44,7 @@ struct gm_ctx {
   int latched = GM_OK;
   bool timing = false;
   int timed_ticks = 0;  // ticks in the current timing window
+  int ktimed = 0;       // band-kernel event pairs recorded in the window
   hipEvent_t e0 = nullptr, e1 = nullptr;
   std::vector<void *> allocs;
   std::vector<int32_t> failed_h;
@@ -53,8 +54,6 @@ struct gm_ctx {
   std::vector<gm_event> pending;
   // SCALED
   SState s{};
-  size_t s_smem = 0;
-  uint64_t ev_counts[6] = {0, 0, 0, 0, 0, 0};
 };
 
 static thread_local char g_errbuf[256];
@@ -200,6 +199,21 @@ static int create_faithful(gm_ctx *c) {
   return GM_OK;
 }
 
+// Band width of the SCALED tick: the largest of 512/256/128/64 columns (dividing
+// the padded row) whose per-band traffic -- N rows x band x (4 B table read +
+// 4 B write + 2 B payload write + 2 B payload read) -- stays within ~160 MB, so
+// a band's payload slices stay resident in the 256 MiB Infinity Cache across
+// their ~5 readers (gm_scaled.hip). gm_config.band / env GM_BAND override.
+static int pick_band(const gm_ctx *c, int n, int wp) {
+  int b = c->cfg.band;
+  if (!b && getenv("GM_BAND")) b = atoi(getenv("GM_BAND"));
+  if (b) return (b == 64 || b == 128 || b == 256 || b == 512) && wp % b == 0 ? b : -1;
+  const double budget = 160e6;
+  for (int cand : {512, 256, 128})
+    if (wp % cand == 0 && 12.0 * n * cand <= budget) return cand;
+  return 64;
+}
+
 static int create_scaled(gm_ctx *c) {
   const int n = c->n;
   const int G = c->cfg.shard_count > 0 ? c->cfg.shard_count : 1;
@@ -212,36 +226,30 @@ static int create_scaled(gm_ctx *c) {
   // contiguous, balanced subject-column ranges
   s.c0 = (int)((int64_t)n * rank / G);
   s.w = (int)((int64_t)n * (rank + 1) / G) - s.c0;
-  s.wp = (n + S_ROW_ALIGN - 1) / S_ROW_ALIGN * S_ROW_ALIGN;
-  s.evcap = std::min(s.wp, 1024);
+  s.wp = (s.w + S_ROW_ALIGN - 1) / S_ROW_ALIGN * S_ROW_ALIGN;
+  s.band = pick_band(c, n, s.wp);
+  if (s.band < 0) return GM_EINVAL;
+  s.nb = s.wp / s.band;
+  s.evs = s.band / 32;
+  if (sizeof(uint32_t) * 4 * (size_t)(s.nb + 624) > 65536) return GM_EUNSUPPORTED;  // draw kernels' LDS
   s.ev_spill_cap = 1u << 24;
   s.rd_seed = c->cfg.rd_seed;
   s.drop_seed = c->cfg.drop_seed;
   const size_t cells = (size_t)n * s.wp;
   TRY(dalloc(c, &s.table, cells));
-  // both parities of a row's payload sit next to each other (one allocation), so
-  // even and odd ticks see the same address pattern (env GM_MSG_SEPARATE=1: two planes)
-  const bool sep = getenv("GM_MSG_SEPARATE") && atoi(getenv("GM_MSG_SEPARATE"));
-  c->nt = !(getenv("GM_NT") && !atoi(getenv("GM_NT")));  // default on (A/B: +1 %)
-  if (sep) {
-    TRY(dalloc(c, &s.msg[0], cells));
-    TRY(dalloc(c, &s.msg[1], cells));
-    s.mstride = s.wp;
-  } else {
-    TRY(dalloc(c, &s.msg[0], 2 * cells));
-    s.msg[1] = s.msg[0] + s.wp;
-    s.mstride = 2 * (size_t)s.wp;
-  }
+  c->nt = !(getenv("GM_NT") && !atoi(getenv("GM_NT")));  // non-temporal table streams, default on
+  TRY(dalloc(c, &s.msg, 2 * cells));
   for (int p = 0; p < 2; p++) {
     TRY(dalloc(c, &s.inbox_cnt[p], n));
     TRY(dalloc(c, &s.inbox[p], (size_t)n * S_KMAX));
   }
   TRY(dalloc(c, &s.hbctr, n));
   TRY(dalloc(c, &s.failed, n));
-  TRY(dalloc(c, &s.ev_rows, (size_t)n * s.evcap));
-  TRY(dalloc(c, &s.ev_cnt, n));
+  TRY(dalloc(c, &s.bcnt, (size_t)n * s.nb));
+  TRY(dalloc(c, &s.ev_band, (size_t)n * s.nb * s.evs));
   TRY(dalloc(c, &s.ev_spill, s.ev_spill_cap));
   TRY(dalloc(c, &s.ev_spill_cnt, 1));
+  TRY(dalloc(c, &s.mtraw, (size_t)n * S_MT_RAW));
   TRY(dalloc(c, &s.rowstat, (size_t)n * 4));
   TRY(dalloc(c, &s.targets, (size_t)n * GM_FANOUT));
   TRY(dalloc(c, &s.err, 1));
@@ -249,28 +257,16 @@ static int create_scaled(gm_ctx *c) {
   const bool warm = c->cfg.init_mode == 1;
   const int t0 = warm ? c->cfg.init_t0 : 0;
   if (c->cfg.init_mode < 0 || c->cfg.init_mode > 1 || (warm && (t0 < 5 || t0 > GM_T_LIMIT / 2))) return GM_EINVAL;
-  if (sep) {
-    HIPCHECK(hipMemset(s.msg[0], 0xFF, sizeof(uint16_t) * cells));
-    HIPCHECK(hipMemset(s.msg[1], 0xFF, sizeof(uint16_t) * cells));
-  } else {
-    HIPCHECK(hipMemset(s.msg[0], 0xFF, sizeof(uint16_t) * 2 * cells));
-  }
+  HIPCHECK(hipMemset(s.msg, 0xFF, sizeof(uint16_t) * 2 * cells));
   for (int p = 0; p < 2; p++) HIPCHECK(hipMemset(s.inbox_cnt[p], 0, sizeof(int32_t) * n));
   HIPCHECK(hipMemset(s.failed, 0, sizeof(int32_t) * n));
-  hipLaunchKernelGGL(gm_s_init, dim3(n), dim3(256), 0, c->stream, s, warm ? 1 : 0, t0, c->cfg.init_seed);
-  HIPCHECK(hipGetLastError());
+  HIPCHECK(gm_launch_init(s, warm ? 1 : 0, t0, c->cfg.init_seed, c->stream));
   HIPCHECK(hipStreamSynchronize(c->stream));
-  HIPCHECK(hipMemset(s.ev_cnt, 0, sizeof(int32_t) * n));
+  HIPCHECK(hipMemset(s.bcnt, 0, sizeof(uint32_t) * (size_t)n * s.nb));
   HIPCHECK(hipMemset(s.ev_spill_cnt, 0, sizeof(uint32_t)));
   HIPCHECK(hipMemset(s.rowstat, 0, sizeof(int32_t) * n * 4));
   HIPCHECK(hipMemset(s.err, 0, sizeof(uint32_t)));
-  const int nw = s.wp / 64;
   if (G > 1) {
-    TRY(dalloc(c, &s.gpres, (size_t)n * nw));
-    TRY(dalloc(c, &s.gfresh, (size_t)n * nw));
-    TRY(dalloc(c, &s.gpre, (size_t)n * nw));
-    TRY(dalloc(c, &s.mt, (size_t)624 * n));
-    TRY(dalloc(c, &s.mtk, (size_t)n * 3));
     TRY(dalloc(c, &s.acc, (size_t)n * 8));
     TRY(dalloc(c, &s.pending, n));
     TRY(dalloc(c, &s.npending, 1));
@@ -280,7 +276,6 @@ static int create_scaled(gm_ctx *c) {
     HIPCHECK(hipMemset(s.pending, 0, sizeof(int32_t) * n));
     HIPCHECK(hipMemset(s.xcnt, 0, sizeof(int32_t) * (size_t)G * n * 2));
   }
-  c->s_smem = (size_t)nw * 8 * 2 + (size_t)nw * 4 + 624 * 4 + (S_KMAX + 16 + 8) * 4;
   c->t = t0 + 1;  // the converged table is the state "as of tick t0"
   return GM_OK;
 }
@@ -318,6 +313,7 @@ extern "C" int gm_destroy(gm_ctx *c) {
   for (void *p : c->allocs) (void)hipFree(p);
   for (hipEvent_t e : {c->e0, c->e1, c->k0, c->k1})
     if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : c->tev) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return GM_OK;
@@ -374,14 +370,23 @@ static int tick_scaled(gm_ctx *c) {
   if (c->s.shard_count > 1) return tick_sharded(c);
   const int t_send = c->t - 1;
   const bool drop = c->cfg.drop_pct > 0 && t_send >= c->cfg.drop_from && t_send < c->cfg.drop_to;
-  if (c->timing && c->timed_ticks == 0) HIPCHECK(hipEventRecord(c->e0, c->stream));
-  hipLaunchKernelGGL(c->nt ? gm_s_tick_nt : gm_s_tick, dim3(c->n), dim3(S_THREADS), c->s_smem, c->stream, c->s,
-                     c->t, drop ? c->cfg.drop_pct : -1);
+  hipEvent_t k0 = nullptr, k1 = nullptr;
+  if (c->timing) {
+    if (c->timed_ticks == 0) HIPCHECK(hipEventRecord(c->e0, c->stream));
+    while (c->tev.size() < 2 * (size_t)(c->ktimed + 1)) {
+      hipEvent_t e;
+      HIPCHECK(hipEventCreate(&e));
+      c->tev.push_back(e);
+    }
+    k0 = c->tev[2 * c->ktimed];
+    k1 = c->tev[2 * c->ktimed + 1];
+    c->ktimed++;
+  }
+  HIPCHECK(gm_launch_tick(c->s, c->t, drop ? c->cfg.drop_pct : -1, c->nt, c->stream, k0, k1, true));
   if (c->timing) {
     HIPCHECK(hipEventRecord(c->e1, c->stream));
     c->timed_ticks++;
   }
-  HIPCHECK(hipGetLastError());
   return GM_OK;
 }
 
@@ -441,31 +446,32 @@ extern "C" int gm_set_dropmsg(gm_ctx *c, int32_t on) {
 
 static int drain_scaled(gm_ctx *c, std::vector<gm_event> &out) {
   const SState &s = c->s;
-  std::vector<int32_t> cnt(c->n);
+  const size_t nrb = (size_t)c->n * s.nb;
+  std::vector<uint32_t> bc(nrb);
   uint32_t nsp = 0;
-  HIPCHECK(hipMemcpyAsync(cnt.data(), s.ev_cnt, sizeof(int32_t) * c->n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHECK(hipMemcpyAsync(bc.data(), s.bcnt, sizeof(uint32_t) * nrb, hipMemcpyDeviceToHost, c->stream));
   HIPCHECK(hipMemcpyAsync(&nsp, s.ev_spill_cnt, sizeof nsp, hipMemcpyDeviceToHost, c->stream));
   HIPCHECK(hipStreamSynchronize(c->stream));
   const int t = c->t - 1;
-  std::vector<uint32_t> row(s.evcap);
-  for (int r = 0; r < c->n; r++) {
-    int k = std::min(cnt[r], s.evcap);
-    if (k <= 0) continue;
-    HIPCHECK(hipMemcpy(row.data(), s.ev_rows + (size_t)r * s.evcap, sizeof(uint32_t) * k, hipMemcpyDeviceToHost));
-    for (int q = 0; q < k; q++)
-      out.push_back(gm_event{t, r, (int)(row[q] >> 30) == (int)S_EV_ADD ? GM_EV_JOINED : GM_EV_REMOVED,
-                             (int32_t)(row[q] & 0x3FFFFFFFu)});
+  auto push = [&](int r, uint32_t rec) {
+    out.push_back(gm_event{t, r, (int)(rec >> 30) == (int)S_EV_ADD ? GM_EV_JOINED : GM_EV_REMOVED,
+                           (int32_t)(rec & 0x3FFFFFFFu)});
+  };
+  bool any = false;
+  for (uint32_t v : bc) any |= S_BC_NEV(v) != 0;
+  if (any) {
+    std::vector<uint32_t> ev(nrb * s.evs);
+    HIPCHECK(hipMemcpy(ev.data(), s.ev_band, sizeof(uint32_t) * ev.size(), hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < nrb; i++) {
+      const int k = std::min<int>((int)S_BC_NEV(bc[i]), s.evs);
+      for (int q = 0; q < k; q++) push((int)(i / s.nb), ev[i * s.evs + q]);
+    }
   }
   nsp = std::min(nsp, s.ev_spill_cap);
   if (nsp) {
     std::vector<uint64_t> sp(nsp);
     HIPCHECK(hipMemcpy(sp.data(), s.ev_spill, sizeof(uint64_t) * nsp, hipMemcpyDeviceToHost));
-    for (uint64_t v : sp) {
-      uint32_t rec = (uint32_t)v;
-      out.push_back(gm_event{t, (int32_t)(v >> 32), (int)(rec >> 30) == (int)S_EV_ADD ? GM_EV_JOINED : GM_EV_REMOVED,
-                             (int32_t)(rec & 0x3FFFFFFFu)});
-    }
-    HIPCHECK(hipMemset(s.ev_spill_cnt, 0, sizeof(uint32_t)));
+    for (uint64_t v : sp) push((int)(v >> 32), (uint32_t)v);
   }
   // canonical SCALED order: loggers descending; joins ascending id, then removals descending id
   std::sort(out.begin(), out.end(), [](const gm_event &a, const gm_event &b) {
@@ -493,13 +499,12 @@ extern "C" int gm_event_counts(gm_ctx *c, uint64_t counts[6]) {
   if (!c || !counts) return GM_EINVAL;
   for (int k = 0; k < 6; k++) counts[k] = 0;
   if (c->cfg.mode == GM_MODE_SCALED) {
-    std::vector<int32_t> cnt(c->n);
-    uint32_t nsp = 0;
-    HIPCHECK(hipMemcpyAsync(cnt.data(), c->s.ev_cnt, sizeof(int32_t) * c->n, hipMemcpyDeviceToHost, c->stream));
-    HIPCHECK(hipMemcpyAsync(&nsp, c->s.ev_spill_cnt, sizeof nsp, hipMemcpyDeviceToHost, c->stream));
+    const size_t nrb = (size_t)c->n * c->s.nb;
+    std::vector<uint32_t> bc(nrb);
+    HIPCHECK(hipMemcpyAsync(bc.data(), c->s.bcnt, sizeof(uint32_t) * nrb, hipMemcpyDeviceToHost, c->stream));
     HIPCHECK(hipStreamSynchronize(c->stream));
-    uint64_t tot = nsp;
-    for (int32_t v : cnt) tot += (uint64_t)std::min(v, c->s.evcap);
+    uint64_t tot = 0;
+    for (uint32_t v : bc) tot += S_BC_NEV(v);  // slots + spilled, per (row, band)
     counts[0] = tot;  // join+remove records of the last tick (per-kind split needs a drain)
   } else {
     for (const gm_event &e : c->pending) counts[e.kind]++;
@@ -524,12 +529,19 @@ extern "C" int gm_msgcount(gm_ctx *c, int32_t t, int32_t *sent, int32_t *recv) {
 }
 
 static int read_table_row(gm_ctx *c, int r, std::vector<uint32_t> &row, int &w) {
-  const bool fm = c->cfg.mode == GM_MODE_FAITHFUL;
-  const int stride = fm ? c->f.np : c->s.wp;
-  w = fm ? c->n : c->s.w;  // this context's columns
+  if (c->cfg.mode == GM_MODE_FAITHFUL) {
+    w = c->n;
+    row.resize(w);
+    HIPCHECK(hipMemcpy(row.data(), c->f.table + (size_t)r * c->f.np, sizeof(uint32_t) * w, hipMemcpyDeviceToHost));
+    return GM_OK;
+  }
+  const SState &s = c->s;  // band-tiled: one B-cell piece of the row per band slab
+  w = s.w;  // this context's columns
+  row.resize(s.wp);
+  const size_t piece = sizeof(uint32_t) * s.band;
+  HIPCHECK(hipMemcpy2D(row.data(), piece, s.table + (size_t)r * s.band, piece * s.n, piece, s.nb,
+                       hipMemcpyDeviceToHost));
   row.resize(w);
-  const uint32_t *base = (fm ? c->f.table : c->s.table) + (size_t)r * stride;
-  HIPCHECK(hipMemcpy(row.data(), base, sizeof(uint32_t) * w, hipMemcpyDeviceToHost));
   return GM_OK;
 }
 
@@ -627,6 +639,7 @@ extern "C" int gm_set_timing(gm_ctx *c, int32_t on) {
   if (!c) return GM_EINVAL;
   c->timing = on != 0;
   c->timed_ticks = 0;  // (re)opens the timing window at the next tick
+  c->ktimed = 0;
   c->kernel_ms_sum = 0;
   return GM_OK;
 }
@@ -640,8 +653,13 @@ extern "C" int gm_last_kernel_ms(gm_ctx *c, float *ms) {
     return GM_OK;
   }
   HIPCHECK(hipEventSynchronize(c->e1));
-  HIPCHECK(hipEventElapsedTime(ms, c->e0, c->e1));
-  *ms /= (float)c->timed_ticks;
+  double sum = 0;
+  for (int i = 0; i < c->ktimed; i++) {
+    float x = 0;
+    HIPCHECK(hipEventElapsedTime(&x, c->tev[2 * i], c->tev[2 * i + 1]));
+    sum += x;
+  }
+  *ms = c->ktimed ? (float)(sum / c->ktimed) : 0.f;
   return GM_OK;
 }
 
@@ -676,8 +694,8 @@ extern "C" int gm_crash_set(int32_t n, int32_t count, uint64_t seed, int32_t *ou
     }                                                                                \
   } while (0)
 
-#define GM_D_FIRST 16  // draws per row in the first round (steady state needs ~5-6)
-#define GM_D_MORE 64   // draws per row in later rounds (transients with many stale entries)
+#define GM_D_FIRST S_MT_RAW  // S2 outputs per row in the first round (steady state needs ~5-6)
+#define GM_D_MORE 64          // S2 outputs per row in later rounds (transients with many stale entries)
 
 extern "C" int gm_comm_unique_id(uint8_t *out128) {
   if (!out128) return GM_EINVAL;
@@ -716,19 +734,16 @@ extern "C" int gm_shard_merge(gm_ctx *c) {
   TRY(shard_ready(c));
   const int t_send = c->t - 1;
   const bool drop = c->cfg.drop_pct > 0 && t_send >= c->cfg.drop_from && t_send < c->cfg.drop_to;
-  if (c->timing) HIPCHECK(hipEventRecord(c->k0, c->stream));
-  hipLaunchKernelGGL(gm_s_tick_shard, dim3(c->n), dim3(S_THREADS), c->s_smem, c->stream, c->s, c->t,
-                     drop ? c->cfg.drop_pct : -1);
-  if (c->timing) HIPCHECK(hipEventRecord(c->k1, c->stream));
-  HIPCHECK(hipGetLastError());
+  HIPCHECK(gm_launch_tick(c->s, c->t, drop ? c->cfg.drop_pct : -1, c->nt, c->stream, c->timing ? c->k0 : nullptr,
+                          c->timing ? c->k1 : nullptr, false));
   return GM_OK;
 }
 
 extern "C" int gm_shard_draw(gm_ctx *c, int32_t round, int32_t D) {
   TRY(shard_ready(c));
-  if (D <= 0 || D > c->dmax || round < 0) return GM_EINVAL;
-  hipLaunchKernelGGL(gm_s_draw, dim3((c->n + 255) / 256), dim3(256), 0, c->stream, c->s, c->t, round, D);
-  HIPCHECK(hipGetLastError());
+  // round 0 covers the precomputed S2 outputs [0, 16), round q >= 1 outputs [16 + 64(q-1), 16 + 64q)
+  if (round < 0 || D != (round == 0 ? GM_D_FIRST : GM_D_MORE)) return GM_EINVAL;
+  HIPCHECK(gm_launch_draw(c->s, c->t, round, D, c->stream));
   return GM_OK;
 }
 
@@ -736,8 +751,7 @@ extern "C" int gm_shard_accept(gm_ctx *c, int32_t D, int32_t *npending) {
   TRY(shard_ready(c));
   if (D <= 0 || D > c->dmax || !npending) return GM_EINVAL;
   HIPCHECK(hipMemsetAsync(c->s.npending, 0, sizeof(int32_t), c->stream));
-  hipLaunchKernelGGL(gm_s_accept, dim3((c->n + 255) / 256), dim3(256), 0, c->stream, c->s, c->t, D);
-  HIPCHECK(hipGetLastError());
+  HIPCHECK(gm_launch_accept(c->s, c->t, D, c->stream));
   HIPCHECK(hipMemcpyAsync(npending, c->s.npending, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
   HIPCHECK(hipStreamSynchronize(c->stream));
   return GM_OK;

@@ -1,27 +1,40 @@
 // gm_scaled.hip -- SCALED-mode tick: the HBM-bound full-membership hot path.
 //
-// One launch per globaltime tick; one 256-thread workgroup owns one observer
-// row r (MP1Node of node r) and does, in a single streaming pass over the row:
-//   1. merge: max-merge the gossip lists delivered to r this tick
-//      (updatelistCallBack, MP1Node.cpp:259-301). A list is the sender's
-//      post-sweep row of the previous tick reduced to 16-bit heartbeats of its
-//      fresh entries (sendMemberList, MP1Node.cpp:360-395: entries with
-//      t - ts < TFAIL), stored once per sender in a payload plane and read by
-//      each of its <= ~5 receivers ("pull"; no atomics, commutative, order-free);
-//   2. self heartbeat bump (nodeLoopOps, MP1Node.cpp:409-415);
-//   3. failure sweep: age >= TFAIL -> numfailed, age >= TREMOVE -> removed
-//      (MP1Node.cpp:426-444), with join/remove events appended to per-row slots;
-//   4. writes the row back and the row's own payload plane for tick t+1;
-//   5. builds presence / freshness bitmaps of the row in LDS, then one lane runs
-//      the gossip-target draw (mt19937 + Lemire + rank-select, MP1Node.cpp:449-489)
-//      and enqueues r into each target's inbox for the next tick -- the
-//      counting sort by destination that replaces EmulNet's buffer scan.
-// Bytes per live row per tick: 4W read + 4W write (table) + 2W write (payload)
-// + 2W per delivered list (payload reads); nothing else touches HBM at scale.
+// One globaltime tick (Application::mp1Run for every node, Application.cpp:121-164)
+// is three launches on the context stream:
+//
+//   gm_s_mtgen  thread per row: the first S_MT_RAW outputs of the row's S2 stream
+//               (the mt19937 that nodeLoopOps seeds per call, MP1Node.cpp:450-452),
+//               computed from 397+16 init words kept in registers.
+//   gm_s_band   the merge / heartbeat / sweep pass over the N x W table, in COLUMN
+//               BANDS: one wave per (band, 64 rows) streams the band's slice of its rows,
+//               max-merges the slices of the gossip payloads delivered to each row
+//               (updatelistCallBack, MP1Node.cpp:259-301), bumps the row's own entry
+//               (MP1Node.cpp:409-415), runs the TFAIL/TREMOVE sweep (MP1Node.cpp:
+//               426-444), writes the row slice back and the row's payload slice for
+//               tick t+1 (the fresh entries' heartbeats, sendMemberList MP1Node.cpp:
+//               360-395), and records per-(row, band) counts and events. Workgroups
+//               are numbered band-major, so the chip sweeps one band of every row at a
+//               time: a sender's payload slice is read by its ~5 receivers while that
+//               band's payload slices (N x band x 2 B) are resident in the 256 MiB
+//               Infinity Cache -- HBM sees each payload byte once instead of once per
+//               delivery (band width sized so one band's traffic fits the cache).
+//   gm_s_pick   wave per row: row totals from the band counts, the gossip-target draw
+//               on the post-sweep list (MP1Node.cpp:449-489: Lemire over the S2
+//               outputs, "memberlist[ix]" = rank-select over band prefix counts and one
+//               table slice, skip me / stale / duplicates), and delivery: the row
+//               appends itself to its targets' inboxes for tick t+1 (counting sort by
+//               destination in place of EmulNet's buffer scan, EmulNet.cpp:144-177).
+//
+// Column-sharded ticks (multi-GPU) run gm_s_mtgen + gm_s_band + gm_s_count on the
+// shard's columns, exchange per-row counts, then gm_s_draw / gm_s_accept rounds.
 #include "gm_device.h"
 #include "gm_scaled.h"
 
+#include <algorithm>
+
 typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ u16x2 as_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
 __device__ __forceinline__ uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
@@ -29,267 +42,510 @@ __device__ __forceinline__ uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(
 // merge key of one payload word pair: hb+1, NONE (0xFFFF) -> 0
 __device__ __forceinline__ u16x2 key2(uint32_t m) { return as_u16x2(m) + (u16x2)(1); }
 
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-// 16-byte row-stream accesses, optionally non-temporal (A/B variant)
+// 16-byte row-stream accesses, optionally non-temporal
 template <bool NT>
-__device__ __forceinline__ uint4 ld(const uint4 *p) {
+__device__ __forceinline__ uint4 ld(const uint32_t *p) {
   u32x4 v = NT ? __builtin_nontemporal_load((const u32x4 *)p) : *(const u32x4 *)p;
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 template <bool NT>
-__device__ __forceinline__ void st(uint4 *p, uint4 v) {
+__device__ __forceinline__ void st(void *p, uint4 v) {
   u32x4 w = {v.x, v.y, v.z, v.w};
   if (NT) __builtin_nontemporal_store(w, (u32x4 *)p);
   else *(u32x4 *)p = w;
 }
 
-template <bool SHARDED, bool NT>
-__device__ __forceinline__ void gm_s_tick_body(SState &s, int t, int drop_pct) {
-  extern __shared__ __align__(16) unsigned char s_smem[];
-  const int wp = s.wp, nw = wp >> 6;
-  uint64_t *s_pres = (uint64_t *)s_smem;               // [nw] present after the sweep
-  uint64_t *s_fresh = s_pres + nw;                     // [nw] present and t - ts < TFAIL
-  uint32_t *s_pre = (uint32_t *)(s_fresh + nw);        // [nw] exclusive prefix popcounts
-  uint32_t *s_mt = s_pre + nw;                         // [624] mt19937 state
-  int *s_send = (int *)(s_mt + 624);                   // [S_KMAX] senders of this tick's lists
-  int *s_tmp = s_send + S_KMAX;                        // [16] scan scratch
-  int *s_misc = s_tmp + 16;                            // [8]
+__device__ __forceinline__ uint32_t mt_temper(uint32_t v) {
+  v ^= v >> 11;
+  v ^= (v << 7) & 0x9d2c5680u;
+  v ^= (v << 15) & 0xefc60000u;
+  return v ^ (v >> 18);
+}
 
-  const int r = blockIdx.x, tid = threadIdx.x;
+// ------------------------------------------------------------------ gm_s_mtgen
+// Outputs 0..15 of mt19937(seed) need init words x[0..16] and x[397..412] only
+// (output k twists x[k], x[k+1], x[k+397]; all still init words for k < 227).
+__global__ __launch_bounds__(256) void gm_s_mtgen(SState s, int t) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= s.n) return;
+  uint32_t lo[S_MT_RAW + 1], hi[S_MT_RAW];
+  uint32_t v = gm_rd_seed(s.rd_seed, t, r + 1);
+  lo[0] = v;
+#pragma unroll
+  for (int i = 1; i <= S_MT_RAW; i++) {
+    v = 1812433253u * (v ^ (v >> 30)) + (uint32_t)i;
+    lo[i] = v;
+  }
+  for (int i = S_MT_RAW + 1; i < 397; i++) v = 1812433253u * (v ^ (v >> 30)) + (uint32_t)i;
+#pragma unroll
+  for (int i = 0; i < S_MT_RAW; i++) {
+    v = 1812433253u * (v ^ (v >> 30)) + (uint32_t)(397 + i);
+    hi[i] = v;
+  }
+  uint32_t out[S_MT_RAW];
+#pragma unroll
+  for (int k = 0; k < S_MT_RAW; k++) {
+    const uint32_t y = (lo[k] & 0x80000000u) | (lo[k + 1] & 0x7fffffffu);
+    out[k] = mt_temper(hi[k] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u));
+  }
+  uint4 *dst = (uint4 *)(s.mtraw + (size_t)r * S_MT_RAW);
+#pragma unroll
+  for (int k = 0; k < S_MT_RAW / 4; k++) dst[k] = make_uint4(out[4 * k], out[4 * k + 1], out[4 * k + 2], out[4 * k + 3]);
+}
+
+// ------------------------------------------------------------------- gm_s_band
+// One wave per work unit: unit u is (band u / U, rows [(u % U) * RPW, +RPW)),
+// U = ceil(n / RPW) units per band, LPR = B/8 lanes per row, 8 columns per lane.
+// Units are numbered band-major, so the waves in flight cover a few consecutive
+// thousand rows of one band: the band's payload slab (n * B * 2 B per parity) is
+// read ~5 times per sender slice while it sits in the Infinity Cache, and HBM sees
+// each payload byte about once. Each wave issues its row's metadata (crash flag,
+// inbox count, first S_SB sender ids) together with its table slice, then the
+// payload slices, merges, sweeps, stores and exits (short-lived waves keep more
+// bytes in flight than a persistent loop; measured with scripts/ubench).
+template <int B>
+struct RowMeta {
+  int k;           // lists delivered to the row (-1: no such row, or a crashed node)
+  int snd[S_SB];   // first S_SB senders
+};
+
+template <int B>
+__device__ __forceinline__ RowMeta<B> row_meta(const SState &s, int r, int par) {
+  RowMeta<B> m;
+  m.k = -1;
+  if (r < s.n) {
+    const int32_t *ib = s.inbox[par] + (size_t)r * S_KMAX;
+    const int4 a = *(const int4 *)ib;
+    const int4 b = *(const int4 *)(ib + 4);
+    m.snd[0] = a.x; m.snd[1] = a.y; m.snd[2] = a.z; m.snd[3] = a.w;
+    m.snd[4] = b.x; m.snd[5] = b.y; m.snd[6] = b.z; m.snd[7] = b.w;
+    const int k = s.inbox_cnt[par][r];
+    m.k = s.failed[r] ? -1 : k;
+  }
+  return m;
+}
+
+template <int B, bool DROP>
+__global__ __launch_bounds__(256) void gm_s_band(SState s, int t, int drop_pct) {
+  constexpr bool NT = true;  // non-temporal table / payload-write streams
+  constexpr int LPR = B / S_COLS_PER_LANE;  // lanes per row
+  constexpr int RPW = 64 / LPR;             // rows per wave
+  const int lane = threadIdx.x & 63;
   const int par = t & 1;
-  int32_t *cnt_in = s.inbox_cnt[par];
-  if (tid == 0) {
-    s_misc[0] = cnt_in[r];
-    cnt_in[r] = 0;  // recycled as the append target of tick t+1
-    s_misc[1] = 0;  // event slots used
-  }
-  __syncthreads();
-  const int kin = s_misc[0];
-  int32_t *stat = s.rowstat + (size_t)r * 4;
-  if (s.failed[r]) {  // crashed node: frozen, receives and sends nothing
-    if (tid == 0) {
-      stat[0] = stat[1] = stat[2] = stat[3] = 0;
-      s.ev_cnt[r] = 0;
-      if (SHARDED) {
-        int32_t *x = s.xcnt + ((size_t)s.shard_rank * s.n + r) * 2;
-        x[0] = x[1] = 0;
-      }
-    }
-    return;
-  }
-  const int k = kin < S_KMAX ? kin : S_KMAX;
-  if (tid == 0 && kin > S_KMAX) atomicOr(s.err, GM_ERR_INBOX);
-  for (int j = tid; j < k; j += S_THREADS) s_send[j] = s.inbox[par][(size_t)r * S_KMAX + j];
-  __syncthreads();
-
-  uint32_t *trow = s.table + (size_t)r * wp;
-  uint16_t *mout = s.msg[par] + (size_t)r * s.mstride;
-  const uint16_t *mprev = s.msg[par ^ 1];
-  const size_t ms = s.mstride;
-  const int selfc = (r >= s.c0 && r < s.c0 + s.w) ? r - s.c0 : -1;  // own column, if in this shard
+  const int sub = lane / LPR, li = lane % LPR;
+  const int U = (s.n + RPW - 1) / RPW;  // units per band
+  const int u = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (u >= U * s.nb) return;  // whole wave
   const uint32_t tt = (uint32_t)t;
   const int t_send = t - 1;
-  int npres = 0, nfail = 0;
-
-  for (int base = tid * S_COLS_PER_THREAD; base < wp; base += S_COLS_PER_STEP) {
-    const uint4 ta = ld<NT>((const uint4 *)(trow + base));
-    const uint4 tb = ld<NT>((const uint4 *)(trow + base + 4));
-    u16x2 k0 = (u16x2)(0), k1 = (u16x2)(0), k2 = (u16x2)(0), k3 = (u16x2)(0);
-    if (drop_pct < 0) {
-      for (int j0 = 0; j0 < k; j0 += 8) {
-        uint4 m[8];
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-          if (j0 + u < k) m[u] = *(const uint4 *)(mprev + (size_t)s_send[j0 + u] * ms + base);
-          else m[u] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
-        }
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-          k0 = __builtin_elementwise_max(k0, key2(m[u].x));
-          k1 = __builtin_elementwise_max(k1, key2(m[u].y));
-          k2 = __builtin_elementwise_max(k2, key2(m[u].z));
-          k3 = __builtin_elementwise_max(k3, key2(m[u].w));
-        }
-      }
-    } else {
-      // per-entry drops keyed by (t_send, src, dst, column) -- SCALED regime
-      uint32_t kk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      for (int j = 0; j < k; j++) {
-        const int snd = s_send[j];
-        const uint4 m = *(const uint4 *)(mprev + (size_t)snd * ms + base);
-        const uint32_t mw[4] = {m.x, m.y, m.z, m.w};
-        const uint64_t pair = gm_mix64(s.drop_seed ^ ((uint64_t)(uint32_t)t_send << 48) ^
-                                       ((uint64_t)(uint32_t)snd << 24) ^ (uint64_t)(uint32_t)r);
-#pragma unroll
-        for (int q = 0; q < 8; q++) {
-          uint32_t hv = (mw[q >> 1] >> (16 * (q & 1))) & 0xFFFFu;
-          uint32_t key = (hv + 1u) & 0xFFFFu;
-          if (key == 0) continue;
-          uint32_t h = (uint32_t)(gm_mix64(pair + (uint64_t)(s.c0 + base + q)) >> 32);
-          if ((int)(h % 100u) < drop_pct) continue;
-          kk[q] = kk[q] > key ? kk[q] : key;
-        }
-      }
-      k0 = as_u16x2(kk[0] | (kk[1] << 16));
-      k1 = as_u16x2(kk[2] | (kk[3] << 16));
-      k2 = as_u16x2(kk[4] | (kk[5] << 16));
-      k3 = as_u16x2(kk[6] | (kk[7] << 16));
+  const int32_t *inbox = s.inbox[par];
+  const int band = u / U;
+  const int r = (u - band * U) * RPW + sub;
+  const int colb = band * B + li * S_COLS_PER_LANE;  // shard-local column of this lane's first cell
+  const size_t slab = (size_t)band * s.n;            // this band's slab (rows of the band-tiled layout)
+  const uint16_t *mprev = s.msg + (size_t)(par ^ 1) * B + li * S_COLS_PER_LANE;  // + (slab + sender) * 2B
+  const RowMeta<B> meta = row_meta<B>(s, r, par);
+  {
+    int k = meta.k;
+    if (k > S_KMAX) {
+      if (li == 0) atomicOr(s.err, GM_ERR_INBOX);
+      k = S_KMAX;
     }
-    uint32_t e[8] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y, tb.z, tb.w};
-    const uint32_t keys[4] = {as_u32(k0), as_u32(k1), as_u32(k2), as_u32(k3)};
-    uint32_t out[4] = {0, 0, 0, 0};
-    uint32_t pbits = 0, fbits = 0;
+    const bool live = k >= 0;
+    int npres = 0, nfail = 0, nev = 0;
+    uint32_t evk = 0;  // 2 bits per cell: event kind
+    uint32_t *trow = s.table + (slab + r) * B + li * S_COLS_PER_LANE;
+    const int32_t *ib = inbox + (size_t)r * S_KMAX;
+    // issue this row's loads (table slice + the prefetched senders' payload slices) ...
+    uint4 ta = make_uint4(0, 0, 0, 0), tb = ta, m[S_SB];
 #pragma unroll
-    for (int q = 0; q < 8; q++) {
-      const int c = base + q;
-      uint32_t en = e[q];
-      const uint32_t key = (keys[q >> 1] >> (16 * (q & 1))) & 0xFFFFu;
-      uint32_t ev = 0;
-      if (key) {  // updatelistCallBack: insert, or raise hb and stamp ts = now
-        const uint32_t hb = key - 1u;
-        if (en == GM_ABSENT) { en = gm_pack(hb, tt); ev = S_EV_ADD; }
-        else if (gm_hb(en) < hb) en = gm_pack(hb, tt);
-      }
-      if (c == selfc) {  // updateMyPos + heartbeat++ + myPos->setheartbeat(heartbeat++)
-        if (en == GM_ABSENT) atomicOr(s.err, GM_ERR_SELF);
-        const int hb = s.hbctr[r] + 1;
-        s.hbctr[r] = hb + 1;
-        en = gm_pack((uint32_t)hb, tt);
-      }
-      uint32_t o = GM_NONE16;
-      if (en != GM_ABSENT) {
-        const int age = t - (int)gm_ts(en);
-        if (age >= GM_TFAIL) {
-          nfail++;
-          if (age >= GM_TREMOVE) { en = GM_ABSENT; ev = S_EV_REMOVE; }
-        } else {
-          o = gm_hb(en);
-          fbits |= 1u << q;
+    for (int j = 0; j < S_SB; j++) m[j] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+    if (r < s.n) {  // the table slice does not wait for the metadata
+      ta = ld<NT>(trow);
+      tb = ld<NT>(trow + 4);
+    }
+    if (live && !DROP) {
+#pragma unroll
+      for (int j = 0; j < S_SB; j++)
+        if (j < k) m[j] = *(const uint4 *)(mprev + (slab + meta.snd[j]) * (2 * B));
+    }
+    if (live) {
+      u16x2 k0 = (u16x2)(0), k1 = (u16x2)(0), k2 = (u16x2)(0), k3 = (u16x2)(0);
+      if (!DROP) {
+#pragma unroll
+        for (int j = 0; j < S_SB; j++) {
+          k0 = __builtin_elementwise_max(k0, key2(m[j].x));
+          k1 = __builtin_elementwise_max(k1, key2(m[j].y));
+          k2 = __builtin_elementwise_max(k2, key2(m[j].z));
+          k3 = __builtin_elementwise_max(k3, key2(m[j].w));
         }
-        if (en != GM_ABSENT) pbits |= 1u << q;
+        for (int j = S_SB; j < k; j++) {  // rare: more lists than prefetched ids
+          const uint4 mm = *(const uint4 *)(mprev + (slab + ib[j]) * (2 * B));
+          k0 = __builtin_elementwise_max(k0, key2(mm.x));
+          k1 = __builtin_elementwise_max(k1, key2(mm.y));
+          k2 = __builtin_elementwise_max(k2, key2(mm.z));
+          k3 = __builtin_elementwise_max(k3, key2(mm.w));
+        }
+      } else {
+        // per-entry drops keyed by (t_send, src, dst, global column) -- SCALED regime
+        uint32_t kk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int j = 0; j < k; j++) {
+          const int sn = ib[j];
+          const uint4 m = *(const uint4 *)(mprev + (slab + sn) * (2 * B));
+          const uint32_t mw[4] = {m.x, m.y, m.z, m.w};
+          const uint64_t pair = gm_mix64(s.drop_seed ^ ((uint64_t)(uint32_t)t_send << 48) ^
+                                         ((uint64_t)(uint32_t)sn << 24) ^ (uint64_t)(uint32_t)r);
+#pragma unroll
+          for (int q = 0; q < 8; q++) {
+            const uint32_t hv = (mw[q >> 1] >> (16 * (q & 1))) & 0xFFFFu;
+            const uint32_t key = (hv + 1u) & 0xFFFFu;
+            if (key == 0) continue;
+            const uint32_t h = (uint32_t)(gm_mix64(pair + (uint64_t)(s.c0 + colb + q)) >> 32);
+            if ((int)(h % 100u) < drop_pct) continue;
+            kk[q] = kk[q] > key ? kk[q] : key;
+          }
+        }
+        k0 = as_u16x2(kk[0] | (kk[1] << 16));
+        k1 = as_u16x2(kk[2] | (kk[3] << 16));
+        k2 = as_u16x2(kk[4] | (kk[5] << 16));
+        k3 = as_u16x2(kk[6] | (kk[7] << 16));
       }
-      e[q] = en;
-      out[q >> 1] |= o << (16 * (q & 1));
-      if (ev) {
-        const int slot = atomicAdd(&s_misc[1], 1);
-        const uint32_t rec = (ev << 30) | (uint32_t)(s.c0 + c + 1);
-        if (slot < s.evcap) {
-          s.ev_rows[(size_t)r * s.evcap + slot] = rec;
+      const int selfc = (r >= s.c0 && r < s.c0 + s.w) ? r - s.c0 : -1;  // own column, if in this shard
+      uint32_t e[8] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y, tb.z, tb.w};
+      const uint32_t keys[4] = {as_u32(k0), as_u32(k1), as_u32(k2), as_u32(k3)};
+      uint32_t out[4] = {0, 0, 0, 0};
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        uint32_t en = e[q];
+        const uint32_t key = (keys[q >> 1] >> (16 * (q & 1))) & 0xFFFFu;
+        uint32_t ev = 0;
+        if (key) {  // updatelistCallBack: insert, or raise hb and stamp ts = now
+          const uint32_t hb = key - 1u;
+          if (en == GM_ABSENT) {
+            en = gm_pack(hb, tt);
+            ev = S_EV_ADD;
+          } else if (gm_hb(en) < hb) {
+            en = gm_pack(hb, tt);
+          }
+        }
+        if (colb + q == selfc) {  // updateMyPos + heartbeat++ + myPos->setheartbeat(heartbeat++)
+          if (en == GM_ABSENT) atomicOr(s.err, GM_ERR_SELF);
+          const int hb = s.hbctr[r] + 1;
+          s.hbctr[r] = hb + 1;
+          en = gm_pack((uint32_t)hb, tt);
+        }
+        uint32_t o = GM_NONE16;
+        if (en != GM_ABSENT) {
+          const int age = t - (int)gm_ts(en);
+          if (age >= GM_TFAIL) {
+            nfail++;
+            if (age >= GM_TREMOVE) {
+              en = GM_ABSENT;
+              ev = S_EV_REMOVE;
+            }
+          } else {
+            o = gm_hb(en);
+          }
+          if (en != GM_ABSENT) npres++;
+        }
+        e[q] = en;
+        out[q >> 1] |= o << (16 * (q & 1));
+        if (ev) {
+          evk |= ev << (2 * q);
+          nev++;
+        }
+      }
+      st<NT>(trow, make_uint4(e[0], e[1], e[2], e[3]));
+      st<NT>(trow + 4, make_uint4(e[4], e[5], e[6], e[7]));
+      st<NT>(s.msg + ((slab + r) * 2 + par) * B + li * S_COLS_PER_LANE, make_uint4(out[0], out[1], out[2], out[3]));
+    }
+    // per-row reductions over the row's LPR lanes (aligned lane segments)
+    int p = npres, f = nfail;
+#pragma unroll
+    for (int o = LPR / 2; o >= 1; o >>= 1) {
+      p += __shfl_xor(p, o, 64);
+      f += __shfl_xor(f, o, 64);
+    }
+    int x = nev;
+#pragma unroll
+    for (int o = 1; o < LPR; o <<= 1) {
+      const int y = __shfl_up(x, o, 64);
+      if (li >= o) x += y;
+    }
+    const int tot = __shfl(x, sub * LPR + LPR - 1, 64);
+    const int E = s.evs;
+    uint32_t sbase = 0;  // one spill-ring reservation per (row, band) that overflows its slots
+    if (live && li == 0 && tot > E) sbase = atomicAdd(s.ev_spill_cnt, (uint32_t)(tot - E));
+    sbase = __shfl(sbase, sub * LPR, 64);
+    if (live && nev) {
+      int slot = x - nev;
+      uint32_t *slots = s.ev_band + ((size_t)r * s.nb + band) * E;
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        const uint32_t kind = (evk >> (2 * q)) & 3u;
+        if (!kind) continue;
+        const uint32_t rec = (kind << 30) | (uint32_t)(s.c0 + colb + q + 1);
+        if (slot < E) {
+          slots[slot] = rec;
         } else {
-          const uint32_t sp = atomicAdd(s.ev_spill_cnt, 1u);
+          const uint32_t sp = sbase + (uint32_t)(slot - E);
           if (sp < s.ev_spill_cap) s.ev_spill[sp] = ((uint64_t)(uint32_t)r << 32) | rec;
           else atomicOr(s.err, GM_ERR_EVENTS);
         }
+        slot++;
       }
     }
-    npres += __builtin_popcount(pbits);
-    st<NT>((uint4 *)(trow + base), make_uint4(e[0], e[1], e[2], e[3]));
-    st<NT>((uint4 *)(trow + base + 4), make_uint4(e[4], e[5], e[6], e[7]));
-    st<NT>((uint4 *)(mout + base), make_uint4(out[0], out[1], out[2], out[3]));
-    ((uint8_t *)s_pres)[base >> 3] = (uint8_t)pbits;
-    ((uint8_t *)s_fresh)[base >> 3] = (uint8_t)fbits;
+    if (li == 0 && r < s.n)
+      s.bcnt[(size_t)r * s.nb + band] = live ? ((uint32_t)p | ((uint32_t)f << 11) | ((uint32_t)min(tot, 1023) << 22)) : 0u;
   }
+}
 
-  // row totals and rank-select prefix over the presence bitmap
-  const int size = gm_block_sum(npres, s_tmp);
-  const int numfailed = gm_block_sum(nfail, s_tmp);
-  {
-    const int per = (nw + S_THREADS - 1) / S_THREADS;
-    const int w0 = tid * per, w1 = min(nw, w0 + per);
-    int part = 0;
-    for (int w = w0; w < w1; w++) part += __builtin_popcountll(s_pres[w]);
-    int tot;
-    int acc = gm_block_scan(part, s_tmp, &tot);
-    for (int w = w0; w < w1; w++) {
-      s_pre[w] = (uint32_t)acc;
-      acc += __builtin_popcountll(s_pres[w]);
+// ------------------------------------------------------- wave-per-row helpers
+// Row totals over this shard's bands; fills pre[0, nb) with the exclusive prefix of
+// the bands' present counts (LDS, this wave only).
+__device__ __forceinline__ void gm_row_totals(const SState &s, int r, int lane, uint32_t *pre, uint32_t &size,
+                                              uint32_t &nfail) {
+  const int nb = s.nb, per = (nb + 63) >> 6;
+  const int b0 = min(nb, lane * per), b1 = min(nb, b0 + per);
+  const uint32_t *bc = s.bcnt + (size_t)r * nb;
+  uint32_t ps = 0, fs = 0;
+  for (int b = b0; b < b1; b++) {
+    const uint32_t v = bc[b];
+    ps += S_BC_PRES(v);
+    fs += S_BC_FAIL(v);
+  }
+  uint32_t x = ps;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) fs += __shfl_xor(fs, o, 64);
+  size = __shfl(x, 63, 64);
+  nfail = fs;
+  if (pre) {
+    uint32_t a = x - ps;
+    for (int b = b0; b < b1; b++) {
+      pre[b] = a;
+      a += S_BC_PRES(bc[b]);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
+// Resolve up to 4 draws at once, one per 16-lane group: group g holds shard-local
+// rank ix_g (valid iff act_g) of a present entry of row r; returns (to every lane of
+// the wave) the shard-local column of each and whether it is fresh (t - ts < TFAIL).
+template <int B>
+__device__ __forceinline__ void gm_resolve4(const SState &s, int r, int t, const uint32_t *pre, bool act, uint32_t ix,
+                                            int lane, int col[4], int fresh[4]) {
+  constexpr int PL = B / 16;  // cells per lane
+  const int gl = lane & 15;
+  int cnt = 0, b = 0;
+  uint32_t en[PL];
+  if (act) {
+    int lo = 0, hi = s.nb - 1;  // largest band with pre[band] <= ix
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (pre[mid] <= ix) lo = mid;
+      else hi = mid - 1;
+    }
+    b = lo;
+    const uint32_t *p = s.table + ((size_t)b * s.n + r) * B + gl * PL;
+#pragma unroll
+    for (int v = 0; v < PL / 4; v++) {
+      const uint4 q = *(const uint4 *)(p + 4 * v);
+      en[4 * v] = q.x;
+      en[4 * v + 1] = q.y;
+      en[4 * v + 2] = q.z;
+      en[4 * v + 3] = q.w;
+    }
+#pragma unroll
+    for (int v = 0; v < PL; v++) cnt += en[v] != GM_ABSENT;
+  }
+  int x = cnt;
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (gl >= o) x += y;
+  }
+  const int excl = x - cnt;
+  int mycol = 0, myfresh = 0;
+  bool holder = false;
+  if (act) {
+    const int q = (int)(ix - pre[b]);
+    if (q >= excl && q < excl + cnt) {
+      holder = true;
+      int need = q - excl;
+#pragma unroll
+      for (int v = 0; v < PL; v++) {
+        if (en[v] != GM_ABSENT) {
+          if (need == 0) {
+            mycol = b * B + gl * PL + v;
+            myfresh = (t - (int)gm_ts(en[v])) < GM_TFAIL;
+          }
+          need--;
+        }
+      }
     }
   }
-  __syncthreads();
+  const uint64_t hm = __ballot(holder);
+#pragma unroll
+  for (int g = 0; g < 4; g++) {
+    const uint32_t seg = (uint32_t)(hm >> (16 * g)) & 0xFFFFu;
+    const int src = seg ? 16 * g + __builtin_ctz(seg) : 0;
+    col[g] = __shfl(mycol, src, 64);
+    fresh[g] = seg ? __shfl(myfresh, src, 64) : 0;
+    if (!seg) col[g] = -1;
+  }
+}
 
-  if (SHARDED) {
-    // publish this shard's slice of the row: counts for the all-gather, bitmaps
-    // and prefix for draw resolution (gm_s_draw); the draw itself needs the
-    // whole row and runs after the exchange
-    uint64_t *gp = s.gpres + (size_t)r * nw, *gf = s.gfresh + (size_t)r * nw;
-    uint32_t *gq = s.gpre + (size_t)r * nw;
-    for (int w = tid; w < nw; w += S_THREADS) {
-      gp[w] = s_pres[w];
-      gf[w] = s_fresh[w];
-      gq[w] = s_pre[w];
-    }
-    if (tid == 0) {
-      int32_t *x = s.xcnt + ((size_t)s.shard_rank * s.n + r) * 2;
-      x[0] = size;
-      x[1] = numfailed;
-      stat[0] = k;
-      s.ev_cnt[r] = s_misc[1];
-    }
+// S2 outputs of a row beyond the precomputed ones: lane 0 runs the lazy generator
+// (state in this wave's LDS), `skip` outputs consumed already; lane q < cnt gets output q.
+__device__ __forceinline__ uint32_t gm_mt_batch(GmLazyMT &mt, uint32_t *mts, uint32_t seed, bool fresh_gen, int skip,
+                                                int cnt, int lane) {
+  if (lane == 0 && fresh_gen) {
+    mt.seed(mts, seed);
+    for (int i = 0; i < skip; i++) (void)mt.next();
+  }
+  uint32_t raw = 0;
+  for (int q = 0; q < cnt; q++) {
+    uint32_t o = 0;
+    if (lane == 0) o = mt.next();
+    o = __shfl(o, 0, 64);
+    if (lane == q) raw = o;
+  }
+  return raw;
+}
+
+// ------------------------------------------------------------------- gm_s_pick
+// Single-context tick, phase 2: one wave per observer row.
+template <int B>
+__global__ __launch_bounds__(256) void gm_s_pick(SState s, int t) {
+  extern __shared__ __align__(16) uint32_t p_smem[];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + wave;
+  if (r >= s.n) return;  // whole wave; no workgroup barrier follows
+  uint32_t *pre = p_smem + wave * s.nb;
+  uint32_t *mts = p_smem + 4 * s.nb + wave * 624;
+  const int par = t & 1;
+  int32_t *stat = s.rowstat + (size_t)r * 4;
+  const int k = s.inbox_cnt[par][r];
+  if (lane == 0) s.inbox_cnt[par][r] = 0;  // consumed by gm_s_band; the append target of tick t+2
+  if (s.failed[r]) {
+    if (lane == 0) stat[0] = stat[1] = stat[2] = stat[3] = 0;
     return;
   }
-
-  if (tid == 0) {
-    // gossip-target draw on the post-sweep list (MP1Node.cpp:449-489); newNodes is
-    // empty in the converged SCALED regime (no JOINREQ traffic)
-    const int numpot = size - 1 - numfailed;
-    int n = 0;
-    int g[GM_FANOUT];
-    if (numpot > 0) {
-      GmLazyMT mt;
-      mt.seed(s_mt, gm_rd_seed(s.rd_seed, t, r + 1));
-      long guard = 0;
-      while (n < GM_FANOUT && n < numpot) {
-        if (++guard > (1l << 22)) { atomicOr(s.err, GM_ERR_DRAWS); break; }
-        const int ix = mt.uniform((uint32_t)size);
-        const int c = gm_rank_select(s_pres, s_pre, nw, (uint32_t)ix);
-        if (c == selfc) continue;                                 // "me"
-        if (!((s_fresh[c >> 6] >> (c & 63)) & 1ull)) continue;    // age >= TFAIL
-        bool dup = false;
-        for (int q = 0; q < n; q++) dup |= g[q] == c;
-        if (!dup) g[n++] = c;
+  uint32_t size, numfailed;
+  gm_row_totals(s, r, lane, pre, size, numfailed);
+  const int numpot = (int)size - 1 - (int)numfailed;  // numfailed counts removed entries too (MP1Node.cpp:463)
+  const int target = min(GM_FANOUT, numpot);
+  int n = 0, g0 = -1, g1 = -1, g2 = -1, g3 = -1, g4 = -1;
+  if (numpot > 0) {
+    const uint32_t thr = (0u - size) % size;  // Lemire rejection threshold (uniform_int_dist.h)
+    GmLazyMT mt;
+    bool done = false;
+    for (int batch = 0; !done; batch++) {
+      if (batch > (1 << 18)) {
+        if (lane == 0) atomicOr(s.err, GM_ERR_DRAWS);
+        break;
+      }
+      uint32_t raw = 0;
+      if (batch == 0) {
+        if (lane < S_MT_RAW) raw = s.mtraw[(size_t)r * S_MT_RAW + lane];
+      } else {
+        raw = gm_mt_batch(mt, mts, gm_rd_seed(s.rd_seed, t, r + 1), batch == 1, S_MT_RAW, S_MT_RAW, lane);
+      }
+      const uint64_t prod = (uint64_t)raw * size;
+      const bool ok = lane < S_MT_RAW && (uint32_t)prod >= thr;
+      const uint32_t ix = (uint32_t)(prod >> 32);
+      uint64_t m = __ballot(ok);
+      while (m && !done) {
+        int d[4], cnt = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          d[i] = m ? __builtin_ctzll(m) : 0;
+          if (m) {
+            m &= m - 1;
+            cnt++;
+          }
+        }
+        const int grp = lane >> 4;
+        const int myd = grp == 0 ? d[0] : grp == 1 ? d[1] : grp == 2 ? d[2] : d[3];
+        const uint32_t myix = __shfl(ix, myd, 64);
+        int col[4], fr[4];
+        gm_resolve4<B>(s, r, t, pre, grp < cnt, myix, lane, col, fr);
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          if (i >= cnt || done) continue;
+          const int c = s.c0 + col[i];
+          if (c == r) continue;  // "me" (MP1Node.cpp:470)
+          if (!fr[i]) continue;  // age >= TFAIL (MP1Node.cpp:471)
+          if ((n > 0 && g0 == c) || (n > 1 && g1 == c) || (n > 2 && g2 == c) || (n > 3 && g3 == c)) continue;
+          if (n == 0) g0 = c;
+          else if (n == 1) g1 = c;
+          else if (n == 2) g2 = c;
+          else if (n == 3) g3 = c;
+          else g4 = c;
+          n++;
+          if (n >= target) done = true;
+        }
       }
     }
+  }
+  if (lane == 0) {
     int32_t *cnt_out = s.inbox_cnt[par ^ 1];
+    const int g[GM_FANOUT] = {g0, g1, g2, g3, g4};
     for (int q = 0; q < n; q++) {
-      const int dst = s.c0 + g[q];
+      const int dst = g[q];
       s.targets[(size_t)r * GM_FANOUT + q] = dst;
       const int slot = atomicAdd(&cnt_out[dst], 1);
       if (slot < S_KMAX) s.inbox[par ^ 1][(size_t)dst * S_KMAX + slot] = r;
       else atomicOr(s.err, GM_ERR_INBOX);
     }
     stat[0] = k;
-    stat[1] = size;
-    stat[2] = numfailed;
+    stat[1] = (int)size;
+    stat[2] = (int)numfailed;
     stat[3] = n;
-    s.ev_cnt[r] = s_misc[1];
   }
 }
 
-__global__ __launch_bounds__(S_THREADS) void gm_s_tick(SState s, int t, int drop_pct) {
-  gm_s_tick_body<false, false>(s, t, drop_pct);
-}
-// same, with non-temporal table / payload-write streams (default; GM_NT=0 selects gm_s_tick)
-__global__ __launch_bounds__(S_THREADS) void gm_s_tick_nt(SState s, int t, int drop_pct) {
-  gm_s_tick_body<false, true>(s, t, drop_pct);
-}
-
-// Column-sharded phase A: merge + sweep of this shard's columns for every row.
-__global__ __launch_bounds__(S_THREADS) void gm_s_tick_shard(SState s, int t, int drop_pct) {
-  gm_s_tick_body<true, false>(s, t, drop_pct);
-}
-
-// Column-sharded phase B: each rank replays every live row's S2 stream (the
-// same mt19937 + Lemire sequence on every rank), and resolves the draws whose
-// rank lands in its own columns: status = (global column << 1) | fresh, else -1.
-// round 0 seeds the generators and the acceptance state from the all-gathered
-// per-shard (present, numfailed) counts.
-__global__ __launch_bounds__(256) void gm_s_draw(SState s, int t, int round, int D) {
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+// ---------------------------------------------------------- column-sharded mode
+// Phase A2: this shard's per-row (present, numfailed) for the all-gather.
+__global__ __launch_bounds__(256) void gm_s_count(SState s, int t) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + wave;
   if (r >= s.n) return;
-  const int G = s.shard_count, nw = s.wp >> 6;
+  uint32_t size = 0, nf = 0;
+  if (!s.failed[r]) gm_row_totals(s, r, lane, nullptr, size, nf);
+  if (lane == 0) {
+    int32_t *x = s.xcnt + ((size_t)s.shard_rank * s.n + r) * 2;
+    x[0] = (int)size;
+    x[1] = (int)nf;
+    const int par = t & 1;
+    s.rowstat[(size_t)r * 4] = s.failed[r] ? 0 : s.inbox_cnt[par][r];
+    s.inbox_cnt[par][r] = 0;  // consumed by gm_s_band; the append target of tick t+2
+  }
+}
+
+// Phase B: every rank replays every pending row's S2 stream (round 0: outputs
+// [0, 16) from gm_s_mtgen; round q >= 1: [16 + 64(q-1), 16 + 64q) from the lazy
+// generator) and resolves the draws whose rank lands in its own columns.
+// status[r][d] = -2 for an output Lemire rejects (same on every rank),
+// (global column << 1) | fresh on the owning rank, -1 elsewhere (MAX-allreduced).
+template <int B>
+__global__ __launch_bounds__(256) void gm_s_draw(SState s, int t, int round, int D) {
+  extern __shared__ __align__(16) uint32_t p_smem[];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + wave;
+  if (r >= s.n) return;
+  uint32_t *pre = p_smem + wave * s.nb;
+  uint32_t *mts = p_smem + 4 * s.nb + wave * 624;
+  const int G = s.shard_count;
   int32_t *acc = s.acc + (size_t)r * 8;
-  int32_t *mtk = s.mtk + (size_t)r * 3;
   if (round == 0) {
     int size = 0, nf = 0;
     for (int g = 0; g < G; g++) {
@@ -298,58 +554,71 @@ __global__ __launch_bounds__(256) void gm_s_draw(SState s, int t, int round, int
     }
     const int numpot = size - 1 - nf;
     const bool live = !s.failed[r];
-    acc[0] = 0;
-    acc[6] = numpot;
-    acc[7] = size;
-    s.pending[r] = live && numpot > 0;
-    int32_t *stat = s.rowstat + (size_t)r * 4;
-    if (!live) stat[0] = 0;
-    stat[1] = live ? size : 0;
-    stat[2] = live ? nf : 0;
-    stat[3] = 0;
-    if (!s.pending[r]) return;
-    GmLazyMT mt;
-    mt.seed(s.mt + r, gm_rd_seed(s.rd_seed, t, r + 1), s.n);
-    mtk[0] = mt.k;
-    mtk[1] = mt.ninit;
-    mtk[2] = 1;
+    const bool pend = live && numpot > 0;
+    if (lane == 0) {
+      acc[0] = 0;
+      acc[6] = numpot;
+      acc[7] = size;
+      s.pending[r] = pend;
+      int32_t *stat = s.rowstat + (size_t)r * 4;
+      stat[1] = live ? size : 0;
+      stat[2] = live ? nf : 0;
+      stat[3] = 0;
+    }
+    if (!pend) return;
+  } else if (!s.pending[r]) {
+    return;
   }
-  if (!s.pending[r]) return;
-  GmLazyMT mt;
-  mt.x = s.mt + r;
-  mt.stride = s.n;
-  mt.k = mtk[0];
-  mt.ninit = mtk[1];
-  mt.first = mtk[2] != 0;
   const uint32_t size = (uint32_t)acc[7];
+  uint32_t own_lo = 0;
+  for (int g = 0; g < s.shard_rank; g++) own_lo += (uint32_t)s.xcnt[((size_t)g * s.n + r) * 2];
+  const uint32_t own_cnt = (uint32_t)s.xcnt[((size_t)s.shard_rank * s.n + r) * 2];
+  uint32_t osz, onf;
+  gm_row_totals(s, r, lane, pre, osz, onf);
+  const uint32_t thr = (0u - size) % size;
+  GmLazyMT mt;
   int32_t *st = s.status + (size_t)r * D;
-  for (int d = 0; d < D; d++) {
-    const uint32_t ix = (uint32_t)mt.uniform(size);
-    // which shard holds the ix-th present entry of row r (shards in column order)
-    uint32_t pre = 0;
-    int owner = G - 1;
-    for (int g = 0; g < G; g++) {
-      const uint32_t c = (uint32_t)s.xcnt[((size_t)g * s.n + r) * 2];
-      if (ix < pre + c) { owner = g; break; }
-      pre += c;
+  for (int d0 = 0; d0 < D; d0 += 64) {
+    const int cnt = min(64, D - d0);
+    uint32_t raw = 0;
+    if (round == 0) {
+      if (lane < cnt) raw = s.mtraw[(size_t)r * S_MT_RAW + d0 + lane];
+    } else {
+      raw = gm_mt_batch(mt, mts, gm_rd_seed(s.rd_seed, t, r + 1), d0 == 0, S_MT_RAW + 64 * (round - 1) + d0, cnt,
+                        lane);
     }
-    int32_t v = -1;
-    if (owner == s.shard_rank) {
-      const int cl = gm_rank_select(s.gpres + (size_t)r * nw, s.gpre + (size_t)r * nw, nw, ix - pre);
-      const int fresh = (int)((s.gfresh[(size_t)r * nw + (cl >> 6)] >> (cl & 63)) & 1ull);
-      v = ((s.c0 + cl) << 1) | fresh;
+    const uint64_t prod = (uint64_t)raw * size;
+    const bool ok = lane < cnt && (uint32_t)prod >= thr;
+    const uint32_t ix = (uint32_t)(prod >> 32);
+    const bool mine = ok && ix >= own_lo && ix < own_lo + own_cnt;
+    int32_t val = ok ? -1 : -2;
+    uint64_t m = __ballot(mine);
+    while (m) {
+      int d[4], c4 = 0;
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        d[i] = m ? __builtin_ctzll(m) : 0;
+        if (m) {
+          m &= m - 1;
+          c4++;
+        }
+      }
+      const int grp = lane >> 4;
+      const int myd = grp == 0 ? d[0] : grp == 1 ? d[1] : grp == 2 ? d[2] : d[3];
+      const uint32_t myix = __shfl(ix, myd, 64) - own_lo;
+      int col[4], fr[4];
+      gm_resolve4<B>(s, r, t, pre, grp < c4, myix, lane, col, fr);
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+        if (i < c4 && lane == d[i]) val = col[i] < 0 ? -1 : (((s.c0 + col[i]) << 1) | fr[i]);
     }
-    st[d] = v;
+    if (lane < cnt) st[d0 + lane] = val;
   }
-  mtk[0] = mt.k;
-  mtk[1] = mt.ninit;
-  mtk[2] = mt.first ? 1 : 0;
 }
 
-// Column-sharded phase C: with every draw resolved (MAX-allreduced status), run
-// the acceptance loop of MP1Node.cpp:466-489 (skip me, skip stale, skip
-// duplicates) identically on every rank; finished rows enqueue themselves into
-// their targets' inboxes for the next tick.
+// Phase C: with every draw resolved (MAX-allreduced status), run the acceptance loop
+// of MP1Node.cpp:466-489 (skip me, skip stale, skip duplicates) identically on every
+// rank; finished rows enqueue themselves into their targets' inboxes for tick t+1.
 __global__ __launch_bounds__(256) void gm_s_accept(SState s, int t, int D) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= s.n || !s.pending[r]) return;
@@ -362,10 +631,15 @@ __global__ __launch_bounds__(256) void gm_s_accept(SState s, int t, int D) {
   bool done = false;
   for (int d = 0; d < D && !done; d++) {
     const int32_t v = st[d];
-    if (v < 0) { atomicOr(s.err, GM_ERR_DRAWS); done = true; break; }
+    if (v == -2) continue;  // output rejected by Lemire: not a draw
+    if (v < 0) {            // a draw no shard resolved
+      atomicOr(s.err, GM_ERR_DRAWS);
+      done = true;
+      break;
+    }
     const int c = v >> 1;
-    if (c == r) continue;        // "me"
-    if (!(v & 1)) continue;      // age >= TFAIL (skipfailed: numpot > 0 here)
+    if (c == r) continue;    // "me"
+    if (!(v & 1)) continue;  // age >= TFAIL
     bool dup = false;
     for (int q = 0; q < n; q++) dup |= g[q] == c;
     if (!dup) g[n++] = c;
@@ -396,7 +670,6 @@ __global__ __launch_bounds__(256) void gm_s_accept(SState s, int t, int D) {
 // gossiping, so the first ticks carry no mass-staleness transient. Padding absent.
 __global__ void gm_s_init(SState s, int warm, int t0, uint64_t seed) {
   const int r = blockIdx.x;
-  uint32_t *row = s.table + (size_t)r * s.wp;
   for (int j = threadIdx.x; j < s.wp; j += blockDim.x) {
     uint32_t e = GM_ABSENT;
     if (j < s.w) {
@@ -408,7 +681,60 @@ __global__ void gm_s_init(SState s, int warm, int t0, uint64_t seed) {
         e = gm_pack((uint32_t)(2 * (t0 - 1 - a) - 1), (uint32_t)(t0 - a));
       }
     }
-    row[j] = e;
+    s.table[((size_t)(j / s.band) * s.n + r) * s.band + j % s.band] = e;
   }
   if (threadIdx.x == 0) s.hbctr[r] = warm ? 2 * t0 : 0;
+}
+
+// ------------------------------------------------------------ launch wrappers
+// (template dispatch over the band width; called by gm_host.hip)
+template <int B>
+static hipError_t launch_tick_b(const SState &s, int t, int drop_pct, bool nt, hipStream_t st, hipEvent_t k0,
+                                hipEvent_t k1, bool pick) {
+  const int nblk = (int)(((int64_t)s.nb * ((s.n + 64 / (B / S_COLS_PER_LANE) - 1) / (64 / (B / S_COLS_PER_LANE))) + 3) / 4);
+  // the event records of a tick (per-(row, band) slots + spill ring) stay readable until the next tick
+  (void)hipMemsetAsync(s.ev_spill_cnt, 0, sizeof(uint32_t), st);
+  hipLaunchKernelGGL(gm_s_mtgen, dim3((s.n + 255) / 256), dim3(256), 0, st, s, t);
+  if (k0) (void)hipEventRecord(k0, st);
+  if (drop_pct >= 0) hipLaunchKernelGGL((gm_s_band<B, true>), dim3(nblk), dim3(256), 0, st, s, t, drop_pct);
+  else hipLaunchKernelGGL((gm_s_band<B, false>), dim3(nblk), dim3(256), 0, st, s, t, drop_pct);
+  if (k1) (void)hipEventRecord(k1, st);
+  const size_t smem = sizeof(uint32_t) * 4 * (size_t)(s.nb + 624);
+  if (pick) hipLaunchKernelGGL((gm_s_pick<B>), dim3((s.n + 3) / 4), dim3(256), smem, st, s, t);
+  else hipLaunchKernelGGL(gm_s_count, dim3((s.n + 3) / 4), dim3(256), 0, st, s, t);
+  return hipGetLastError();
+}
+
+hipError_t gm_launch_tick(const SState &s, int t, int drop_pct, bool nt, hipStream_t st, hipEvent_t k0, hipEvent_t k1,
+                          bool pick) {
+  switch (s.band) {
+    case 64: return launch_tick_b<64>(s, t, drop_pct, nt, st, k0, k1, pick);
+    case 128: return launch_tick_b<128>(s, t, drop_pct, nt, st, k0, k1, pick);
+    case 256: return launch_tick_b<256>(s, t, drop_pct, nt, st, k0, k1, pick);
+    case 512: return launch_tick_b<512>(s, t, drop_pct, nt, st, k0, k1, pick);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t gm_launch_draw(const SState &s, int t, int round, int D, hipStream_t st) {
+  const size_t smem = sizeof(uint32_t) * 4 * (size_t)(s.nb + 624);
+  const dim3 grid((s.n + 3) / 4), blk(256);
+  switch (s.band) {
+    case 64: hipLaunchKernelGGL(gm_s_draw<64>, grid, blk, smem, st, s, t, round, D); break;
+    case 128: hipLaunchKernelGGL(gm_s_draw<128>, grid, blk, smem, st, s, t, round, D); break;
+    case 256: hipLaunchKernelGGL(gm_s_draw<256>, grid, blk, smem, st, s, t, round, D); break;
+    case 512: hipLaunchKernelGGL(gm_s_draw<512>, grid, blk, smem, st, s, t, round, D); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t gm_launch_accept(const SState &s, int t, int D, hipStream_t st) {
+  hipLaunchKernelGGL(gm_s_accept, dim3((s.n + 255) / 256), dim3(256), 0, st, s, t, D);
+  return hipGetLastError();
+}
+
+hipError_t gm_launch_init(const SState &s, int warm, int t0, uint64_t seed, hipStream_t st) {
+  hipLaunchKernelGGL(gm_s_init, dim3(s.n), dim3(256), 0, st, s, warm, t0, seed);
+  return hipGetLastError();
 }

@@ -24,7 +24,7 @@ class GmConfig(ctypes.Structure):
                 ("drop_seed", ctypes.c_uint64),
                 ("device", ctypes.c_int32), ("shard_rank", ctypes.c_int32), ("shard_count", ctypes.c_int32),
                 ("init_mode", ctypes.c_int32), ("init_t0", ctypes.c_int32), ("init_seed", ctypes.c_uint64),
-                ("reserved", ctypes.c_int32 * 4)]
+                ("band", ctypes.c_int32), ("reserved", ctypes.c_int32 * 3)]
 
 
 class GmEvent(ctypes.Structure):
@@ -108,7 +108,7 @@ class Simulator:
 
     def __init__(self, n, mode=GM_MODE_FAITHFUL, single_failure=1, drop_msg=0, drop_prob=0.1, time_seed=0,
                  rd_seed=0, drop_pct=0, drop_from=0, drop_to=0, drop_seed=0, device=0, shard_rank=0, shard_count=1,
-                 init_mode=0, init_t0=0, init_seed=0):
+                 init_mode=0, init_t0=0, init_seed=0, band=0):
         self.lib = load_library()
         cfg = GmConfig()
         cfg.abi_version = GM_ABI_VERSION
@@ -118,6 +118,7 @@ class Simulator:
         cfg.drop_pct, cfg.drop_from, cfg.drop_to, cfg.drop_seed = drop_pct, drop_from, drop_to, drop_seed
         cfg.device, cfg.shard_rank, cfg.shard_count = device, shard_rank, shard_count
         cfg.init_mode, cfg.init_t0, cfg.init_seed = init_mode, init_t0, init_seed
+        cfg.band = band
         self.cfg = cfg
         self.n = n
         self.mode = mode

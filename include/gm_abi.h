@@ -95,7 +95,8 @@ typedef struct gm_config {
   int32_t init_mode;
   int32_t init_t0;
   uint64_t init_seed;
-  int32_t reserved[4];
+  int32_t band;            /* SCALED columns per band of the tick kernel (64/128/256/512; 0 = auto) */
+  int32_t reserved[3];
 } gm_config;
 
 /* one log record; `order` sorts records of a drain into reference log order */

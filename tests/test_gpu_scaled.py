@@ -14,13 +14,13 @@ pytestmark = pytest.mark.gpu
 
 
 def run_pair(n, ticks, crash_tick, crash_count, drop_pct=0, drop_from=0, drop_to=0, rd_seed=7, seed=42, seen=None,
-             init_mode=0, init_t0=0):
+             init_mode=0, init_t0=0, band=0):
     init = dict(init_mode=init_mode, init_t0=init_t0, init_seed=seed + 1)
     ora = oracle_py.Oracle(n, oracle_py.OC_SCALED, rd_seed=rd_seed, crash_tick=crash_tick, crash_count=crash_count,
                            crash_seed=seed, drop_pct=drop_pct, drop_from=drop_from, drop_to=drop_to, drop_seed=seed,
                            **init)
     sim = Simulator(n, GM_MODE_SCALED, rd_seed=rd_seed, drop_pct=drop_pct, drop_from=drop_from, drop_to=drop_to,
-                    drop_seed=seed, **init)
+                    drop_seed=seed, band=band, **init)
     crash = crash_set(n, crash_count, seed)
     assert np.array_equal(crash, oracle_py.crash_set(n, crash_count, seed))
     kinds = {GM_EV_JOINED: 1, GM_EV_REMOVED: 2}
@@ -45,6 +45,13 @@ def run_pair(n, ticks, crash_tick, crash_count, drop_pct=0, drop_from=0, drop_to
 @pytest.mark.parametrize("n", [64, 300, 1024])
 def test_scaled_matches_oracle(n):
     run_pair(n, 40, crash_tick=8, crash_count=max(1, n // 50))
+
+
+@pytest.mark.parametrize("band", [64, 128, 256, 512])
+def test_scaled_every_band_width_matches_oracle(band):
+    # the band width changes only the tiling of gm_s_band / the rank-select of gm_s_pick
+    run_pair(700, 36, crash_tick=9, crash_count=9, drop_pct=15, drop_from=4, drop_to=22, init_mode=1, init_t0=7,
+             band=band)
 
 
 @pytest.mark.parametrize("n", [200, 777])
