@@ -200,17 +200,17 @@ static int create_faithful(gm_ctx *c) {
 }
 
 // Band width of the SCALED tick: the largest of 512/256/128/64 columns (dividing
-// the padded row) whose per-band traffic -- N rows x band x (4 B table read +
-// 4 B write + 2 B payload write + 2 B payload read) -- stays within ~160 MB, so
-// a band's payload slices stay resident in the 256 MiB Infinity Cache across
-// their ~5 readers (gm_scaled.hip). gm_config.band / env GM_BAND override.
+// the padded row) whose per-band traffic -- N rows x band x (2 B cell read + 2 B
+// write + 1 B payload write + 1 B payload read) -- stays within ~210 MB, so a band's
+// payload slab stays resident in the 256 MiB Infinity Cache across its ~5 readers
+// per sender slice (gm_scaled.hip). gm_config.band / env GM_BAND override.
 static int pick_band(const gm_ctx *c, int n, int wp) {
   int b = c->cfg.band;
   if (!b && getenv("GM_BAND")) b = atoi(getenv("GM_BAND"));
   if (b) return (b == 64 || b == 128 || b == 256 || b == 512) && wp % b == 0 ? b : -1;
-  const double budget = 160e6;
+  const double budget = 210e6;
   for (int cand : {512, 256, 128})
-    if (wp % cand == 0 && 12.0 * n * cand <= budget) return cand;
+    if (wp % cand == 0 && 6.0 * n * cand <= budget) return cand;
   return 64;
 }
 
@@ -230,6 +230,7 @@ static int create_scaled(gm_ctx *c) {
   s.band = pick_band(c, n, s.wp);
   if (s.band < 0) return GM_EINVAL;
   s.nb = s.wp / s.band;
+  if ((size_t)n * s.band * 2 >= (1ull << 31)) return GM_EUNSUPPORTED;  // 32-bit buffer offsets per band slab
   s.evs = s.band / 32;
   if (sizeof(uint32_t) * 4 * (size_t)(s.nb + 624) > 65536) return GM_EUNSUPPORTED;  // draw kernels' LDS
   s.ev_spill_cap = 1u << 24;
@@ -244,6 +245,7 @@ static int create_scaled(gm_ctx *c) {
     TRY(dalloc(c, &s.inbox[p], (size_t)n * S_KMAX));
   }
   TRY(dalloc(c, &s.hbctr, n));
+  TRY(dalloc(c, &s.wtick, n));
   TRY(dalloc(c, &s.failed, n));
   TRY(dalloc(c, &s.bcnt, (size_t)n * s.nb));
   TRY(dalloc(c, &s.ev_band, (size_t)n * s.nb * s.evs));
@@ -257,7 +259,7 @@ static int create_scaled(gm_ctx *c) {
   const bool warm = c->cfg.init_mode == 1;
   const int t0 = warm ? c->cfg.init_t0 : 0;
   if (c->cfg.init_mode < 0 || c->cfg.init_mode > 1 || (warm && (t0 < 5 || t0 > GM_T_LIMIT / 2))) return GM_EINVAL;
-  HIPCHECK(hipMemset(s.msg, 0xFF, sizeof(uint16_t) * 2 * cells));
+  HIPCHECK(hipMemset(s.msg, 0, sizeof(uint8_t) * 2 * cells));
   for (int p = 0; p < 2; p++) HIPCHECK(hipMemset(s.inbox_cnt[p], 0, sizeof(int32_t) * n));
   HIPCHECK(hipMemset(s.failed, 0, sizeof(int32_t) * n));
   HIPCHECK(gm_launch_init(s, warm ? 1 : 0, t0, c->cfg.init_seed, c->stream));
@@ -528,34 +530,48 @@ extern "C" int gm_msgcount(gm_ctx *c, int32_t t, int32_t *sent, int32_t *recv) {
   return GM_OK;
 }
 
-static int read_table_row(gm_ctx *c, int r, std::vector<uint32_t> &row, int &w) {
+// Row r of this context's table as absolute (hb, ts) per column, -1 = absent.
+static int read_table_row(gm_ctx *c, int r, std::vector<int32_t> &hb, std::vector<int32_t> &ts, int &w) {
   if (c->cfg.mode == GM_MODE_FAITHFUL) {
     w = c->n;
-    row.resize(w);
+    std::vector<uint32_t> row(w);
     HIPCHECK(hipMemcpy(row.data(), c->f.table + (size_t)r * c->f.np, sizeof(uint32_t) * w, hipMemcpyDeviceToHost));
+    hb.resize(w);
+    ts.resize(w);
+    for (int j = 0; j < w; j++) {
+      hb[j] = row[j] == GM_ABSENT ? -1 : (int32_t)(row[j] & 0xFFFF);
+      ts[j] = row[j] == GM_ABSENT ? -1 : (int32_t)(row[j] >> 16);
+    }
     return GM_OK;
   }
   const SState &s = c->s;  // band-tiled: one B-cell piece of the row per band slab
   w = s.w;  // this context's columns
-  row.resize(s.wp);
-  const size_t piece = sizeof(uint32_t) * s.band;
+  std::vector<uint16_t> row(s.wp);
+  int32_t wt = 0;
+  const size_t piece = sizeof(uint16_t) * s.band;
   HIPCHECK(hipMemcpy2D(row.data(), piece, s.table + (size_t)r * s.band, piece * s.n, piece, s.nb,
                        hipMemcpyDeviceToHost));
-  row.resize(w);
+  HIPCHECK(hipMemcpy(&wt, s.wtick + r, sizeof wt, hipMemcpyDeviceToHost));
+  hb.resize(w);
+  ts.resize(w);
+  for (int j = 0; j < w; j++) {  // cells are relative to the row's last written tick
+    const uint32_t e = row[j];
+    hb[j] = e == 0 ? -1 : 2 * wt - 255 + (int32_t)S_H(e);
+    ts[j] = e == 0 ? -1 : wt - (int32_t)S_AGE(e);
+  }
   return GM_OK;
 }
 
 extern "C" int gm_read_row(gm_ctx *c, int32_t r, int32_t c0, int32_t len, int32_t *hb, int32_t *ts) {
   if (!c || !hb || !ts || r < 0 || r >= c->n || c0 < 0 || len < 0) return GM_EINVAL;
   HIPCHECK(hipStreamSynchronize(c->stream));
-  std::vector<uint32_t> row;
+  std::vector<int32_t> rh, rt;
   int w;
-  TRY(read_table_row(c, r, row, w));
+  TRY(read_table_row(c, r, rh, rt, w));
   if (c0 + len > w) return GM_EINVAL;
   for (int j = 0; j < len; j++) {
-    uint32_t e = row[c0 + j];
-    hb[j] = e == GM_ABSENT ? -1 : (int32_t)(e & 0xFFFF);
-    ts[j] = e == GM_ABSENT ? -1 : (int32_t)(e >> 16);
+    hb[j] = rh[c0 + j];
+    ts[j] = rt[c0 + j];
   }
   return GM_OK;
 }
@@ -592,18 +608,18 @@ extern "C" int gm_dump_tables(gm_ctx *c, char *buf, size_t cap, size_t *len) {
   std::string out;
   char tmp[96];
   const int t = c->t - 1;
-  std::vector<uint32_t> row;
+  std::vector<int32_t> rh, rt;
   for (int i = 0; i < c->n; i++) {
     int w;
-    TRY(read_table_row(c, i, row, w));
+    TRY(read_table_row(c, i, rh, rt, w));
     int cnt = 0;
     const int c0 = c->cfg.mode == GM_MODE_FAITHFUL ? 0 : c->s.c0;
-    for (int j = 0; j < w; j++) cnt += row[j] != GM_ABSENT;
+    for (int j = 0; j < w; j++) cnt += rh[j] >= 0;
     snprintf(tmp, sizeof tmp, "%d %d %d %d %d %d %d", t, i, st[4 * i], st[4 * i + 1], st[4 * i + 2], st[4 * i + 3], cnt);
     out += tmp;
     for (int j = 0; j < w; j++) {
-      if (row[j] == GM_ABSENT) continue;
-      snprintf(tmp, sizeof tmp, " %d:%u:%u", c0 + j + 1, row[j] & 0xFFFFu, row[j] >> 16);
+      if (rh[j] < 0) continue;
+      snprintf(tmp, sizeof tmp, " %d:%d:%d", c0 + j + 1, rh[j], rt[j]);
       out += tmp;
     }
     out += "\n";

@@ -3,10 +3,24 @@
 #include <stdint.h>
 
 #define S_KMAX 64                // inbox capacity (gossip lists per receiver per tick)
-#define S_COLS_PER_LANE 8        // 32 B of table + 16 B per sender payload per lane and row
+#define S_COLS_PER_LANE 16       // 32 B of table + 16 B per sender payload per lane and row
 #define S_ROW_ALIGN 512          // padded row width granule (a multiple of every band width)
 #define S_SB 8                   // sender ids prefetched per row; payload loads in flight per lane
 #define S_MT_RAW 16              // mt19937 outputs precomputed per row and tick (gm_s_mtgen)
+
+// SCALED cell (16 bits), relative to the tick w the row was last written at:
+//   h = 255 - (2w - hb) (8 bits, the heartbeat; larger = newer), age = w - ts (5 bits);
+//   cell = h << 5 | age, 0 = absent. Every tick rewrites every live cell, re-basing it
+// to the new tick (h -= 2, age += 1: cell - 63). Ordering cells by value orders them
+// by heartbeat first and, for equal heartbeats, keeps the older timestamp -- so the
+// merge of updatelistCallBack is a max. In the SCALED regime a live node's heartbeat
+// at tick t is 2t-1 (h = 254); h falls by 2 per tick of heartbeat lag, and a present
+// entry lagging more than ~126 ticks sets GM_ERR_LAG instead of wrapping.
+#define S_CELL(h, age) (((h) << 5) | (age))
+#define S_H(c) ((c) >> 5)
+#define S_AGE(c) ((c) & 31u)
+// payload cell (8 bits): h of a fresh entry re-based to the receiving tick (h - 2 >= 1),
+// 0 = not sent.
 
 #define S_EV_ADD 1u
 #define S_EV_REMOVE 2u
@@ -28,8 +42,9 @@ struct SState {
   uint64_t rd_seed, drop_seed;
   // Band-tiled layout: cell (r, c) of band b = c / band lives at ((b * n + r) * band + c % band),
   // so one band of all rows is one contiguous slab (the unit gm_s_band sweeps).
-  uint32_t *table;         // [nb][n][band] packed {hb | ts<<16}, GM_ABSENT
-  uint16_t *msg;           // [nb][n][2][band] gossip payloads, both tick parities of a (band, row) adjacent
+  uint16_t *table;         // [nb][n][band] S_CELL
+  uint8_t *msg;            // [nb][n][2][band] gossip payload cells, both tick parities of a (band, row) adjacent
+  int32_t *wtick;          // [n] tick each row's cells are relative to (last written)
   int32_t *inbox_cnt[2];   // [n] lists queued for each receiver, by delivery-tick parity
   int32_t *inbox[2];       // [n][S_KMAX] sender rows
   int32_t *hbctr;          // [n] MP1Node heartbeat counter (Member::heartbeat)

@@ -33,27 +33,8 @@
 
 #include <algorithm>
 
-typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ u16x2 as_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
-__device__ __forceinline__ uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
-
-// merge key of one payload word pair: hb+1, NONE (0xFFFF) -> 0
-__device__ __forceinline__ u16x2 key2(uint32_t m) { return as_u16x2(m) + (u16x2)(1); }
-
-// 16-byte row-stream accesses, optionally non-temporal
-template <bool NT>
-__device__ __forceinline__ uint4 ld(const uint32_t *p) {
-  u32x4 v = NT ? __builtin_nontemporal_load((const u32x4 *)p) : *(const u32x4 *)p;
-  return make_uint4(v.x, v.y, v.z, v.w);
-}
-template <bool NT>
-__device__ __forceinline__ void st(void *p, uint4 v) {
-  u32x4 w = {v.x, v.y, v.z, v.w};
-  if (NT) __builtin_nontemporal_store(w, (u32x4 *)p);
-  else *(u32x4 *)p = w;
-}
+typedef uint8_t u8x16 __attribute__((ext_vector_type(16)));
 
 __device__ __forceinline__ uint32_t mt_temper(uint32_t v) {
   v ^= v >> 11;
@@ -125,179 +106,239 @@ __device__ __forceinline__ RowMeta<B> row_meta(const SState &s, int r, int par) 
   return m;
 }
 
+// Buffer resource over [p, p + bytes) built from wave-uniform values (SGPRs): loads
+// beyond `bytes` return 0 without touching memory, stores beyond it are dropped.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t gm_rsrc(const void *p, uint32_t bytes) {
+  const uint64_t a = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), (short)0,
+                                           (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+#define GM_AUX_NT 2  // non-temporal (streamed once)
+#define GM_OOB 0x80000000u
+
+// Packed 16-bit lanes of a 32-bit register: two cells per VGPR, v_pk_* arithmetic.
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u16x2 pk(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
+__device__ __forceinline__ uint32_t unpk(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+// payload bytes 0,1 / 2,3 of a dword, zero-extended into the two halves
+__device__ __forceinline__ u16x2 bytes01(uint32_t w) { return pk(__builtin_amdgcn_perm(0u, w, 0x0c010c00u)); }
+__device__ __forceinline__ u16x2 bytes23(uint32_t w) { return pk(__builtin_amdgcn_perm(0u, w, 0x0c030c02u)); }
+
 template <int B, bool DROP>
 __global__ __launch_bounds__(256) void gm_s_band(SState s, int t, int drop_pct) {
-  constexpr bool NT = true;  // non-temporal table / payload-write streams
   constexpr int LPR = B / S_COLS_PER_LANE;  // lanes per row
   constexpr int RPW = 64 / LPR;             // rows per wave
+  constexpr int Q = S_COLS_PER_LANE;        // cells per lane (8 packed pairs)
   const int lane = threadIdx.x & 63;
   const int par = t & 1;
   const int sub = lane / LPR, li = lane % LPR;
   const int U = (s.n + RPW - 1) / RPW;  // units per band
-  const int u = blockIdx.x * 4 + (threadIdx.x >> 6);
+  // wave-uniform unit index (scalar registers: the band / row split stays on the SALU)
+  const int u = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
   if (u >= U * s.nb) return;  // whole wave
-  const uint32_t tt = (uint32_t)t;
-  const int t_send = t - 1;
-  const int32_t *inbox = s.inbox[par];
   const int band = u / U;
   const int r = (u - band * U) * RPW + sub;
-  const int colb = band * B + li * S_COLS_PER_LANE;  // shard-local column of this lane's first cell
-  const size_t slab = (size_t)band * s.n;            // this band's slab (rows of the band-tiled layout)
-  const uint16_t *mprev = s.msg + (size_t)(par ^ 1) * B + li * S_COLS_PER_LANE;  // + (slab + sender) * 2B
+  const int colb = band * B + li * Q;  // shard-local column of this lane's first cell
+  const size_t slab = (size_t)band * s.n;
+  // this band's slabs: table [n][B] cells, payload [n][2][B] bytes (32-bit offsets)
+  const __amdgpu_buffer_rsrc_t trs = gm_rsrc(s.table + slab * B, (uint32_t)(s.n * B * 2));
+  const __amdgpu_buffer_rsrc_t prs = gm_rsrc(s.msg + slab * 2 * B, (uint32_t)(s.n * B * 2));
+  const uint32_t toff = (uint32_t)(r * B + li * Q) * 2;            // r >= n: out of range -> zeros, dropped
+  const uint32_t poff = (uint32_t)((par ^ 1) * B + li * Q);        // + sender * 2B
   const RowMeta<B> meta = row_meta<B>(s, r, par);
+  int k = meta.k;
+  if (k > S_KMAX) {
+    if (li == 0) atomicOr(s.err, GM_ERR_INBOX);
+    k = S_KMAX;
+  }
+  const bool live = k >= 0;
+  // issue the table slice (independent of the metadata) and every payload slice at
+  // once; slots j >= k read out of range (zeros = "not sent"), so no branches
+  const u32x4 ta = __builtin_amdgcn_raw_buffer_load_b128(trs, toff, 0, GM_AUX_NT);
+  const u32x4 tb = __builtin_amdgcn_raw_buffer_load_b128(trs, toff + 16, 0, GM_AUX_NT);
+  u32x4 m[S_SB];
+#pragma unroll
+  for (int j = 0; j < S_SB; j++)
+    m[j] = __builtin_amdgcn_raw_buffer_load_b128(prs, (!DROP && j < k) ? poff + (uint32_t)meta.snd[j] * (2 * B) : GM_OOB, 0, 0);
+  // lists to merge in this wave (uniform loop bound)
+  int kw = 0;
   {
-    int k = meta.k;
-    if (k > S_KMAX) {
-      if (li == 0) atomicOr(s.err, GM_ERR_INBOX);
-      k = S_KMAX;
-    }
-    const bool live = k >= 0;
-    int npres = 0, nfail = 0, nev = 0;
-    uint32_t evk = 0;  // 2 bits per cell: event kind
-    uint32_t *trow = s.table + (slab + r) * B + li * S_COLS_PER_LANE;
-    const int32_t *ib = inbox + (size_t)r * S_KMAX;
-    // issue this row's loads (table slice + the prefetched senders' payload slices) ...
-    uint4 ta = make_uint4(0, 0, 0, 0), tb = ta, m[S_SB];
+    const int kl = live ? k : 0;
 #pragma unroll
-    for (int j = 0; j < S_SB; j++) m[j] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
-    if (r < s.n) {  // the table slice does not wait for the metadata
-      ta = ld<NT>(trow);
-      tb = ld<NT>(trow + 4);
-    }
-    if (live && !DROP) {
+    for (int w = 0; w < RPW; w++) kw = max(kw, __builtin_amdgcn_readlane(kl, w * LPR));
+  }
+  int npres = 0, nfail = 0, nev = 0;
+  uint32_t evk = 0;  // 2 bits per cell: event kind
+  if (live) {
+    // merge key per cell = the largest delivered payload h (0 = nothing delivered).
+    // Bytewise max of packed payload words: as u16 lanes, max() is decided by the high
+    // byte, so odd bytes are maxed on the raw words and even bytes on the words
+    // shifted up by 8 within each u16 (3 packed ops per 4 cells per list).
+    u16x2 key[8];
+    const int32_t *ib = s.inbox[par] + (size_t)r * S_KMAX;
+    if (!DROP) {
+      u16x2 ko[4], ke[4];
 #pragma unroll
-      for (int j = 0; j < S_SB; j++)
-        if (j < k) m[j] = *(const uint4 *)(mprev + (slab + meta.snd[j]) * (2 * B));
-    }
-    if (live) {
-      u16x2 k0 = (u16x2)(0), k1 = (u16x2)(0), k2 = (u16x2)(0), k3 = (u16x2)(0);
-      if (!DROP) {
+      for (int i = 0; i < 4; i++) ko[i] = ke[i] = (u16x2)(0);
 #pragma unroll
-        for (int j = 0; j < S_SB; j++) {
-          k0 = __builtin_elementwise_max(k0, key2(m[j].x));
-          k1 = __builtin_elementwise_max(k1, key2(m[j].y));
-          k2 = __builtin_elementwise_max(k2, key2(m[j].z));
-          k3 = __builtin_elementwise_max(k3, key2(m[j].w));
-        }
-        for (int j = S_SB; j < k; j++) {  // rare: more lists than prefetched ids
-          const uint4 mm = *(const uint4 *)(mprev + (slab + ib[j]) * (2 * B));
-          k0 = __builtin_elementwise_max(k0, key2(mm.x));
-          k1 = __builtin_elementwise_max(k1, key2(mm.y));
-          k2 = __builtin_elementwise_max(k2, key2(mm.z));
-          k3 = __builtin_elementwise_max(k3, key2(mm.w));
-        }
-      } else {
-        // per-entry drops keyed by (t_send, src, dst, global column) -- SCALED regime
-        uint32_t kk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        for (int j = 0; j < k; j++) {
-          const int sn = ib[j];
-          const uint4 m = *(const uint4 *)(mprev + (slab + sn) * (2 * B));
-          const uint32_t mw[4] = {m.x, m.y, m.z, m.w};
-          const uint64_t pair = gm_mix64(s.drop_seed ^ ((uint64_t)(uint32_t)t_send << 48) ^
-                                         ((uint64_t)(uint32_t)sn << 24) ^ (uint64_t)(uint32_t)r);
+      for (int j = 0; j < S_SB; j++) {
+        if (j < kw) {
+          const uint32_t w[4] = {m[j].x, m[j].y, m[j].z, m[j].w};
 #pragma unroll
-          for (int q = 0; q < 8; q++) {
-            const uint32_t hv = (mw[q >> 1] >> (16 * (q & 1))) & 0xFFFFu;
-            const uint32_t key = (hv + 1u) & 0xFFFFu;
-            if (key == 0) continue;
-            const uint32_t h = (uint32_t)(gm_mix64(pair + (uint64_t)(s.c0 + colb + q)) >> 32);
-            if ((int)(h % 100u) < drop_pct) continue;
-            kk[q] = kk[q] > key ? kk[q] : key;
+          for (int i = 0; i < 4; i++) {
+            ko[i] = __builtin_elementwise_max(ko[i], pk(w[i]));
+            ke[i] = __builtin_elementwise_max(ke[i], pk(w[i]) << (u16x2)(8));
           }
-        }
-        k0 = as_u16x2(kk[0] | (kk[1] << 16));
-        k1 = as_u16x2(kk[2] | (kk[3] << 16));
-        k2 = as_u16x2(kk[4] | (kk[5] << 16));
-        k3 = as_u16x2(kk[6] | (kk[7] << 16));
-      }
-      const int selfc = (r >= s.c0 && r < s.c0 + s.w) ? r - s.c0 : -1;  // own column, if in this shard
-      uint32_t e[8] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y, tb.z, tb.w};
-      const uint32_t keys[4] = {as_u32(k0), as_u32(k1), as_u32(k2), as_u32(k3)};
-      uint32_t out[4] = {0, 0, 0, 0};
-#pragma unroll
-      for (int q = 0; q < 8; q++) {
-        uint32_t en = e[q];
-        const uint32_t key = (keys[q >> 1] >> (16 * (q & 1))) & 0xFFFFu;
-        uint32_t ev = 0;
-        if (key) {  // updatelistCallBack: insert, or raise hb and stamp ts = now
-          const uint32_t hb = key - 1u;
-          if (en == GM_ABSENT) {
-            en = gm_pack(hb, tt);
-            ev = S_EV_ADD;
-          } else if (gm_hb(en) < hb) {
-            en = gm_pack(hb, tt);
-          }
-        }
-        if (colb + q == selfc) {  // updateMyPos + heartbeat++ + myPos->setheartbeat(heartbeat++)
-          if (en == GM_ABSENT) atomicOr(s.err, GM_ERR_SELF);
-          const int hb = s.hbctr[r] + 1;
-          s.hbctr[r] = hb + 1;
-          en = gm_pack((uint32_t)hb, tt);
-        }
-        uint32_t o = GM_NONE16;
-        if (en != GM_ABSENT) {
-          const int age = t - (int)gm_ts(en);
-          if (age >= GM_TFAIL) {
-            nfail++;
-            if (age >= GM_TREMOVE) {
-              en = GM_ABSENT;
-              ev = S_EV_REMOVE;
-            }
-          } else {
-            o = gm_hb(en);
-          }
-          if (en != GM_ABSENT) npres++;
-        }
-        e[q] = en;
-        out[q >> 1] |= o << (16 * (q & 1));
-        if (ev) {
-          evk |= ev << (2 * q);
-          nev++;
         }
       }
-      st<NT>(trow, make_uint4(e[0], e[1], e[2], e[3]));
-      st<NT>(trow + 4, make_uint4(e[4], e[5], e[6], e[7]));
-      st<NT>(s.msg + ((slab + r) * 2 + par) * B + li * S_COLS_PER_LANE, make_uint4(out[0], out[1], out[2], out[3]));
-    }
-    // per-row reductions over the row's LPR lanes (aligned lane segments)
-    int p = npres, f = nfail;
+      for (int j = S_SB; j < k; j++) {  // rare: more lists than prefetched ids
+        const u32x4 mm = __builtin_amdgcn_raw_buffer_load_b128(prs, poff + (uint32_t)ib[j] * (2 * B), 0, 0);
+        const uint32_t w[4] = {mm.x, mm.y, mm.z, mm.w};
 #pragma unroll
-    for (int o = LPR / 2; o >= 1; o >>= 1) {
-      p += __shfl_xor(p, o, 64);
-      f += __shfl_xor(f, o, 64);
+        for (int i = 0; i < 4; i++) {
+          ko[i] = __builtin_elementwise_max(ko[i], pk(w[i]));
+          ke[i] = __builtin_elementwise_max(ke[i], pk(w[i]) << (u16x2)(8));
+        }
+      }
+      // cells 4i..4i+3 live in bytes 0..3 of word i: even cells in ke's high bytes,
+      // odd cells in ko's high bytes; key pairs = (cell 4i, 4i+1), (4i+2, 4i+3)
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const uint32_t e = unpk(ke[i]), o = unpk(ko[i]);
+        key[2 * i] = pk(__builtin_amdgcn_perm(o, e, 0x0c050c01u));      // [e.byte1, o.byte1]
+        key[2 * i + 1] = pk(__builtin_amdgcn_perm(o, e, 0x0c070c03u));  // [e.byte3, o.byte3]
+      }
+    } else {
+      // per-entry drops keyed by (t_send, src, dst, global column) -- SCALED regime
+      uint32_t kk[Q];
+#pragma unroll
+      for (int q = 0; q < Q; q++) kk[q] = 0;
+      for (int j = 0; j < k; j++) {
+        const int sn = ib[j];
+        const u32x4 mv = __builtin_amdgcn_raw_buffer_load_b128(prs, poff + (uint32_t)sn * (2 * B), 0, 0);
+        const uint32_t w[4] = {mv.x, mv.y, mv.z, mv.w};
+        const uint64_t pair = gm_mix64(s.drop_seed ^ ((uint64_t)(uint32_t)(t - 1) << 48) ^
+                                       ((uint64_t)(uint32_t)sn << 24) ^ (uint64_t)(uint32_t)r);
+#pragma unroll
+        for (int q = 0; q < Q; q++) {
+          const uint32_t pv = (w[q >> 2] >> (8 * (q & 3))) & 0xFFu;
+          if (!pv) continue;
+          const uint32_t h = (uint32_t)(gm_mix64(pair + (uint64_t)(s.c0 + colb + q)) >> 32);
+          if ((int)(h % 100u) < drop_pct) continue;
+          kk[q] = kk[q] > pv ? kk[q] : pv;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 8; i++) key[i] = pk(kk[2 * i] | (kk[2 * i + 1] << 16));
     }
-    int x = nev;
+    // merge: re-base the cell to tick t (h -= 2, age += 1; absent stays 0), then max
+    // with the delivered key (insert if absent; raise hb and stamp ts = t if newer)
+    const uint32_t tw[8] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y, tb.z, tb.w};
+    u16x2 mm[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+      mm[i] = __builtin_elementwise_max(__builtin_elementwise_sub_sat(pk(tw[i]), (u16x2)(63)), key[i] << (u16x2)(5));
+    const int selfc = (r >= s.c0 && r < s.c0 + s.w) ? r - s.c0 - colb : -1;
+    if (selfc >= 0 && selfc < Q) {  // updateMyPos + heartbeat++ + myPos->setheartbeat(heartbeat++)
+      const int hb = s.hbctr[r] + 1;
+      s.hbctr[r] = hb + 1;
+      const int h = 255 - (2 * t - hb);
+      if (h < 3 || h > 255) atomicOr(s.err, GM_ERR_LAG);
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        if ((selfc >> 1) != i) continue;
+        uint32_t v = unpk(mm[i]);
+        const int sh = 16 * (selfc & 1);
+        if (((v >> sh) & 0xFFFFu) == 0) atomicOr(s.err, GM_ERR_SELF);
+        v = (v & ~(0xFFFFu << sh)) | ((uint32_t)S_CELL(h, 0) << sh);
+        mm[i] = pk(v);
+      }
+    }
+    // sweep (MP1Node.cpp:426-444), one packed pass: age >= TFAIL counts toward numfailed,
+    // age >= TREMOVE removes; fresh entries (age < TFAIL) form the payload sent at tick t
+    u16x2 np2 = (u16x2)(0), nf2 = (u16x2)(0), evany = (u16x2)(0), lagmin = (u16x2)(0xFFFF);
+    uint32_t cw[8], pw[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const u16x2 v = mm[i];
+      const u16x2 a = v & (u16x2)(31);
+      const u16x2 stale = (a + (u16x2)(32 - GM_TFAIL)) >> (u16x2)(5);   // age >= TFAIL
+      const u16x2 gone = (a + (u16x2)(32 - GM_TREMOVE)) >> (u16x2)(5);  // age >= TREMOVE
+      const u16x2 v2 = v * ((u16x2)(1) - gone);
+      nf2 += stale;
+      np2 += __builtin_elementwise_min(v2, (u16x2)(1));
+      // h - 2 for fresh cells; stale ones subtract >= 257 and saturate to 0 (not sent)
+      pw[i] = unpk(__builtin_elementwise_sub_sat(v >> (u16x2)(5), stale * (u16x2)(255) + (u16x2)(2)));
+      // joins: absent before, present after the merge; removals: gone
+      evany |= __builtin_elementwise_sub_sat(__builtin_elementwise_min(v, (u16x2)(1)),
+                                             __builtin_elementwise_min(pk(tw[i]), (u16x2)(1))) | gone;
+      lagmin = __builtin_elementwise_min(lagmin, v2 - (u16x2)(32));  // present with h <= 2
+      cw[i] = unpk(v2);
+    }
+    nfail = (int)nf2.x + (int)nf2.y;
+    npres = (int)np2.x + (int)np2.y;
+    if (__builtin_elementwise_min(lagmin.x, lagmin.y) < 64) atomicOr(s.err, GM_ERR_LAG);
+    if (unpk(evany)) {  // rare: this lane's joins / removals, as 2-bit kinds per cell
+#pragma unroll
+      for (int q = 0; q < Q; q++) {
+        const uint32_t before = (tw[q >> 1] >> (16 * (q & 1))) & 0xFFFFu;
+        const uint32_t merged = (unpk(mm[q >> 1]) >> (16 * (q & 1))) & 0xFFFFu;
+        const uint32_t after = (cw[q >> 1] >> (16 * (q & 1))) & 0xFFFFu;
+        const uint32_t ev = merged ? (!before ? S_EV_ADD : !after ? S_EV_REMOVE : 0u) : 0u;
+        evk |= ev << (2 * q);
+      }
+      nev = __builtin_popcount((evk | (evk >> 1)) & 0x55555555u);
+    }
+    const u32x4 na = {cw[0], cw[1], cw[2], cw[3]}, nb = {cw[4], cw[5], cw[6], cw[7]};
+    __builtin_amdgcn_raw_buffer_store_b128(na, trs, toff, 0, GM_AUX_NT);
+    __builtin_amdgcn_raw_buffer_store_b128(nb, trs, toff + 16, 0, GM_AUX_NT);
+    const u32x4 ov = {__builtin_amdgcn_perm(pw[1], pw[0], 0x06040200u), __builtin_amdgcn_perm(pw[3], pw[2], 0x06040200u),
+                      __builtin_amdgcn_perm(pw[5], pw[4], 0x06040200u), __builtin_amdgcn_perm(pw[7], pw[6], 0x06040200u)};
+    __builtin_amdgcn_raw_buffer_store_b128(ov, prs, (uint32_t)(r * 2 * B + par * B + li * Q), 0, GM_AUX_NT);
+    if (band == 0 && li == 0) s.wtick[r] = t;
+  }
+  // per-row reductions over the row's LPR lanes (aligned lane segments): counts packed
+  // as present | numfailed << 16 (each <= B)
+  int pf = npres | (nfail << 16);
+#pragma unroll
+  for (int o = LPR / 2; o >= 1; o >>= 1) pf += __shfl_xor(pf, o, 64);
+  int x = 0, tot = 0;
+  if (__builtin_amdgcn_ballot_w64(nev != 0)) {  // wave-uniform: events anywhere in this wave
+    x = nev;
 #pragma unroll
     for (int o = 1; o < LPR; o <<= 1) {
       const int y = __shfl_up(x, o, 64);
       if (li >= o) x += y;
     }
-    const int tot = __shfl(x, sub * LPR + LPR - 1, 64);
-    const int E = s.evs;
-    uint32_t sbase = 0;  // one spill-ring reservation per (row, band) that overflows its slots
-    if (live && li == 0 && tot > E) sbase = atomicAdd(s.ev_spill_cnt, (uint32_t)(tot - E));
-    sbase = __shfl(sbase, sub * LPR, 64);
-    if (live && nev) {
-      int slot = x - nev;
-      uint32_t *slots = s.ev_band + ((size_t)r * s.nb + band) * E;
-#pragma unroll
-      for (int q = 0; q < 8; q++) {
-        const uint32_t kind = (evk >> (2 * q)) & 3u;
-        if (!kind) continue;
-        const uint32_t rec = (kind << 30) | (uint32_t)(s.c0 + colb + q + 1);
-        if (slot < E) {
-          slots[slot] = rec;
-        } else {
-          const uint32_t sp = sbase + (uint32_t)(slot - E);
-          if (sp < s.ev_spill_cap) s.ev_spill[sp] = ((uint64_t)(uint32_t)r << 32) | rec;
-          else atomicOr(s.err, GM_ERR_EVENTS);
-        }
-        slot++;
-      }
-    }
-    if (li == 0 && r < s.n)
-      s.bcnt[(size_t)r * s.nb + band] = live ? ((uint32_t)p | ((uint32_t)f << 11) | ((uint32_t)min(tot, 1023) << 22)) : 0u;
+    tot = __shfl(x, sub * LPR + LPR - 1, 64);
   }
+  const int E = s.evs;
+  uint32_t sbase = 0;  // one spill-ring reservation per (row, band) that overflows its slots
+  if (live && li == 0 && tot > E) sbase = atomicAdd(s.ev_spill_cnt, (uint32_t)(tot - E));
+  sbase = __shfl(sbase, sub * LPR, 64);
+  if (live && nev) {
+    int slot = x - nev;
+    uint32_t *slots = s.ev_band + ((size_t)r * s.nb + band) * E;
+    for (uint32_t ek = evk; ek; ek &= ek - 1) {
+      const int bit = __builtin_ctz(ek);  // low bit of a set 2-bit kind field (ADD=1, REMOVE=2)
+      const int q = bit >> 1;
+      const uint32_t kind = (evk >> (2 * q)) & 3u;
+      const uint32_t rec = (kind << 30) | (uint32_t)(s.c0 + colb + q + 1);
+      if (slot < E) {
+        slots[slot] = rec;
+      } else {
+        const uint32_t sp = sbase + (uint32_t)(slot - E);
+        if (sp < s.ev_spill_cap) s.ev_spill[sp] = ((uint64_t)(uint32_t)r << 32) | rec;
+        else atomicOr(s.err, GM_ERR_EVENTS);
+      }
+      slot++;
+    }
+  }
+  if (li == 0 && r < s.n)
+    s.bcnt[(size_t)r * s.nb + band] =
+        live ? ((uint32_t)(pf & 0xFFFF) | ((uint32_t)(pf >> 16) << 11) | ((uint32_t)min(tot, 1023) << 22)) : 0u;
 }
 
 // ------------------------------------------------------- wave-per-row helpers
@@ -346,6 +387,8 @@ __device__ __forceinline__ void gm_resolve4(const SState &s, int r, int t, const
   const int gl = lane & 15;
   int cnt = 0, b = 0;
   uint32_t en[PL];
+#pragma unroll
+  for (int v = 0; v < PL; v++) en[v] = 0;
   if (act) {
     int lo = 0, hi = s.nb - 1;  // largest band with pre[band] <= ix
     while (lo < hi) {
@@ -354,17 +397,23 @@ __device__ __forceinline__ void gm_resolve4(const SState &s, int r, int t, const
       else hi = mid - 1;
     }
     b = lo;
-    const uint32_t *p = s.table + ((size_t)b * s.n + r) * B + gl * PL;
+    const uint16_t *p = s.table + ((size_t)b * s.n + r) * B + gl * PL;
+    if (PL >= 8) {
 #pragma unroll
-    for (int v = 0; v < PL / 4; v++) {
-      const uint4 q = *(const uint4 *)(p + 4 * v);
-      en[4 * v] = q.x;
-      en[4 * v + 1] = q.y;
-      en[4 * v + 2] = q.z;
-      en[4 * v + 3] = q.w;
+      for (int v = 0; v < PL / 8; v++) {
+        const uint4 q = *(const uint4 *)(p + 8 * v);
+        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int i = 0; i < 8; i++) en[8 * v + i] = (w[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+      }
+    } else {
+      const uint2 q = *(const uint2 *)p;
+      const uint32_t w[2] = {q.x, q.y};
+#pragma unroll
+      for (int i = 0; i < PL; i++) en[i] = (w[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
     }
 #pragma unroll
-    for (int v = 0; v < PL; v++) cnt += en[v] != GM_ABSENT;
+    for (int v = 0; v < PL; v++) cnt += en[v] != 0;
   }
   int x = cnt;
 #pragma unroll
@@ -382,10 +431,10 @@ __device__ __forceinline__ void gm_resolve4(const SState &s, int r, int t, const
       int need = q - excl;
 #pragma unroll
       for (int v = 0; v < PL; v++) {
-        if (en[v] != GM_ABSENT) {
+        if (en[v] != 0) {
           if (need == 0) {
             mycol = b * B + gl * PL + v;
-            myfresh = (t - (int)gm_ts(en[v])) < GM_TFAIL;
+            myfresh = S_AGE(en[v]) < GM_TFAIL;  // the table is as of tick t
           }
           need--;
         }
@@ -668,22 +717,26 @@ __global__ __launch_bounds__(256) void gm_s_accept(SState s, int t, int D) {
 // Cold: {hb 0, ts 0}. Warm at t0: own entry {2*t0-1, t0}; others {2*(t0-1-a)-1,
 // t0-a}, a = splitmix64(seed ^ r<<32 ^ c) % 4 -- values as if the cluster had been
 // gossiping, so the first ticks carry no mass-staleness transient. Padding absent.
+// Cells are encoded relative to tick t0 (S_CELL: h = 255 - (2*t0 - hb), age = t0 - ts).
 __global__ void gm_s_init(SState s, int warm, int t0, uint64_t seed) {
   const int r = blockIdx.x;
   for (int j = threadIdx.x; j < s.wp; j += blockDim.x) {
-    uint32_t e = GM_ABSENT;
+    uint32_t e = 0;  // absent
     if (j < s.w) {
       const int c = s.c0 + j;
-      if (!warm) e = gm_pack(0, 0);
-      else if (c == r) e = gm_pack((uint32_t)(2 * t0 - 1), (uint32_t)t0);
+      if (!warm) e = S_CELL(255u, 0u);  // hb 0 = 2*t0 at t0 = 0
+      else if (c == r) e = S_CELL(254u, 0u);
       else {
         const int a = (int)((gm_mix64(seed ^ ((uint64_t)(uint32_t)r << 32) ^ (uint64_t)(uint32_t)c) >> 40) % 4);
-        e = gm_pack((uint32_t)(2 * (t0 - 1 - a) - 1), (uint32_t)(t0 - a));
+        e = S_CELL((uint32_t)(252 - 2 * a), (uint32_t)a);
       }
     }
-    s.table[((size_t)(j / s.band) * s.n + r) * s.band + j % s.band] = e;
+    s.table[((size_t)(j / s.band) * s.n + r) * s.band + j % s.band] = (uint16_t)e;
   }
-  if (threadIdx.x == 0) s.hbctr[r] = warm ? 2 * t0 : 0;
+  if (threadIdx.x == 0) {
+    s.hbctr[r] = warm ? 2 * t0 : 0;
+    s.wtick[r] = t0;
+  }
 }
 
 // ------------------------------------------------------------ launch wrappers
