@@ -141,10 +141,12 @@ def main():
 
     n_live, m_lists = st["live"], st["lists"]
     W = sim.shard_layout()[1] if world > 1 else n  # this rank's subject columns
-    # algorithmic HBM bytes of one tick in this layout:
-    # per live row 4W read + 4W write (packed table) + 2W write (payload plane),
-    # plus 2W per delivered gossip list (payload read)
-    b_alg = (10 * n_live + 2 * m_lists) * W
+    # algorithmic bytes of one tick in this layout: per live row and
+    # column 2 B cell read + 2 B cell write + 1 B payload write, plus 1 B per delivered
+    # gossip list (payload read) -- the survey's formulation (read and
+    # write the receiver's row once, read each delivered sender row once per delivery)
+    # in this build's 16-bit cell / 8-bit payload units
+    b_alg = (5 * n_live + m_lists) * W
     # the survey's int32 (hb, ts) formulation of the same work
     b_survey = 16 * n_live * W + 8 * m_lists * W
     achieved = b_alg / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else None
@@ -153,7 +155,9 @@ def main():
     tpath = os.path.join(REPO, "profiles", f"traffic_n{n}.json")
     if tpath_ok and os.path.exists(tpath):
         with open(tpath) as f:
-            traffic = json.load(f).get("hbm_bytes_per_launch")
+            tj = json.load(f)
+        if tj.get("layout") == "narrow-band":
+            traffic = tj.get("hbm_bytes_per_launch")
 
     value = n * a.steps / elapsed
     out = {
@@ -167,7 +171,7 @@ def main():
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        "dtype": "u16",
+        "dtype": "u16 cells / u8 payload (integer)",
         "data": "synthetic (converged full-membership table, seeded crash set)",
         "config": {"workload": "S-A: SCALED full membership, 1% crash at tick 10, fanout 5, TFAIL 5, TREMOVE 20",
                    "n": n, "start": f"warm t0={a.t0}" if a.t0 > 0 else "cold", "prologue_to_tick": a.prologue, "crashed": ncrash, "live": n_live,
