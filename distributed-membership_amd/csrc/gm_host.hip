@@ -232,7 +232,7 @@ static int create_scaled(gm_ctx *c) {
   s.nb = s.wp / s.band;
   if ((size_t)n * s.band * 2 >= (1ull << 31)) return GM_EUNSUPPORTED;  // 32-bit buffer offsets per band slab
   s.evs = s.band / 32;
-  if (sizeof(uint32_t) * 4 * (size_t)(s.nb + 624) > 65536) return GM_EUNSUPPORTED;  // draw kernels' LDS
+  if (sizeof(uint32_t) * 4 * ((size_t)(s.wp >> 6) + 1 + 624) > 65536) return GM_EUNSUPPORTED;  // draw kernels' LDS
   s.ev_spill_cap = 1u << 24;
   s.rd_seed = c->cfg.rd_seed;
   s.drop_seed = c->cfg.drop_seed;
@@ -248,6 +248,7 @@ static int create_scaled(gm_ctx *c) {
   TRY(dalloc(c, &s.wtick, n));
   TRY(dalloc(c, &s.failed, n));
   TRY(dalloc(c, &s.bcnt, (size_t)n * s.nb));
+  TRY(dalloc(c, &s.ccnt, (size_t)n * (s.wp >> 6)));
   TRY(dalloc(c, &s.ev_band, (size_t)n * s.nb * s.evs));
   TRY(dalloc(c, &s.ev_spill, s.ev_spill_cap));
   TRY(dalloc(c, &s.ev_spill_cnt, 1));

@@ -50,6 +50,7 @@ struct SState {
   int32_t *hbctr;          // [n] MP1Node heartbeat counter (Member::heartbeat)
   int32_t *failed;         // [n] Member::bFailed
   uint32_t *bcnt;          // [n][nb] per-(row, band) counts after the sweep (S_BC_*)
+  uint8_t *ccnt;           // [nb][n][band/64] present cells per 64-column chunk after the sweep (rank-select)
   uint32_t *ev_band;       // [n][nb][evs] kind<<30 | subject id
   uint64_t *ev_spill;      // overflow: (logger<<32) | kind<<30 | subject id
   uint32_t *ev_spill_cnt;

@@ -299,6 +299,23 @@ __global__ __launch_bounds__(256) void gm_s_band(SState s, int t, int drop_pct) 
     __builtin_amdgcn_raw_buffer_store_b128(ov, prs, (uint32_t)(r * 2 * B + par * B + li * Q), 0, GM_AUX_NT);
     if (band == 0 && li == 0) s.wtick[r] = t;
   }
+  // present cells per 64-column chunk (4 lanes) for the draw's rank-select, gathered
+  // into the row's first lane and stored as one B/64-byte piece of the band slab
+  int cc = npres;
+  cc += __shfl_xor(cc, 1, 64);
+  cc += __shfl_xor(cc, 2, 64);
+  {
+    uint64_t piece = 0;
+#pragma unroll
+    for (int c = 0; c < B / 64; c++) piece |= (uint64_t)(__shfl(cc, sub * LPR + 4 * c, 64) & 0xFF) << (8 * c);
+    if (live && li == 0) {
+      uint8_t *dst = s.ccnt + (slab + r) * (B / 64);
+      if (B == 64) *dst = (uint8_t)piece;
+      else if (B == 128) *(uint16_t *)dst = (uint16_t)piece;
+      else if (B == 256) *(uint32_t *)dst = (uint32_t)piece;
+      else *(uint64_t *)dst = piece;
+    }
+  }
   // per-row reductions over the row's LPR lanes (aligned lane segments): counts packed
   // as present | numfailed << 16 (each <= B)
   int pf = npres | (nfail << 16);
@@ -342,113 +359,116 @@ __global__ __launch_bounds__(256) void gm_s_band(SState s, int t, int drop_pct) 
 }
 
 // ------------------------------------------------------- wave-per-row helpers
-// Row totals over this shard's bands; fills pre[0, nb) with the exclusive prefix of
-// the bands' present counts (LDS, this wave only).
+// LDS per wave of the draw kernels: chunk prefix [wp/64 + 1] u32, the fallback
+// generator's state [624] u32.
+__host__ __device__ __forceinline__ size_t gm_draw_lds_words(int wp) { return (size_t)(wp >> 6) + 1 + 624; }
+
+// Row r of this shard: numfailed (band counts), size and the chunk prefix
+// pre[c] = present cells in chunks [0, c) (pre[nc] = size), from the chunk counts.
+template <int B>
 __device__ __forceinline__ void gm_row_totals(const SState &s, int r, int lane, uint32_t *pre, uint32_t &size,
                                               uint32_t &nfail) {
-  const int nb = s.nb, per = (nb + 63) >> 6;
-  const int b0 = min(nb, lane * per), b1 = min(nb, b0 + per);
+  constexpr int CPB = B / 64;  // chunks per band
+  const int nb = s.nb, perb = (nb + 63) >> 6;
+  const int b0 = min(nb, lane * perb), b1 = min(nb, b0 + perb);
   const uint32_t *bc = s.bcnt + (size_t)r * nb;
-  uint32_t ps = 0, fs = 0;
+  uint32_t fs = 0, ps = 0;
   for (int b = b0; b < b1; b++) {
-    const uint32_t v = bc[b];
-    ps += S_BC_PRES(v);
-    fs += S_BC_FAIL(v);
+    fs += S_BC_FAIL(bc[b]);
+    ps += S_BC_PRES(bc[b]);
   }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) fs += __shfl_xor(fs, o, 64);
+  nfail = fs;
   uint32_t x = ps;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
     const uint32_t y = __shfl_up(x, o, 64);
     if (lane >= o) x += y;
   }
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) fs += __shfl_xor(fs, o, 64);
   size = __shfl(x, 63, 64);
-  nfail = fs;
   if (pre) {
     uint32_t a = x - ps;
     for (int b = b0; b < b1; b++) {
-      pre[b] = a;
-      a += S_BC_PRES(bc[b]);
+      const uint8_t *pc = s.ccnt + ((size_t)b * s.n + r) * CPB;
+      uint64_t v;
+      if (CPB == 1) v = *pc;
+      else if (CPB == 2) v = *(const uint16_t *)pc;
+      else if (CPB == 4) v = *(const uint32_t *)pc;
+      else v = *(const uint64_t *)pc;
+#pragma unroll
+      for (int c = 0; c < CPB; c++) {
+        pre[b * CPB + c] = a;
+        a += (uint32_t)(v >> (8 * c)) & 0xFFu;
+      }
     }
+    if (lane == 63) pre[nb * CPB] = a;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
 }
 
-// Resolve up to 4 draws at once, one per 16-lane group: group g holds shard-local
-// rank ix_g (valid iff act_g) of a present entry of row r; returns (to every lane of
-// the wave) the shard-local column of each and whether it is fresh (t - ts < TFAIL).
+// Resolve up to 8 draws at once, one per 8-lane group: group g holds shard-local rank
+// ix_g (valid iff act) of a present entry of row r. The chunk-word prefix finds the
+// 64-column chunk; its 64 cells (128 B, 8 per lane) give the column. Returns, to every
+// lane, the shard-local column of each draw (-1 if none) and whether it is fresh.
 template <int B>
-__device__ __forceinline__ void gm_resolve4(const SState &s, int r, int t, const uint32_t *pre, bool act, uint32_t ix,
-                                            int lane, int col[4], int fresh[4]) {
-  constexpr int PL = B / 16;  // cells per lane
-  const int gl = lane & 15;
-  int cnt = 0, b = 0;
-  uint32_t en[PL];
+__device__ __forceinline__ void gm_resolve8(const SState &s, int r, const uint32_t *pre, bool act, uint32_t ix, int lane,
+                                            int col[8], int fresh[8]) {
+  const int gl = lane & 7;
+  int cnt = 0, base = 0;
+  uint32_t en[8];
 #pragma unroll
-  for (int v = 0; v < PL; v++) en[v] = 0;
+  for (int v = 0; v < 8; v++) en[v] = 0;
+  uint32_t q = 0;
   if (act) {
-    int lo = 0, hi = s.nb - 1;  // largest band with pre[band] <= ix
+    int lo = 0, hi = (s.wp >> 6) - 1;  // largest chunk with pre[c] <= ix (a non-empty one)
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
       if (pre[mid] <= ix) lo = mid;
       else hi = mid - 1;
     }
-    b = lo;
-    const uint16_t *p = s.table + ((size_t)b * s.n + r) * B + gl * PL;
-    if (PL >= 8) {
+    q = ix - pre[lo];
+    const int col0 = lo * 64 + gl * 8;  // this lane's 8 cells
+    base = col0;
+    const uint4 t4 = *(const uint4 *)(s.table + ((size_t)(col0 / B) * s.n + r) * B + (col0 % B));
+    const uint32_t w[4] = {t4.x, t4.y, t4.z, t4.w};
 #pragma unroll
-      for (int v = 0; v < PL / 8; v++) {
-        const uint4 q = *(const uint4 *)(p + 8 * v);
-        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+    for (int v = 0; v < 8; v++) en[v] = (w[v >> 1] >> (16 * (v & 1))) & 0xFFFFu;
 #pragma unroll
-        for (int i = 0; i < 8; i++) en[8 * v + i] = (w[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
-      }
-    } else {
-      const uint2 q = *(const uint2 *)p;
-      const uint32_t w[2] = {q.x, q.y};
-#pragma unroll
-      for (int i = 0; i < PL; i++) en[i] = (w[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
-    }
-#pragma unroll
-    for (int v = 0; v < PL; v++) cnt += en[v] != 0;
+    for (int v = 0; v < 8; v++) cnt += en[v] != 0;
   }
   int x = cnt;
 #pragma unroll
-  for (int o = 1; o < 16; o <<= 1) {
+  for (int o = 1; o < 8; o <<= 1) {
     const int y = __shfl_up(x, o, 64);
     if (gl >= o) x += y;
   }
   const int excl = x - cnt;
-  int mycol = 0, myfresh = 0;
+  int mycol = -1, myfresh = 0;
   bool holder = false;
-  if (act) {
-    const int q = (int)(ix - pre[b]);
-    if (q >= excl && q < excl + cnt) {
-      holder = true;
-      int need = q - excl;
+  if (act && (int)q >= excl && (int)q < excl + cnt) {
+    holder = true;
+    int need = (int)q - excl;
 #pragma unroll
-      for (int v = 0; v < PL; v++) {
-        if (en[v] != 0) {
-          if (need == 0) {
-            mycol = b * B + gl * PL + v;
-            myfresh = S_AGE(en[v]) < GM_TFAIL;  // the table is as of tick t
-          }
-          need--;
+    for (int v = 0; v < 8; v++) {
+      if (en[v] != 0) {
+        if (need == 0) {
+          mycol = base + v;
+          myfresh = S_AGE(en[v]) < GM_TFAIL;  // the table is as of tick t
         }
+        need--;
       }
     }
   }
   const uint64_t hm = __ballot(holder);
 #pragma unroll
-  for (int g = 0; g < 4; g++) {
-    const uint32_t seg = (uint32_t)(hm >> (16 * g)) & 0xFFFFu;
-    const int src = seg ? 16 * g + __builtin_ctz(seg) : 0;
-    col[g] = __shfl(mycol, src, 64);
+  for (int g = 0; g < 8; g++) {
+    const uint32_t seg = (uint32_t)(hm >> (8 * g)) & 0xFFu;
+    const int src = seg ? 8 * g + __builtin_ctz(seg) : 0;
+    col[g] = seg ? __shfl(mycol, src, 64) : -1;
     fresh[g] = seg ? __shfl(myfresh, src, 64) : 0;
-    if (!seg) col[g] = -1;
   }
 }
 
@@ -478,8 +498,8 @@ __global__ __launch_bounds__(256) void gm_s_pick(SState s, int t) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = blockIdx.x * 4 + wave;
   if (r >= s.n) return;  // whole wave; no workgroup barrier follows
-  uint32_t *pre = p_smem + wave * s.nb;
-  uint32_t *mts = p_smem + 4 * s.nb + wave * 624;
+  uint32_t *pre = p_smem + wave * gm_draw_lds_words(s.wp);
+  uint32_t *mts = pre + (s.wp >> 6) + 1;
   const int par = t & 1;
   int32_t *stat = s.rowstat + (size_t)r * 4;
   const int k = s.inbox_cnt[par][r];
@@ -489,7 +509,7 @@ __global__ __launch_bounds__(256) void gm_s_pick(SState s, int t) {
     return;
   }
   uint32_t size, numfailed;
-  gm_row_totals(s, r, lane, pre, size, numfailed);
+  gm_row_totals<B>(s, r, lane, pre, size, numfailed);
   const int numpot = (int)size - 1 - (int)numfailed;  // numfailed counts removed entries too (MP1Node.cpp:463)
   const int target = min(GM_FANOUT, numpot);
   int n = 0, g0 = -1, g1 = -1, g2 = -1, g3 = -1, g4 = -1;
@@ -513,23 +533,30 @@ __global__ __launch_bounds__(256) void gm_s_pick(SState s, int t) {
       const uint32_t ix = (uint32_t)(prod >> 32);
       uint64_t m = __ballot(ok);
       while (m && !done) {
-        int d[4], cnt = 0;
+        // the next (up to) 8 draws, in order: group g of 8 lanes takes the g-th
+        const int grp = lane >> 3;
+        uint64_t mm = m;
+        int myd = 0, cnt = 0;
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
-          d[i] = m ? __builtin_ctzll(m) : 0;
-          if (m) {
-            m &= m - 1;
+        for (int i = 0; i < 8; i++) {
+          if (mm) {
+            if (grp == i) myd = __builtin_ctzll(mm);
+            mm &= mm - 1;
             cnt++;
           }
         }
-        const int grp = lane >> 4;
-        const int myd = grp == 0 ? d[0] : grp == 1 ? d[1] : grp == 2 ? d[2] : d[3];
+        m = mm;
         const uint32_t myix = __shfl(ix, myd, 64);
-        int col[4], fr[4];
-        gm_resolve4<B>(s, r, t, pre, grp < cnt, myix, lane, col, fr);
+        int col[8], fr[8];
+        gm_resolve8<B>(s, r, pre, grp < cnt, myix, lane, col, fr);
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
+        for (int i = 0; i < 8; i++) {
           if (i >= cnt || done) continue;
+          if (col[i] < 0) {  // a draw no chunk resolved: counts and cells disagree
+            if (lane == 0) atomicOr(s.err, GM_ERR_DRAWS);
+            done = true;
+            continue;
+          }
           const int c = s.c0 + col[i];
           if (c == r) continue;  // "me" (MP1Node.cpp:470)
           if (!fr[i]) continue;  // age >= TFAIL (MP1Node.cpp:471)
@@ -569,7 +596,14 @@ __global__ __launch_bounds__(256) void gm_s_count(SState s, int t) {
   const int r = blockIdx.x * 4 + wave;
   if (r >= s.n) return;
   uint32_t size = 0, nf = 0;
-  if (!s.failed[r]) gm_row_totals(s, r, lane, nullptr, size, nf);
+  if (!s.failed[r]) {
+    switch (s.band) {
+      case 64: gm_row_totals<64>(s, r, lane, nullptr, size, nf); break;
+      case 128: gm_row_totals<128>(s, r, lane, nullptr, size, nf); break;
+      case 256: gm_row_totals<256>(s, r, lane, nullptr, size, nf); break;
+      default: gm_row_totals<512>(s, r, lane, nullptr, size, nf); break;
+    }
+  }
   if (lane == 0) {
     int32_t *x = s.xcnt + ((size_t)s.shard_rank * s.n + r) * 2;
     x[0] = (int)size;
@@ -591,8 +625,8 @@ __global__ __launch_bounds__(256) void gm_s_draw(SState s, int t, int round, int
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = blockIdx.x * 4 + wave;
   if (r >= s.n) return;
-  uint32_t *pre = p_smem + wave * s.nb;
-  uint32_t *mts = p_smem + 4 * s.nb + wave * 624;
+  uint32_t *pre = p_smem + wave * gm_draw_lds_words(s.wp);
+  uint32_t *mts = pre + (s.wp >> 6) + 1;
   const int G = s.shard_count;
   int32_t *acc = s.acc + (size_t)r * 8;
   if (round == 0) {
@@ -623,7 +657,7 @@ __global__ __launch_bounds__(256) void gm_s_draw(SState s, int t, int round, int
   for (int g = 0; g < s.shard_rank; g++) own_lo += (uint32_t)s.xcnt[((size_t)g * s.n + r) * 2];
   const uint32_t own_cnt = (uint32_t)s.xcnt[((size_t)s.shard_rank * s.n + r) * 2];
   uint32_t osz, onf;
-  gm_row_totals(s, r, lane, pre, osz, onf);
+  gm_row_totals<B>(s, r, lane, pre, osz, onf);
   const uint32_t thr = (0u - size) % size;
   GmLazyMT mt;
   int32_t *st = s.status + (size_t)r * D;
@@ -643,23 +677,23 @@ __global__ __launch_bounds__(256) void gm_s_draw(SState s, int t, int round, int
     int32_t val = ok ? -1 : -2;
     uint64_t m = __ballot(mine);
     while (m) {
-      int d[4], c4 = 0;
+      const int grp = lane >> 3;
+      int myd = 0, c8 = 0, d[8];
 #pragma unroll
-      for (int i = 0; i < 4; i++) {
-        d[i] = m ? __builtin_ctzll(m) : 0;
+      for (int i = 0; i < 8; i++) {
+        d[i] = m ? __builtin_ctzll(m) : 64;
         if (m) {
+          if (grp == i) myd = d[i];
           m &= m - 1;
-          c4++;
+          c8++;
         }
       }
-      const int grp = lane >> 4;
-      const int myd = grp == 0 ? d[0] : grp == 1 ? d[1] : grp == 2 ? d[2] : d[3];
       const uint32_t myix = __shfl(ix, myd, 64) - own_lo;
-      int col[4], fr[4];
-      gm_resolve4<B>(s, r, t, pre, grp < c4, myix, lane, col, fr);
+      int col[8], fr[8];
+      gm_resolve8<B>(s, r, pre, grp < c8, myix, lane, col, fr);
 #pragma unroll
-      for (int i = 0; i < 4; i++)
-        if (i < c4 && lane == d[i]) val = col[i] < 0 ? -1 : (((s.c0 + col[i]) << 1) | fr[i]);
+      for (int i = 0; i < 8; i++)
+        if (i < c8 && lane == d[i]) val = col[i] < 0 ? -1 : (((s.c0 + col[i]) << 1) | fr[i]);
     }
     if (lane < cnt) st[d0 + lane] = val;
   }
@@ -752,7 +786,7 @@ static hipError_t launch_tick_b(const SState &s, int t, int drop_pct, bool nt, h
   if (drop_pct >= 0) hipLaunchKernelGGL((gm_s_band<B, true>), dim3(nblk), dim3(256), 0, st, s, t, drop_pct);
   else hipLaunchKernelGGL((gm_s_band<B, false>), dim3(nblk), dim3(256), 0, st, s, t, drop_pct);
   if (k1) (void)hipEventRecord(k1, st);
-  const size_t smem = sizeof(uint32_t) * 4 * (size_t)(s.nb + 624);
+  const size_t smem = sizeof(uint32_t) * 4 * gm_draw_lds_words(s.wp);
   if (pick) hipLaunchKernelGGL((gm_s_pick<B>), dim3((s.n + 3) / 4), dim3(256), smem, st, s, t);
   else hipLaunchKernelGGL(gm_s_count, dim3((s.n + 3) / 4), dim3(256), 0, st, s, t);
   return hipGetLastError();
@@ -770,7 +804,7 @@ hipError_t gm_launch_tick(const SState &s, int t, int drop_pct, bool nt, hipStre
 }
 
 hipError_t gm_launch_draw(const SState &s, int t, int round, int D, hipStream_t st) {
-  const size_t smem = sizeof(uint32_t) * 4 * (size_t)(s.nb + 624);
+  const size_t smem = sizeof(uint32_t) * 4 * gm_draw_lds_words(s.wp);
   const dim3 grid((s.n + 3) / 4), blk(256);
   switch (s.band) {
     case 64: hipLaunchKernelGGL(gm_s_draw<64>, grid, blk, smem, st, s, t, round, D); break;
