@@ -751,6 +751,8 @@ extern "C" int gm_shard_merge(gm_ctx *c) {
   TRY(shard_ready(c));
   const int t_send = c->t - 1;
   const bool drop = c->cfg.drop_pct > 0 && t_send >= c->cfg.drop_from && t_send < c->cfg.drop_to;
+  HIPCHECK(hipMemsetAsync(c->s.xcnt + (size_t)c->s.shard_rank * c->n * 2, 0, sizeof(int32_t) * 2 * (size_t)c->n,
+                          c->stream));
   HIPCHECK(gm_launch_tick(c->s, c->t, drop ? c->cfg.drop_pct : -1, c->nt, c->stream, c->timing ? c->k0 : nullptr,
                           c->timing ? c->k1 : nullptr, false));
   return GM_OK;

@@ -26,8 +26,9 @@
 //               appends itself to its targets' inboxes for tick t+1 (counting sort by
 //               destination in place of EmulNet's buffer scan, EmulNet.cpp:144-177).
 //
-// Column-sharded ticks (multi-GPU) run gm_s_mtgen + gm_s_band + gm_s_count on the
-// shard's columns, exchange per-row counts, then gm_s_draw / gm_s_accept rounds.
+// Column-sharded ticks (multi-GPU) run gm_s_mtgen + gm_s_band on the shard's columns
+// (which also accumulates the shard's per-row counts), exchange the counts, then
+// gm_s_draw / gm_s_accept rounds.
 #include "gm_device.h"
 #include "gm_scaled.h"
 
@@ -353,9 +354,15 @@ __global__ __launch_bounds__(256) void gm_s_band(SState s, int t, int drop_pct) 
       slot++;
     }
   }
-  if (li == 0 && r < s.n)
+  if (li == 0 && r < s.n) {
     s.bcnt[(size_t)r * s.nb + band] =
         live ? ((uint32_t)(pf & 0xFFFF) | ((uint32_t)(pf >> 16) << 11) | ((uint32_t)min(tot, 1023) << 22)) : 0u;
+    // column shard: this shard's row totals (present, numfailed) for the all-gather,
+    // accumulated as one packed 64-bit add per (row, band) into the zeroed slot
+    if (s.shard_count > 1 && live)
+      atomicAdd((unsigned long long *)(s.xcnt + ((size_t)s.shard_rank * s.n + r) * 2),
+                (unsigned long long)(pf & 0xFFFF) | ((unsigned long long)(pf >> 16) << 32));
+  }
 }
 
 // ------------------------------------------------------- wave-per-row helpers
@@ -590,29 +597,8 @@ __global__ __launch_bounds__(256) void gm_s_pick(SState s, int t) {
 }
 
 // ---------------------------------------------------------- column-sharded mode
-// Phase A2: this shard's per-row (present, numfailed) for the all-gather.
-__global__ __launch_bounds__(256) void gm_s_count(SState s, int t) {
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int r = blockIdx.x * 4 + wave;
-  if (r >= s.n) return;
-  uint32_t size = 0, nf = 0;
-  if (!s.failed[r]) {
-    switch (s.band) {
-      case 64: gm_row_totals<64>(s, r, lane, nullptr, size, nf); break;
-      case 128: gm_row_totals<128>(s, r, lane, nullptr, size, nf); break;
-      case 256: gm_row_totals<256>(s, r, lane, nullptr, size, nf); break;
-      default: gm_row_totals<512>(s, r, lane, nullptr, size, nf); break;
-    }
-  }
-  if (lane == 0) {
-    int32_t *x = s.xcnt + ((size_t)s.shard_rank * s.n + r) * 2;
-    x[0] = (int)size;
-    x[1] = (int)nf;
-    const int par = t & 1;
-    s.rowstat[(size_t)r * 4] = s.failed[r] ? 0 : s.inbox_cnt[par][r];
-    s.inbox_cnt[par][r] = 0;  // consumed by gm_s_band; the append target of tick t+2
-  }
-}
+// Phase A (gm_s_band, sharded): merge / sweep of this shard's columns; each row's
+// shard totals (present, numfailed) accumulate into xcnt[rank] for the all-gather.
 
 // Phase B: every rank replays every pending row's S2 stream (round 0: outputs
 // [0, 16) from gm_s_mtgen; round q >= 1: [16 + 64(q-1), 16 + 64q) from the lazy
@@ -630,6 +616,11 @@ __global__ __launch_bounds__(256) void gm_s_draw(SState s, int t, int round, int
   const int G = s.shard_count;
   int32_t *acc = s.acc + (size_t)r * 8;
   if (round == 0) {
+    if (lane == 0) {  // lists delivered this tick; consumed by gm_s_band, the append target of tick t+2
+      const int par = t & 1;
+      s.rowstat[(size_t)r * 4] = s.failed[r] ? 0 : s.inbox_cnt[par][r];
+      s.inbox_cnt[par][r] = 0;
+    }
     int size = 0, nf = 0;
     for (int g = 0; g < G; g++) {
       size += s.xcnt[((size_t)g * s.n + r) * 2];
@@ -656,8 +647,7 @@ __global__ __launch_bounds__(256) void gm_s_draw(SState s, int t, int round, int
   uint32_t own_lo = 0;
   for (int g = 0; g < s.shard_rank; g++) own_lo += (uint32_t)s.xcnt[((size_t)g * s.n + r) * 2];
   const uint32_t own_cnt = (uint32_t)s.xcnt[((size_t)s.shard_rank * s.n + r) * 2];
-  uint32_t osz, onf;
-  gm_row_totals<B>(s, r, lane, pre, osz, onf);
+  bool have_pre = false;  // this shard's chunk prefix of the row, built on first use
   const uint32_t thr = (0u - size) % size;
   GmLazyMT mt;
   int32_t *st = s.status + (size_t)r * D;
@@ -676,6 +666,11 @@ __global__ __launch_bounds__(256) void gm_s_draw(SState s, int t, int round, int
     const bool mine = ok && ix >= own_lo && ix < own_lo + own_cnt;
     int32_t val = ok ? -1 : -2;
     uint64_t m = __ballot(mine);
+    if (m && !have_pre) {
+      uint32_t osz, onf;
+      gm_row_totals<B>(s, r, lane, pre, osz, onf);
+      have_pre = true;
+    }
     while (m) {
       const int grp = lane >> 3;
       int myd = 0, c8 = 0, d[8];
@@ -788,7 +783,6 @@ static hipError_t launch_tick_b(const SState &s, int t, int drop_pct, bool nt, h
   if (k1) (void)hipEventRecord(k1, st);
   const size_t smem = sizeof(uint32_t) * 4 * gm_draw_lds_words(s.wp);
   if (pick) hipLaunchKernelGGL((gm_s_pick<B>), dim3((s.n + 3) / 4), dim3(256), smem, st, s, t);
-  else hipLaunchKernelGGL(gm_s_count, dim3((s.n + 3) / 4), dim3(256), 0, st, s, t);
   return hipGetLastError();
 }
 

@@ -1,11 +1,12 @@
 """A numpy model of the column-sharded SCALED tick (membership/sharded.py,
-gm_s_tick_shard / gm_s_draw / gm_s_accept) -- TEST INFRASTRUCTURE.
+gm_s_band / gm_s_draw / gm_s_accept) -- TEST INFRASTRUCTURE.
 
 Each instance owns subject columns [c0, c0+w) of every row and talks to the
 other shards only through the two collectives of the protocol (all-gather of
 per-row (present, numfailed), MAX-allreduce of resolved draws), supplied as
 callables -- torch.distributed gloo in the multi-process CPU test. The S2
-stream comes from the oracle's mt19937 + Lemire restatement."""
+stream is a pure-Python mt19937 checked against the oracle's mt19937 + Lemire
+restatement (tests/test_rng_kat.py)."""
 import numpy as np
 
 import oracle_py
@@ -19,6 +20,41 @@ def mix64(z):
     z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M64
     z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M64
     return z ^ (z >> 31)
+
+
+def mt19937_outputs(seed, k):
+    """First k outputs of std::mt19937(seed) (the S2 stream before Lemire)."""
+    x = [seed & 0xFFFFFFFF]
+    for i in range(1, 624):
+        x.append((1812433253 * (x[-1] ^ (x[-1] >> 30)) + i) & 0xFFFFFFFF)
+    out, idx = [], 624
+    while len(out) < k:
+        if idx == 624:
+            for i in range(624):
+                y = (x[i] & 0x80000000) | (x[(i + 1) % 624] & 0x7FFFFFFF)
+                x[i] = x[(i + 397) % 624] ^ (y >> 1) ^ (0x9908B0DF if y & 1 else 0)
+            idx = 0
+        v = x[idx]
+        idx += 1
+        v ^= v >> 11
+        v ^= (v << 7) & 0x9D2C5680
+        v ^= (v << 15) & 0xEFC60000
+        v ^= v >> 18
+        out.append(v & 0xFFFFFFFF)
+    return out
+
+
+def lemire_draws(seed, size, k):
+    """libstdc++-11 uniform_int_distribution<int>(0, size-1) over mt19937_outputs (test helper)."""
+    thr = ((1 << 32) - size) % size
+    out = []
+    for x in mt19937_outputs(seed, 4 * k + 64):
+        prod = x * size
+        if (prod & 0xFFFFFFFF) >= thr:
+            out.append(prod >> 32)
+            if len(out) == k:
+                break
+    return out
 
 
 class ShardModel:
@@ -102,29 +138,39 @@ class ShardModel:
         size = allc[:, :, 0].sum(0)
         numpot = size - 1 - allc[:, :, 1].sum(0)
         cols = [np.nonzero(present[r])[0] for r in range(n)]
-        drawn = {r: 0 for r in range(n) if not self.failed[r] and numpot[r] > 0}
+        drawn = [r for r in range(n) if not self.failed[r] and numpot[r] > 0]
         acc = {r: [] for r in drawn}
         targets = {r: [] for r in range(n)}
-        d = 16
+        # rounds over the S2 OUTPUTS of each row's mt19937 (gm_s_draw): round 0 the first
+        # 16, round q >= 1 the next 64; -2 marks an output Lemire rejects (no draw)
+        off, d = 0, 16
         while drawn:
             status = np.full((n, d), -1, np.int64)
             for r in drawn:
-                ix = oracle_py.mt_uniform(oracle_py.lib().oc_rd_seed(self.rd_seed, t, r + 1), int(size[r]),
-                                          drawn[r] + d)[drawn[r]:]
-                for k, x in enumerate(ix):
+                size_r = int(size[r])
+                thr = ((1 << 32) - size_r) % size_r
+                raw = mt19937_outputs(oracle_py.lib().oc_rd_seed(self.rd_seed, t, r + 1), off + d)[off:]
+                for k, x in enumerate(raw):
+                    prod = x * size_r
+                    if (prod & 0xFFFFFFFF) < thr:
+                        status[r, k] = -2
+                        continue
+                    ix = prod >> 32
                     pre = 0
                     for g in range(self.world):
-                        if x < pre + allc[g, r, 0]:
+                        if ix < pre + allc[g, r, 0]:
                             break
                         pre += allc[g, r, 0]
                     if g == self.rank:
-                        j = cols[r][x - pre]
+                        j = cols[r][ix - pre]
                         status[r, k] = ((c0 + j) << 1) | int(fresh[r, j])
             status = all_reduce_max(status)
             done = []
             for r in drawn:
                 for k in range(d):
                     v = int(status[r, k])
+                    if v == -2:
+                        continue
                     assert v >= 0
                     c = v >> 1
                     if c == r or not (v & 1) or c in acc[r]:
@@ -132,13 +178,12 @@ class ShardModel:
                     acc[r].append(c)
                     if len(acc[r]) >= FANOUT or len(acc[r]) >= numpot[r]:
                         break
-                drawn[r] += d
                 if len(acc[r]) >= FANOUT or len(acc[r]) >= numpot[r]:
                     done.append(r)
             for r in done:
                 targets[r] = acc.pop(r)
-                del drawn[r]
-            d = 64
+                drawn.remove(r)
+            off, d = off + d, 64
         self.inbox = [[] for _ in range(n)]
         for r in range(n):
             for c in targets[r]:

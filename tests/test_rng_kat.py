@@ -46,3 +46,18 @@ def test_rd_seed_contract():
         return z & 0xFFFFFFFF
     for rd, t, i in [(0, 0, 1), (7, 5, 3), (2**63 + 5, 699, 1000), (42, 12345, 65536)]:
         assert oracle_py.lib().oc_rd_seed(rd, t, i) == ref(rd, t, i)
+
+
+def test_shard_model_mt19937_matches_kat():
+    # the protocol model's pure-Python mt19937 (raw outputs, Lemire on top) must be the
+    # libstdc++ stream the golden KATs hold
+    from shard_model import lemire_draws
+    kat = np.load(os.path.join(GOLDEN, "kat_mt19937_lemire.npz"))
+    seeds = kat["seeds"]
+    for key in kat.files:
+        if key == "seeds":
+            continue
+        n = int(key.split("_")[1])
+        exp = kat[key]
+        for row in range(0, len(seeds), 97):
+            assert lemire_draws(int(seeds[row]), n, exp.shape[1]) == list(exp[row]), (key, row)
