@@ -10,8 +10,8 @@ PKG := distributed-membership_amd
 CSRC := $(PKG)/csrc
 HIPFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Iinclude -I$(CSRC) -Wall -Wno-unused-result
 LIB := $(PKG)/lib/libgm.so
-KOBJS := $(PKG)/build/gm_faithful.o $(PKG)/build/gm_scaled.o $(PKG)/build/gm_host.o
-HDRS := include/gm_abi.h $(CSRC)/gm_device.h $(CSRC)/gm_faithful.h $(CSRC)/gm_scaled.h
+KOBJS := $(PKG)/build/gm_faithful.o $(PKG)/build/gm_scaled.o $(PKG)/build/gm_partial.o $(PKG)/build/gm_host.o
+HDRS := include/gm_abi.h $(CSRC)/gm_device.h $(CSRC)/gm_faithful.h $(CSRC)/gm_scaled.h $(CSRC)/gm_partial.h
 
 all: $(LIB) Application oracle
 

@@ -108,6 +108,35 @@ struct GmLazyMT {
   }
 };
 
+// The first 16 outputs of mt19937(seed): outputs 0..15 need init words x[0..16] and
+// x[397..412] only (output k twists x[k], x[k+1], x[k+397], all still init words for
+// k < 227), so 413 init steps in registers replace the 624-word state.
+__device__ __forceinline__ void gm_mt_first16(uint32_t seed, uint32_t out[16]) {
+  uint32_t lo[17], hi[16];
+  uint32_t v = seed;
+  lo[0] = v;
+#pragma unroll
+  for (int i = 1; i <= 16; i++) {
+    v = 1812433253u * (v ^ (v >> 30)) + (uint32_t)i;
+    lo[i] = v;
+  }
+  for (int i = 17; i < 397; i++) v = 1812433253u * (v ^ (v >> 30)) + (uint32_t)i;
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    v = 1812433253u * (v ^ (v >> 30)) + (uint32_t)(397 + i);
+    hi[i] = v;
+  }
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const uint32_t y = (lo[k] & 0x80000000u) | (lo[k + 1] & 0x7fffffffu);
+    uint32_t o = hi[k] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    o ^= o >> 11;
+    o ^= (o << 7) & 0x9d2c5680u;
+    o ^= (o << 15) & 0xefc60000u;
+    out[k] = o ^ (o >> 18);
+  }
+}
+
 // Index of the ix-th set bit (0-based) of a bitmap `bits` with exclusive
 // per-word prefix popcounts `pre` (nw words). Caller guarantees ix < total.
 __device__ __forceinline__ int gm_rank_select(const uint64_t *bits, const uint32_t *pre, int nw, uint32_t ix) {

@@ -16,6 +16,7 @@
 #include "gm_abi.h"
 #include "gm_device.h"
 #include "gm_faithful.h"
+#include "gm_partial.h"
 #include "gm_scaled.h"
 
 __global__ void gm_f_recv(FState s, int t);
@@ -26,6 +27,10 @@ hipError_t gm_launch_tick(const SState &s, int t, int drop_pct, bool nt, hipStre
 hipError_t gm_launch_draw(const SState &s, int t, int round, int D, hipStream_t st);
 hipError_t gm_launch_accept(const SState &s, int t, int D, hipStream_t st);
 hipError_t gm_launch_init(const SState &s, int warm, int t0, uint64_t seed, hipStream_t st);
+hipError_t gm_launch_partial_tick(const PState &s, int t, uint32_t *mtraw, hipStream_t st, hipEvent_t k0,
+                                  hipEvent_t k1);
+hipError_t gm_launch_partial_init(const PState &s, int t0, uint64_t init_seed, hipStream_t st);
+size_t gm_partial_lds_bytes();
 
 #define GM_T_LIMIT 32766  // packed 16-bit hb/ts stay exact: hb <= 2t+1 < 0xFFFF
 
@@ -54,6 +59,9 @@ struct gm_ctx {
   std::vector<gm_event> pending;
   // SCALED
   SState s{};
+  // PARTIAL
+  PState p{};
+  uint32_t *p_mtraw = nullptr;
 };
 
 static thread_local char g_errbuf[256];
@@ -283,11 +291,52 @@ static int create_scaled(gm_ctx *c) {
   return GM_OK;
 }
 
+// PARTIAL: V-entry views (scenario S-C), warm start at init_t0 (oracle op_create)
+static int create_partial(gm_ctx *c) {
+  const int n = c->n;
+  PState &p = c->p;
+  p.n = n;
+  p.V = c->cfg.view ? c->cfg.view : 32;
+  // the per-wave LDS table holds the own list + P_KP delivered lists at <= 0.55 load
+  if (p.V < 2 || p.V > 32 || p.V > n) return GM_EUNSUPPORTED;
+  const int t0 = c->cfg.init_t0;
+  if (c->cfg.init_mode != 1 || t0 < 5 || t0 > GM_T_LIMIT / 2) return GM_EINVAL;
+  if (c->cfg.shard_count > 1) return GM_EUNSUPPORTED;
+  p.rd_seed = c->cfg.rd_seed;
+  p.view_seed = c->cfg.view_seed;
+  p.drop_seed = c->cfg.drop_seed;
+  p.drop_pct = -1;
+  TRY(dalloc(c, &p.lists, (size_t)2 * n * p.V));
+  for (int q = 0; q < 2; q++) {
+    TRY(dalloc(c, &p.inbox_cnt[q], n));
+    TRY(dalloc(c, &p.inbox[q], (size_t)n * P_KMAX));
+    HIPCHECK(hipMemset(p.inbox_cnt[q], 0, sizeof(int32_t) * n));
+  }
+  TRY(dalloc(c, &p.hbctr, n));
+  TRY(dalloc(c, &p.failed, n));
+  TRY(dalloc(c, &p.ev, (size_t)n * 2 * p.V));
+  TRY(dalloc(c, &p.ev_cnt, n));
+  TRY(dalloc(c, &p.rowstat, (size_t)n * 4));
+  TRY(dalloc(c, &p.targets, (size_t)n * GM_FANOUT));
+  TRY(dalloc(c, &p.err, 1));
+  TRY(dalloc(c, &c->p_mtraw, (size_t)n * 16));
+  HIPCHECK(hipMemset(p.lists, 0, sizeof(uint64_t) * 2 * n * p.V));
+  HIPCHECK(hipMemset(p.failed, 0, sizeof(int32_t) * n));
+  HIPCHECK(hipMemset(p.ev_cnt, 0, sizeof(int32_t) * n));
+  HIPCHECK(hipMemset(p.rowstat, 0, sizeof(int32_t) * n * 4));
+  HIPCHECK(hipMemset(p.err, 0, sizeof(uint32_t)));
+  HIPCHECK(gm_launch_partial_init(p, t0, c->cfg.init_seed, c->stream));
+  HIPCHECK(hipStreamSynchronize(c->stream));
+  c->t = t0 + 1;
+  return GM_OK;
+}
+
 extern "C" int gm_create(const gm_config *cfg, gm_ctx **out) {
   if (!cfg || !out) return GM_EINVAL;
   *out = nullptr;
   if (cfg->abi_version != GM_ABI_VERSION) return GM_EINVAL;
-  if (cfg->n <= 0 || (cfg->mode != GM_MODE_FAITHFUL && cfg->mode != GM_MODE_SCALED)) return GM_EINVAL;
+  if (cfg->n <= 0 || (cfg->mode != GM_MODE_FAITHFUL && cfg->mode != GM_MODE_SCALED && cfg->mode != GM_MODE_PARTIAL))
+    return GM_EINVAL;
   g_errbuf[0] = 0;
   gm_ctx *c = new gm_ctx();
   c->cfg = *cfg;
@@ -300,7 +349,9 @@ extern "C" int gm_create(const gm_config *cfg, gm_ctx **out) {
     snprintf(g_errbuf, sizeof g_errbuf, "HIP device %d unavailable", cfg->device);
     rc = GM_EDEVICE;
   }
-  if (rc == GM_OK) rc = cfg->mode == GM_MODE_FAITHFUL ? create_faithful(c) : create_scaled(c);
+  if (rc == GM_OK)
+    rc = cfg->mode == GM_MODE_FAITHFUL ? create_faithful(c) : cfg->mode == GM_MODE_SCALED ? create_scaled(c)
+                                                                                        : create_partial(c);
   if (rc != GM_OK) {
     gm_destroy(c);
     return rc;
@@ -323,7 +374,7 @@ extern "C" int gm_destroy(gm_ctx *c) {
 }
 
 static int check_err(gm_ctx *c) {
-  uint32_t *errp = c->cfg.mode == GM_MODE_FAITHFUL ? c->f.err : c->s.err;
+  uint32_t *errp = c->cfg.mode == GM_MODE_FAITHFUL ? c->f.err : c->cfg.mode == GM_MODE_SCALED ? c->s.err : c->p.err;
   uint32_t e = 0;
   HIPCHECK(hipMemcpyAsync(&e, errp, sizeof e, hipMemcpyDeviceToHost, c->stream));
   HIPCHECK(hipStreamSynchronize(c->stream));
@@ -393,10 +444,37 @@ static int tick_scaled(gm_ctx *c) {
   return GM_OK;
 }
 
+static int tick_partial(gm_ctx *c) {
+  if (c->t > GM_T_LIMIT) return GM_ERANGE;
+  const int t_send = c->t - 1;
+  const bool drop = c->cfg.drop_pct > 0 && t_send >= c->cfg.drop_from && t_send < c->cfg.drop_to;
+  PState st = c->p;
+  st.drop_pct = drop ? c->cfg.drop_pct : -1;
+  hipEvent_t k0 = nullptr, k1 = nullptr;
+  if (c->timing) {
+    if (c->timed_ticks == 0) HIPCHECK(hipEventRecord(c->e0, c->stream));
+    while (c->tev.size() < 2 * (size_t)(c->ktimed + 1)) {
+      hipEvent_t e;
+      HIPCHECK(hipEventCreate(&e));
+      c->tev.push_back(e);
+    }
+    k0 = c->tev[2 * c->ktimed];
+    k1 = c->tev[2 * c->ktimed + 1];
+    c->ktimed++;
+  }
+  HIPCHECK(gm_launch_partial_tick(st, c->t, c->p_mtraw, c->stream, k0, k1));
+  if (c->timing) {
+    HIPCHECK(hipEventRecord(c->e1, c->stream));
+    c->timed_ticks++;
+  }
+  return GM_OK;
+}
+
 extern "C" int gm_tick(gm_ctx *c) {
   if (!c) return GM_EINVAL;
   if (c->latched != GM_OK) return c->latched;
-  int rc = c->cfg.mode == GM_MODE_FAITHFUL ? tick_faithful(c) : tick_scaled(c);
+  int rc = c->cfg.mode == GM_MODE_FAITHFUL ? tick_faithful(c) : c->cfg.mode == GM_MODE_SCALED ? tick_scaled(c)
+                                                                                             : tick_partial(c);
   if (rc == GM_OK) c->t++;
   return rc;
 }
@@ -435,7 +513,7 @@ extern "C" int gm_set_failed(gm_ctx *c, const int32_t *idx, int32_t n) {
     if (idx[k] < 0 || idx[k] >= c->n) return GM_EINVAL;
     c->failed_h[idx[k]] = 1;
   }
-  int32_t *dst = c->cfg.mode == GM_MODE_FAITHFUL ? c->f.failed : c->s.failed;
+  int32_t *dst = c->cfg.mode == GM_MODE_FAITHFUL ? c->f.failed : c->cfg.mode == GM_MODE_SCALED ? c->s.failed : c->p.failed;
   HIPCHECK(hipStreamSynchronize(c->stream));
   HIPCHECK(hipMemcpy(dst, c->failed_h.data(), sizeof(int32_t) * c->n, hipMemcpyHostToDevice));
   return GM_OK;
@@ -485,11 +563,43 @@ static int drain_scaled(gm_ctx *c, std::vector<gm_event> &out) {
   return GM_OK;
 }
 
+static void sort_canonical(std::vector<gm_event> &out) {
+  // canonical order of the build-defined modes: loggers descending; joins ascending id, then removals descending id
+  std::sort(out.begin(), out.end(), [](const gm_event &a, const gm_event &b) {
+    if (a.logger != b.logger) return a.logger > b.logger;
+    if (a.kind != b.kind) return a.kind < b.kind;
+    return a.kind == GM_EV_JOINED ? a.subject < b.subject : a.subject > b.subject;
+  });
+}
+
+static int drain_partial(gm_ctx *c, std::vector<gm_event> &out) {
+  const PState &p = c->p;
+  std::vector<int32_t> cnt(c->n);
+  HIPCHECK(hipMemcpyAsync(cnt.data(), p.ev_cnt, sizeof(int32_t) * c->n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHECK(hipStreamSynchronize(c->stream));
+  size_t tot = 0;
+  for (int32_t v : cnt) tot += (size_t)v;
+  if (!tot) return GM_OK;
+  std::vector<uint32_t> ev((size_t)c->n * 2 * p.V);
+  HIPCHECK(hipMemcpy(ev.data(), p.ev, sizeof(uint32_t) * ev.size(), hipMemcpyDeviceToHost));
+  const int t = c->t - 1;
+  for (int r = 0; r < c->n; r++)
+    for (int q = 0; q < cnt[r]; q++) {
+      const uint32_t rec = ev[(size_t)r * 2 * p.V + q];
+      out.push_back(gm_event{t, r, (rec >> 30) == P_EV_ADD ? GM_EV_JOINED : GM_EV_REMOVED, (int32_t)(rec & 0x3FFFFFFFu)});
+    }
+  sort_canonical(out);
+  return GM_OK;
+}
+
 extern "C" int gm_drain_events(gm_ctx *c, gm_event *out, size_t cap, size_t *n) {
   if (!c || !n) return GM_EINVAL;
   if (c->cfg.mode == GM_MODE_SCALED) {
     c->pending.clear();
     TRY(drain_scaled(c, c->pending));
+  } else if (c->cfg.mode == GM_MODE_PARTIAL) {
+    c->pending.clear();
+    TRY(drain_partial(c, c->pending));
   }
   *n = c->pending.size();
   if (c->pending.size() > cap) return GM_ERANGE;
@@ -509,6 +619,11 @@ extern "C" int gm_event_counts(gm_ctx *c, uint64_t counts[6]) {
     uint64_t tot = 0;
     for (uint32_t v : bc) tot += S_BC_NEV(v);  // slots + spilled, per (row, band)
     counts[0] = tot;  // join+remove records of the last tick (per-kind split needs a drain)
+  } else if (c->cfg.mode == GM_MODE_PARTIAL) {
+    std::vector<int32_t> cnt(c->n);
+    HIPCHECK(hipMemcpyAsync(cnt.data(), c->p.ev_cnt, sizeof(int32_t) * c->n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHECK(hipStreamSynchronize(c->stream));
+    for (int32_t v : cnt) counts[0] += (uint64_t)v;
   } else {
     for (const gm_event &e : c->pending) counts[e.kind]++;
   }
@@ -542,6 +657,23 @@ static int read_table_row(gm_ctx *c, int r, std::vector<int32_t> &hb, std::vecto
     for (int j = 0; j < w; j++) {
       hb[j] = row[j] == GM_ABSENT ? -1 : (int32_t)(row[j] & 0xFFFF);
       ts[j] = row[j] == GM_ABSENT ? -1 : (int32_t)(row[j] >> 16);
+    }
+    return GM_OK;
+  }
+  if (c->cfg.mode == GM_MODE_PARTIAL) {  // the node's V-entry list as of the last tick
+    const PState &p = c->p;
+    std::vector<uint64_t> lst(p.V);
+    HIPCHECK(hipMemcpy(lst.data(), p.lists + ((size_t)((c->t - 1) & 1) * c->n + r) * p.V, sizeof(uint64_t) * p.V,
+                       hipMemcpyDeviceToHost));
+    w = c->n;
+    hb.assign(w, -1);
+    ts.assign(w, -1);
+    for (uint64_t e : lst) {
+      if (!e) continue;
+      const int id = (int)(e >> 32), h = (int)(uint32_t)e;
+      if (id < 1 || id > c->n) return GM_ESTATE;
+      hb[id - 1] = h;
+      ts[id - 1] = (h + 1) / 2;
     }
     return GM_OK;
   }
@@ -588,10 +720,11 @@ extern "C" int gm_read_nodes(gm_ctx *c, int32_t *st4) {
     HIPCHECK(hipMemcpy(f.data(), c->f.failed, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
     HIPCHECK(hipMemcpy(h.data(), c->f.hbctr, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
   } else {
+    const bool part = c->cfg.mode == GM_MODE_PARTIAL;
     std::fill(a.begin(), a.end(), 1);
     std::fill(b.begin(), b.end(), 1);
-    HIPCHECK(hipMemcpy(f.data(), c->s.failed, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
-    HIPCHECK(hipMemcpy(h.data(), c->s.hbctr, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(f.data(), part ? c->p.failed : c->s.failed, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(h.data(), part ? c->p.hbctr : c->s.hbctr, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
   }
   for (int i = 0; i < n; i++) {
     st4[4 * i] = a[i];
@@ -614,7 +747,7 @@ extern "C" int gm_dump_tables(gm_ctx *c, char *buf, size_t cap, size_t *len) {
     int w;
     TRY(read_table_row(c, i, rh, rt, w));
     int cnt = 0;
-    const int c0 = c->cfg.mode == GM_MODE_FAITHFUL ? 0 : c->s.c0;
+    const int c0 = c->cfg.mode == GM_MODE_SCALED ? c->s.c0 : 0;
     for (int j = 0; j < w; j++) cnt += rh[j] >= 0;
     snprintf(tmp, sizeof tmp, "%d %d %d %d %d %d %d", t, i, st[4 * i], st[4 * i + 1], st[4 * i + 2], st[4 * i + 3], cnt);
     out += tmp;
@@ -633,11 +766,13 @@ extern "C" int gm_dump_tables(gm_ctx *c, char *buf, size_t cap, size_t *len) {
 
 extern "C" int gm_tick_stats(gm_ctx *c, int64_t stats[4]) {
   if (!c || !stats) return GM_EINVAL;
-  if (c->cfg.mode != GM_MODE_SCALED) return GM_EUNSUPPORTED;
+  if (c->cfg.mode == GM_MODE_FAITHFUL) return GM_EUNSUPPORTED;
+  const bool part = c->cfg.mode == GM_MODE_PARTIAL;
   std::vector<int32_t> rs((size_t)c->n * 4);
   uint32_t e = 0;
-  HIPCHECK(hipMemcpyAsync(rs.data(), c->s.rowstat, sizeof(int32_t) * rs.size(), hipMemcpyDeviceToHost, c->stream));
-  HIPCHECK(hipMemcpyAsync(&e, c->s.err, sizeof e, hipMemcpyDeviceToHost, c->stream));
+  HIPCHECK(hipMemcpyAsync(rs.data(), part ? c->p.rowstat : c->s.rowstat, sizeof(int32_t) * rs.size(),
+                          hipMemcpyDeviceToHost, c->stream));
+  HIPCHECK(hipMemcpyAsync(&e, part ? c->p.err : c->s.err, sizeof e, hipMemcpyDeviceToHost, c->stream));
   HIPCHECK(hipStreamSynchronize(c->stream));
   int64_t m = 0, live = 0, mx = 0;
   for (int r = 0; r < c->n; r++) {
@@ -664,8 +799,8 @@ extern "C" int gm_set_timing(gm_ctx *c, int32_t on) {
 extern "C" int gm_last_kernel_ms(gm_ctx *c, float *ms) {
   if (!c || !ms) return GM_EINVAL;
   *ms = 0.f;
-  if (!c->timing || c->cfg.mode != GM_MODE_SCALED || c->timed_ticks == 0) return GM_OK;
-  if (c->s.shard_count > 1) {  // per-tick merge-kernel events, summed at each tick end
+  if (!c->timing || c->cfg.mode == GM_MODE_FAITHFUL || c->timed_ticks == 0) return GM_OK;
+  if (c->cfg.mode == GM_MODE_SCALED && c->s.shard_count > 1) {  // per-tick merge-kernel events, summed at each tick end
     *ms = (float)(c->kernel_ms_sum / c->timed_ticks);
     return GM_OK;
   }

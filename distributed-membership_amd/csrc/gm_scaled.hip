@@ -37,39 +37,12 @@
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint8_t u8x16 __attribute__((ext_vector_type(16)));
 
-__device__ __forceinline__ uint32_t mt_temper(uint32_t v) {
-  v ^= v >> 11;
-  v ^= (v << 7) & 0x9d2c5680u;
-  v ^= (v << 15) & 0xefc60000u;
-  return v ^ (v >> 18);
-}
-
 // ------------------------------------------------------------------ gm_s_mtgen
-// Outputs 0..15 of mt19937(seed) need init words x[0..16] and x[397..412] only
-// (output k twists x[k], x[k+1], x[k+397]; all still init words for k < 227).
 __global__ __launch_bounds__(256) void gm_s_mtgen(SState s, int t) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= s.n) return;
-  uint32_t lo[S_MT_RAW + 1], hi[S_MT_RAW];
-  uint32_t v = gm_rd_seed(s.rd_seed, t, r + 1);
-  lo[0] = v;
-#pragma unroll
-  for (int i = 1; i <= S_MT_RAW; i++) {
-    v = 1812433253u * (v ^ (v >> 30)) + (uint32_t)i;
-    lo[i] = v;
-  }
-  for (int i = S_MT_RAW + 1; i < 397; i++) v = 1812433253u * (v ^ (v >> 30)) + (uint32_t)i;
-#pragma unroll
-  for (int i = 0; i < S_MT_RAW; i++) {
-    v = 1812433253u * (v ^ (v >> 30)) + (uint32_t)(397 + i);
-    hi[i] = v;
-  }
   uint32_t out[S_MT_RAW];
-#pragma unroll
-  for (int k = 0; k < S_MT_RAW; k++) {
-    const uint32_t y = (lo[k] & 0x80000000u) | (lo[k + 1] & 0x7fffffffu);
-    out[k] = mt_temper(hi[k] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u));
-  }
+  gm_mt_first16(gm_rd_seed(s.rd_seed, t, r + 1), out);
   uint4 *dst = (uint4 *)(s.mtraw + (size_t)r * S_MT_RAW);
 #pragma unroll
   for (int k = 0; k < S_MT_RAW / 4; k++) dst[k] = make_uint4(out[4 * k], out[4 * k + 1], out[4 * k + 2], out[4 * k + 3]);

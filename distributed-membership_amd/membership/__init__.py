@@ -7,5 +7,5 @@ CPU fallback: constructing a Simulator without the built library, or without a
 GPU, raises.
 """
 from .abi import (GM_EV_JOINED, GM_EV_REMOVED, GM_EV_START_GROUP, GM_EV_TIME_MARK, GM_EV_TRY_JOIN,  # noqa: F401
-                  GM_MODE_FAITHFUL, GM_MODE_SCALED, GmError, Simulator, crash_set, lib_path, load_library)
+                  GM_MODE_FAITHFUL, GM_MODE_PARTIAL, GM_MODE_SCALED, GmError, Simulator, crash_set, lib_path, load_library)
 from .app import Application, Params, format_msgcount, log_addr  # noqa: F401

@@ -4,8 +4,8 @@ import os
 
 import numpy as np
 
-GM_ABI_VERSION = 1
-GM_MODE_FAITHFUL, GM_MODE_SCALED = 0, 1
+GM_ABI_VERSION = 2
+GM_MODE_FAITHFUL, GM_MODE_SCALED, GM_MODE_PARTIAL = 0, 1, 2
 GM_EV_JOINED, GM_EV_REMOVED, GM_EV_START_GROUP, GM_EV_TRY_JOIN, GM_EV_TIME_MARK = 1, 2, 3, 4, 5
 GM_OK, GM_ERANGE = 0, -4
 
@@ -24,7 +24,8 @@ class GmConfig(ctypes.Structure):
                 ("drop_seed", ctypes.c_uint64),
                 ("device", ctypes.c_int32), ("shard_rank", ctypes.c_int32), ("shard_count", ctypes.c_int32),
                 ("init_mode", ctypes.c_int32), ("init_t0", ctypes.c_int32), ("init_seed", ctypes.c_uint64),
-                ("band", ctypes.c_int32), ("reserved", ctypes.c_int32 * 3)]
+                ("band", ctypes.c_int32), ("view", ctypes.c_int32), ("view_seed", ctypes.c_uint64),
+                ("reserved", ctypes.c_int32 * 2)]
 
 
 class GmEvent(ctypes.Structure):
@@ -108,7 +109,7 @@ class Simulator:
 
     def __init__(self, n, mode=GM_MODE_FAITHFUL, single_failure=1, drop_msg=0, drop_prob=0.1, time_seed=0,
                  rd_seed=0, drop_pct=0, drop_from=0, drop_to=0, drop_seed=0, device=0, shard_rank=0, shard_count=1,
-                 init_mode=0, init_t0=0, init_seed=0, band=0):
+                 init_mode=0, init_t0=0, init_seed=0, band=0, view=0, view_seed=0):
         self.lib = load_library()
         cfg = GmConfig()
         cfg.abi_version = GM_ABI_VERSION
@@ -119,6 +120,7 @@ class Simulator:
         cfg.device, cfg.shard_rank, cfg.shard_count = device, shard_rank, shard_count
         cfg.init_mode, cfg.init_t0, cfg.init_seed = init_mode, init_t0, init_seed
         cfg.band = band
+        cfg.view, cfg.view_seed = view, view_seed
         self.cfg = cfg
         self.n = n
         self.mode = mode

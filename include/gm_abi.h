@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define GM_ABI_VERSION 1
+#define GM_ABI_VERSION 2
 
 enum gm_status {
   GM_OK = 0,
@@ -59,7 +59,8 @@ enum gm_status {
 
 enum gm_mode {
   GM_MODE_FAITHFUL = 0, /* the reference: EmulNet cap 30000, per-entry messages, S1 drops */
-  GM_MODE_SCALED = 1    /* build-defined large-N regime: converged start, keyed drops */
+  GM_MODE_SCALED = 1,   /* build-defined large-N regime: converged start, keyed drops */
+  GM_MODE_PARTIAL = 2   /* build-defined V-entry membership views (scenario S-C; oracle/ref_cpu.c PARTIAL) */
 };
 
 enum gm_event_kind {
@@ -96,7 +97,9 @@ typedef struct gm_config {
   int32_t init_t0;
   uint64_t init_seed;
   int32_t band;            /* SCALED columns per band of the tick kernel (64/128/256/512; 0 = auto) */
-  int32_t reserved[3];
+  int32_t view;            /* PARTIAL view capacity V (2..64; 0 = 32) */
+  uint64_t view_seed;      /* PARTIAL initial views and eviction tie-break */
+  int32_t reserved[2];
 } gm_config;
 
 /* one log record; `order` sorts records of a drain into reference log order */

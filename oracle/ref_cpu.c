@@ -806,3 +806,259 @@ int oc_bench_sample(int n, int lists, int max_nodes, double min_seconds, int *ou
   free(c);
   return 0;
 }
+
+/* ===================================================================== PARTIAL
+ * V-entry views (scenario S-C): the reference protocol with
+ * every membership list capped at V entries. The reference is full-membership
+ * only, so the semantics below are build-defined; each step cites the reference
+ * rule it keeps. This restatement IS the specification of GM_MODE_PARTIAL.
+ *
+ *  - entry (id, hb); its timestamp is the tick the heartbeat was produced:
+ *    every live node's self heartbeat at tick t is 2t-1 (MP1Node.cpp:412-415
+ *    bumps twice per nodeLoopOps), so ts = (hb+1)/2 travels with the heartbeat
+ *    (a bounded view churns: stamping ts = receive tick, as the full list does,
+ *    would let a crashed node's entry circulate forever as "fresh");
+ *  - merge (updatelistCallBack, MP1Node.cpp:259-301): per id keep the largest hb;
+ *    absent ids are inserted; a node merges at most OP_KP = 16 lists per tick (a node
+ *    receiving more merges those of the 16 lowest sender indices);
+ *  - self bump; sweep (MP1Node.cpp:426-444): age >= TFAIL counts toward numfailed,
+ *    age >= TREMOVE removes (REMOVE event);
+ *  - eviction to V: self first, then the largest hb (freshest), ties broken by a
+ *    keyed hash (view_seed, t, observer, id); evictions are silent; ids present
+ *    after the tick and absent before are joins (ADD events);
+ *  - numfailed = removed + stale entries of the final list; gossip draw over the
+ *    final list in id order exactly as MP1Node.cpp:449-489; the sent list is the
+ *    final list's fresh entries (sendMemberList, MP1Node.cpp:360-395);
+ *  - drops keyed by (t_send, src, dst, id-1) as in OC_SCALED; crash set at the end
+ *    of crash_tick; warm start at t0: self {2t0-1} plus V-1 distinct peers chosen by
+ *    mix64(view_seed ^ i<<32 ^ j) % n, peer hb 2(t0-1-a)-1, a = mix64(init_seed ^
+ *    i<<32 ^ p)>>40 % 4. */
+#define OP_KP 16 /* lists merged per node and tick; more: those of the lowest sender indices */
+typedef struct pnode { int32_t *ids, *hbs; int cnt; int32_t hbctr; int failed; } pnode;
+struct op_ctx {
+  op_config cfg;
+  int n, t, V;
+  pnode *nd;
+  snap *snaps, *snaps_next;         /* sent lists of the previous / current tick */
+  int32_t *tgt, *tgt_next, *ntgt, *ntgt_next;
+  int32_t *crash;
+  oc_event *ev;
+  int nev, evcap;
+  sbuf dump;
+  /* scratch */
+  int32_t *cid, *chb, *cown;
+  int ccap;
+};
+
+static void op_emit(op_ctx *c, int logger, int kind, int32_t subject) {
+  if (c->nev == c->evcap) {
+    c->evcap = c->evcap ? 2 * c->evcap : 1024;
+    c->ev = (oc_event *)realloc(c->ev, sizeof(oc_event) * (size_t)c->evcap);
+  }
+  oc_event e = {c->t, logger, kind, subject};
+  c->ev[c->nev++] = e;
+}
+
+uint64_t op_evict_key(uint64_t view_seed, int32_t t, int32_t obs, int32_t id) {
+  return mix64(mix64(view_seed ^ (uint64_t)(uint32_t)t) ^ (((uint64_t)(uint32_t)obs << 32) | (uint32_t)id));
+}
+
+op_ctx *op_create(const op_config *cfg) {
+  if (cfg->n < 2 || cfg->v < 2 || cfg->v > 64 || cfg->v > cfg->n || cfg->init_t0 < 5) return NULL;
+  op_ctx *c = (op_ctx *)calloc(1, sizeof(op_ctx));
+  c->cfg = *cfg;
+  c->n = cfg->n;
+  c->V = cfg->v;
+  c->t = cfg->init_t0 + 1;
+  const int n = c->n, V = c->V, t0 = cfg->init_t0;
+  c->nd = (pnode *)calloc((size_t)n, sizeof(pnode));
+  for (int i = 0; i < n; i++) {
+    pnode *p = &c->nd[i];
+    p->ids = (int32_t *)malloc(sizeof(int32_t) * (size_t)V);
+    p->hbs = (int32_t *)malloc(sizeof(int32_t) * (size_t)V);
+    p->hbctr = 2 * t0;
+    p->ids[0] = i + 1;
+    p->hbs[0] = 2 * t0 - 1;
+    p->cnt = 1;
+    for (uint64_t j = 0; p->cnt < V; j++) {
+      int32_t q = (int32_t)(mix64(cfg->view_seed ^ ((uint64_t)(uint32_t)i << 32) ^ j) % (uint64_t)n);
+      int dup = q == i;
+      for (int k = 1; k < p->cnt && !dup; k++) dup = p->ids[k] == q + 1;
+      if (dup) continue;
+      int a = (int)((mix64(cfg->init_seed ^ ((uint64_t)(uint32_t)i << 32) ^ (uint64_t)(uint32_t)q) >> 40) % 4);
+      p->ids[p->cnt] = q + 1;
+      p->hbs[p->cnt] = 2 * (t0 - 1 - a) - 1;
+      p->cnt++;
+    }
+    /* keep the list sorted by id (the reference's memberList order) */
+    for (int a = 1; a < p->cnt; a++)
+      for (int b = a; b > 0 && p->ids[b - 1] > p->ids[b]; b--) {
+        int32_t x = p->ids[b]; p->ids[b] = p->ids[b - 1]; p->ids[b - 1] = x;
+        x = p->hbs[b]; p->hbs[b] = p->hbs[b - 1]; p->hbs[b - 1] = x;
+      }
+  }
+  c->snaps = (snap *)calloc((size_t)n, sizeof(snap));
+  c->snaps_next = (snap *)calloc((size_t)n, sizeof(snap));
+  for (int i = 0; i < n; i++) {
+    c->snaps[i].ids = (int32_t *)malloc(sizeof(int32_t) * (size_t)V);
+    c->snaps[i].hbs = (int32_t *)malloc(sizeof(int32_t) * (size_t)V);
+    c->snaps_next[i].ids = (int32_t *)malloc(sizeof(int32_t) * (size_t)V);
+    c->snaps_next[i].hbs = (int32_t *)malloc(sizeof(int32_t) * (size_t)V);
+  }
+  c->tgt = (int32_t *)calloc((size_t)n * FANOUT, sizeof(int32_t));
+  c->tgt_next = (int32_t *)calloc((size_t)n * FANOUT, sizeof(int32_t));
+  c->ntgt = (int32_t *)calloc((size_t)n, sizeof(int32_t));
+  c->ntgt_next = (int32_t *)calloc((size_t)n, sizeof(int32_t));
+  c->crash = (int32_t *)calloc((size_t)(cfg->crash_count > 0 ? cfg->crash_count : 1), sizeof(int32_t));
+  if (cfg->crash_count > 0) oc_crash_set(n, cfg->crash_count, cfg->crash_seed, c->crash);
+  return c;
+}
+
+void op_destroy(op_ctx *c) {
+  if (!c) return;
+  for (int i = 0; i < c->n; i++) {
+    free(c->nd[i].ids); free(c->nd[i].hbs);
+    free(c->snaps[i].ids); free(c->snaps[i].hbs);
+    free(c->snaps_next[i].ids); free(c->snaps_next[i].hbs);
+  }
+  free(c->nd); free(c->snaps); free(c->snaps_next);
+  free(c->tgt); free(c->tgt_next); free(c->ntgt); free(c->ntgt_next);
+  free(c->crash); free(c->ev); free(c->dump.p);
+  free(c->cid); free(c->chb); free(c->cown);
+  free(c);
+}
+
+typedef struct pcand { int32_t id, hb, own; uint64_t key; } pcand;
+static int pc_evict_cmp(const void *x, const void *y) { /* self first, hb desc, key asc */
+  const pcand *a = (const pcand *)x, *b = (const pcand *)y;
+  if (a->own != b->own && (a->own == 2 || b->own == 2)) return a->own == 2 ? -1 : 1;
+  if (a->hb != b->hb) return a->hb > b->hb ? -1 : 1;
+  return a->key < b->key ? -1 : (a->key > b->key);
+}
+static int pc_id_cmp(const void *x, const void *y) {
+  const pcand *a = (const pcand *)x, *b = (const pcand *)y;
+  return a->id - b->id;
+}
+
+static void op_node(op_ctx *c, int i, pcand *m) {
+  const int t = c->t, V = c->V;
+  pnode *p = &c->nd[i];
+  int cnt = 0;
+  for (int k = 0; k < p->cnt; k++) { m[cnt].id = p->ids[k]; m[cnt].hb = p->hbs[k]; m[cnt].own = 1; cnt++; }
+  /* lists delivered to i: every sender that targeted i at t-1 (BSP, order-free) */
+  const int t_send = t - 1;
+  const int dropping = c->cfg.drop_pct > 0 && t_send >= c->cfg.drop_from && t_send < c->cfg.drop_to;
+  int lists = 0;
+  for (int s = 0; s < c->n && lists < OP_KP; s++)
+    for (int q = 0; q < c->ntgt[s]; q++) {
+      if (c->tgt[(size_t)s * FANOUT + q] != i) continue;
+      if (++lists > OP_KP) break;
+      const snap *sp = &c->snaps[s];
+      uint64_t pair = mix64(c->cfg.drop_seed ^ ((uint64_t)(uint32_t)t_send << 48) ^ ((uint64_t)s << 24) ^ (uint64_t)i);
+      for (int e = 0; e < sp->n; e++) {
+        if (dropping) {
+          uint32_t h = (uint32_t)(mix64(pair + (uint64_t)(sp->ids[e] - 1)) >> 32);
+          if ((int)(h % 100u) < c->cfg.drop_pct) continue;
+        }
+        int k = 0;
+        while (k < cnt && m[k].id != sp->ids[e]) k++;
+        if (k == cnt) { m[cnt].id = sp->ids[e]; m[cnt].hb = sp->hbs[e]; m[cnt].own = 0; cnt++; }
+        else if (sp->hbs[e] > m[k].hb) m[k].hb = sp->hbs[e];
+      }
+    }
+  /* self bump (heartbeat++; myPos->setheartbeat(heartbeat++)) */
+  int selfk = -1;
+  for (int k = 0; k < cnt; k++) if (m[k].id == i + 1) selfk = k;
+  if (selfk < 0) { fprintf(stderr, "partial: node %d lost its own entry\n", i); abort(); }
+  p->hbctr++;
+  m[selfk].hb = p->hbctr++;
+  m[selfk].own = 2;
+  /* sweep */
+  int removed = 0, w = 0;
+  for (int k = 0; k < cnt; k++) {
+    int age = t - (m[k].hb + 1) / 2;
+    if (age >= TREMOVE) {
+      removed++;
+      if (m[k].own) op_emit(c, i, OC_EV_REMOVE, m[k].id);
+      continue;
+    }
+    m[w++] = m[k];
+  }
+  cnt = w;
+  /* evict to V */
+  if (cnt > V) {
+    for (int k = 0; k < cnt; k++) m[k].key = op_evict_key(c->cfg.view_seed, t, i, m[k].id);
+    qsort(m, (size_t)cnt, sizeof(pcand), pc_evict_cmp);
+    cnt = V;
+  }
+  qsort(m, (size_t)cnt, sizeof(pcand), pc_id_cmp);
+  int nfail = removed;
+  for (int k = 0; k < cnt; k++) {
+    if (!m[k].own) op_emit(c, i, OC_EV_ADD, m[k].id);
+    if (t - (m[k].hb + 1) / 2 >= TFAIL) nfail++;
+  }
+  p->cnt = cnt;
+  for (int k = 0; k < cnt; k++) { p->ids[k] = m[k].id; p->hbs[k] = m[k].hb; }
+  /* gossip draw (MP1Node.cpp:449-489) over the final list in id order */
+  int numpot = cnt - 1 - nfail, ng = 0;
+  int32_t g[FANOUT];
+  if (numpot > 0) {
+    mt r;
+    mt_seed(&r, oc_rd_seed(c->cfg.rd_seed, t, i + 1));
+    while (ng < FANOUT && ng < numpot) {
+      int ix = mt_uniform(&r, (uint32_t)cnt);
+      if (m[ix].id == i + 1) continue;
+      if (t - (m[ix].hb + 1) / 2 >= TFAIL) continue;
+      int dup = 0;
+      for (int q = 0; q < ng; q++) dup |= g[q] == m[ix].id - 1;
+      if (!dup) g[ng++] = m[ix].id - 1;
+    }
+  }
+  c->ntgt_next[i] = ng;
+  for (int q = 0; q < ng; q++) c->tgt_next[(size_t)i * FANOUT + q] = g[q];
+  snap *sn = &c->snaps_next[i];
+  sn->n = 0;
+  for (int k = 0; k < cnt; k++)
+    if (t - (m[k].hb + 1) / 2 < TFAIL) { sn->ids[sn->n] = m[k].id; sn->hbs[sn->n] = m[k].hb; sn->n++; }
+}
+
+int op_tick(op_ctx *c) {
+  const int n = c->n;
+  pcand *m = (pcand *)malloc(sizeof(pcand) * (size_t)c->V * (size_t)(n + 1));
+  c->nev = 0;
+  for (int i = n - 1; i >= 0; i--) {
+    c->ntgt_next[i] = 0;
+    c->snaps_next[i].n = 0;
+    if (c->nd[i].failed) continue;
+    op_node(c, i, m);
+  }
+  free(m);
+  qsort(c->ev, (size_t)c->nev, sizeof(oc_event), ev_canon);
+  snap *ts = c->snaps; c->snaps = c->snaps_next; c->snaps_next = ts;
+  int32_t *tt = c->tgt; c->tgt = c->tgt_next; c->tgt_next = tt;
+  tt = c->ntgt; c->ntgt = c->ntgt_next; c->ntgt_next = tt;
+  if (c->t == c->cfg.crash_tick)
+    for (int k = 0; k < c->cfg.crash_count; k++) c->nd[c->crash[k]].failed = 1;
+  c->t++;
+  return 0;
+}
+
+int op_time(const op_ctx *c) { return c->t; }
+
+size_t op_events(op_ctx *c, const oc_event **ev) {
+  *ev = c->ev;
+  return (size_t)c->nev;
+}
+
+const char *op_dump(op_ctx *c, size_t *len) {
+  c->dump.n = 0;
+  const int t = c->t - 1;
+  for (int i = 0; i < c->n; i++) {
+    const pnode *p = &c->nd[i];
+    sb_printf(&c->dump, "%d %d 1 1 %d %d %d", t, i, p->failed, p->hbctr, p->cnt);
+    for (int k = 0; k < p->cnt; k++) sb_printf(&c->dump, " %d:%d:%d", p->ids[k], p->hbs[k], (p->hbs[k] + 1) / 2);
+    sb_put(&c->dump, "\n", 1);
+  }
+  *len = c->dump.n;
+  return c->dump.p ? c->dump.p : "";
+}

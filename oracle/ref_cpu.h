@@ -80,6 +80,28 @@ int oc_node(oc_ctx *c, int r, int32_t *state4);
 /* the crash set the SCALED driver uses (host fault injection) */
 int oc_crash_set(int n, int count, uint64_t seed, int32_t *out);
 
+/* PARTIAL mode (V-entry views, scenario S-C; semantics in ref_cpu.c): */
+typedef struct op_config {
+  int n, v;              /* nodes, view capacity V (2..64) */
+  uint64_t rd_seed;      /* S2 seed contract */
+  uint64_t view_seed;    /* initial views, eviction tie-break */
+  int init_t0;           /* warm start tick (>= 5) */
+  uint64_t init_seed;    /* initial heartbeat lags */
+  int crash_tick, crash_count;
+  uint64_t crash_seed;
+  int drop_pct, drop_from, drop_to;
+  uint64_t drop_seed;
+} op_config;
+typedef struct op_ctx op_ctx;
+op_ctx *op_create(const op_config *cfg);
+void op_destroy(op_ctx *c);
+int op_tick(op_ctx *c);
+int op_time(const op_ctx *c);
+size_t op_events(op_ctx *c, const oc_event **ev);
+/* "t i 1 1 failed hbctr cnt id:hb:ts ..." per node, ts = (hb+1)/2 */
+const char *op_dump(op_ctx *c, size_t *len);
+uint64_t op_evict_key(uint64_t view_seed, int32_t t, int32_t obs, int32_t id);
+
 /* CPU-baseline sample: time node-ticks of the SCALED workload at size n (see ref_cpu.c) */
 int oc_bench_sample(int n, int lists, int max_nodes, double min_seconds, int *out_nodes, double *out_seconds);
 

@@ -21,6 +21,14 @@ class OcConfig(ctypes.Structure):
                 ("init_t0", ctypes.c_int), ("init_seed", ctypes.c_uint64)]
 
 
+class OpConfig(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int), ("v", ctypes.c_int), ("rd_seed", ctypes.c_uint64),
+                ("view_seed", ctypes.c_uint64), ("init_t0", ctypes.c_int), ("init_seed", ctypes.c_uint64),
+                ("crash_tick", ctypes.c_int), ("crash_count", ctypes.c_int), ("crash_seed", ctypes.c_uint64),
+                ("drop_pct", ctypes.c_int), ("drop_from", ctypes.c_int), ("drop_to", ctypes.c_int),
+                ("drop_seed", ctypes.c_uint64)]
+
+
 class OcEvent(ctypes.Structure):
     _fields_ = [("t", ctypes.c_int32), ("logger", ctypes.c_int32), ("kind", ctypes.c_int32),
                 ("subject", ctypes.c_int32)]
@@ -59,6 +67,17 @@ def lib():
         L.oc_rd_seed.argtypes = [ctypes.c_uint64, ctypes.c_int32, ctypes.c_int32]
         L.oc_rd_seed.restype = ctypes.c_uint32
         L.oc_mt_uniform.argtypes = [ctypes.c_uint32, ctypes.c_int, ctypes.c_int, P(ctypes.c_int32)]
+        L.op_create.argtypes = [P(OpConfig)]
+        L.op_create.restype = ctypes.c_void_p
+        L.op_destroy.argtypes = [ctypes.c_void_p]
+        L.op_tick.argtypes = [ctypes.c_void_p]
+        L.op_time.argtypes = [ctypes.c_void_p]
+        L.op_dump.argtypes = [ctypes.c_void_p, P(ctypes.c_size_t)]
+        L.op_dump.restype = ctypes.c_void_p
+        L.op_events.argtypes = [ctypes.c_void_p, P(P(OcEvent))]
+        L.op_events.restype = ctypes.c_size_t
+        L.op_evict_key.argtypes = [ctypes.c_uint64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]
+        L.op_evict_key.restype = ctypes.c_uint64
         _lib = L
     return _lib
 
@@ -121,6 +140,45 @@ class Oracle:
         st = np.zeros(4, dtype=np.int32)
         self.L.oc_node(self.h, r, _i32p(st))
         return st
+
+
+class PartialOracle:
+    """PARTIAL mode (V-entry views, scenario S-C): the oracle IS the specification."""
+
+    def __init__(self, n, v=32, rd_seed=7, view_seed=5, init_t0=8, init_seed=11, crash_tick=-1, crash_count=0,
+                 crash_seed=42, drop_pct=0, drop_from=0, drop_to=0, drop_seed=0):
+        self.L = lib()
+        cfg = OpConfig(n, v, rd_seed, view_seed, init_t0, init_seed, crash_tick, crash_count, crash_seed, drop_pct,
+                       drop_from, drop_to, drop_seed)
+        self.h = self.L.op_create(ctypes.byref(cfg))
+        if not self.h:
+            raise ValueError("op_create failed")
+        self.n = n
+
+    def close(self):
+        if self.h:
+            self.L.op_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def tick(self):
+        self.L.op_tick(self.h)
+
+    @property
+    def time(self):
+        return self.L.op_time(self.h)
+
+    def dump(self):
+        n = ctypes.c_size_t()
+        p = self.L.op_dump(self.h, ctypes.byref(n))
+        return ctypes.string_at(p, n.value) if n.value else b""
+
+    def events(self):
+        p = ctypes.POINTER(OcEvent)()
+        n = self.L.op_events(self.h, ctypes.byref(p))
+        return [(p[k].t, p[k].logger, p[k].kind, p[k].subject) for k in range(n)]
 
 
 def crash_set(n, count, seed):
