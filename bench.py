@@ -64,7 +64,10 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--cluster", type=int, default=65536, help="N, simulated nodes")
+    p.add_argument("--scenario", choices=["S-A", "S-C"], default="S-A",
+                   help="S-A: full membership N=65,536 (headline); S-C: partial views V=32, N=16M, 5%% drop")
+    p.add_argument("--cluster", type=int, default=0, help="N, simulated nodes (0: the scenario's)")
+    p.add_argument("--view", type=int, default=32, help="S-C view capacity V")
     p.add_argument("--prologue", type=int, default=25)
     p.add_argument("--t0", type=int, default=8, help="warm converged start at tick t0 (0: cold start)")
     p.add_argument("--crash-tick", type=int, default=10)
@@ -76,6 +79,9 @@ def parse():
 
 def main():
     a = parse()
+    if a.scenario == "S-C":
+        return main_partial(a)
+    a.cluster = a.cluster or 65536
     rtx = Roctx()
     rtx.pause()
     rank = int(os.environ.get("RANK", "0"))
@@ -194,6 +200,96 @@ def main():
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def main_partial(a):
+    """Scenario S-C (BASELINE.json configs[4]): N = 16,777,216 nodes
+    with V = 32-entry partial views (GM_MODE_PARTIAL, oracle/ref_cpu.c "PARTIAL"),
+    5 % per-entry message drop on every tick, the S-A crash schedule (1 % at tick 10).
+    One step = one tick of gm_p_tick (+ the S2 precompute gm_p_mtgen)."""
+    rtx = Roctx()
+    rtx.pause()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from membership import GM_MODE_PARTIAL, Simulator, crash_set, load_library
+    load_library()
+    if world > 1:
+        raise SystemExit("S-C multi-GPU: not in this build yet")
+    n = a.cluster or (1 << 24)
+    V = a.view
+    ncrash = int(round(n * a.crash_frac))
+    t0 = max(a.t0, 5)
+    kw = dict(rd_seed=7, view=V, view_seed=5, init_mode=1, init_t0=t0, init_seed=11,
+              drop_pct=5, drop_from=0, drop_to=1 << 20, drop_seed=42)
+    sim = Simulator(n, GM_MODE_PARTIAL, device=local, **kw)
+    crash = crash_set(n, ncrash, 42)
+    while sim.time <= a.prologue:
+        t = sim.time
+        sim.tick()
+        if t == a.crash_tick:
+            sim.set_failed(crash)
+    for _ in range(a.warmup):
+        sim.tick()
+    sim.sync()
+    sim.set_timing(1)
+    rtx.resume()
+    t_0 = time.perf_counter()
+    for _ in range(a.steps):
+        sim.tick()
+    sim.sync()
+    t_1 = time.perf_counter()
+    rtx.pause()
+    elapsed = t_1 - t_0
+    kernel_ms = sim.last_kernel_ms()
+    st = sim.tick_stats()
+    assert st["err"] == 0, st
+    n_live, m_lists = st["live"], st["lists"]
+    # algorithmic bytes of one gm_p_tick launch (DESIGN.md §PARTIAL): per live node the own
+    # list read + the new list written (2 x 8V B) + inbox/state/S2/targets/stat words (120 B);
+    # per delivered list the sender's list (8V B) + its inbox word
+    b_alg = n_live * (16 * V + 120) + m_lists * (8 * V + 4)
+    achieved = b_alg / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else None
+    out = {
+        "metric": "simulated node-ticks/sec (S-C partial view)",
+        "value": n * a.steps / elapsed,
+        "unit": "node-ticks/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": elapsed / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64 view entries (id<<32|hb, integer)",
+        "data": "synthetic (warm random V-entry views, seeded crash set, keyed 5% drops)",
+        "config": {"workload": f"S-C: PARTIAL V={V} views, 5% per-entry drop, 1% crash at tick {a.crash_tick}, "
+                               "fanout 5, TFAIL 5, TREMOVE 20",
+                   "n": n, "view": V, "start": f"warm t0={t0}", "prologue_to_tick": a.prologue, "crashed": ncrash,
+                   "live": n_live, "lists_per_tick": m_lists, "max_inbox": st["max_inbox"],
+                   "parallelism": "single GPU"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+                     "frac": (achieved / PEAK_HBM_GBPS) if achieved else None, "traffic": None,
+                     "kernel": "gm_p_tick", "kernel_ms": kernel_ms, "alg_bytes_per_launch": b_alg},
+    }
+    if not a.no_cpu:
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        import oracle_py  # the oracle is the CPU baseline here, never the measured path
+        ns = min(n, 1 << 17)
+        ora = oracle_py.PartialOracle(ns, v=V, rd_seed=7, view_seed=5, init_t0=t0, init_seed=11,
+                                      drop_pct=5, drop_from=0, drop_to=1 << 20, drop_seed=42)
+        ora.tick()  # first tick: empty inboxes
+        ora.tick()
+        ticks, secs = 0, 0.0
+        while secs < a.cpu_seconds and ticks < 8:
+            c0 = time.perf_counter()
+            ora.tick()
+            secs += time.perf_counter() - c0
+            ticks += 1
+        out["cpu_baseline"] = {"value": ns * ticks / secs, "unit": "node-ticks/s", "cores": 1, "kind": "port",
+                               "sample": f"{ticks} steady ticks of an N={ns} S-C cluster (V={V}, 5% drop) on one host "
+                                         f"core ({secs:.1f} s, oracle/ref_cpu.c op_tick)"}
+    print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":

@@ -318,6 +318,8 @@ static int create_partial(gm_ctx *c) {
   TRY(dalloc(c, &p.ev_cnt, n));
   TRY(dalloc(c, &p.rowstat, (size_t)n * 4));
   TRY(dalloc(c, &p.targets, (size_t)n * GM_FANOUT));
+  TRY(dalloc(c, &p.big, n));
+  TRY(dalloc(c, &p.big_cnt, 1));
   TRY(dalloc(c, &p.err, 1));
   TRY(dalloc(c, &c->p_mtraw, (size_t)n * 16));
   HIPCHECK(hipMemset(p.lists, 0, sizeof(uint64_t) * 2 * n * p.V));
@@ -578,16 +580,20 @@ static int drain_partial(gm_ctx *c, std::vector<gm_event> &out) {
   HIPCHECK(hipMemcpyAsync(cnt.data(), p.ev_cnt, sizeof(int32_t) * c->n, hipMemcpyDeviceToHost, c->stream));
   HIPCHECK(hipStreamSynchronize(c->stream));
   size_t tot = 0;
-  for (int32_t v : cnt) tot += (size_t)v;
+  for (int32_t v : cnt) tot += (size_t)(v & 0xFFFF) + (size_t)(v >> 16);
   if (!tot) return GM_OK;
-  std::vector<uint32_t> ev((size_t)c->n * 2 * p.V);
+  const size_t row = 2 * (size_t)p.V;  // joins from the front, removals from the back
+  std::vector<uint32_t> ev((size_t)c->n * row);
   HIPCHECK(hipMemcpy(ev.data(), p.ev, sizeof(uint32_t) * ev.size(), hipMemcpyDeviceToHost));
   const int t = c->t - 1;
-  for (int r = 0; r < c->n; r++)
-    for (int q = 0; q < cnt[r]; q++) {
-      const uint32_t rec = ev[(size_t)r * 2 * p.V + q];
+  out.reserve(out.size() + tot);
+  for (int r = 0; r < c->n; r++) {
+    const int nj = cnt[r] & 0xFFFF, nr = cnt[r] >> 16;
+    for (int q = 0; q < nj + nr; q++) {
+      const uint32_t rec = ev[(size_t)r * row + (q < nj ? q : row - 1 - (q - nj))];
       out.push_back(gm_event{t, r, (rec >> 30) == P_EV_ADD ? GM_EV_JOINED : GM_EV_REMOVED, (int32_t)(rec & 0x3FFFFFFFu)});
     }
+  }
   sort_canonical(out);
   return GM_OK;
 }
@@ -623,7 +629,7 @@ extern "C" int gm_event_counts(gm_ctx *c, uint64_t counts[6]) {
     std::vector<int32_t> cnt(c->n);
     HIPCHECK(hipMemcpyAsync(cnt.data(), c->p.ev_cnt, sizeof(int32_t) * c->n, hipMemcpyDeviceToHost, c->stream));
     HIPCHECK(hipStreamSynchronize(c->stream));
-    for (int32_t v : cnt) counts[0] += (uint64_t)v;
+    for (int32_t v : cnt) counts[0] += (uint64_t)(v & 0xFFFF) + (uint64_t)(v >> 16);
   } else {
     for (const gm_event &e : c->pending) counts[e.kind]++;
   }
@@ -742,6 +748,30 @@ extern "C" int gm_dump_tables(gm_ctx *c, char *buf, size_t cap, size_t *len) {
   std::string out;
   char tmp[96];
   const int t = c->t - 1;
+  if (c->cfg.mode == GM_MODE_PARTIAL) {  // the V-entry lists (id order) of the last tick, one copy
+    const PState &p = c->p;
+    std::vector<uint64_t> all((size_t)c->n * p.V);
+    HIPCHECK(hipMemcpy(all.data(), p.lists + (size_t)(t & 1) * c->n * p.V, sizeof(uint64_t) * all.size(),
+                       hipMemcpyDeviceToHost));
+    for (int i = 0; i < c->n; i++) {
+      const uint64_t *row = all.data() + (size_t)i * p.V;
+      int cnt = 0;
+      for (int j = 0; j < p.V; j++) cnt += row[j] != 0;
+      snprintf(tmp, sizeof tmp, "%d %d %d %d %d %d %d", t, i, st[4 * i], st[4 * i + 1], st[4 * i + 2], st[4 * i + 3], cnt);
+      out += tmp;
+      for (int j = 0; j < p.V; j++) {
+        if (!row[j]) continue;
+        const int h = (int)(uint32_t)row[j];
+        snprintf(tmp, sizeof tmp, " %d:%d:%d", (int)(row[j] >> 32), h, (h + 1) / 2);
+        out += tmp;
+      }
+      out += "\n";
+    }
+    *len = out.size();
+    if (!buf || cap < out.size()) return GM_ERANGE;
+    memcpy(buf, out.data(), out.size());
+    return GM_OK;
+  }
   std::vector<int32_t> rh, rt;
   for (int i = 0; i < c->n; i++) {
     int w;

@@ -2,9 +2,11 @@
 #pragma once
 #include <stdint.h>
 
-#define P_VMAX 64        // view capacity limit (one wave lane per entry)
+#define P_VMAX 32        // view capacity limit (a list is one half-wave of 8-byte entries)
 #define P_KP 16          // gossip lists merged per node and tick (oracle OP_KP)
-#define P_H 1024         // per-wave LDS hash table slots (>= (P_KP + 1) * P_VMAX / 0.75 for V <= 32)
+#define P_KSMALL 10      // nodes with <= P_KSMALL delivered lists take the small-table kernel
+#define P_HS 512         // small kernel: LDS hash slots per wave (>= (1 + P_KSMALL) * P_VMAX / 0.69)
+#define P_HB 1024        // big kernel: LDS hash slots per wave (>= (1 + P_KP) * P_VMAX / 0.53)
 #define P_KMAX 64        // inbox capacity (lists queued per receiver per tick)
 #define P_EV_ADD 1u
 #define P_EV_REMOVE 2u
@@ -19,9 +21,11 @@ struct PState {
   int32_t *inbox[2];     // [n][P_KMAX] sender indices
   int32_t *hbctr;        // [n] heartbeat counter
   int32_t *failed;       // [n]
-  uint32_t *ev;          // [n][2V] kind<<30 | subject id (joins ascending id, then removals)
-  int32_t *ev_cnt;       // [n]
+  uint32_t *ev;          // [n][2V] kind<<30 | subject id: joins from the front (ascending id), removals from the back
+  int32_t *ev_cnt;       // [n] joins | removals << 16
   int32_t *rowstat;      // [n][4]: lists merged, view size, numfailed, targets chosen
   int32_t *targets;      // [n][GM_FANOUT]
+  int32_t *big;          // [n] worklist of nodes with > P_KSMALL lists (big-table kernel)
+  int32_t *big_cnt;      // [1]
   uint32_t *err;
 };

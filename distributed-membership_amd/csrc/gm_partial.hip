@@ -9,17 +9,42 @@
 // over the final list (MP1Node.cpp:449-489) and sendMemberList of its fresh
 // entries (MP1Node.cpp:360-395).
 //
-// One wave per node per tick (gm_p_tick), everything in the wave's LDS slice:
-// an open-addressing table keyed by id (64-bit CAS insert + max-merge), a sweep
-// over the table, radix selection of the V freshest, a 64-lane bitonic sort of
-// the survivors by id, the draw, and the counting-sort append into the targets'
-// inboxes. Lists are double-buffered by tick parity: a receiver reads its
-// senders' lists of tick t-1 directly and keeps their fresh entries, so no
-// separate payload copy is written.
+// One wave per node, everything in a ~4.8 KB LDS slice so 8 waves share a SIMD
+// (the per-node work is short dependent-load chains + LDS atomics: latency is
+// hidden by occupancy, and the instruction count per node is what bounds the
+// kernel once it is):
+//   1. loads issue together: the node's own list (one 8-byte entry per lane),
+//      its inbox (sender indices), its 16 precomputed S2 outputs, then every
+//      delivered list (V lanes per list, several lists per wave step);
+//   2. merge into an open-addressing LDS table keyed by id (32-bit CAS claim +
+//      ds_max of the heartbeat word), own entries first so they carry the
+//      "own" bit, delivered entries filtered to fresh + not dropped;
+//   3. self bump, then one sweep compacts the table in place into a dense
+//      array (TREMOVE removals counted and logged on the way);
+//   4. eviction to V only when the union exceeds V: an LDS histogram of the
+//      heartbeat distance from the top finds the cut heartbeat; inside the cut
+//      bucket a 6-bit radix histogram of the eviction keys and (rarely) an
+//      exact min-selection pick the smallest keys -- no full sort;
+//   5. the <= V kept entries are ranked by id (broadcast LDS compare) = the
+//      id-sorted list, stored as one coalesced row;
+//   6. the gossip draw runs on scalar registers (readlane of the drawn entry).
+// Nodes with more than P_KSMALL delivered lists (Poisson tail, ~1.4 %) do not fit
+// the small table: the small kernel defers them to a worklist that the big
+// kernel (1024-slot table, sender sort for > P_KP lists) drains.
+// Lists are double-buffered by tick parity: a receiver reads its senders' lists
+// of tick t-1 directly, so no separate payload copy is written.
 #include "gm_device.h"
 #include "gm_partial.h"
 
-#define P_LDS_BYTES (P_H * 8 + P_H + 256 * 4 + 624 * 4 + P_KMAX * 4 + P_VMAX * 8 + P_VMAX * 4)
+#define P_IDMASK 0x01FFFFFFu  // ids <= 2^25
+#define P_OWN 0x80000000u     // table id-word flag: the id was in the node's own list
+#define P_SELF 0x40000000u    // table id-word flag: the node's own entry
+#define P_MISC_BYTES (64 * 4 + P_VMAX * 4 + P_VMAX * 4 + P_VMAX * 8)
+
+template <int H>
+struct PLds {
+  static constexpr int bytes = H * 8 + P_MISC_BYTES;
+};
 
 __device__ __forceinline__ void p_wsync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -27,45 +52,13 @@ __device__ __forceinline__ void p_wsync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-__device__ __forceinline__ uint32_t p_hash(uint32_t id) { return (id * 0x9E3779B1u) >> (32 - 10); }
-
-// insert (id, hb) or raise the slot's hb to the max; returns the slot
-__device__ __forceinline__ int p_insert(unsigned long long *tab, uint64_t key) {
-  const uint32_t id = (uint32_t)(key >> 32);
-  uint32_t h = p_hash(id);
-  for (;;) {
-    unsigned long long cur = tab[h];
-    if (cur == 0) {
-      cur = atomicCAS(&tab[h], 0ull, (unsigned long long)key);
-      if (cur == 0) return (int)h;
-    }
-    if ((uint32_t)(cur >> 32) == id) {
-      atomicMax(&tab[h], (unsigned long long)key);
-      return (int)h;
-    }
-    h = (h + 1) & (P_H - 1);
-  }
-}
-
-__device__ __forceinline__ int p_find(const unsigned long long *tab, uint32_t id) {
-  uint32_t h = p_hash(id);
-  for (int probe = 0; probe < P_H; probe++) {
-    const unsigned long long cur = tab[h];
-    if (cur == 0) return -1;
-    if ((uint32_t)(cur >> 32) == id) return (int)h;
-    h = (h + 1) & (P_H - 1);
-  }
-  return -1;
-}
-
-__device__ __forceinline__ uint64_t p_mix64(uint64_t z) { return gm_mix64(z); }
-
-// eviction tie-break key (oracle op_evict_key): distinct ids give distinct keys
-__device__ __forceinline__ uint64_t p_evict_key(uint64_t view_seed, int t, int obs, uint32_t id) {
-  return p_mix64(p_mix64(view_seed ^ (uint64_t)(uint32_t)t) ^ (((uint64_t)(uint32_t)obs << 32) | id));
-}
-
 __device__ __forceinline__ int p_age(int t, uint32_t hb) { return t - (int)((hb + 1u) >> 1); }
+
+// eviction tie-break key (oracle op_evict_key): distinct ids give distinct keys;
+// kseed = mix64(view_seed ^ t) is wave-uniform
+__device__ __forceinline__ uint64_t p_evict_key(uint64_t kseed, int obs, uint32_t id) {
+  return gm_mix64(kseed ^ (((uint64_t)(uint32_t)obs << 32) | id));
+}
 
 // wave-wide inclusive scan of ints
 __device__ __forceinline__ int p_scan(int v, int lane) {
@@ -77,45 +70,83 @@ __device__ __forceinline__ int p_scan(int v, int lane) {
   return v;
 }
 
-__global__ __launch_bounds__(256) void gm_p_tick(PState s, int t, const uint32_t *mtraw) {
-  extern __shared__ __align__(16) unsigned char p_smem[];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int i = blockIdx.x * 4 + wave;
-  if (i >= s.n) return;  // whole wave; no workgroup barrier in this kernel
-  unsigned char *base = p_smem + (size_t)wave * P_LDS_BYTES;
-  unsigned long long *tab = (unsigned long long *)base;          // [P_H]
-  uint8_t *flg = base + P_H * 8;                                 // [P_H] bit0 own, bit1 self
-  uint32_t *hist = (uint32_t *)(flg + P_H);                      // [256]
-  uint32_t *mts = hist + 256;                                    // [624]
-  int32_t *snd = (int32_t *)(mts + 624);                         // [P_KMAX]
-  uint64_t *fin = (uint64_t *)(snd + P_KMAX);                    // [P_VMAX]
-  uint32_t *finf = (uint32_t *)(fin + P_VMAX);                   // [P_VMAX]
+__device__ __forceinline__ int p_below(uint64_t bal) {  // set bits of bal below this lane
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+}
+
+// exclusive wave prefix of small per-lane counts c < 2^BITS (ballot per bit + mbcnt)
+template <int BITS>
+__device__ __forceinline__ int p_excl(int c, int *total) {
+  int pos = 0, tot = 0;
+#pragma unroll
+  for (int b = 0; b < BITS; b++) {
+    const uint64_t bal = __ballot((c >> b) & 1);
+    pos += p_below(bal) << b;
+    tot += __builtin_popcountll(bal) << b;
+  }
+  *total = tot;
+  return pos;
+}
+
+__device__ __forceinline__ uint64_t p_readlane64(uint64_t v, int l) {
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, l);
+  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), l);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// claim or find the slot of `id` (idw = id | flags on claim), raise its heartbeat word
+template <int H>
+__device__ __forceinline__ int p_insert(uint32_t *tid, uint32_t *thb, uint32_t id, uint32_t idw, uint32_t hb) {
+  constexpr int LOGH = H == 512 ? 9 : 10;
+  uint32_t h = (id * 0x9E3779B1u) >> (32 - LOGH);
+  for (;;) {
+    uint32_t cur = tid[h];
+    if (cur == 0) {
+      cur = atomicCAS(&tid[h], 0u, idw);
+      if (cur == 0) break;
+    }
+    if ((cur & P_IDMASK) == id) break;
+    h = (h + 1) & (H - 1);
+  }
+  atomicMax(&thb[h], hb);
+  return (int)h;
+}
+
+// One node's tick on one wave. i: node index; k: lists queued for it this tick.
+template <int H, bool BIG>
+__device__ __forceinline__ void p_node(const PState &s, int t, const uint32_t *mtraw, int i, int k, int lane,
+                                       unsigned char *base) {
+  constexpr int TS = H / 64;                          // table slots per lane
+  constexpr int KK = BIG ? P_KP : P_KSMALL;           // lists merged at most
+  constexpr int DS = ((1 + KK) * P_VMAX + 63) / 64;   // dense entries per lane
+  constexpr int NSTEP = (KK + 1) / 2;                 // list-load steps (>= 2 lists per step)
+  uint32_t *tid = (uint32_t *)base;
+  uint32_t *thb = tid + H;
+  uint32_t *hist = thb + H;
+  uint32_t *kid = hist + 64;
+  uint32_t *khb = kid + P_VMAX;
+  uint64_t *fin = (uint64_t *)(khb + P_VMAX);
   const int V = s.V;
   const int par = t & 1;
-  int32_t *stat = s.rowstat + (size_t)i * 4;
-  int k = s.inbox_cnt[par][i];
-  if (lane == 0) s.inbox_cnt[par][i] = 0;  // consumed; the append target of tick t+2
-  if (s.failed[i]) {  // crashed: frozen (its list carried to this tick's buffer unchanged)
-    if (lane < V) s.lists[((size_t)par * s.n + i) * V + lane] = s.lists[((size_t)(par ^ 1) * s.n + i) * V + lane];
-    if (lane == 0) {
-      stat[0] = stat[1] = stat[2] = stat[3] = 0;
-      s.ev_cnt[i] = 0;
-    }
-    return;
-  }
-  if (k > P_KMAX) {
+  const uint64_t *prev = s.lists + (size_t)(par ^ 1) * s.n * V;
+  uint64_t *cur = s.lists + (size_t)par * s.n * V;
+
+  if (lane == 0) s.inbox_cnt[par][i] = 0;  // consumed; the append target of tick t+1
+  if (BIG && k > P_KMAX) {
     if (lane == 0) atomicOr(s.err, GM_ERR_INBOX);
     k = P_KMAX;
   }
-  const uint64_t *prev = s.lists + (size_t)(par ^ 1) * s.n * V;
-  uint64_t *cur = s.lists + (size_t)par * s.n * V;
-  for (int q = lane; q < P_H; q += 64) {
-    tab[q] = 0;
-    flg[q] = 0;
-  }
-  // senders of the delivered lists; with more than P_KP, the P_KP lowest indices
+  // ---- 1. loads
+  const uint64_t own = lane < V ? prev[(size_t)i * V + lane] : 0ull;
   int sv = lane < k ? s.inbox[par][(size_t)i * P_KMAX + lane] : 0x7FFFFFFF;
-  if (k > P_KP) {  // bitonic sort of the (<= 64) sender indices across the wave
+  const uint32_t raw0 = lane < 16 ? mtraw[(size_t)i * 16 + lane] : 0u;
+  const int hbnew = s.hbctr[i] + 1;
+  {  // clear the table (both word arrays are contiguous)
+    uint4 *z = (uint4 *)tid;
+#pragma unroll
+    for (int q = 0; q < H / 128; q++) z[lane + 64 * q] = make_uint4(0, 0, 0, 0);
+  }
+  if (BIG && k > P_KP) {  // the P_KP lowest sender indices: bitonic sort across the wave
 #pragma unroll
     for (int k2 = 2; k2 <= 64; k2 <<= 1)
 #pragma unroll
@@ -125,199 +156,239 @@ __global__ __launch_bounds__(256) void gm_p_tick(PState s, int t, const uint32_t
         sv = (lower == up) ? min(sv, o) : max(sv, o);
       }
   }
-  snd[lane] = sv;
-  const int kk = min(k, P_KP);
-  p_wsync();
-  // own entries (the row's list as of tick t-1)
-  if (lane < V) {
-    const uint64_t e = prev[(size_t)i * V + lane];
-    if (e) flg[p_insert(tab, e)] = 1;
+  const int kk = min(k, KK);
+  const int per = 64 / V, l = lane % V, jo = lane / V;
+  uint64_t dv[NSTEP];
+  int dsn[NSTEP];
+#pragma unroll
+  for (int st = 0; st < NSTEP; st++) {
+    const int j = st * per + jo;
+    const bool ok = jo < per && j < kk;
+    const int sn = __shfl(sv, ok ? j : 0, 64);
+    dsn[st] = sn;
+    dv[st] = ok ? prev[(size_t)sn * V + l] : 0ull;
   }
   p_wsync();
-  // delivered lists: each sender's list of tick t-1, fresh entries only (age < TFAIL at t-1)
+  // ---- 2. merge: own entries first (they carry P_OWN), then the delivered lists
+  int hslot = -1;
+  const uint32_t self_id = (uint32_t)(i + 1);
+  if (own != 0) {
+    const uint32_t id = (uint32_t)(own >> 32);
+    hslot = p_insert<H>(tid, thb, id, id | P_OWN, (uint32_t)own);
+  }
+  p_wsync();
   {
-    const int per = 64 / V;  // senders per wave step
-    const int l = lane % V, jo = lane / V;
     const uint32_t tfresh = (uint32_t)max(0, 2 * t - 11);  // hb >= 2t-11 <=> (t-1) - (hb+1)/2 < TFAIL
-    for (int j0 = 0; j0 < kk; j0 += per) {
-      const int j = j0 + jo;
-      if (jo < per && j < kk) {
-        const int sn = snd[j];
-        const uint64_t e = prev[(size_t)sn * V + l];
-        const uint32_t hb = (uint32_t)e, id = (uint32_t)(e >> 32);
-        bool take = e != 0 && hb >= tfresh;
-        if (take && s.drop_pct >= 0) {  // per-entry drops keyed by (t_send, src, dst, id-1)
-          const uint64_t pair = p_mix64(s.drop_seed ^ ((uint64_t)(uint32_t)(t - 1) << 48) ^
-                                        ((uint64_t)(uint32_t)sn << 24) ^ (uint64_t)(uint32_t)i);
-          const uint32_t h = (uint32_t)(p_mix64(pair + (uint64_t)(id - 1)) >> 32);
-          take = (int)(h % 100u) >= s.drop_pct;
-        }
-        if (take) (void)p_insert(tab, e);
+    const bool dropping = s.drop_pct >= 0;
+#pragma unroll
+    for (int st = 0; st < NSTEP; st++) {
+      const uint64_t e = dv[st];
+      bool take = e != 0 && (uint32_t)e >= tfresh;
+      const uint32_t id = (uint32_t)(e >> 32);
+      if (dropping && __ballot(take)) {  // per-entry drops keyed by (t_send, src, dst, id-1)
+        const uint64_t pair = gm_mix64(s.drop_seed ^ ((uint64_t)(uint32_t)(t - 1) << 48) ^
+                                       ((uint64_t)(uint32_t)dsn[st] << 24) ^ (uint64_t)(uint32_t)i);
+        const uint32_t h = (uint32_t)(gm_mix64(pair + (uint64_t)(id - 1)) >> 32);
+        take = take && (int)(h % 100u) >= s.drop_pct;
+      }
+      if (take) (void)p_insert<H>(tid, thb, id, id, (uint32_t)e);
+    }
+  }
+  p_wsync();
+  // ---- 3. self bump (heartbeat++; myPos->setheartbeat(heartbeat++)), then sweep + compaction
+  {
+    const uint64_t sb = __ballot(own != 0 && (uint32_t)(own >> 32) == self_id);
+    int hs;
+    if (sb) {
+      hs = __builtin_amdgcn_readlane(hslot, __builtin_ctzll(sb));
+    } else {  // cannot happen for a live node (the oracle aborts): flag, and re-insert self
+      hs = 0;
+      if (lane == 0) {
+        atomicOr(s.err, GM_ERR_SELF);
+        hs = p_insert<H>(tid, thb, self_id, self_id | P_OWN, 1u);
+      }
+      hs = __builtin_amdgcn_readfirstlane(hs);
+    }
+    if (lane == 0) {
+      thb[hs] = (uint32_t)hbnew;
+      tid[hs] |= P_SELF | P_OWN;
+      s.hbctr[i] = hbnew + 1;
+    }
+  }
+  p_wsync();
+  uint32_t *evr = s.ev + (size_t)i * 2 * V;
+  int m, removed, nrem;
+  {
+    uint32_t w[TS], hh[TS];
+#pragma unroll
+    for (int q = 0; q < TS / 4; q++) {
+      const uint4 a = ((const uint4 *)tid)[lane * (TS / 4) + q];
+      const uint4 b = ((const uint4 *)thb)[lane * (TS / 4) + q];
+      w[4 * q] = a.x; w[4 * q + 1] = a.y; w[4 * q + 2] = a.z; w[4 * q + 3] = a.w;
+      hh[4 * q] = b.x; hh[4 * q + 1] = b.y; hh[4 * q + 2] = b.z; hh[4 * q + 3] = b.w;
+    }
+    uint32_t alive = 0, rown = 0;
+    int rcount = 0;
+#pragma unroll
+    for (int u = 0; u < TS; u++) {
+      if (!(w[u] & P_IDMASK)) continue;
+      if (p_age(t, hh[u]) >= GM_TREMOVE) {
+        rcount++;
+        if (w[u] & P_OWN) rown |= 1u << u;
+      } else {
+        alive |= 1u << u;
       }
     }
-  }
-  p_wsync();
-  // self bump (heartbeat++; myPos->setheartbeat(heartbeat++))
-  if (lane == 0) {
-    int h = p_find(tab, (uint32_t)(i + 1));
-    if (h < 0) {
-      atomicOr(s.err, GM_ERR_SELF);
-      h = p_insert(tab, (uint64_t)(uint32_t)(i + 1) << 32 | 1u);
-    }
-    const int hb = s.hbctr[i] + 1;
-    s.hbctr[i] = hb + 1;
-    tab[h] = ((uint64_t)(uint32_t)(i + 1) << 32) | (uint32_t)hb;
-    flg[h] |= 2;
-  }
-  p_wsync();
-  // sweep: age >= TREMOVE removes; the rest are eviction candidates
-  uint32_t alive = 0, removed_own = 0;
-  int removed = 0;
-  for (int u = 0; u < P_H / 64; u++) {
-    const unsigned long long e = tab[lane + 64 * u];
-    if (!e) continue;
-    if (p_age(t, (uint32_t)e) >= GM_TREMOVE) {
-      removed++;
-      if (flg[lane + 64 * u] & 1) removed_own |= 1u << u;
-      continue;
-    }
-    alive |= 1u << u;
-  }
-  int m = __builtin_popcount(alive);
+    int tot;
+    (void)p_excl<TS == 8 ? 4 : 5>(rcount, &removed);
+    const int ro = __builtin_popcount(rown);
+    int rpos = p_excl<TS == 8 ? 4 : 5>(ro, &nrem);
+    if (nrem) {  // REMOVE events of the node's own entries, from the back of its event row
 #pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) {
-    m += __shfl_xor(m, o, 64);
-    removed += __shfl_xor(removed, o, 64);
+      for (int u = 0; u < TS; u++)
+        if ((rown >> u) & 1) evr[2 * V - 1 - rpos++] = (P_EV_REMOVE << 30) | (w[u] & P_IDMASK);
+    }
+    int pos = p_excl<TS == 8 ? 4 : 5>(__builtin_popcount(alive), &tot);
+    m = tot;
+#pragma unroll
+    for (int u = 0; u < TS; u++)
+      if ((alive >> u) & 1) {
+        tid[pos] = w[u];
+        thb[pos] = hh[u];
+        pos++;
+      }
   }
-  uint32_t keep = alive;
-  if (m > V) {
-    // evict to V: self, then the freshest (largest hb = smallest age), ties by the
-    // smallest eviction key. Age histogram (ages < TREMOVE) finds the cut age.
-    if (lane < 32) hist[lane] = 0;
+  p_wsync();
+  // ---- 4. dense entries e = s*64 + lane; eviction to V
+  uint32_t dw[DS], dh[DS];
+#pragma unroll
+  for (int q = 0; q < DS; q++) {
+    const int e = q * 64 + lane;
+    dw[q] = e < m ? tid[e] : 0u;
+    dh[q] = e < m ? thb[e] : 0u;
+  }
+  uint32_t keep = 0;
+  if (m <= V) {
+#pragma unroll
+    for (int q = 0; q < DS; q++)
+      if (dw[q]) keep |= 1u << q;
+  } else {
+    // heartbeat distance from the top (2t-1 = this tick's self heartbeat); alive
+    // entries have age < TREMOVE, i.e. distance <= 40 < 64
+    const int top = 2 * t - 1;
+    hist[lane] = 0;
     p_wsync();
-    for (int u = 0; u < P_H / 64; u++)
-      if (((alive >> u) & 1) && !(flg[lane + 64 * u] & 2)) atomicAdd(&hist[p_age(t, (uint32_t)tab[lane + 64 * u])], 1u);
+#pragma unroll
+    for (int q = 0; q < DS; q++)
+      if (dw[q] && !(dw[q] & P_SELF)) atomicAdd(&hist[min(max(top - (int)dh[q], 0), 63)], 1u);
     p_wsync();
     const int need = V - 1;  // self is always kept
-    const int hc = lane < 32 ? (int)hist[lane] : 0;
-    const int inc = p_scan(hc, lane);
-    const uint64_t over = __ballot(lane < 32 && inc >= need);
-    const int acut = __builtin_ctzll(over);  // the cut age
-    const int before = __shfl(inc - hc, acut, 64);
-    uint32_t needb = (uint32_t)(need - before);
+    int c = (int)hist[lane];
+    int inc = p_scan(c, lane);
+    const uint64_t over = __ballot(inc >= need);
+    const int dcut = __builtin_ctzll(over);
+    const int before = __builtin_amdgcn_readlane(inc - c, dcut);
+    const int bsz = __builtin_amdgcn_readlane(c, dcut);
+    const int needb = need - before;  // 1 <= needb <= bsz
     uint32_t bucket = 0;
-    keep = 0;
-    uint64_t key[P_H / 64];
 #pragma unroll
-    for (int u = 0; u < P_H / 64; u++) {
-      key[u] = 0;
-      if (!((alive >> u) & 1)) continue;
-      const unsigned long long e = tab[lane + 64 * u];
-      const int a = p_age(t, (uint32_t)e);
-      if ((flg[lane + 64 * u] & 2) || a < acut) keep |= 1u << u;
-      else if (a == acut) {
-        bucket |= 1u << u;
-        key[u] = p_evict_key(s.view_seed, t, i, (uint32_t)(e >> 32));
-      }
+    for (int q = 0; q < DS; q++) {
+      if (!dw[q]) continue;
+      const int d = min(max(top - (int)dh[q], 0), 63);
+      if ((dw[q] & P_SELF) || d < dcut) keep |= 1u << q;
+      else if (d == dcut) bucket |= 1u << q;
     }
-    // radix select of the needb smallest keys in the cut bucket (distinct keys)
-    uint64_t prefix = 0;
-    for (int d = 7; d >= 0; d--) {
-      p_wsync();
-      for (int q = lane; q < 256; q += 64) hist[q] = 0;
-      p_wsync();
-      const uint64_t hmask = d == 7 ? 0ull : ~0ull << (8 * (d + 1));
+    if (needb == bsz) {
+      keep |= bucket;
+    } else {
+      // the needb smallest eviction keys of the bucket: 6-bit radix on the top bits,
+      // then exact min-selection inside the cut bin
+      const uint64_t kseed = gm_mix64(s.view_seed ^ (uint64_t)(uint32_t)t);
+      uint64_t key[DS];
 #pragma unroll
-      for (int u = 0; u < P_H / 64; u++)
-        if (((bucket >> u) & 1) && ((key[u] ^ prefix) & hmask) == 0) atomicAdd(&hist[(key[u] >> (8 * d)) & 255u], 1u);
+      for (int q = 0; q < DS; q++) key[q] = ((bucket >> q) & 1) ? p_evict_key(kseed, i, dw[q] & P_IDMASK) : ~0ull;
       p_wsync();
-      uint32_t c4[4];
-      int csum = 0;
+      hist[lane] = 0;
+      p_wsync();
 #pragma unroll
-      for (int q = 0; q < 4; q++) {
-        c4[q] = hist[4 * lane + q];
-        csum += (int)c4[q];
+      for (int q = 0; q < DS; q++)
+        if ((bucket >> q) & 1) atomicAdd(&hist[key[q] >> 58], 1u);
+      p_wsync();
+      c = (int)hist[lane];
+      inc = p_scan(c, lane);
+      const uint64_t over2 = __ballot(inc >= needb);
+      const int bcut = __builtin_ctzll(over2);
+      const int before2 = __builtin_amdgcn_readlane(inc - c, bcut);
+      const int bsz2 = __builtin_amdgcn_readlane(c, bcut);
+      int needc = needb - before2;  // 1 <= needc <= bsz2
+      uint32_t cand = 0;
+#pragma unroll
+      for (int q = 0; q < DS; q++) {
+        if (!((bucket >> q) & 1)) continue;
+        const int bin = (int)(key[q] >> 58);
+        if (bin < bcut) keep |= 1u << q;
+        else if (bin == bcut) cand |= 1u << q;
       }
-      const int cinc = p_scan(csum, lane);
-      const uint64_t hit = __ballot(cinc >= (int)needb);
-      const int ln = __builtin_ctzll(hit);
-      int cb = __shfl(cinc - csum, ln, 64);  // count below lane ln's bins
-      int bsel = 0;
-      if (lane == ln) {
-        int acc = cb;
-        for (int q = 0; q < 4; q++) {
-          if (acc + (int)c4[q] >= (int)needb) {
-            bsel = 4 * lane + q;
-            cb = acc;
-            break;
+      if (needc == bsz2) {
+        keep |= cand;
+      } else {
+        for (; needc > 0; needc--) {  // take the smallest remaining candidate key (keys are distinct)
+          uint64_t mn = ~0ull;
+#pragma unroll
+          for (int q = 0; q < DS; q++)
+            if ((cand >> q) & 1) mn = min(mn, key[q]);
+#pragma unroll
+          for (int o = 32; o >= 1; o >>= 1) {
+            const uint32_t lo = __shfl_xor((uint32_t)mn, o, 64), hi = __shfl_xor((uint32_t)(mn >> 32), o, 64);
+            mn = min(mn, ((uint64_t)hi << 32) | lo);
           }
-          acc += (int)c4[q];
+#pragma unroll
+          for (int q = 0; q < DS; q++)
+            if (((cand >> q) & 1) && key[q] == mn) {
+              keep |= 1u << q;
+              cand &= ~(1u << q);
+            }
         }
       }
-      bsel = __shfl(bsel, ln, 64);
-      cb = __shfl(cb, ln, 64);
-      needb -= (uint32_t)cb;
-      prefix |= (uint64_t)bsel << (8 * d);
     }
-#pragma unroll
-    for (int u = 0; u < P_H / 64; u++)
-      if (((bucket >> u) & 1) && key[u] <= prefix) keep |= 1u << u;
   }
-  // compact the kept entries, then sort them by id (bitonic across the wave)
-  int kc = __builtin_popcount(keep);
-  const int kinc = p_scan(kc, lane);
-  int pos = kinc - kc;
-  const int cnt = __shfl(kinc, 63, 64);
-  for (int u = 0; u < P_H / 64; u++)
-    if ((keep >> u) & 1) {
-      fin[pos] = tab[lane + 64 * u];
-      finf[pos] = flg[lane + 64 * u];
-      pos++;
+  // ---- 5. compact the kept entries (<= V), rank them by id
+  int cnt = 0;
+#pragma unroll
+  for (int q = 0; q < DS; q++) {
+    const uint64_t bal = __ballot((keep >> q) & 1);
+    if ((keep >> q) & 1) {
+      const int p = cnt + p_below(bal);
+      kid[p] = dw[q];
+      khb[p] = dh[q];
     }
+    cnt += __builtin_popcountll(bal);
+  }
   p_wsync();
-  uint64_t x = lane < cnt ? fin[lane] : ~0ull;
-  uint32_t f = lane < cnt ? finf[lane] : 0u;
-#pragma unroll
-  for (int k2 = 2; k2 <= 64; k2 <<= 1)
-#pragma unroll
-    for (int j2 = k2 >> 1; j2 > 0; j2 >>= 1) {
-      const uint64_t ox = __shfl_xor(x, j2, 64);
-      const uint32_t of = __shfl_xor(f, j2, 64);
-      const bool up = (lane & k2) == 0, lower = (lane & j2) == 0;
-      const bool take_min = lower == up;
-      const bool swap = take_min ? (ox < x) : (ox > x);
-      if (swap) {
-        x = ox;
-        f = of;
-      }
-    }
-  // the final list (id order) of tick t: lane j holds entry j
-  if (lane < V) cur[(size_t)i * V + lane] = lane < cnt ? x : 0ull;
-  const bool valid = lane < cnt;
-  const uint32_t hbx = (uint32_t)x;
-  const bool stale = valid && p_age(t, hbx) >= GM_TFAIL;
-  const bool joined = valid && !(f & 1u);
-  int nstale = stale ? 1 : 0;
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) nstale += __shfl_xor(nstale, o, 64);
-  const int numfailed = removed + nstale;  // numfailed counts removed entries too (MP1Node.cpp:463)
-  // events: joins (ascending id) then this row's own removed entries
-  uint32_t *evr = s.ev + (size_t)i * 2 * V;
-  const uint64_t jb = __ballot(joined);
-  const int nj = __builtin_popcountll(jb);
-  if (joined) evr[__builtin_popcountll(jb & ((1ull << lane) - 1))] = (P_EV_ADD << 30) | (uint32_t)(x >> 32);
   {
-    const int rc = __builtin_popcount(removed_own);
-    const int rinc = p_scan(rc, lane);
-    int rp = nj + rinc - rc;
-    for (int u = 0; u < P_H / 64; u++)
-      if ((removed_own >> u) & 1) evr[rp++] = (P_EV_REMOVE << 30) | (uint32_t)(tab[lane + 64 * u] >> 32);
-    if (lane == 63) s.ev_cnt[i] = nj + rinc;
+    const uint32_t mw = lane < cnt ? kid[lane] : 0u, mh = lane < cnt ? khb[lane] : 0u;
+    const uint32_t myid = mw & P_IDMASK;
+    int rank = 0;
+    for (int q = 0; q < cnt; q++) rank += (kid[q] & P_IDMASK) < myid;
+    p_wsync();
+    if (lane < cnt) {
+      fin[rank] = ((uint64_t)myid << 32) | mh;
+      kid[rank] = mw;
+    }
   }
-  // gossip draw over the final list (MP1Node.cpp:449-489)
+  p_wsync();
+  const uint64_t x = lane < cnt ? fin[lane] : 0ull;
+  const uint32_t f = lane < cnt ? kid[lane] : 0u;
+  if (lane < V) cur[(size_t)i * V + lane] = x;
+  // joins (ascending id) from the front of the event row
+  const uint64_t jb = __ballot(lane < cnt && !(f & P_OWN));
+  const int nj = __builtin_popcountll(jb);
+  if (lane < cnt && !(f & P_OWN)) evr[p_below(jb)] = (P_EV_ADD << 30) | (uint32_t)(x >> 32);
+  const int numfailed = removed + __builtin_popcountll(__ballot(lane < cnt && p_age(t, (uint32_t)x) >= GM_TFAIL));
+  // ---- 6. gossip draw over the final list (MP1Node.cpp:449-489), on scalar registers
   const int numpot = cnt - 1 - numfailed;
   const int target = min(GM_FANOUT, numpot);
-  int n = 0, g0 = -1, g1 = -1, g2 = -1, g3 = -1, g4 = -1;
+  int ng = 0, g0 = -1, g1 = -1, g2 = -1, g3 = -1, g4 = -1;
   if (numpot > 0) {
     const uint32_t size = (uint32_t)cnt;
     const uint32_t thr = (0u - size) % size;
@@ -328,64 +399,98 @@ __global__ __launch_bounds__(256) void gm_p_tick(PState s, int t, const uint32_t
         if (lane == 0) atomicOr(s.err, GM_ERR_DRAWS);
         break;
       }
-      uint32_t raw = 0;
-      if (batch == 0) {
-        if (lane < 16) raw = mtraw[(size_t)i * 16 + lane];
-      } else {
+      uint32_t raw = raw0;
+      if (batch > 0) {  // outputs past the precomputed 16: lazy generator in the (free) table region
         if (lane == 0 && batch == 1) {
-          mt.seed(mts, gm_rd_seed(s.rd_seed, t, i + 1));
+          mt.seed(tid, gm_rd_seed(s.rd_seed, t, i + 1));
           for (int q = 0; q < 16; q++) (void)mt.next();
         }
+        raw = 0;
         for (int q = 0; q < 16; q++) {
           uint32_t o = 0;
           if (lane == 0) o = mt.next();
-          o = __shfl(o, 0, 64);
+          o = __builtin_amdgcn_readfirstlane(o);
           if (lane == q) raw = o;
         }
       }
       const uint64_t prod = (uint64_t)raw * size;
-      const bool ok = lane < 16 && (uint32_t)prod >= thr;
       const int ix = (int)(prod >> 32);
-      uint64_t mk = __ballot(ok);
+      uint64_t mk = __ballot(lane < 16 && (uint32_t)prod >= thr);
       while (mk && !done) {
         const int d = __builtin_ctzll(mk);
         mk &= mk - 1;
-        const int ixd = __shfl(ix, d, 64);
-        const uint64_t e = __shfl(x, ixd, 64);
+        const int ixd = __builtin_amdgcn_readlane(ix, d);
+        const uint64_t e = p_readlane64(x, ixd);
         const int c = (int)(e >> 32) - 1;
         if (c == i) continue;                                    // "me"
         if (p_age(t, (uint32_t)e) >= GM_TFAIL) continue;          // age >= TFAIL
-        if ((n > 0 && g0 == c) || (n > 1 && g1 == c) || (n > 2 && g2 == c) || (n > 3 && g3 == c)) continue;
-        if (n == 0) g0 = c;
-        else if (n == 1) g1 = c;
-        else if (n == 2) g2 = c;
-        else if (n == 3) g3 = c;
+        if ((ng > 0 && g0 == c) || (ng > 1 && g1 == c) || (ng > 2 && g2 == c) || (ng > 3 && g3 == c)) continue;
+        if (ng == 0) g0 = c;
+        else if (ng == 1) g1 = c;
+        else if (ng == 2) g2 = c;
+        else if (ng == 3) g3 = c;
         else g4 = c;
-        n++;
-        if (n >= target) done = true;
+        ng++;
+        if (ng >= target) done = true;
       }
     }
   }
+  // ---- sends: one parallel round of inbox appends, one lane per target
+  if (lane < ng) {
+    const int dst = lane == 0 ? g0 : lane == 1 ? g1 : lane == 2 ? g2 : lane == 3 ? g3 : g4;
+    s.targets[(size_t)i * GM_FANOUT + lane] = dst;
+    const int slot = atomicAdd(&s.inbox_cnt[par ^ 1][dst], 1);
+    if (slot < P_KMAX) s.inbox[par ^ 1][(size_t)dst * P_KMAX + slot] = i;
+    else atomicOr(s.err, GM_ERR_INBOX);
+  }
+  if (lane < 4) s.rowstat[(size_t)i * 4 + lane] = lane == 0 ? kk : lane == 1 ? cnt : lane == 2 ? numfailed : ng;
+  if (lane == 0) s.ev_cnt[i] = nj | (nrem << 16);
+}
+
+// crashed node: frozen (its list carried to this tick's buffer unchanged), inbox dropped
+__device__ __forceinline__ void p_frozen(const PState &s, int t, int i, int lane) {
+  const int par = t & 1, V = s.V;
+  if (lane < V) s.lists[((size_t)par * s.n + i) * V + lane] = s.lists[((size_t)(par ^ 1) * s.n + i) * V + lane];
+  if (lane < 4) s.rowstat[(size_t)i * 4 + lane] = 0;
   if (lane == 0) {
-    int32_t *cnt_out = s.inbox_cnt[par ^ 1];
-    const int g[GM_FANOUT] = {g0, g1, g2, g3, g4};
-    for (int q = 0; q < n; q++) {
-      const int dst = g[q];
-      s.targets[(size_t)i * GM_FANOUT + q] = dst;
-      const int slot = atomicAdd(&cnt_out[dst], 1);
-      if (slot < P_KMAX) s.inbox[par ^ 1][(size_t)dst * P_KMAX + slot] = i;
-      else atomicOr(s.err, GM_ERR_INBOX);
-    }
-    stat[0] = kk;
-    stat[1] = cnt;
-    stat[2] = numfailed;
-    stat[3] = n;
+    s.inbox_cnt[par][i] = 0;
+    s.ev_cnt[i] = 0;
   }
 }
 
-// first 16 S2 outputs of every node for tick t (see gm_mt_first16)
+__global__ __launch_bounds__(256) void gm_p_tick_small(PState s, int t, const uint32_t *mtraw) {
+  extern __shared__ __align__(16) unsigned char p_smem[];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + wave;
+  if (i >= s.n) return;  // whole wave; no workgroup barrier in this kernel
+  if (s.failed[i]) {
+    p_frozen(s, t, i, lane);
+    return;
+  }
+  const int k = s.inbox_cnt[t & 1][i];
+  if (k > P_KSMALL) {  // deferred to gm_p_tick_big
+    if (lane == 0) s.big[atomicAdd(s.big_cnt, 1)] = i;
+    return;
+  }
+  p_node<P_HS, false>(s, t, mtraw, i, k, lane, p_smem + (size_t)wave * PLds<P_HS>::bytes);
+}
+
+// drains the worklist gm_p_tick_small filled (a fixed grid; every wave exits when the list is done)
+__global__ __launch_bounds__(256) void gm_p_tick_big(PState s, int t, const uint32_t *mtraw) {
+  extern __shared__ __align__(16) unsigned char p_smem[];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int nbig = *s.big_cnt;
+  for (int w = blockIdx.x * 4 + wave; w < nbig; w += gridDim.x * 4) {
+    const int i = s.big[w];
+    const int k = s.inbox_cnt[t & 1][i];
+    p_node<P_HB, true>(s, t, mtraw, i, k, lane, p_smem + (size_t)wave * PLds<P_HB>::bytes);
+  }
+}
+
+// first 16 S2 outputs of every node for tick t (see gm_mt_first16); resets the big worklist
 __global__ __launch_bounds__(256) void gm_p_mtgen(PState s, int t, uint32_t *mtraw) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r == 0) *s.big_cnt = 0;
   if (r >= s.n) return;
   uint32_t out[16];
   gm_mt_first16(gm_rd_seed(s.rd_seed, t, r + 1), out);
@@ -423,11 +528,16 @@ __global__ __launch_bounds__(64) void gm_p_init(PState s, int t0, uint64_t init_
   s.hbctr[i] = 2 * t0;
 }
 
+#define P_BIG_GRID 1024
+
 hipError_t gm_launch_partial_tick(const PState &s, int t, uint32_t *mtraw, hipStream_t st, hipEvent_t k0,
                                   hipEvent_t k1) {
   hipLaunchKernelGGL(gm_p_mtgen, dim3((s.n + 255) / 256), dim3(256), 0, st, s, t, mtraw);
   if (k0) (void)hipEventRecord(k0, st);
-  hipLaunchKernelGGL(gm_p_tick, dim3((s.n + 3) / 4), dim3(256), 4 * P_LDS_BYTES, st, s, t, (const uint32_t *)mtraw);
+  hipLaunchKernelGGL(gm_p_tick_small, dim3((s.n + 3) / 4), dim3(256), 4 * PLds<P_HS>::bytes, st, s, t,
+                     (const uint32_t *)mtraw);
+  hipLaunchKernelGGL(gm_p_tick_big, dim3(P_BIG_GRID), dim3(256), 4 * PLds<P_HB>::bytes, st, s, t,
+                     (const uint32_t *)mtraw);
   if (k1) (void)hipEventRecord(k1, st);
   return hipGetLastError();
 }
@@ -437,4 +547,4 @@ hipError_t gm_launch_partial_init(const PState &s, int t0, uint64_t init_seed, h
   return hipGetLastError();
 }
 
-size_t gm_partial_lds_bytes() { return 4 * (size_t)P_LDS_BYTES; }
+size_t gm_partial_lds_bytes() { return 4 * (size_t)PLds<P_HB>::bytes; }

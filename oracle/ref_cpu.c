@@ -845,6 +845,8 @@ struct op_ctx {
   oc_event *ev;
   int nev, evcap;
   sbuf dump;
+  /* per-receiver sender lists of this tick's deliveries, senders ascending (CSR) */
+  int32_t *rcv_off, *rcv_src;
   /* scratch */
   int32_t *cid, *chb, *cown;
   int ccap;
@@ -911,6 +913,8 @@ op_ctx *op_create(const op_config *cfg) {
   c->ntgt_next = (int32_t *)calloc((size_t)n, sizeof(int32_t));
   c->crash = (int32_t *)calloc((size_t)(cfg->crash_count > 0 ? cfg->crash_count : 1), sizeof(int32_t));
   if (cfg->crash_count > 0) oc_crash_set(n, cfg->crash_count, cfg->crash_seed, c->crash);
+  c->rcv_off = (int32_t *)calloc((size_t)n + 1, sizeof(int32_t));
+  c->rcv_src = (int32_t *)calloc((size_t)n * FANOUT + 1, sizeof(int32_t));
   return c;
 }
 
@@ -925,6 +929,7 @@ void op_destroy(op_ctx *c) {
   free(c->tgt); free(c->tgt_next); free(c->ntgt); free(c->ntgt_next);
   free(c->crash); free(c->ev); free(c->dump.p);
   free(c->cid); free(c->chb); free(c->cown);
+  free(c->rcv_off); free(c->rcv_src);
   free(c);
 }
 
@@ -940,32 +945,44 @@ static int pc_id_cmp(const void *x, const void *y) {
   return a->id - b->id;
 }
 
+static int pc_idown_cmp(const void *x, const void *y) { /* id asc, then hb desc */
+  const pcand *a = (const pcand *)x, *b = (const pcand *)y;
+  if (a->id != b->id) return a->id < b->id ? -1 : 1;
+  return (a->hb < b->hb) - (a->hb > b->hb);
+}
+
 static void op_node(op_ctx *c, int i, pcand *m) {
   const int t = c->t, V = c->V;
   pnode *p = &c->nd[i];
   int cnt = 0;
   for (int k = 0; k < p->cnt; k++) { m[cnt].id = p->ids[k]; m[cnt].hb = p->hbs[k]; m[cnt].own = 1; cnt++; }
-  /* lists delivered to i: every sender that targeted i at t-1 (BSP, order-free) */
+  /* lists delivered to i: every sender that targeted i at t-1 (BSP, order-free for the
+   * table); the OP_KP lowest sender indices when more arrived (rcv_* lists them ascending) */
   const int t_send = t - 1;
   const int dropping = c->cfg.drop_pct > 0 && t_send >= c->cfg.drop_from && t_send < c->cfg.drop_to;
-  int lists = 0;
-  for (int s = 0; s < c->n && lists < OP_KP; s++)
-    for (int q = 0; q < c->ntgt[s]; q++) {
-      if (c->tgt[(size_t)s * FANOUT + q] != i) continue;
-      if (++lists > OP_KP) break;
-      const snap *sp = &c->snaps[s];
-      uint64_t pair = mix64(c->cfg.drop_seed ^ ((uint64_t)(uint32_t)t_send << 48) ^ ((uint64_t)s << 24) ^ (uint64_t)i);
-      for (int e = 0; e < sp->n; e++) {
-        if (dropping) {
-          uint32_t h = (uint32_t)(mix64(pair + (uint64_t)(sp->ids[e] - 1)) >> 32);
-          if ((int)(h % 100u) < c->cfg.drop_pct) continue;
-        }
-        int k = 0;
-        while (k < cnt && m[k].id != sp->ids[e]) k++;
-        if (k == cnt) { m[cnt].id = sp->ids[e]; m[cnt].hb = sp->hbs[e]; m[cnt].own = 0; cnt++; }
-        else if (sp->hbs[e] > m[k].hb) m[k].hb = sp->hbs[e];
+  const int nrcv = c->rcv_off[i + 1] - c->rcv_off[i];
+  for (int q = 0; q < nrcv && q < OP_KP; q++) {
+    const int s = c->rcv_src[c->rcv_off[i] + q];
+    const snap *sp = &c->snaps[s];
+    uint64_t pair = mix64(c->cfg.drop_seed ^ ((uint64_t)(uint32_t)t_send << 48) ^ ((uint64_t)s << 24) ^ (uint64_t)i);
+    for (int e = 0; e < sp->n; e++) {
+      if (dropping) {
+        uint32_t h = (uint32_t)(mix64(pair + (uint64_t)(sp->ids[e] - 1)) >> 32);
+        if ((int)(h % 100u) < c->cfg.drop_pct) continue;
       }
+      m[cnt].id = sp->ids[e]; m[cnt].hb = sp->hbs[e]; m[cnt].own = 0; cnt++;
     }
+  }
+  /* merge per id (updatelistCallBack): the largest hb; "own" if the id was in i's list */
+  qsort(m, (size_t)cnt, sizeof(pcand), pc_idown_cmp);
+  {
+    int w = 0;
+    for (int k = 0; k < cnt; k++) {
+      if (w > 0 && m[w - 1].id == m[k].id) { m[w - 1].own |= m[k].own; continue; }
+      m[w++] = m[k];
+    }
+    cnt = w;
+  }
   /* self bump (heartbeat++; myPos->setheartbeat(heartbeat++)) */
   int selfk = -1;
   for (int k = 0; k < cnt; k++) if (m[k].id == i + 1) selfk = k;
@@ -1024,8 +1041,20 @@ static void op_node(op_ctx *c, int i, pcand *m) {
 
 int op_tick(op_ctx *c) {
   const int n = c->n;
-  pcand *m = (pcand *)malloc(sizeof(pcand) * (size_t)c->V * (size_t)(n + 1));
+  pcand *m = (pcand *)malloc(sizeof(pcand) * (size_t)c->V * (OP_KP + 2));
   c->nev = 0;
+  /* counting sort of last tick's (sender, target) pairs by target, senders ascending */
+  memset(c->rcv_off, 0, sizeof(int32_t) * (size_t)(n + 1));
+  for (int s = 0; s < n; s++)
+    for (int q = 0; q < c->ntgt[s]; q++) c->rcv_off[c->tgt[(size_t)s * FANOUT + q] + 1]++;
+  for (int i = 0; i < n; i++) c->rcv_off[i + 1] += c->rcv_off[i];
+  {
+    int32_t *fill = (int32_t *)malloc(sizeof(int32_t) * (size_t)n);
+    memcpy(fill, c->rcv_off, sizeof(int32_t) * (size_t)n);
+    for (int s = 0; s < n; s++)
+      for (int q = 0; q < c->ntgt[s]; q++) c->rcv_src[fill[c->tgt[(size_t)s * FANOUT + q]]++] = s;
+    free(fill);
+  }
   for (int i = n - 1; i >= 0; i--) {
     c->ntgt_next[i] = 0;
     c->snaps_next[i].n = 0;
