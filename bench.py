@@ -74,6 +74,8 @@ def parse():
     p.add_argument("--crash-frac", type=float, default=0.01)
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--force-shard", action="store_true",
+                   help="diagnostics: at N=1 run the column-shard protocol with RCCL over one rank")
     return p.parse_args()
 
 
@@ -108,6 +110,11 @@ def main():
     init = dict(init_mode=1 if a.t0 > 0 else 0, init_t0=a.t0, init_seed=11)
     if world > 1:
         sim = distributed_shard(n, rank, world, local, rd_seed=7, **init)
+    elif a.force_shard:
+        os.environ["GM_FORCE_SHARD"] = "1"
+        sim = Simulator(n, GM_MODE_SCALED, rd_seed=7, device=local, shard_rank=0, shard_count=1, **init)
+        from membership.abi import comm_unique_id
+        sim.comm_init(comm_unique_id(), 1, 0)
     else:
         sim = Simulator(n, GM_MODE_SCALED, rd_seed=7, device=local, **init)
     crash = crash_set(n, ncrash, 42)
@@ -181,7 +188,8 @@ def main():
         "data": "synthetic (converged full-membership table, seeded crash set)",
         "config": {"workload": "S-A: SCALED full membership, 1% crash at tick 10, fanout 5, TFAIL 5, TREMOVE 20",
                    "n": n, "start": f"warm t0={a.t0}" if a.t0 > 0 else "cold", "prologue_to_tick": a.prologue, "crashed": ncrash, "live": n_live,
-                   "lists_per_tick": m_lists, "parallelism": f"column-shard x{world}" if world > 1 else "single GPU"},
+                   "lists_per_tick": m_lists, "parallelism": f"column-shard x{world}" if world > 1 else
+                   ("column-shard x1 (RCCL, forced)" if a.force_shard else "single GPU")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                      "frac": (achieved / PEAK_HBM_GBPS) if achieved else None, "traffic": traffic,
                      "kernel": "gm_s_band", "kernel_ms": kernel_ms,

@@ -231,6 +231,8 @@ static int create_scaled(gm_ctx *c) {
   s.n = n;
   s.shard_rank = rank;
   s.shard_count = G;
+  // one forced shard (diagnostics/tests): the sharded tick + RCCL with a single rank
+  s.sharded = G > 1 || (getenv("GM_FORCE_SHARD") && atoi(getenv("GM_FORCE_SHARD")) == 1);
   // contiguous, balanced subject-column ranges
   s.c0 = (int)((int64_t)n * rank / G);
   s.w = (int)((int64_t)n * (rank + 1) / G) - s.c0;
@@ -277,7 +279,7 @@ static int create_scaled(gm_ctx *c) {
   HIPCHECK(hipMemset(s.ev_spill_cnt, 0, sizeof(uint32_t)));
   HIPCHECK(hipMemset(s.rowstat, 0, sizeof(int32_t) * n * 4));
   HIPCHECK(hipMemset(s.err, 0, sizeof(uint32_t)));
-  if (G > 1) {
+  if (s.sharded) {
     TRY(dalloc(c, &s.acc, (size_t)n * 8));
     TRY(dalloc(c, &s.pending, n));
     TRY(dalloc(c, &s.npending, 1));
@@ -423,7 +425,7 @@ static int tick_sharded(gm_ctx *c);
 
 static int tick_scaled(gm_ctx *c) {
   if (c->t > GM_T_LIMIT) return GM_ERANGE;
-  if (c->s.shard_count > 1) return tick_sharded(c);
+  if (c->s.sharded) return tick_sharded(c);
   const int t_send = c->t - 1;
   const bool drop = c->cfg.drop_pct > 0 && t_send >= c->cfg.drop_from && t_send < c->cfg.drop_to;
   hipEvent_t k0 = nullptr, k1 = nullptr;
@@ -830,7 +832,7 @@ extern "C" int gm_last_kernel_ms(gm_ctx *c, float *ms) {
   if (!c || !ms) return GM_EINVAL;
   *ms = 0.f;
   if (!c->timing || c->cfg.mode == GM_MODE_FAITHFUL || c->timed_ticks == 0) return GM_OK;
-  if (c->cfg.mode == GM_MODE_SCALED && c->s.shard_count > 1) {  // per-tick merge-kernel events, summed at each tick end
+  if (c->cfg.mode == GM_MODE_SCALED && c->s.sharded) {  // per-tick merge-kernel events, summed at each tick end
     *ms = (float)(c->kernel_ms_sum / c->timed_ticks);
     return GM_OK;
   }
@@ -906,7 +908,7 @@ extern "C" int gm_shard_layout(gm_ctx *c, int32_t *c0, int32_t *w) {
 }
 
 static int shard_ready(gm_ctx *c) {
-  if (!c || c->cfg.mode != GM_MODE_SCALED || c->s.shard_count < 2) return GM_EINVAL;
+  if (!c || c->cfg.mode != GM_MODE_SCALED || !c->s.sharded) return GM_EINVAL;
   if (c->latched != GM_OK) return c->latched;
   if (c->t > GM_T_LIMIT) return GM_ERANGE;
   return GM_OK;

@@ -58,8 +58,10 @@ struct SState {
   int32_t *rowstat;        // [n][4]: lists delivered, present, numfailed, targets chosen
   int32_t *targets;        // [n][GM_FANOUT]
   uint32_t *err;
-  // ---- column-sharded mode (shard_count > 1; see gm_s_draw / gm_s_accept)
+  // ---- column-sharded mode (shard_count > 1, or one shard forced by GM_FORCE_SHARD=1 to
+  // rehearse the sharded protocol + RCCL on one GPU; see gm_s_draw / gm_s_accept)
   int shard_rank, shard_count;
+  int sharded;
   int32_t *xcnt;             // bound exchange buffer [shard_count][n][2]: (present, numfailed) per shard
   int32_t *status;           // bound exchange buffer [n][D]: resolved draws, MAX-allreduced
   int32_t *acc;              // [n][8]: targets so far, g[5], numpot, size

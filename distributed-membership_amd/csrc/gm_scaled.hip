@@ -332,7 +332,7 @@ __global__ __launch_bounds__(256) void gm_s_band(SState s, int t, int drop_pct) 
         live ? ((uint32_t)(pf & 0xFFFF) | ((uint32_t)(pf >> 16) << 11) | ((uint32_t)min(tot, 1023) << 22)) : 0u;
     // column shard: this shard's row totals (present, numfailed) for the all-gather,
     // accumulated as one packed 64-bit add per (row, band) into the zeroed slot
-    if (s.shard_count > 1 && live)
+    if (s.sharded && live)
       atomicAdd((unsigned long long *)(s.xcnt + ((size_t)s.shard_rank * s.n + r) * 2),
                 (unsigned long long)(pf & 0xFFFF) | ((unsigned long long)(pf >> 16) << 32));
   }

@@ -13,7 +13,7 @@ for f in $(find gpurun_out/scpmc -name '*counter_collection.csv'); do python3 - 
 import csv, sys, collections
 acc = collections.defaultdict(float); cnt = collections.Counter()
 for r in csv.DictReader(open(sys.argv[1])):
-    if "gm_p_tick" not in r.get("Kernel_Name", ""): continue
+    if "gm_p_tick_small" not in r.get("Kernel_Name", ""): continue
     acc[r["Counter_Name"]] += float(r["Counter_Value"]); cnt[r["Counter_Name"]] += 1
 for k in sorted(acc): print(k, acc[k] / max(1, cnt[k]) * 1.0, "(per-dispatch avg over", cnt[k], "rows)")
 PY

@@ -52,3 +52,28 @@ def test_shards_match_fused_kernel(n, world, drop, warm):
         st = s.tick_stats()
         assert st["err"] == 0
         assert st["lists"] == ref.tick_stats()["lists"]
+
+
+@pytest.mark.parametrize("n,drop", [(777, 0), (2048, 20)])
+def test_rccl_single_rank_matches_fused_kernel(n, drop, monkeypatch):
+    """The RCCL-driven sharded tick (gm_tick -> ncclAllGather / ncclAllReduce on the
+    context stream) with one forced shard on the one GPU this box has: the exact
+    collective calls the multi-GPU run makes, degenerate only in the rank count."""
+    from membership.abi import comm_unique_id
+    kw = dict(rd_seed=7, drop_pct=drop, drop_from=3, drop_to=25, drop_seed=42, init_mode=1, init_t0=6, init_seed=5)
+    ref = Simulator(n, GM_MODE_SCALED, **kw)
+    monkeypatch.setenv("GM_FORCE_SHARD", "1")
+    sh = Simulator(n, GM_MODE_SCALED, shard_rank=0, shard_count=1, **kw)
+    monkeypatch.delenv("GM_FORCE_SHARD")
+    sh.comm_init(comm_unique_id(), 1, 0)
+    crash = crash_set(n, max(2, n // 64), 42)
+    for _ in range(32):
+        t = ref.time
+        ref.tick()
+        sh.tick()
+        if t == 8:
+            ref.set_failed(crash)
+            sh.set_failed(crash)
+        assert sorted(sh.drain_events()) == sorted(ref.drain_events()), f"events differ at tick {t}"
+        assert sh.dump_tables() == ref.dump_tables(), f"tables differ at tick {t}"
+    assert sh.tick_stats()["err"] == 0
