@@ -221,16 +221,25 @@ def main_partial(a):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     from membership import GM_MODE_PARTIAL, Simulator, crash_set, load_library
+    from membership.abi import comm_unique_id
+    from membership.sharded import rendezvous_uid
     load_library()
-    if world > 1:
-        raise SystemExit("S-C multi-GPU: not in this build yet")
+    dist = None
+    if world > 1:  # row shards; RCCL all-to-all(v) inside libgm, gloo for rendezvous + timing
+        import torch.distributed as tdist
+        tdist.init_process_group("gloo")
+        dist = tdist
     n = a.cluster or (1 << 24)
     V = a.view
     ncrash = int(round(n * a.crash_frac))
     t0 = max(a.t0, 5)
     kw = dict(rd_seed=7, view=V, view_seed=5, init_mode=1, init_t0=t0, init_seed=11,
               drop_pct=5, drop_from=0, drop_to=1 << 20, drop_seed=42)
-    sim = Simulator(n, GM_MODE_PARTIAL, device=local, **kw)
+    if a.force_shard and world == 1:  # diagnostics: the row-shard exchange with one RCCL rank
+        os.environ["GM_FORCE_SHARD"] = "1"
+    sim = Simulator(n, GM_MODE_PARTIAL, device=local, shard_rank=rank, shard_count=world, **kw)
+    if world > 1 or a.force_shard:
+        sim.comm_init(rendezvous_uid(rank, world) if world > 1 else comm_unique_id(), world, rank)
     crash = crash_set(n, ncrash, 42)
     while sim.time <= a.prologue:
         t = sim.time
@@ -239,6 +248,9 @@ def main_partial(a):
             sim.set_failed(crash)
     for _ in range(a.warmup):
         sim.tick()
+    sim.sync()
+    if dist is not None:
+        dist.barrier()
     sim.sync()
     sim.set_timing(1)
     rtx.resume()
@@ -253,6 +265,18 @@ def main_partial(a):
     st = sim.tick_stats()
     assert st["err"] == 0, st
     n_live, m_lists = st["live"], st["lists"]
+    if dist is not None:  # max time over ranks; this rank's kernel bytes, whole-cluster counts
+        import torch
+        dist.barrier()
+        x = torch.tensor([elapsed, float(n_live), float(m_lists), float(st["max_inbox"])], dtype=torch.float64)
+        y = x.clone()
+        dist.all_reduce(x, op=dist.ReduceOp.SUM)
+        dist.all_reduce(y, op=dist.ReduceOp.MAX)
+        elapsed = float(y[0])
+        st["max_inbox"] = int(y[3])
+        n_live_all, m_lists_all = int(x[1]), int(x[2])
+    else:
+        n_live_all, m_lists_all = n_live, m_lists
     # algorithmic bytes of one gm_p_tick launch: per live node the own
     # list read + the new list written (2 x 8V B) + inbox/state/S2/targets/stat words (120 B);
     # per delivered list the sender's list (8V B) + its inbox word
@@ -267,20 +291,22 @@ def main_partial(a):
         "warmup": a.warmup,
         "ms_per_step": elapsed / a.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "u64 view entries (id<<32|hb, integer)",
         "data": "synthetic (warm random V-entry views, seeded crash set, keyed 5% drops)",
         "config": {"workload": f"S-C: PARTIAL V={V} views, 5% per-entry drop, 1% crash at tick {a.crash_tick}, "
                                "fanout 5, TFAIL 5, TREMOVE 20",
                    "n": n, "view": V, "start": f"warm t0={t0}", "prologue_to_tick": a.prologue, "crashed": ncrash,
-                   "live": n_live, "lists_per_tick": m_lists, "max_inbox": st["max_inbox"],
-                   "parallelism": "single GPU"},
+                   "live": n_live_all, "lists_per_tick": m_lists_all, "max_inbox": st["max_inbox"],
+                   "parallelism": f"row-shard x{world} (RCCL all-to-allv of lists)" if world > 1 else "single GPU"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                      "frac": (achieved / PEAK_HBM_GBPS) if achieved else None, "traffic": None,
                      "kernel": "gm_p_tick", "kernel_ms": kernel_ms, "alg_bytes_per_launch": b_alg},
     }
-    if not a.no_cpu:
+    if world > 1:
+        out["roofline"]["note"] = "rank 0's local kernels (its n/G nodes)"
+    if rank == 0 and world == 1 and not a.no_cpu:
         sys.path.insert(0, os.path.join(REPO, "tests"))
         import oracle_py  # the oracle is the CPU baseline here, never the measured path
         ns = min(n, 1 << 17)
@@ -297,7 +323,10 @@ def main_partial(a):
         out["cpu_baseline"] = {"value": ns * ticks / secs, "unit": "node-ticks/s", "cores": 1, "kind": "port",
                                "sample": f"{ticks} steady ticks of an N={ns} S-C cluster (V={V}, 5% drop) on one host "
                                          f"core ({secs:.1f} s, oracle/ref_cpu.c op_tick)"}
-    print(json.dumps(out), flush=True)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -30,6 +30,7 @@ hipError_t gm_launch_init(const SState &s, int warm, int t0, uint64_t seed, hipS
 hipError_t gm_launch_partial_tick(const PState &s, int t, uint32_t *mtraw, hipStream_t st, hipEvent_t k0,
                                   hipEvent_t k1);
 hipError_t gm_launch_partial_init(const PState &s, int t0, uint64_t init_seed, hipStream_t st);
+hipError_t gm_launch_partial_unpack(const PState &s, int t, int nrecv, hipStream_t st);
 size_t gm_partial_lds_bytes();
 
 #define GM_T_LIMIT 32766  // packed 16-bit hb/ts stay exact: hb <= 2t+1 < 0xFFFF
@@ -62,6 +63,8 @@ struct gm_ctx {
   // PARTIAL
   PState p{};
   uint32_t *p_mtraw = nullptr;
+  int64_t p_recv_last = 0;  // lists received from other row shards in the last tick
+  bool p_sharded = false;   // row-shard exchange each tick (G > 1, or one rank forced by GM_FORCE_SHARD=1)
 };
 
 static thread_local char g_errbuf[256];
@@ -293,7 +296,11 @@ static int create_scaled(gm_ctx *c) {
   return GM_OK;
 }
 
-// PARTIAL: V-entry views (scenario S-C), warm start at init_t0 (oracle op_create)
+// PARTIAL: V-entry views (scenario S-C), warm start at init_t0 (oracle op_create).
+// shard_count = G > 1: row shard `shard_rank` owns nodes [n*g/G, n*(g+1)/G) and
+// exchanges the lists its nodes send to other shards every tick (gm_tick with RCCL
+// attached: all-to-all of record counts + two all-to-allv; gm_partial_loopback for
+// G contexts on one device).
 static int create_partial(gm_ctx *c) {
   const int n = c->n;
   PState &p = c->p;
@@ -303,31 +310,50 @@ static int create_partial(gm_ctx *c) {
   if (p.V < 2 || p.V > 32 || p.V > n) return GM_EUNSUPPORTED;
   const int t0 = c->cfg.init_t0;
   if (c->cfg.init_mode != 1 || t0 < 5 || t0 > GM_T_LIMIT / 2) return GM_EINVAL;
-  if (c->cfg.shard_count > 1) return GM_EUNSUPPORTED;
+  if (n > (1 << 25) - 1) return GM_EUNSUPPORTED;  // ids live in 25 bits of the LDS table words
+  const int G = c->cfg.shard_count > 0 ? c->cfg.shard_count : 1;
+  const int rank = c->cfg.shard_rank;
+  if (rank < 0 || rank >= G || G > n || G > 256) return GM_EINVAL;
+  p.G = G;
+  p.rank = rank;
+  p.n0 = (int)((int64_t)n * rank / G);
+  p.nloc = (int)((int64_t)n * (rank + 1) / G) - p.n0;
+  p.rows = n;  // nloc own rows + room for one received list per remote sender (n - nloc)
+  const int nl = p.nloc, R = n - nl;
   p.rd_seed = c->cfg.rd_seed;
   p.view_seed = c->cfg.view_seed;
   p.drop_seed = c->cfg.drop_seed;
   p.drop_pct = -1;
-  TRY(dalloc(c, &p.lists, (size_t)2 * n * p.V));
+  TRY(dalloc(c, &p.lists, (size_t)2 * p.rows * p.V));
   for (int q = 0; q < 2; q++) {
-    TRY(dalloc(c, &p.inbox_cnt[q], n));
-    TRY(dalloc(c, &p.inbox[q], (size_t)n * P_KMAX));
-    HIPCHECK(hipMemset(p.inbox_cnt[q], 0, sizeof(int32_t) * n));
+    TRY(dalloc(c, &p.inbox_cnt[q], nl));
+    TRY(dalloc(c, &p.inbox[q], (size_t)nl * P_KMAX));
+    HIPCHECK(hipMemset(p.inbox_cnt[q], 0, sizeof(int32_t) * nl));
+    if (G > 1) TRY(dalloc(c, &p.rsrc[q], R));
+    if (G == 1) p.rsrc[q] = nullptr;
   }
-  TRY(dalloc(c, &p.hbctr, n));
-  TRY(dalloc(c, &p.failed, n));
-  TRY(dalloc(c, &p.ev, (size_t)n * 2 * p.V));
-  TRY(dalloc(c, &p.ev_cnt, n));
-  TRY(dalloc(c, &p.rowstat, (size_t)n * 4));
-  TRY(dalloc(c, &p.targets, (size_t)n * GM_FANOUT));
-  TRY(dalloc(c, &p.big, n));
+  TRY(dalloc(c, &p.hbctr, nl));
+  TRY(dalloc(c, &p.failed, nl));
+  TRY(dalloc(c, &p.ev, (size_t)nl * 2 * p.V));
+  TRY(dalloc(c, &p.ev_cnt, nl));
+  TRY(dalloc(c, &p.rowstat, (size_t)nl * 4));
+  TRY(dalloc(c, &p.targets, (size_t)nl * GM_FANOUT));
+  TRY(dalloc(c, &p.big, nl));
   TRY(dalloc(c, &p.big_cnt, 1));
   TRY(dalloc(c, &p.err, 1));
-  TRY(dalloc(c, &c->p_mtraw, (size_t)n * 16));
-  HIPCHECK(hipMemset(p.lists, 0, sizeof(uint64_t) * 2 * n * p.V));
-  HIPCHECK(hipMemset(p.failed, 0, sizeof(int32_t) * n));
-  HIPCHECK(hipMemset(p.ev_cnt, 0, sizeof(int32_t) * n));
-  HIPCHECK(hipMemset(p.rowstat, 0, sizeof(int32_t) * n * 4));
+  TRY(dalloc(c, &c->p_mtraw, (size_t)nl * 16));
+  c->p_sharded = G > 1 || (getenv("GM_FORCE_SHARD") && atoi(getenv("GM_FORCE_SHARD")) == 1);
+  if (c->p_sharded) {
+    TRY(dalloc(c, &p.send_cnt, G));
+    TRY(dalloc(c, &p.send_hdr, (size_t)G * nl * 8));
+    TRY(dalloc(c, &p.send_list, (size_t)G * nl * p.V));
+    TRY(dalloc(c, &p.recv_hdr, (size_t)std::max(R, 1) * 8));
+    TRY(dalloc(c, &p.recv_cnt, G));
+  }
+  HIPCHECK(hipMemset(p.lists, 0, sizeof(uint64_t) * 2 * p.rows * p.V));
+  HIPCHECK(hipMemset(p.failed, 0, sizeof(int32_t) * nl));
+  HIPCHECK(hipMemset(p.ev_cnt, 0, sizeof(int32_t) * nl));
+  HIPCHECK(hipMemset(p.rowstat, 0, sizeof(int32_t) * nl * 4));
   HIPCHECK(hipMemset(p.err, 0, sizeof(uint32_t)));
   HIPCHECK(gm_launch_partial_init(p, t0, c->cfg.init_seed, c->stream));
   HIPCHECK(hipStreamSynchronize(c->stream));
@@ -448,8 +474,11 @@ static int tick_scaled(gm_ctx *c) {
   return GM_OK;
 }
 
+static int partial_exchange_rccl(gm_ctx *c);
+
 static int tick_partial(gm_ctx *c) {
   if (c->t > GM_T_LIMIT) return GM_ERANGE;
+  if (c->p_sharded && !c->comm) return GM_EUNSUPPORTED;  // row shards need gm_comm_init (or gm_partial_loopback)
   const int t_send = c->t - 1;
   const bool drop = c->cfg.drop_pct > 0 && t_send >= c->cfg.drop_from && t_send < c->cfg.drop_to;
   PState st = c->p;
@@ -467,6 +496,7 @@ static int tick_partial(gm_ctx *c) {
     c->ktimed++;
   }
   HIPCHECK(gm_launch_partial_tick(st, c->t, c->p_mtraw, c->stream, k0, k1));
+  if (c->p_sharded) TRY(partial_exchange_rccl(c));
   if (c->timing) {
     HIPCHECK(hipEventRecord(c->e1, c->stream));
     c->timed_ticks++;
@@ -518,8 +548,10 @@ extern "C" int gm_set_failed(gm_ctx *c, const int32_t *idx, int32_t n) {
     c->failed_h[idx[k]] = 1;
   }
   int32_t *dst = c->cfg.mode == GM_MODE_FAITHFUL ? c->f.failed : c->cfg.mode == GM_MODE_SCALED ? c->s.failed : c->p.failed;
+  const bool part = c->cfg.mode == GM_MODE_PARTIAL;  // a row shard holds its own nodes' flags only
   HIPCHECK(hipStreamSynchronize(c->stream));
-  HIPCHECK(hipMemcpy(dst, c->failed_h.data(), sizeof(int32_t) * c->n, hipMemcpyHostToDevice));
+  HIPCHECK(hipMemcpy(dst, c->failed_h.data() + (part ? c->p.n0 : 0), sizeof(int32_t) * (part ? c->p.nloc : c->n),
+                     hipMemcpyHostToDevice));
   return GM_OK;
 }
 
@@ -578,22 +610,23 @@ static void sort_canonical(std::vector<gm_event> &out) {
 
 static int drain_partial(gm_ctx *c, std::vector<gm_event> &out) {
   const PState &p = c->p;
-  std::vector<int32_t> cnt(c->n);
-  HIPCHECK(hipMemcpyAsync(cnt.data(), p.ev_cnt, sizeof(int32_t) * c->n, hipMemcpyDeviceToHost, c->stream));
+  std::vector<int32_t> cnt(p.nloc);
+  HIPCHECK(hipMemcpyAsync(cnt.data(), p.ev_cnt, sizeof(int32_t) * p.nloc, hipMemcpyDeviceToHost, c->stream));
   HIPCHECK(hipStreamSynchronize(c->stream));
   size_t tot = 0;
   for (int32_t v : cnt) tot += (size_t)(v & 0xFFFF) + (size_t)(v >> 16);
   if (!tot) return GM_OK;
   const size_t row = 2 * (size_t)p.V;  // joins from the front, removals from the back
-  std::vector<uint32_t> ev((size_t)c->n * row);
+  std::vector<uint32_t> ev((size_t)p.nloc * row);
   HIPCHECK(hipMemcpy(ev.data(), p.ev, sizeof(uint32_t) * ev.size(), hipMemcpyDeviceToHost));
   const int t = c->t - 1;
   out.reserve(out.size() + tot);
-  for (int r = 0; r < c->n; r++) {
+  for (int r = 0; r < p.nloc; r++) {
     const int nj = cnt[r] & 0xFFFF, nr = cnt[r] >> 16;
     for (int q = 0; q < nj + nr; q++) {
       const uint32_t rec = ev[(size_t)r * row + (q < nj ? q : row - 1 - (q - nj))];
-      out.push_back(gm_event{t, r, (rec >> 30) == P_EV_ADD ? GM_EV_JOINED : GM_EV_REMOVED, (int32_t)(rec & 0x3FFFFFFFu)});
+      out.push_back(gm_event{t, p.n0 + r, (rec >> 30) == P_EV_ADD ? GM_EV_JOINED : GM_EV_REMOVED,
+                             (int32_t)(rec & 0x3FFFFFFFu)});
     }
   }
   sort_canonical(out);
@@ -628,8 +661,8 @@ extern "C" int gm_event_counts(gm_ctx *c, uint64_t counts[6]) {
     for (uint32_t v : bc) tot += S_BC_NEV(v);  // slots + spilled, per (row, band)
     counts[0] = tot;  // join+remove records of the last tick (per-kind split needs a drain)
   } else if (c->cfg.mode == GM_MODE_PARTIAL) {
-    std::vector<int32_t> cnt(c->n);
-    HIPCHECK(hipMemcpyAsync(cnt.data(), c->p.ev_cnt, sizeof(int32_t) * c->n, hipMemcpyDeviceToHost, c->stream));
+    std::vector<int32_t> cnt(c->p.nloc);
+    HIPCHECK(hipMemcpyAsync(cnt.data(), c->p.ev_cnt, sizeof(int32_t) * c->p.nloc, hipMemcpyDeviceToHost, c->stream));
     HIPCHECK(hipStreamSynchronize(c->stream));
     for (int32_t v : cnt) counts[0] += (uint64_t)(v & 0xFFFF) + (uint64_t)(v >> 16);
   } else {
@@ -670,9 +703,10 @@ static int read_table_row(gm_ctx *c, int r, std::vector<int32_t> &hb, std::vecto
   }
   if (c->cfg.mode == GM_MODE_PARTIAL) {  // the node's V-entry list as of the last tick
     const PState &p = c->p;
+    if (r < p.n0 || r >= p.n0 + p.nloc) return GM_EINVAL;  // another row shard's node
     std::vector<uint64_t> lst(p.V);
-    HIPCHECK(hipMemcpy(lst.data(), p.lists + ((size_t)((c->t - 1) & 1) * c->n + r) * p.V, sizeof(uint64_t) * p.V,
-                       hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(lst.data(), p.lists + ((size_t)((c->t - 1) & 1) * p.rows + (r - p.n0)) * p.V,
+                       sizeof(uint64_t) * p.V, hipMemcpyDeviceToHost));
     w = c->n;
     hb.assign(w, -1);
     ts.assign(w, -1);
@@ -720,7 +754,7 @@ extern "C" int gm_read_row(gm_ctx *c, int32_t r, int32_t c0, int32_t len, int32_
 extern "C" int gm_read_nodes(gm_ctx *c, int32_t *st4) {
   if (!c || !st4) return GM_EINVAL;
   HIPCHECK(hipStreamSynchronize(c->stream));
-  const int n = c->n;
+  const int n = c->cfg.mode == GM_MODE_PARTIAL ? c->p.nloc : c->n;  // a row shard reports its own nodes
   std::vector<int32_t> a(n), b(n), f(n), h(n);
   if (c->cfg.mode == GM_MODE_FAITHFUL) {
     HIPCHECK(hipMemcpy(a.data(), c->f.inited, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
@@ -751,15 +785,16 @@ extern "C" int gm_dump_tables(gm_ctx *c, char *buf, size_t cap, size_t *len) {
   char tmp[96];
   const int t = c->t - 1;
   if (c->cfg.mode == GM_MODE_PARTIAL) {  // the V-entry lists (id order) of the last tick, one copy
-    const PState &p = c->p;
-    std::vector<uint64_t> all((size_t)c->n * p.V);
-    HIPCHECK(hipMemcpy(all.data(), p.lists + (size_t)(t & 1) * c->n * p.V, sizeof(uint64_t) * all.size(),
+    const PState &p = c->p;          // a row shard renders its own nodes (global indices)
+    std::vector<uint64_t> all((size_t)p.nloc * p.V);
+    HIPCHECK(hipMemcpy(all.data(), p.lists + (size_t)(t & 1) * p.rows * p.V, sizeof(uint64_t) * all.size(),
                        hipMemcpyDeviceToHost));
-    for (int i = 0; i < c->n; i++) {
+    for (int i = 0; i < p.nloc; i++) {
       const uint64_t *row = all.data() + (size_t)i * p.V;
       int cnt = 0;
       for (int j = 0; j < p.V; j++) cnt += row[j] != 0;
-      snprintf(tmp, sizeof tmp, "%d %d %d %d %d %d %d", t, i, st[4 * i], st[4 * i + 1], st[4 * i + 2], st[4 * i + 3], cnt);
+      snprintf(tmp, sizeof tmp, "%d %d %d %d %d %d %d", t, p.n0 + i, st[4 * i], st[4 * i + 1], st[4 * i + 2],
+               st[4 * i + 3], cnt);
       out += tmp;
       for (int j = 0; j < p.V; j++) {
         if (!row[j]) continue;
@@ -800,17 +835,18 @@ extern "C" int gm_tick_stats(gm_ctx *c, int64_t stats[4]) {
   if (!c || !stats) return GM_EINVAL;
   if (c->cfg.mode == GM_MODE_FAITHFUL) return GM_EUNSUPPORTED;
   const bool part = c->cfg.mode == GM_MODE_PARTIAL;
-  std::vector<int32_t> rs((size_t)c->n * 4);
+  const int rows = part ? c->p.nloc : c->n, r0 = part ? c->p.n0 : 0;  // a row shard reports its own nodes
+  std::vector<int32_t> rs((size_t)rows * 4);
   uint32_t e = 0;
   HIPCHECK(hipMemcpyAsync(rs.data(), part ? c->p.rowstat : c->s.rowstat, sizeof(int32_t) * rs.size(),
                           hipMemcpyDeviceToHost, c->stream));
   HIPCHECK(hipMemcpyAsync(&e, part ? c->p.err : c->s.err, sizeof e, hipMemcpyDeviceToHost, c->stream));
   HIPCHECK(hipStreamSynchronize(c->stream));
   int64_t m = 0, live = 0, mx = 0;
-  for (int r = 0; r < c->n; r++) {
+  for (int r = 0; r < rows; r++) {
     m += rs[4 * r];
     mx = std::max<int64_t>(mx, rs[4 * r]);
-    live += c->failed_h[r] ? 0 : 1;
+    live += c->failed_h[r0 + r] ? 0 : 1;
   }
   stats[0] = m;
   stats[1] = live;
@@ -890,7 +926,9 @@ extern "C" int gm_comm_unique_id(uint8_t *out128) {
 }
 
 extern "C" int gm_comm_init(gm_ctx *c, const uint8_t *id128, int32_t nranks, int32_t rank) {
-  if (!c || !id128 || c->cfg.mode != GM_MODE_SCALED || c->s.shard_count != nranks || c->s.shard_rank != rank)
+  if (!c || !id128) return GM_EINVAL;
+  if (c->cfg.mode == GM_MODE_SCALED ? (c->s.shard_count != nranks || c->s.shard_rank != rank)
+      : c->cfg.mode == GM_MODE_PARTIAL ? (c->p.G != nranks || c->p.rank != rank) : true)
     return GM_EINVAL;
   if (c->comm) return GM_OK;
   ncclUniqueId id;
@@ -901,6 +939,11 @@ extern "C" int gm_comm_init(gm_ctx *c, const uint8_t *id128, int32_t nranks, int
 }
 
 extern "C" int gm_shard_layout(gm_ctx *c, int32_t *c0, int32_t *w) {
+  if (c && c0 && w && c->cfg.mode == GM_MODE_PARTIAL) {  // row shard: nodes [n0, n0 + nloc)
+    *c0 = c->p.n0;
+    *w = c->p.nloc;
+    return GM_OK;
+  }
   if (!c || !c0 || !w || c->cfg.mode != GM_MODE_SCALED) return GM_EINVAL;
   *c0 = c->s.c0;
   *w = c->s.w;
@@ -1008,5 +1051,98 @@ static int tick_sharded(gm_ctx *c) {
   }
   c->t--;  // gm_tick advances globaltime
   TRY(gm_shard_end_tick(c));
+  return GM_OK;
+}
+
+// ------------------------------------------------------------ PARTIAL row shards
+// After the local kernels of tick t every shard holds, per remote shard q, the
+// records its nodes address to q (header + list). All-to-all of the record counts,
+// then all-to-allv of the headers and of the lists, which land directly in rows
+// nloc.. of parity t&1 (where tick t+1 reads its senders' lists); gm_p_unpack
+// appends each received row to its targets' inboxes.
+static int partial_exchange_rccl(gm_ctx *c) {
+  PState &p = c->p;
+  const int G = p.G, V = p.V, nl = p.nloc;
+  NCCLCHECK(ncclAllToAll(p.send_cnt, p.recv_cnt, 1, ncclInt32, c->comm, c->stream));
+  std::vector<int32_t> sc(G), rc(G);
+  HIPCHECK(hipMemcpyAsync(sc.data(), p.send_cnt, sizeof(int32_t) * G, hipMemcpyDeviceToHost, c->stream));
+  HIPCHECK(hipMemcpyAsync(rc.data(), p.recv_cnt, sizeof(int32_t) * G, hipMemcpyDeviceToHost, c->stream));
+  HIPCHECK(hipStreamSynchronize(c->stream));
+  std::vector<size_t> hs(G), hsd(G), hr(G), hrd(G), ls(G), lsd(G), lr(G), lrd(G);
+  size_t off = 0;
+  for (int q = 0; q < G; q++) {
+    if (sc[q] < 0 || sc[q] > nl || rc[q] < 0) return GM_ESTATE;
+    hs[q] = (size_t)sc[q] * 8;
+    hsd[q] = (size_t)q * nl * 8;
+    ls[q] = (size_t)sc[q] * V;
+    lsd[q] = (size_t)q * nl * V;
+    hr[q] = (size_t)rc[q] * 8;
+    hrd[q] = off * 8;
+    lr[q] = (size_t)rc[q] * V;
+    lrd[q] = off * V;
+    off += (size_t)rc[q];
+  }
+  if (off > (size_t)(p.n - nl)) return GM_ESTATE;
+  uint64_t *rows_in = p.lists + ((size_t)(c->t & 1) * p.rows + nl) * V;
+  NCCLCHECK(ncclAllToAllv(p.send_hdr, hs.data(), hsd.data(), p.recv_hdr, hr.data(), hrd.data(), ncclInt32, c->comm,
+                          c->stream));
+  NCCLCHECK(ncclAllToAllv(p.send_list, ls.data(), lsd.data(), rows_in, lr.data(), lrd.data(), ncclUint64, c->comm,
+                          c->stream));
+  HIPCHECK(gm_launch_partial_unpack(p, c->t, (int)off, c->stream));
+  c->p_recv_last = (int64_t)off;
+  return GM_OK;
+}
+
+// One PARTIAL tick of G row-shard contexts living on one device (tests): the local
+// kernels of every shard, the same exchange as partial_exchange_rccl by device copies,
+// the unpack, and the globaltime advance gm_tick does.
+extern "C" int gm_partial_loopback_tick(gm_ctx **ctxs, int32_t G) {
+  if (!ctxs || G < 2) return GM_EINVAL;
+  for (int g = 0; g < G; g++) {
+    gm_ctx *c = ctxs[g];
+    if (!c || c->cfg.mode != GM_MODE_PARTIAL || c->p.G != G || c->p.rank != g || c->t != ctxs[0]->t ||
+        c->n != ctxs[0]->n || c->p.V != ctxs[0]->p.V)
+      return GM_EINVAL;
+    if (c->latched != GM_OK) return c->latched;
+  }
+  for (int g = 0; g < G; g++) {
+    gm_ctx *c = ctxs[g];
+    const int t_send = c->t - 1;
+    const bool drop = c->cfg.drop_pct > 0 && t_send >= c->cfg.drop_from && t_send < c->cfg.drop_to;
+    PState st = c->p;
+    st.drop_pct = drop ? c->cfg.drop_pct : -1;
+    HIPCHECK(gm_launch_partial_tick(st, c->t, c->p_mtraw, c->stream, nullptr, nullptr));
+  }
+  std::vector<std::vector<int32_t>> sc(G, std::vector<int32_t>(G));
+  for (int g = 0; g < G; g++) {
+    HIPCHECK(hipMemcpyAsync(sc[g].data(), ctxs[g]->p.send_cnt, sizeof(int32_t) * G, hipMemcpyDeviceToHost,
+                            ctxs[g]->stream));
+    HIPCHECK(hipStreamSynchronize(ctxs[g]->stream));
+  }
+  const int V = ctxs[0]->p.V;
+  for (int q = 0; q < G; q++) {
+    PState &dq = ctxs[q]->p;
+    hipStream_t st = ctxs[q]->stream;
+    size_t off = 0;
+    for (int g = 0; g < G; g++) {
+      const PState &sg = ctxs[g]->p;
+      const size_t cnt = (size_t)sc[g][q];
+      if (g == q || !cnt) continue;
+      if (cnt > (size_t)sg.nloc || off + cnt > (size_t)(dq.n - dq.nloc)) return GM_ESTATE;
+      HIPCHECK(hipMemcpyAsync(dq.recv_hdr + off * 8, sg.send_hdr + (size_t)q * sg.nloc * 8, sizeof(int32_t) * 8 * cnt,
+                              hipMemcpyDeviceToDevice, st));
+      HIPCHECK(hipMemcpyAsync(dq.lists + ((size_t)(ctxs[q]->t & 1) * dq.rows + dq.nloc + off) * V,
+                              sg.send_list + (size_t)q * sg.nloc * V, sizeof(uint64_t) * V * cnt,
+                              hipMemcpyDeviceToDevice, st));
+      off += cnt;
+    }
+    HIPCHECK(gm_launch_partial_unpack(dq, ctxs[q]->t, (int)off, st));
+    ctxs[q]->p_recv_last = (int64_t)off;
+  }
+  for (int g = 0; g < G; g++) {
+    HIPCHECK(hipStreamSynchronize(ctxs[g]->stream));
+    TRY(check_err(ctxs[g]));
+    ctxs[g]->t++;
+  }
   return GM_OK;
 }

@@ -12,20 +12,31 @@
 #define P_EV_REMOVE 2u
 
 struct PState {
-  int n;                 // nodes
+  int n;                 // nodes of the whole cluster
   int V;                 // view capacity
+  // row shard (multi-GPU S-C): this context owns nodes [n0, n0 + nloc); local row li = i - n0.
+  // Single context: n0 = 0, nloc = n, G = 1.
+  int n0, nloc, G, rank;
+  int rows;              // list rows per parity: nloc own rows + (n - nloc) rows of received remote lists
   int drop_pct;          // per-entry drop percentage for this tick's deliveries (-1: none)
   uint64_t rd_seed, view_seed, drop_seed;
-  uint64_t *lists;       // [2][n][V] entries (id << 32 | hb), 0 = empty, sorted by id; parity t&1 written at tick t
-  int32_t *inbox_cnt[2]; // [n] lists queued for each receiver, by delivery-tick parity
-  int32_t *inbox[2];     // [n][P_KMAX] sender indices
-  int32_t *hbctr;        // [n] heartbeat counter
-  int32_t *failed;       // [n]
-  uint32_t *ev;          // [n][2V] kind<<30 | subject id: joins from the front (ascending id), removals from the back
-  int32_t *ev_cnt;       // [n] joins | removals << 16
-  int32_t *rowstat;      // [n][4]: lists merged, view size, numfailed, targets chosen
-  int32_t *targets;      // [n][GM_FANOUT]
-  int32_t *big;          // [n] worklist of nodes with > P_KSMALL lists (big-table kernel)
+  uint64_t *lists;       // [2][rows][V] entries (id << 32 | hb), 0 = empty, sorted by id; parity t&1 written at tick t
+  int32_t *inbox_cnt[2]; // [nloc] lists queued for each receiver, by delivery-tick parity
+  int32_t *inbox[2];     // [nloc][P_KMAX] list rows of the senders (local row, or nloc + received record)
+  int32_t *rsrc[2];      // [n - nloc] global sender index of each received list row, by parity
+  int32_t *hbctr;        // [nloc] heartbeat counter
+  int32_t *failed;       // [nloc]
+  uint32_t *ev;          // [nloc][2V] kind<<30 | subject id: joins from the front (ascending id), removals from the back
+  int32_t *ev_cnt;       // [nloc] joins | removals << 16
+  int32_t *rowstat;      // [nloc][4]: lists merged, view size, numfailed, targets chosen
+  int32_t *targets;      // [nloc][GM_FANOUT] (global node indices)
+  int32_t *big;          // [nloc] worklist of nodes with > P_KSMALL lists (big-table kernel)
   int32_t *big_cnt;      // [1]
+  // outgoing lists to the other row shards (sharded only): one record per (sender, remote rank)
+  int32_t *send_cnt;     // [G]
+  int32_t *send_hdr;     // [G][nloc][8]: sender global index, #targets on that rank, targets (global), 0
+  uint64_t *send_list;   // [G][nloc][V]: the sender's final list of the tick
+  int32_t *recv_hdr;     // [n - nloc][8] received headers (their lists land in rows nloc.. of the tick's parity)
+  int32_t *recv_cnt;     // [G] records received from each shard this tick
   uint32_t *err;
 };

@@ -112,10 +112,21 @@ __device__ __forceinline__ int p_insert(uint32_t *tid, uint32_t *thb, uint32_t i
   return (int)h;
 }
 
-// One node's tick on one wave. i: node index; k: lists queued for it this tick.
+// first node of row shard g (contiguous balanced ranges)
+__device__ __forceinline__ int p_shard_n0(const PState &s, int g) { return (int)((int64_t)s.n * g / s.G); }
+__device__ __forceinline__ int p_owner(const PState &s, int d) {
+  int g = (int)((int64_t)d * s.G / s.n);
+  while (g + 1 < s.G && p_shard_n0(s, g + 1) <= d) g++;
+  while (g > 0 && p_shard_n0(s, g) > d) g--;
+  return g;
+}
+
+// One node's tick on one wave. li: the node's local row (global index n0 + li);
+// k: lists queued for it this tick.
 template <int H, bool BIG>
-__device__ __forceinline__ void p_node(const PState &s, int t, const uint32_t *mtraw, int i, int k, int lane,
+__device__ __forceinline__ void p_node(const PState &s, int t, const uint32_t *mtraw, int li, int k, int lane,
                                        unsigned char *base) {
+  const int i = s.n0 + li;  // global node index (ids, keys, seeds, targets)
   constexpr int TS = H / 64;                          // table slots per lane
   constexpr int KK = BIG ? P_KP : P_KSMALL;           // lists merged at most
   constexpr int DS = ((1 + KK) * P_VMAX + 63) / 64;   // dense entries per lane
@@ -128,33 +139,39 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const uint32_t *m
   uint64_t *fin = (uint64_t *)(khb + P_VMAX);
   const int V = s.V;
   const int par = t & 1;
-  const uint64_t *prev = s.lists + (size_t)(par ^ 1) * s.n * V;
-  uint64_t *cur = s.lists + (size_t)par * s.n * V;
+  const uint64_t *prev = s.lists + (size_t)(par ^ 1) * s.rows * V;
+  uint64_t *cur = s.lists + (size_t)par * s.rows * V;
 
-  if (lane == 0) s.inbox_cnt[par][i] = 0;  // consumed; the append target of tick t+1
+  if (lane == 0) s.inbox_cnt[par][li] = 0;  // consumed; the append target of tick t+1
   if (BIG && k > P_KMAX) {
     if (lane == 0) atomicOr(s.err, GM_ERR_INBOX);
     k = P_KMAX;
   }
   // ---- 1. loads
-  const uint64_t own = lane < V ? prev[(size_t)i * V + lane] : 0ull;
-  int sv = lane < k ? s.inbox[par][(size_t)i * P_KMAX + lane] : 0x7FFFFFFF;
-  const uint32_t raw0 = lane < 16 ? mtraw[(size_t)i * 16 + lane] : 0u;
-  const int hbnew = s.hbctr[i] + 1;
+  const uint64_t own = lane < V ? prev[(size_t)li * V + lane] : 0ull;
+  int sv = lane < k ? s.inbox[par][(size_t)li * P_KMAX + lane] : 0x7FFFFFFF;  // list rows
+  const uint32_t raw0 = lane < 16 ? mtraw[(size_t)li * 16 + lane] : 0u;
+  const int hbnew = s.hbctr[li] + 1;
+  // global sender index of each row (drop keys, the lowest-sender rule)
+  int sg = lane < k ? (sv < s.nloc ? s.n0 + sv : s.rsrc[par ^ 1][sv - s.nloc]) : 0x7FFFFFFF;
   {  // clear the table (both word arrays are contiguous)
     uint4 *z = (uint4 *)tid;
 #pragma unroll
     for (int q = 0; q < H / 128; q++) z[lane + 64 * q] = make_uint4(0, 0, 0, 0);
   }
-  if (BIG && k > P_KP) {  // the P_KP lowest sender indices: bitonic sort across the wave
+  if (BIG && k > P_KP) {  // the P_KP lowest sender indices: bitonic sort of (sender, row) across the wave
+    uint64_t key = ((uint64_t)(uint32_t)sg << 32) | (uint32_t)sv;
 #pragma unroll
     for (int k2 = 2; k2 <= 64; k2 <<= 1)
 #pragma unroll
       for (int j2 = k2 >> 1; j2 > 0; j2 >>= 1) {
-        const int o = __shfl_xor(sv, j2, 64);
+        const uint32_t olo = __shfl_xor((uint32_t)key, j2, 64), ohi = __shfl_xor((uint32_t)(key >> 32), j2, 64);
+        const uint64_t o = ((uint64_t)ohi << 32) | olo;
         const bool up = (lane & k2) == 0, lower = (lane & j2) == 0;
-        sv = (lower == up) ? min(sv, o) : max(sv, o);
+        key = (lower == up) ? min(key, o) : max(key, o);
       }
+    sv = (int)(uint32_t)key;
+    sg = (int)(key >> 32);
   }
   const int kk = min(k, KK);
   const int per = 64 / V, l = lane % V, jo = lane / V;
@@ -165,7 +182,7 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const uint32_t *m
     const int j = st * per + jo;
     const bool ok = jo < per && j < kk;
     const int sn = __shfl(sv, ok ? j : 0, 64);
-    dsn[st] = sn;
+    dsn[st] = __shfl(sg, ok ? j : 0, 64);
     dv[st] = ok ? prev[(size_t)sn * V + l] : 0ull;
   }
   p_wsync();
@@ -212,11 +229,11 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const uint32_t *m
     if (lane == 0) {
       thb[hs] = (uint32_t)hbnew;
       tid[hs] |= P_SELF | P_OWN;
-      s.hbctr[i] = hbnew + 1;
+      s.hbctr[li] = hbnew + 1;
     }
   }
   p_wsync();
-  uint32_t *evr = s.ev + (size_t)i * 2 * V;
+  uint32_t *evr = s.ev + (size_t)li * 2 * V;
   int m, removed, nrem;
   {
     uint32_t w[TS], hh[TS];
@@ -379,7 +396,7 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const uint32_t *m
   p_wsync();
   const uint64_t x = lane < cnt ? fin[lane] : 0ull;
   const uint32_t f = lane < cnt ? kid[lane] : 0u;
-  if (lane < V) cur[(size_t)i * V + lane] = x;
+  if (lane < V) cur[(size_t)li * V + lane] = x;
   // joins (ascending id) from the front of the event row
   const uint64_t jb = __ballot(lane < cnt && !(f & P_OWN));
   const int nj = __builtin_popcountll(jb);
@@ -435,44 +452,78 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const uint32_t *m
       }
     }
   }
-  // ---- sends: one parallel round of inbox appends, one lane per target
+  // ---- sends: one parallel round of inbox appends, one lane per target; targets owned by
+  // another row shard get one record per (sender, shard): header + this tick's list
+  const int dst = lane >= ng ? 0 : lane == 0 ? g0 : lane == 1 ? g1 : lane == 2 ? g2 : lane == 3 ? g3 : g4;
+  const int owner = (s.G > 1 && lane < ng) ? p_owner(s, dst) : s.rank;
   if (lane < ng) {
-    const int dst = lane == 0 ? g0 : lane == 1 ? g1 : lane == 2 ? g2 : lane == 3 ? g3 : g4;
-    s.targets[(size_t)i * GM_FANOUT + lane] = dst;
-    const int slot = atomicAdd(&s.inbox_cnt[par ^ 1][dst], 1);
-    if (slot < P_KMAX) s.inbox[par ^ 1][(size_t)dst * P_KMAX + slot] = i;
-    else atomicOr(s.err, GM_ERR_INBOX);
+    s.targets[(size_t)li * GM_FANOUT + lane] = dst;
+    if (owner == s.rank) {
+      const int slot = atomicAdd(&s.inbox_cnt[par ^ 1][dst - s.n0], 1);
+      if (slot < P_KMAX) s.inbox[par ^ 1][(size_t)(dst - s.n0) * P_KMAX + slot] = li;
+      else atomicOr(s.err, GM_ERR_INBOX);
+    }
   }
-  if (lane < 4) s.rowstat[(size_t)i * 4 + lane] = lane == 0 ? kk : lane == 1 ? cnt : lane == 2 ? numfailed : ng;
-  if (lane == 0) s.ev_cnt[i] = nj | (nrem << 16);
+  if (s.G > 1 && __ballot(lane < ng && owner != s.rank)) {
+    bool first = lane < ng && owner != s.rank;
+#pragma unroll
+    for (int q = 0; q < GM_FANOUT - 1; q++)
+      if (q < lane && __builtin_amdgcn_readlane(owner, q) == owner) first = false;
+    uint64_t fm = __ballot(first);
+    const int slot = first ? atomicAdd(&s.send_cnt[owner], 1) : 0;
+    while (fm) {
+      const int fl = __builtin_ctzll(fm);
+      fm &= fm - 1;
+      const int rr = __builtin_amdgcn_readlane(owner, fl);
+      const size_t rec = (size_t)rr * s.nloc + (size_t)__builtin_amdgcn_readlane(slot, fl);
+      uint64_t tm = __ballot(lane < ng && owner == rr);
+      const int nt = __builtin_popcountll(tm);
+      int tv0 = -1, tv1 = -1, tv2 = -1, tv3 = -1, tv4 = -1;
+      for (int q = 0; tm; q++) {
+        const int d = __builtin_amdgcn_readlane(dst, __builtin_ctzll(tm));
+        tm &= tm - 1;
+        if (q == 0) tv0 = d;
+        else if (q == 1) tv1 = d;
+        else if (q == 2) tv2 = d;
+        else if (q == 3) tv3 = d;
+        else tv4 = d;
+      }
+      if (lane < 8)
+        s.send_hdr[rec * 8 + lane] = lane == 0 ? i : lane == 1 ? nt : lane == 2 ? tv0 : lane == 3 ? tv1
+                                   : lane == 4 ? tv2 : lane == 5 ? tv3 : lane == 6 ? tv4 : 0;
+      if (lane < V) s.send_list[rec * V + lane] = x;
+    }
+  }
+  if (lane < 4) s.rowstat[(size_t)li * 4 + lane] = lane == 0 ? kk : lane == 1 ? cnt : lane == 2 ? numfailed : ng;
+  if (lane == 0) s.ev_cnt[li] = nj | (nrem << 16);
 }
 
 // crashed node: frozen (its list carried to this tick's buffer unchanged), inbox dropped
-__device__ __forceinline__ void p_frozen(const PState &s, int t, int i, int lane) {
+__device__ __forceinline__ void p_frozen(const PState &s, int t, int li, int lane) {
   const int par = t & 1, V = s.V;
-  if (lane < V) s.lists[((size_t)par * s.n + i) * V + lane] = s.lists[((size_t)(par ^ 1) * s.n + i) * V + lane];
-  if (lane < 4) s.rowstat[(size_t)i * 4 + lane] = 0;
+  if (lane < V) s.lists[((size_t)par * s.rows + li) * V + lane] = s.lists[((size_t)(par ^ 1) * s.rows + li) * V + lane];
+  if (lane < 4) s.rowstat[(size_t)li * 4 + lane] = 0;
   if (lane == 0) {
-    s.inbox_cnt[par][i] = 0;
-    s.ev_cnt[i] = 0;
+    s.inbox_cnt[par][li] = 0;
+    s.ev_cnt[li] = 0;
   }
 }
 
 __global__ __launch_bounds__(256) void gm_p_tick_small(PState s, int t, const uint32_t *mtraw) {
   extern __shared__ __align__(16) unsigned char p_smem[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int i = blockIdx.x * 4 + wave;
-  if (i >= s.n) return;  // whole wave; no workgroup barrier in this kernel
-  if (s.failed[i]) {
-    p_frozen(s, t, i, lane);
+  const int li = blockIdx.x * 4 + wave;
+  if (li >= s.nloc) return;  // whole wave; no workgroup barrier in this kernel
+  if (s.failed[li]) {
+    p_frozen(s, t, li, lane);
     return;
   }
-  const int k = s.inbox_cnt[t & 1][i];
+  const int k = s.inbox_cnt[t & 1][li];
   if (k > P_KSMALL) {  // deferred to gm_p_tick_big
-    if (lane == 0) s.big[atomicAdd(s.big_cnt, 1)] = i;
+    if (lane == 0) s.big[atomicAdd(s.big_cnt, 1)] = li;
     return;
   }
-  p_node<P_HS, false>(s, t, mtraw, i, k, lane, p_smem + (size_t)wave * PLds<P_HS>::bytes);
+  p_node<P_HS, false>(s, t, mtraw, li, k, lane, p_smem + (size_t)wave * PLds<P_HS>::bytes);
 }
 
 // drains the worklist gm_p_tick_small filled (a fixed grid; every wave exits when the list is done)
@@ -481,19 +532,21 @@ __global__ __launch_bounds__(256) void gm_p_tick_big(PState s, int t, const uint
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int nbig = *s.big_cnt;
   for (int w = blockIdx.x * 4 + wave; w < nbig; w += gridDim.x * 4) {
-    const int i = s.big[w];
-    const int k = s.inbox_cnt[t & 1][i];
-    p_node<P_HB, true>(s, t, mtraw, i, k, lane, p_smem + (size_t)wave * PLds<P_HB>::bytes);
+    const int li = s.big[w];
+    const int k = s.inbox_cnt[t & 1][li];
+    p_node<P_HB, true>(s, t, mtraw, li, k, lane, p_smem + (size_t)wave * PLds<P_HB>::bytes);
   }
 }
 
-// first 16 S2 outputs of every node for tick t (see gm_mt_first16); resets the big worklist
+// first 16 S2 outputs of every node for tick t (see gm_mt_first16); resets the big
+// worklist and the outgoing record counts
 __global__ __launch_bounds__(256) void gm_p_mtgen(PState s, int t, uint32_t *mtraw) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r == 0) *s.big_cnt = 0;
-  if (r >= s.n) return;
+  if (s.send_cnt && r < s.G) s.send_cnt[r] = 0;
+  if (r >= s.nloc) return;
   uint32_t out[16];
-  gm_mt_first16(gm_rd_seed(s.rd_seed, t, r + 1), out);
+  gm_mt_first16(gm_rd_seed(s.rd_seed, t, s.n0 + r + 1), out);
   uint4 *dst = (uint4 *)(mtraw + (size_t)r * 16);
 #pragma unroll
   for (int q = 0; q < 4; q++) dst[q] = make_uint4(out[4 * q], out[4 * q + 1], out[4 * q + 2], out[4 * q + 3]);
@@ -503,8 +556,9 @@ __global__ __launch_bounds__(256) void gm_p_mtgen(PState s, int t, uint32_t *mtr
 // mix64(view_seed ^ i<<32 ^ j) % n with hb 2(t0-1-a)-1, sorted by id; written to the
 // parity of tick t0.
 __global__ __launch_bounds__(64) void gm_p_init(PState s, int t0, uint64_t init_seed) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= s.n) return;
+  const int li = blockIdx.x * blockDim.x + threadIdx.x;
+  if (li >= s.nloc) return;
+  const int i = s.n0 + li;
   const int V = s.V;
   uint64_t ent[P_VMAX];
   int cnt = 1;
@@ -523,18 +577,40 @@ __global__ __launch_bounds__(64) void gm_p_init(PState s, int t0, uint64_t init_
       ent[b] = ent[b - 1];
       ent[b - 1] = x;
     }
-  uint64_t *dst = s.lists + ((size_t)(t0 & 1) * s.n + i) * V;
+  uint64_t *dst = s.lists + ((size_t)(t0 & 1) * s.rows + li) * V;
   for (int a = 0; a < V; a++) dst[a] = a < cnt ? ent[a] : 0ull;
-  s.hbctr[i] = 2 * t0;
+  s.hbctr[li] = 2 * t0;
+}
+
+// received records of tick t (row shards): remote lists already sit in rows nloc + j of
+// parity t&1; record each row's sender and append the row to its local targets' inboxes
+__global__ __launch_bounds__(256) void gm_p_unpack(PState s, int t, int nrecv) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= nrecv) return;
+  const int par = t & 1;
+  const int4 h0 = ((const int4 *)s.recv_hdr)[2 * (size_t)j];
+  const int4 h1 = ((const int4 *)s.recv_hdr)[2 * (size_t)j + 1];
+  s.rsrc[par][j] = h0.x;
+  const int tg[GM_FANOUT] = {h0.z, h0.w, h1.x, h1.y, h1.z};
+  for (int q = 0; q < h0.y && q < GM_FANOUT; q++) {
+    const int d = tg[q] - s.n0;
+    if (d < 0 || d >= s.nloc) {
+      atomicOr(s.err, GM_ERR_INBOX);
+      continue;
+    }
+    const int slot = atomicAdd(&s.inbox_cnt[par ^ 1][d], 1);
+    if (slot < P_KMAX) s.inbox[par ^ 1][(size_t)d * P_KMAX + slot] = s.nloc + j;
+    else atomicOr(s.err, GM_ERR_INBOX);
+  }
 }
 
 #define P_BIG_GRID 1024
 
 hipError_t gm_launch_partial_tick(const PState &s, int t, uint32_t *mtraw, hipStream_t st, hipEvent_t k0,
                                   hipEvent_t k1) {
-  hipLaunchKernelGGL(gm_p_mtgen, dim3((s.n + 255) / 256), dim3(256), 0, st, s, t, mtraw);
+  hipLaunchKernelGGL(gm_p_mtgen, dim3((s.nloc + 255) / 256), dim3(256), 0, st, s, t, mtraw);
   if (k0) (void)hipEventRecord(k0, st);
-  hipLaunchKernelGGL(gm_p_tick_small, dim3((s.n + 3) / 4), dim3(256), 4 * PLds<P_HS>::bytes, st, s, t,
+  hipLaunchKernelGGL(gm_p_tick_small, dim3((s.nloc + 3) / 4), dim3(256), 4 * PLds<P_HS>::bytes, st, s, t,
                      (const uint32_t *)mtraw);
   hipLaunchKernelGGL(gm_p_tick_big, dim3(P_BIG_GRID), dim3(256), 4 * PLds<P_HB>::bytes, st, s, t,
                      (const uint32_t *)mtraw);
@@ -543,7 +619,12 @@ hipError_t gm_launch_partial_tick(const PState &s, int t, uint32_t *mtraw, hipSt
 }
 
 hipError_t gm_launch_partial_init(const PState &s, int t0, uint64_t init_seed, hipStream_t st) {
-  hipLaunchKernelGGL(gm_p_init, dim3((s.n + 63) / 64), dim3(64), 0, st, s, t0, init_seed);
+  hipLaunchKernelGGL(gm_p_init, dim3((s.nloc + 63) / 64), dim3(64), 0, st, s, t0, init_seed);
+  return hipGetLastError();
+}
+
+hipError_t gm_launch_partial_unpack(const PState &s, int t, int nrecv, hipStream_t st) {
+  if (nrecv > 0) hipLaunchKernelGGL(gm_p_unpack, dim3((nrecv + 255) / 256), dim3(256), 0, st, s, t, nrecv);
   return hipGetLastError();
 }
 

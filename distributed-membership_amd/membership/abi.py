@@ -37,7 +37,7 @@ EXPORTS = ["gm_parse_conf", "gm_create", "gm_destroy", "gm_tick", "gm_sync", "gm
            "gm_set_dropmsg", "gm_drain_events", "gm_event_counts", "gm_msgcount", "gm_read_row", "gm_read_nodes",
            "gm_dump_tables", "gm_tick_stats", "gm_set_timing", "gm_last_kernel_ms", "gm_crash_set", "gm_strerror",
            "gm_comm_unique_id", "gm_comm_init", "gm_shard_layout", "gm_shard_merge", "gm_shard_draw",
-           "gm_shard_accept", "gm_shard_end_tick", "gm_shard_loopback"]
+           "gm_shard_accept", "gm_shard_end_tick", "gm_shard_loopback", "gm_partial_loopback_tick"]
 
 _lib = None
 
@@ -78,6 +78,7 @@ def load_library():
         "gm_comm_init": [ctypes.c_void_p, ctypes.c_char_p, i32, i32],
         "gm_shard_layout": [ctypes.c_void_p, P(i32), P(i32)],
         "gm_shard_loopback": [P(ctypes.c_void_p), i32, i32, i32],
+        "gm_partial_loopback_tick": [P(ctypes.c_void_p), i32],
         "gm_shard_merge": [ctypes.c_void_p], "gm_shard_draw": [ctypes.c_void_p, i32, i32],
         "gm_shard_accept": [ctypes.c_void_p, i32, P(i32)], "gm_shard_end_tick": [ctypes.c_void_p],
     }
@@ -199,7 +200,8 @@ class Simulator:
         return hb, ts
 
     def read_nodes(self):
-        st = np.zeros((self.n, 4), dtype=np.int32)
+        rows = self.shard_layout()[1] if self.mode == GM_MODE_PARTIAL else self.n  # a row shard: its own nodes
+        st = np.zeros((rows, 4), dtype=np.int32)
         self._call("gm_read_nodes", self.h, _ptr(st))
         return st
 
@@ -263,3 +265,11 @@ def shard_loopback(sims, what, d=0):
     rc = load_library().gm_shard_loopback(arr, len(sims), what, d)
     if rc:
         raise GmError(rc, "gm_shard_loopback")
+
+
+def partial_loopback_tick(sims):
+    """One PARTIAL tick of G row-shard contexts on one device (exchange by device copies)."""
+    arr = (ctypes.c_void_p * len(sims))(*[s.h for s in sims])
+    rc = load_library().gm_partial_loopback_tick(arr, len(sims))
+    if rc:
+        raise GmError(rc, "gm_partial_loopback_tick")

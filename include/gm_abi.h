@@ -178,6 +178,16 @@ int gm_shard_end_tick(gm_ctx *ctx);
 /* what = 0: all-gather the per-row counts; what = 1: MAX-allreduce the first n*D draws */
 int gm_shard_loopback(gm_ctx **ctxs, int32_t G, int32_t what, int32_t D);
 
+/* ---- PARTIAL row sharding (scenario S-C multi-GPU). A PARTIAL context with
+ * shard_count = G > 1 owns nodes [n*g/G, n*(g+1)/G) (gm_shard_layout returns the
+ * range; gm_read_nodes / gm_dump_tables / gm_drain_events / gm_tick_stats report
+ * its own nodes, with global indices). With RCCL attached (gm_comm_init) gm_tick
+ * runs the local kernels, then ncclAllToAll of per-shard record counts and two
+ * ncclAllToAllv (record headers; the V-entry lists, straight into the rows the
+ * next tick reads), then appends the received rows to their targets inboxes.
+ * gm_partial_loopback_tick does one such tick for G contexts on one device. */
+int gm_partial_loopback_tick(gm_ctx **ctxs, int32_t G);
+
 /* Crash set of the SCALED fault schedule: `count` node indices, ascending,
  * chosen by a splitmix64-keyed permutation of [0, n) (host fault injection). */
 int gm_crash_set(int32_t n, int32_t count, uint64_t seed, int32_t *out);

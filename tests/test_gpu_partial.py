@@ -74,3 +74,60 @@ def test_partial_large_cluster_matches_oracle():
             assert digest64(sim.dump_tables()) == digest64(ora.dump()), f"views differ at tick {t}"
     st = sim.tick_stats()
     assert st["err"] == 0 and st["max_inbox"] == 16, st
+
+
+@pytest.mark.parametrize("n,v,world,drop", [(300, 16, 2, 0), (1000, 32, 3, 30), (4099, 32, 4, 5)])
+def test_row_shards_match_oracle(n, v, world, drop):
+    """S-C multi-GPU protocol on one device: G row-shard contexts exchange their
+    outgoing (header, list) records through device copies laid out exactly as the
+    RCCL all-to-allv lays them out, and must reproduce the oracle tick for tick."""
+    from membership.abi import partial_loopback_tick
+    kw = dict(rd_seed=7, view_seed=5, init_t0=8, init_seed=11)
+    ora = oracle_py.PartialOracle(n, v=v, crash_tick=12, crash_count=max(1, n // 50), crash_seed=42, drop_pct=drop,
+                                  drop_from=5, drop_to=30, drop_seed=42, **kw)
+    shards = [Simulator(n, GM_MODE_PARTIAL, rd_seed=7, view=v, view_seed=5, init_mode=1, init_t0=8, init_seed=11,
+                        drop_pct=drop, drop_from=5, drop_to=30, drop_seed=42, shard_rank=g, shard_count=world)
+              for g in range(world)]
+    lay = [s.shard_layout() for s in shards]
+    assert lay[0][0] == 0 and sum(w for _, w in lay) == n
+    crash = crash_set(n, max(1, n // 50), 42)
+    assert b"".join(s.dump_tables() for s in shards) == ora.dump(), "initial views differ"
+    for _ in range(36):
+        t = shards[0].time
+        ora.tick()
+        partial_loopback_tick(shards)
+        if t == 12:
+            for s in shards:
+                s.set_failed(crash)
+        ev = sorted((e[0], e[1], 1 if e[2] == GM_EV_JOINED else 2, e[3]) for s in shards for e in s.drain_events())
+        assert ev == sorted(ora.events()), f"events differ at tick {t}"
+        assert b"".join(s.dump_tables() for s in shards) == ora.dump(), f"views differ at tick {t}"
+    for s in shards:
+        assert s.tick_stats()["err"] == 0
+
+
+def test_rccl_single_rank_row_shard_matches_oracle(monkeypatch):
+    """The RCCL exchange of the row-shard tick (ncclAllToAll of record counts, two
+    ncclAllToAllv) forced on with one rank: the multi-GPU call sequence on this box's
+    one GPU (every target is local, so the exchanged counts are zero)."""
+    from membership.abi import comm_unique_id
+    n, v = 2000, 32
+    kw = dict(rd_seed=7, view_seed=5, init_t0=8, init_seed=11)
+    ora = oracle_py.PartialOracle(n, v=v, crash_tick=12, crash_count=40, crash_seed=42, drop_pct=5, drop_from=0,
+                                  drop_to=100, drop_seed=42, **kw)
+    monkeypatch.setenv("GM_FORCE_SHARD", "1")
+    sim = Simulator(n, GM_MODE_PARTIAL, rd_seed=7, view=v, view_seed=5, init_mode=1, init_t0=8, init_seed=11,
+                    drop_pct=5, drop_from=0, drop_to=100, drop_seed=42, shard_rank=0, shard_count=1)
+    monkeypatch.delenv("GM_FORCE_SHARD")
+    sim.comm_init(comm_unique_id(), 1, 0)
+    crash = crash_set(n, 40, 42)
+    for _ in range(24):
+        t = sim.time
+        ora.tick()
+        sim.tick()
+        if t == 12:
+            sim.set_failed(crash)
+        ev = [(e[0], e[1], 1 if e[2] == GM_EV_JOINED else 2, e[3]) for e in sim.drain_events()]
+        assert ev == ora.events(), f"events differ at tick {t}"
+        assert sim.dump_tables() == ora.dump(), f"views differ at tick {t}"
+    assert sim.tick_stats()["err"] == 0
