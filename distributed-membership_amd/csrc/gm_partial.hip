@@ -247,14 +247,12 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const uint32_t *m
     uint32_t alive = 0, rown = 0;
     int rcount = 0;
 #pragma unroll
-    for (int u = 0; u < TS; u++) {
-      if (!(w[u] & P_IDMASK)) continue;
-      if (p_age(t, hh[u]) >= GM_TREMOVE) {
-        rcount++;
-        if (w[u] & P_OWN) rown |= 1u << u;
-      } else {
-        alive |= 1u << u;
-      }
+    for (int u = 0; u < TS; u++) {  // branch-free: exec-mask traffic is what this kernel spends SALU on
+      const uint32_t valid = (w[u] & P_IDMASK) != 0;
+      const uint32_t rem = valid & (uint32_t)(p_age(t, hh[u]) >= GM_TREMOVE);
+      rcount += (int)rem;
+      rown |= (rem & (w[u] >> 31)) << u;
+      alive |= (valid & ~rem) << u;
     }
     int tot;
     (void)p_excl<TS == 8 ? 4 : 5>(rcount, &removed);
@@ -267,22 +265,26 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const uint32_t *m
     }
     int pos = p_excl<TS == 8 ? 4 : 5>(__builtin_popcount(alive), &tot);
     m = tot;
+    // every slot is stored: dead ones to a per-lane slot of [H-64, H), past the dense
+    // range (m <= (1+KK)V+1 < H-64) and free of bank conflicts
 #pragma unroll
-    for (int u = 0; u < TS; u++)
-      if ((alive >> u) & 1) {
-        tid[pos] = w[u];
-        thb[pos] = hh[u];
-        pos++;
-      }
+    for (int u = 0; u < TS; u++) {
+      const bool a = (alive >> u) & 1;
+      const int at = a ? pos : H - 64 + lane;
+      tid[at] = w[u];
+      thb[at] = hh[u];
+      pos += a;
+    }
   }
   p_wsync();
   // ---- 4. dense entries e = s*64 + lane; eviction to V
   uint32_t dw[DS], dh[DS];
 #pragma unroll
-  for (int q = 0; q < DS; q++) {
+  for (int q = 0; q < DS; q++) {  // DS*64 < H: the reads stay inside the table
     const int e = q * 64 + lane;
-    dw[q] = e < m ? tid[e] : 0u;
-    dh[q] = e < m ? thb[e] : 0u;
+    const uint32_t a = tid[e], b = thb[e];
+    dw[q] = e < m ? a : 0u;
+    dh[q] = e < m ? b : 0u;
   }
   uint32_t keep = 0;
   if (m <= V) {
@@ -296,8 +298,8 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const uint32_t *m
     hist[lane] = 0;
     p_wsync();
 #pragma unroll
-    for (int q = 0; q < DS; q++)
-      if (dw[q] && !(dw[q] & P_SELF)) atomicAdd(&hist[min(max(top - (int)dh[q], 0), 63)], 1u);
+    for (int q = 0; q < DS; q++)  // entries that do not count go to a private trash word
+      atomicAdd((dw[q] && !(dw[q] & P_SELF)) ? &hist[min(max(top - (int)dh[q], 0), 63)] : &tid[H - 64 + lane], 1u);
     p_wsync();
     const int need = V - 1;  // self is always kept
     int c = (int)hist[lane];
@@ -310,10 +312,10 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const uint32_t *m
     uint32_t bucket = 0;
 #pragma unroll
     for (int q = 0; q < DS; q++) {
-      if (!dw[q]) continue;
       const int d = min(max(top - (int)dh[q], 0), 63);
-      if ((dw[q] & P_SELF) || d < dcut) keep |= 1u << q;
-      else if (d == dcut) bucket |= 1u << q;
+      const uint32_t v = dw[q] != 0;
+      keep |= (v & (uint32_t)(((dw[q] & P_SELF) != 0) | (d < dcut))) << q;
+      bucket |= (v & (uint32_t)(!(dw[q] & P_SELF) && d == dcut)) << q;
     }
     if (needb == bsz) {
       keep |= bucket;
@@ -323,13 +325,15 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const uint32_t *m
       const uint64_t kseed = gm_mix64(s.view_seed ^ (uint64_t)(uint32_t)t);
       uint64_t key[DS];
 #pragma unroll
-      for (int q = 0; q < DS; q++) key[q] = ((bucket >> q) & 1) ? p_evict_key(kseed, i, dw[q] & P_IDMASK) : ~0ull;
+      for (int q = 0; q < DS; q++) {
+        key[q] = ~0ull;
+        if (__ballot((bucket >> q) & 1)) key[q] = ((bucket >> q) & 1) ? p_evict_key(kseed, i, dw[q] & P_IDMASK) : ~0ull;
+      }
       p_wsync();
       hist[lane] = 0;
       p_wsync();
 #pragma unroll
-      for (int q = 0; q < DS; q++)
-        if ((bucket >> q) & 1) atomicAdd(&hist[key[q] >> 58], 1u);
+      for (int q = 0; q < DS; q++) atomicAdd(((bucket >> q) & 1) ? &hist[key[q] >> 58] : &tid[H - 64 + lane], 1u);
       p_wsync();
       c = (int)hist[lane];
       inc = p_scan(c, lane);
@@ -341,10 +345,10 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const uint32_t *m
       uint32_t cand = 0;
 #pragma unroll
       for (int q = 0; q < DS; q++) {
-        if (!((bucket >> q) & 1)) continue;
+        const uint32_t b = (bucket >> q) & 1;
         const int bin = (int)(key[q] >> 58);
-        if (bin < bcut) keep |= 1u << q;
-        else if (bin == bcut) cand |= 1u << q;
+        keep |= (b & (uint32_t)(bin < bcut)) << q;
+        cand |= (b & (uint32_t)(bin == bcut)) << q;
       }
       if (needc == bsz2) {
         keep |= cand;
@@ -371,22 +375,28 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const uint32_t *m
   }
   // ---- 5. compact the kept entries (<= V), rank them by id
   int cnt = 0;
+  p_wsync();  // the eviction histogram is dead: it takes the stores of the entries not kept
 #pragma unroll
   for (int q = 0; q < DS; q++) {
-    const uint64_t bal = __ballot((keep >> q) & 1);
-    if ((keep >> q) & 1) {
-      const int p = cnt + p_below(bal);
-      kid[p] = dw[q];
-      khb[p] = dh[q];
-    }
+    const bool kq = (keep >> q) & 1;
+    const uint64_t bal = __ballot(kq);
+    const int p = cnt + p_below(bal);
+    *(kq ? kid + p : hist + lane) = dw[q];
+    *(kq ? khb + p : hist + lane) = dh[q];
     cnt += __builtin_popcountll(bal);
   }
+  if (lane >= cnt && lane < P_VMAX) kid[lane] = P_IDMASK;  // sentinel ids rank after every real one
   p_wsync();
   {
     const uint32_t mw = lane < cnt ? kid[lane] : 0u, mh = lane < cnt ? khb[lane] : 0u;
     const uint32_t myid = mw & P_IDMASK;
     int rank = 0;
-    for (int q = 0; q < cnt; q++) rank += (kid[q] & P_IDMASK) < myid;
+#pragma unroll
+    for (int q = 0; q < P_VMAX / 4; q++) {  // broadcast reads, 4 ids each
+      const uint4 v = ((const uint4 *)kid)[q];
+      rank += ((v.x & P_IDMASK) < myid) + ((v.y & P_IDMASK) < myid) + ((v.z & P_IDMASK) < myid) +
+              ((v.w & P_IDMASK) < myid);
+    }
     p_wsync();
     if (lane < cnt) {
       fin[rank] = ((uint64_t)myid << 32) | mh;
