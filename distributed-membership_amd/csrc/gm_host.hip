@@ -30,7 +30,9 @@ hipError_t gm_launch_init(const SState &s, int warm, int t0, uint64_t seed, hipS
 hipError_t gm_launch_partial_tick(const PState &s, int t, uint32_t *mtraw, hipStream_t st, hipEvent_t k0,
                                   hipEvent_t k1);
 hipError_t gm_launch_partial_init(const PState &s, int t0, uint64_t init_seed, hipStream_t st);
-hipError_t gm_launch_partial_unpack(const PState &s, int t, int nrecv, hipStream_t st);
+hipError_t gm_launch_partial_unpack(const PState &s, int t, int base, int nrecv, hipStream_t st);
+hipError_t gm_launch_partial_mtgen(const PState &s, int t, uint32_t *mtraw, hipStream_t st);
+hipError_t gm_launch_partial_chunk(const PState &s, int t, const uint32_t *mtraw, int c, hipStream_t st);
 size_t gm_partial_lds_bytes();
 
 #define GM_T_LIMIT 32766  // packed 16-bit hb/ts stay exact: hb <= 2t+1 < 0xFFFF
@@ -65,6 +67,9 @@ struct gm_ctx {
   uint32_t *p_mtraw = nullptr;
   int64_t p_recv_last = 0;  // lists received from other row shards in the last tick
   bool p_sharded = false;   // row-shard exchange each tick (G > 1, or one rank forced by GM_FORCE_SHARD=1)
+  hipStream_t p_comm = nullptr;        // row shards: RCCL exchange stream (overlaps the next chunk's kernels)
+  std::vector<hipEvent_t> p_chev;      // per chunk: its node ticks are done (compute stream)
+  hipEvent_t p_done = nullptr;         // the tick's exchange + unpacks are done (comm stream)
 };
 
 static thread_local char g_errbuf[256];
@@ -339,16 +344,23 @@ static int create_partial(gm_ctx *c) {
   TRY(dalloc(c, &p.rowstat, (size_t)nl * 4));
   TRY(dalloc(c, &p.targets, (size_t)nl * GM_FANOUT));
   TRY(dalloc(c, &p.big, nl));
-  TRY(dalloc(c, &p.big_cnt, 1));
   TRY(dalloc(c, &p.err, 1));
   TRY(dalloc(c, &c->p_mtraw, (size_t)nl * 16));
   c->p_sharded = G > 1 || (getenv("GM_FORCE_SHARD") && atoi(getenv("GM_FORCE_SHARD")) == 1);
+  // row shards pipeline their exchange over K chunks of their nodes (GM_CHUNKS, default 4)
+  p.nchunk = c->p_sharded ? (getenv("GM_CHUNKS") ? atoi(getenv("GM_CHUNKS")) : 4) : 1;
+  if (p.nchunk < 1 || p.nchunk > 64) return GM_EINVAL;
+  TRY(dalloc(c, &p.big_cnt, p.nchunk));
   if (c->p_sharded) {
-    TRY(dalloc(c, &p.send_cnt, G));
+    HIPCHECK(hipStreamCreateWithFlags(&c->p_comm, hipStreamNonBlocking));
+    c->p_chev.assign(p.nchunk, nullptr);
+    for (hipEvent_t &e : c->p_chev) HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIPCHECK(hipEventCreateWithFlags(&c->p_done, hipEventDisableTiming));
+    TRY(dalloc(c, &p.send_cnt, (size_t)p.nchunk * G));
     TRY(dalloc(c, &p.send_hdr, (size_t)G * nl * 8));
     TRY(dalloc(c, &p.send_list, (size_t)G * nl * p.V));
     TRY(dalloc(c, &p.recv_hdr, (size_t)std::max(R, 1) * 8));
-    TRY(dalloc(c, &p.recv_cnt, G));
+    TRY(dalloc(c, &p.recv_cnt, (size_t)p.nchunk * G));
   }
   HIPCHECK(hipMemset(p.lists, 0, sizeof(uint64_t) * 2 * p.rows * p.V));
   HIPCHECK(hipMemset(p.failed, 0, sizeof(int32_t) * nl));
@@ -398,6 +410,9 @@ extern "C" int gm_destroy(gm_ctx *c) {
   for (hipEvent_t e : {c->e0, c->e1, c->k0, c->k1})
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : c->tev) (void)hipEventDestroy(e);
+  for (hipEvent_t e : c->p_chev) (void)hipEventDestroy(e);
+  if (c->p_done) (void)hipEventDestroy(c->p_done);
+  if (c->p_comm) (void)hipStreamDestroy(c->p_comm);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return GM_OK;
@@ -474,7 +489,7 @@ static int tick_scaled(gm_ctx *c) {
   return GM_OK;
 }
 
-static int partial_exchange_rccl(gm_ctx *c);
+static int partial_exchange_chunk(gm_ctx *c, int q, int64_t *roff);
 
 static int tick_partial(gm_ctx *c) {
   if (c->t > GM_T_LIMIT) return GM_ERANGE;
@@ -495,8 +510,27 @@ static int tick_partial(gm_ctx *c) {
     k1 = c->tev[2 * c->ktimed + 1];
     c->ktimed++;
   }
-  HIPCHECK(gm_launch_partial_tick(st, c->t, c->p_mtraw, c->stream, k0, k1));
-  if (c->p_sharded) TRY(partial_exchange_rccl(c));
+  if (!c->p_sharded) {
+    HIPCHECK(gm_launch_partial_tick(st, c->t, c->p_mtraw, c->stream, k0, k1));
+  } else {
+    // chunk pipeline: every chunk's node ticks queue on the compute stream; the exchange of
+    // chunk q runs on the comm stream once q's kernels are done, while q+1.. still compute
+    HIPCHECK(gm_launch_partial_mtgen(st, c->t, c->p_mtraw, c->stream));
+    if (k0) HIPCHECK(hipEventRecord(k0, c->stream));
+    for (int q = 0; q < st.nchunk; q++) {
+      HIPCHECK(gm_launch_partial_chunk(st, c->t, c->p_mtraw, q, c->stream));
+      HIPCHECK(hipEventRecord(c->p_chev[q], c->stream));
+    }
+    if (k1) HIPCHECK(hipEventRecord(k1, c->stream));
+    int64_t roff = 0;
+    for (int q = 0; q < st.nchunk; q++) {
+      HIPCHECK(hipStreamWaitEvent(c->p_comm, c->p_chev[q], 0));
+      TRY(partial_exchange_chunk(c, q, &roff));
+    }
+    c->p_recv_last = roff;
+    HIPCHECK(hipEventRecord(c->p_done, c->p_comm));
+    HIPCHECK(hipStreamWaitEvent(c->stream, c->p_done, 0));  // the next tick reads the unpacked inboxes
+  }
   if (c->timing) {
     HIPCHECK(hipEventRecord(c->e1, c->stream));
     c->timed_ticks++;
@@ -1060,22 +1094,24 @@ static int tick_sharded(gm_ctx *c) {
 // then all-to-allv of the headers and of the lists, which land directly in rows
 // nloc.. of parity t&1 (where tick t+1 reads its senders' lists); gm_p_unpack
 // appends each received row to its targets' inboxes.
-static int partial_exchange_rccl(gm_ctx *c) {
+static int partial_exchange_chunk(gm_ctx *c, int ch, int64_t *roff) {
   PState &p = c->p;
   const int G = p.G, V = p.V, nl = p.nloc;
-  NCCLCHECK(ncclAllToAll(p.send_cnt, p.recv_cnt, 1, ncclInt32, c->comm, c->stream));
+  const int r0 = (int)((int64_t)nl * ch / p.nchunk), r1 = (int)((int64_t)nl * (ch + 1) / p.nchunk);
+  hipStream_t cs = c->p_comm;
+  NCCLCHECK(ncclAllToAll(p.send_cnt + (size_t)ch * G, p.recv_cnt + (size_t)ch * G, 1, ncclInt32, c->comm, cs));
   std::vector<int32_t> sc(G), rc(G);
-  HIPCHECK(hipMemcpyAsync(sc.data(), p.send_cnt, sizeof(int32_t) * G, hipMemcpyDeviceToHost, c->stream));
-  HIPCHECK(hipMemcpyAsync(rc.data(), p.recv_cnt, sizeof(int32_t) * G, hipMemcpyDeviceToHost, c->stream));
-  HIPCHECK(hipStreamSynchronize(c->stream));
+  HIPCHECK(hipMemcpyAsync(sc.data(), p.send_cnt + (size_t)ch * G, sizeof(int32_t) * G, hipMemcpyDeviceToHost, cs));
+  HIPCHECK(hipMemcpyAsync(rc.data(), p.recv_cnt + (size_t)ch * G, sizeof(int32_t) * G, hipMemcpyDeviceToHost, cs));
+  HIPCHECK(hipStreamSynchronize(cs));  // the compute stream keeps running the next chunks meanwhile
   std::vector<size_t> hs(G), hsd(G), hr(G), hrd(G), ls(G), lsd(G), lr(G), lrd(G);
-  size_t off = 0;
+  size_t off = (size_t)*roff;
   for (int q = 0; q < G; q++) {
-    if (sc[q] < 0 || sc[q] > nl || rc[q] < 0) return GM_ESTATE;
+    if (sc[q] < 0 || sc[q] > r1 - r0 || rc[q] < 0) return GM_ESTATE;
     hs[q] = (size_t)sc[q] * 8;
-    hsd[q] = (size_t)q * nl * 8;
+    hsd[q] = ((size_t)q * nl + r0) * 8;
     ls[q] = (size_t)sc[q] * V;
-    lsd[q] = (size_t)q * nl * V;
+    lsd[q] = ((size_t)q * nl + r0) * V;
     hr[q] = (size_t)rc[q] * 8;
     hrd[q] = off * 8;
     lr[q] = (size_t)rc[q] * V;
@@ -1085,16 +1121,15 @@ static int partial_exchange_rccl(gm_ctx *c) {
   if (off > (size_t)(p.n - nl)) return GM_ESTATE;
   uint64_t *rows_in = p.lists + ((size_t)(c->t & 1) * p.rows + nl) * V;
   NCCLCHECK(ncclAllToAllv(p.send_hdr, hs.data(), hsd.data(), p.recv_hdr, hr.data(), hrd.data(), ncclInt32, c->comm,
-                          c->stream));
-  NCCLCHECK(ncclAllToAllv(p.send_list, ls.data(), lsd.data(), rows_in, lr.data(), lrd.data(), ncclUint64, c->comm,
-                          c->stream));
-  HIPCHECK(gm_launch_partial_unpack(p, c->t, (int)off, c->stream));
-  c->p_recv_last = (int64_t)off;
+                          cs));
+  NCCLCHECK(ncclAllToAllv(p.send_list, ls.data(), lsd.data(), rows_in, lr.data(), lrd.data(), ncclUint64, c->comm, cs));
+  HIPCHECK(gm_launch_partial_unpack(p, c->t, (int)*roff, (int)(off - (size_t)*roff), cs));
+  *roff = (int64_t)off;
   return GM_OK;
 }
 
 // One PARTIAL tick of G row-shard contexts living on one device (tests): the local
-// kernels of every shard, the same exchange as partial_exchange_rccl by device copies,
+// kernels of every shard, the exchange partial_exchange_chunk does by device copies (same layout),
 // the unpack, and the globaltime advance gm_tick does.
 extern "C" int gm_partial_loopback_tick(gm_ctx **ctxs, int32_t G) {
   if (!ctxs || G < 2) return GM_EINVAL;
@@ -1113,32 +1148,38 @@ extern "C" int gm_partial_loopback_tick(gm_ctx **ctxs, int32_t G) {
     st.drop_pct = drop ? c->cfg.drop_pct : -1;
     HIPCHECK(gm_launch_partial_tick(st, c->t, c->p_mtraw, c->stream, nullptr, nullptr));
   }
-  std::vector<std::vector<int32_t>> sc(G, std::vector<int32_t>(G));
+  const int K = ctxs[0]->p.nchunk;
+  std::vector<std::vector<int32_t>> sc(G, std::vector<int32_t>((size_t)K * G));
   for (int g = 0; g < G; g++) {
-    HIPCHECK(hipMemcpyAsync(sc[g].data(), ctxs[g]->p.send_cnt, sizeof(int32_t) * G, hipMemcpyDeviceToHost,
+    if (ctxs[g]->p.nchunk != K) return GM_EINVAL;
+    HIPCHECK(hipMemcpyAsync(sc[g].data(), ctxs[g]->p.send_cnt, sizeof(int32_t) * K * G, hipMemcpyDeviceToHost,
                             ctxs[g]->stream));
     HIPCHECK(hipStreamSynchronize(ctxs[g]->stream));
   }
+  // the layout partial_exchange_chunk gives: per chunk, per source shard ascending
   const int V = ctxs[0]->p.V;
-  for (int q = 0; q < G; q++) {
-    PState &dq = ctxs[q]->p;
-    hipStream_t st = ctxs[q]->stream;
-    size_t off = 0;
-    for (int g = 0; g < G; g++) {
-      const PState &sg = ctxs[g]->p;
-      const size_t cnt = (size_t)sc[g][q];
-      if (g == q || !cnt) continue;
-      if (cnt > (size_t)sg.nloc || off + cnt > (size_t)(dq.n - dq.nloc)) return GM_ESTATE;
-      HIPCHECK(hipMemcpyAsync(dq.recv_hdr + off * 8, sg.send_hdr + (size_t)q * sg.nloc * 8, sizeof(int32_t) * 8 * cnt,
-                              hipMemcpyDeviceToDevice, st));
-      HIPCHECK(hipMemcpyAsync(dq.lists + ((size_t)(ctxs[q]->t & 1) * dq.rows + dq.nloc + off) * V,
-                              sg.send_list + (size_t)q * sg.nloc * V, sizeof(uint64_t) * V * cnt,
-                              hipMemcpyDeviceToDevice, st));
-      off += cnt;
+  std::vector<size_t> roff(G, 0);
+  for (int ch = 0; ch < K; ch++)
+    for (int q = 0; q < G; q++) {
+      PState &dq = ctxs[q]->p;
+      hipStream_t st = ctxs[q]->stream;
+      const size_t base = roff[q];
+      for (int g = 0; g < G; g++) {
+        const PState &sg = ctxs[g]->p;
+        const size_t cnt = (size_t)sc[g][(size_t)ch * G + q];
+        const size_t r0 = (size_t)((int64_t)sg.nloc * ch / K);
+        if (g == q || !cnt) continue;
+        if (cnt > (size_t)sg.nloc || roff[q] + cnt > (size_t)(dq.n - dq.nloc)) return GM_ESTATE;
+        HIPCHECK(hipMemcpyAsync(dq.recv_hdr + roff[q] * 8, sg.send_hdr + ((size_t)q * sg.nloc + r0) * 8,
+                                sizeof(int32_t) * 8 * cnt, hipMemcpyDeviceToDevice, st));
+        HIPCHECK(hipMemcpyAsync(dq.lists + ((size_t)(ctxs[q]->t & 1) * dq.rows + dq.nloc + roff[q]) * V,
+                                sg.send_list + ((size_t)q * sg.nloc + r0) * V, sizeof(uint64_t) * V * cnt,
+                                hipMemcpyDeviceToDevice, st));
+        roff[q] += cnt;
+      }
+      HIPCHECK(gm_launch_partial_unpack(dq, ctxs[q]->t, (int)base, (int)(roff[q] - base), st));
     }
-    HIPCHECK(gm_launch_partial_unpack(dq, ctxs[q]->t, (int)off, st));
-    ctxs[q]->p_recv_last = (int64_t)off;
-  }
+  for (int q = 0; q < G; q++) ctxs[q]->p_recv_last = (int64_t)roff[q];
   for (int g = 0; g < G; g++) {
     HIPCHECK(hipStreamSynchronize(ctxs[g]->stream));
     TRY(check_err(ctxs[g]));

@@ -18,6 +18,7 @@ struct PState {
   // Single context: n0 = 0, nloc = n, G = 1.
   int n0, nloc, G, rank;
   int rows;              // list rows per parity: nloc own rows + (n - nloc) rows of received remote lists
+  int nchunk;            // K: the node ticks run in K row chunks; a shard ships chunk c's records while c+1 runs
   int drop_pct;          // per-entry drop percentage for this tick's deliveries (-1: none)
   uint64_t rd_seed, view_seed, drop_seed;
   uint64_t *lists;       // [2][rows][V] entries (id << 32 | hb), 0 = empty, sorted by id; parity t&1 written at tick t
@@ -30,13 +31,14 @@ struct PState {
   int32_t *ev_cnt;       // [nloc] joins | removals << 16
   int32_t *rowstat;      // [nloc][4]: lists merged, view size, numfailed, targets chosen
   int32_t *targets;      // [nloc][GM_FANOUT] (global node indices)
-  int32_t *big;          // [nloc] worklist of nodes with > P_KSMALL lists (big-table kernel)
-  int32_t *big_cnt;      // [1]
+  int32_t *big;          // [nloc] worklists of nodes with > P_KSMALL lists (big-table kernel), chunk c at rows r0_c..
+  int32_t *big_cnt;      // [K]
   // outgoing lists to the other row shards (sharded only): one record per (sender, remote rank)
-  int32_t *send_cnt;     // [G]
-  int32_t *send_hdr;     // [G][nloc][8]: sender global index, #targets on that rank, targets (global), 0
+  int32_t *send_cnt;     // [K][G] records of chunk c addressed to shard q
+  int32_t *send_hdr;     // [G][nloc][8]: sender global index, #targets on that rank, targets (global), 0;
+                         //   chunk c's records to q from slot q*nloc + r0_c on
   uint64_t *send_list;   // [G][nloc][V]: the sender's final list of the tick
   int32_t *recv_hdr;     // [n - nloc][8] received headers (their lists land in rows nloc.. of the tick's parity)
-  int32_t *recv_cnt;     // [G] records received from each shard this tick
+  int32_t *recv_cnt;     // [K][G] records received from each shard, per chunk
   uint32_t *err;
 };

@@ -33,6 +33,8 @@
 // kernel (1024-slot table, sender sort for > P_KP lists) drains.
 // Lists are double-buffered by tick parity: a receiver reads its senders' lists
 // of tick t-1 directly, so no separate payload copy is written.
+#include <algorithm>
+
 #include "gm_device.h"
 #include "gm_partial.h"
 
@@ -125,7 +127,7 @@ __device__ __forceinline__ int p_owner(const PState &s, int d) {
 // k: lists queued for it this tick.
 template <int H, bool BIG>
 __device__ __forceinline__ void p_node(const PState &s, int t, const uint32_t *mtraw, int li, int k, int lane,
-                                       unsigned char *base) {
+                                       unsigned char *base, int chunk, int r0) {
   const int i = s.n0 + li;  // global node index (ids, keys, seeds, targets)
   constexpr int TS = H / 64;                          // table slots per lane
   constexpr int KK = BIG ? P_KP : P_KSMALL;           // lists merged at most
@@ -480,12 +482,13 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const uint32_t *m
     for (int q = 0; q < GM_FANOUT - 1; q++)
       if (q < lane && __builtin_amdgcn_readlane(owner, q) == owner) first = false;
     uint64_t fm = __ballot(first);
-    const int slot = first ? atomicAdd(&s.send_cnt[owner], 1) : 0;
+    // chunk c's records to shard q: slots [q*nloc + r0_c, ...) (at most one per sender of the chunk)
+    const int slot = first ? atomicAdd(&s.send_cnt[chunk * s.G + owner], 1) : 0;
     while (fm) {
       const int fl = __builtin_ctzll(fm);
       fm &= fm - 1;
       const int rr = __builtin_amdgcn_readlane(owner, fl);
-      const size_t rec = (size_t)rr * s.nloc + (size_t)__builtin_amdgcn_readlane(slot, fl);
+      const size_t rec = (size_t)rr * s.nloc + r0 + (size_t)__builtin_amdgcn_readlane(slot, fl);
       uint64_t tm = __ballot(lane < ng && owner == rr);
       const int nt = __builtin_popcountll(tm);
       int tv0 = -1, tv1 = -1, tv2 = -1, tv3 = -1, tv4 = -1;
@@ -519,32 +522,34 @@ __device__ __forceinline__ void p_frozen(const PState &s, int t, int li, int lan
   }
 }
 
-__global__ __launch_bounds__(256) void gm_p_tick_small(PState s, int t, const uint32_t *mtraw) {
+// rows [r0, r1) = chunk `chunk` of this shard's nodes
+__global__ __launch_bounds__(256) void gm_p_tick_small(PState s, int t, const uint32_t *mtraw, int chunk, int r0,
+                                                       int r1) {
   extern __shared__ __align__(16) unsigned char p_smem[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int li = blockIdx.x * 4 + wave;
-  if (li >= s.nloc) return;  // whole wave; no workgroup barrier in this kernel
+  const int li = r0 + blockIdx.x * 4 + wave;
+  if (li >= r1) return;  // whole wave; no workgroup barrier in this kernel
   if (s.failed[li]) {
     p_frozen(s, t, li, lane);
     return;
   }
   const int k = s.inbox_cnt[t & 1][li];
   if (k > P_KSMALL) {  // deferred to gm_p_tick_big
-    if (lane == 0) s.big[atomicAdd(s.big_cnt, 1)] = li;
+    if (lane == 0) s.big[r0 + atomicAdd(&s.big_cnt[chunk], 1)] = li;
     return;
   }
-  p_node<P_HS, false>(s, t, mtraw, li, k, lane, p_smem + (size_t)wave * PLds<P_HS>::bytes);
+  p_node<P_HS, false>(s, t, mtraw, li, k, lane, p_smem + (size_t)wave * PLds<P_HS>::bytes, chunk, r0);
 }
 
 // drains the worklist gm_p_tick_small filled (a fixed grid; every wave exits when the list is done)
-__global__ __launch_bounds__(256) void gm_p_tick_big(PState s, int t, const uint32_t *mtraw) {
+__global__ __launch_bounds__(256) void gm_p_tick_big(PState s, int t, const uint32_t *mtraw, int chunk, int r0) {
   extern __shared__ __align__(16) unsigned char p_smem[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int nbig = *s.big_cnt;
+  const int nbig = s.big_cnt[chunk];
   for (int w = blockIdx.x * 4 + wave; w < nbig; w += gridDim.x * 4) {
-    const int li = s.big[w];
+    const int li = s.big[r0 + w];
     const int k = s.inbox_cnt[t & 1][li];
-    p_node<P_HB, true>(s, t, mtraw, li, k, lane, p_smem + (size_t)wave * PLds<P_HB>::bytes);
+    p_node<P_HB, true>(s, t, mtraw, li, k, lane, p_smem + (size_t)wave * PLds<P_HB>::bytes, chunk, r0);
   }
 }
 
@@ -552,8 +557,8 @@ __global__ __launch_bounds__(256) void gm_p_tick_big(PState s, int t, const uint
 // worklist and the outgoing record counts
 __global__ __launch_bounds__(256) void gm_p_mtgen(PState s, int t, uint32_t *mtraw) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r == 0) *s.big_cnt = 0;
-  if (s.send_cnt && r < s.G) s.send_cnt[r] = 0;
+  if (r < s.nchunk) s.big_cnt[r] = 0;
+  if (s.send_cnt && r < s.nchunk * s.G) s.send_cnt[r] = 0;
   if (r >= s.nloc) return;
   uint32_t out[16];
   gm_mt_first16(gm_rd_seed(s.rd_seed, t, s.n0 + r + 1), out);
@@ -594,9 +599,9 @@ __global__ __launch_bounds__(64) void gm_p_init(PState s, int t0, uint64_t init_
 
 // received records of tick t (row shards): remote lists already sit in rows nloc + j of
 // parity t&1; record each row's sender and append the row to its local targets' inboxes
-__global__ __launch_bounds__(256) void gm_p_unpack(PState s, int t, int nrecv) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= nrecv) return;
+__global__ __launch_bounds__(256) void gm_p_unpack(PState s, int t, int base, int nrecv) {
+  const int j = base + blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= base + nrecv) return;
   const int par = t & 1;
   const int4 h0 = ((const int4 *)s.recv_hdr)[2 * (size_t)j];
   const int4 h1 = ((const int4 *)s.recv_hdr)[2 * (size_t)j + 1];
@@ -616,16 +621,30 @@ __global__ __launch_bounds__(256) void gm_p_unpack(PState s, int t, int nrecv) {
 
 #define P_BIG_GRID 1024
 
+// S2 precompute for every row + reset of the per-chunk worklists and record counts
+hipError_t gm_launch_partial_mtgen(const PState &s, int t, uint32_t *mtraw, hipStream_t st) {
+  hipLaunchKernelGGL(gm_p_mtgen, dim3((std::max(s.nloc, s.nchunk * s.G) + 255) / 256), dim3(256), 0, st, s, t, mtraw);
+  return hipGetLastError();
+}
+
+// the node ticks of chunk c (rows [nloc*c/K, nloc*(c+1)/K))
+hipError_t gm_launch_partial_chunk(const PState &s, int t, const uint32_t *mtraw, int c, hipStream_t st) {
+  const int r0 = (int)((int64_t)s.nloc * c / s.nchunk), r1 = (int)((int64_t)s.nloc * (c + 1) / s.nchunk);
+  if (r1 > r0)
+    hipLaunchKernelGGL(gm_p_tick_small, dim3((r1 - r0 + 3) / 4), dim3(256), 4 * PLds<P_HS>::bytes, st, s, t, mtraw, c,
+                       r0, r1);
+  hipLaunchKernelGGL(gm_p_tick_big, dim3(P_BIG_GRID), dim3(256), 4 * PLds<P_HB>::bytes, st, s, t, mtraw, c, r0);
+  return hipGetLastError();
+}
+
 hipError_t gm_launch_partial_tick(const PState &s, int t, uint32_t *mtraw, hipStream_t st, hipEvent_t k0,
                                   hipEvent_t k1) {
-  hipLaunchKernelGGL(gm_p_mtgen, dim3((s.nloc + 255) / 256), dim3(256), 0, st, s, t, mtraw);
+  hipError_t e = gm_launch_partial_mtgen(s, t, mtraw, st);
+  if (e != hipSuccess) return e;
   if (k0) (void)hipEventRecord(k0, st);
-  hipLaunchKernelGGL(gm_p_tick_small, dim3((s.nloc + 3) / 4), dim3(256), 4 * PLds<P_HS>::bytes, st, s, t,
-                     (const uint32_t *)mtraw);
-  hipLaunchKernelGGL(gm_p_tick_big, dim3(P_BIG_GRID), dim3(256), 4 * PLds<P_HB>::bytes, st, s, t,
-                     (const uint32_t *)mtraw);
+  for (int c = 0; c < s.nchunk && e == hipSuccess; c++) e = gm_launch_partial_chunk(s, t, mtraw, c, st);
   if (k1) (void)hipEventRecord(k1, st);
-  return hipGetLastError();
+  return e != hipSuccess ? e : hipGetLastError();
 }
 
 hipError_t gm_launch_partial_init(const PState &s, int t0, uint64_t init_seed, hipStream_t st) {
@@ -633,8 +652,8 @@ hipError_t gm_launch_partial_init(const PState &s, int t0, uint64_t init_seed, h
   return hipGetLastError();
 }
 
-hipError_t gm_launch_partial_unpack(const PState &s, int t, int nrecv, hipStream_t st) {
-  if (nrecv > 0) hipLaunchKernelGGL(gm_p_unpack, dim3((nrecv + 255) / 256), dim3(256), 0, st, s, t, nrecv);
+hipError_t gm_launch_partial_unpack(const PState &s, int t, int base, int nrecv, hipStream_t st) {
+  if (nrecv > 0) hipLaunchKernelGGL(gm_p_unpack, dim3((nrecv + 255) / 256), dim3(256), 0, st, s, t, base, nrecv);
   return hipGetLastError();
 }
 

@@ -76,12 +76,15 @@ def test_partial_large_cluster_matches_oracle():
     assert st["err"] == 0 and st["max_inbox"] == 16, st
 
 
-@pytest.mark.parametrize("n,v,world,drop", [(300, 16, 2, 0), (1000, 32, 3, 30), (4099, 32, 4, 5)])
-def test_row_shards_match_oracle(n, v, world, drop):
+@pytest.mark.parametrize("n,v,world,drop,chunks", [(300, 16, 2, 0, 4), (1000, 32, 3, 30, 1), (4099, 32, 4, 5, 4),
+                                                   (2500, 32, 2, 5, 7)])
+def test_row_shards_match_oracle(n, v, world, drop, chunks, monkeypatch):
     """S-C multi-GPU protocol on one device: G row-shard contexts exchange their
-    outgoing (header, list) records through device copies laid out exactly as the
-    RCCL all-to-allv lays them out, and must reproduce the oracle tick for tick."""
+    outgoing (header, list) records -- chunk by chunk of their nodes, as the RCCL path
+    pipelines them -- through device copies laid out exactly as the all-to-allv lays
+    them out, and must reproduce the oracle tick for tick."""
     from membership.abi import partial_loopback_tick
+    monkeypatch.setenv("GM_CHUNKS", str(chunks))
     kw = dict(rd_seed=7, view_seed=5, init_t0=8, init_seed=11)
     ora = oracle_py.PartialOracle(n, v=v, crash_tick=12, crash_count=max(1, n // 50), crash_seed=42, drop_pct=drop,
                                   drop_from=5, drop_to=30, drop_seed=42, **kw)

@@ -3,7 +3,7 @@
 Pins the CPU restatement before it is trusted as the checker of the HIP path:
 dbg.log, msgcount.log and stdout byte-for-byte and the per-tick membership
 tables (digest of the dump of every tick) for the 3 reference testcases x 25
-seed pairs and 9 synthetic clusters (N=20..520: healthy, drop, multi-failure,
+seed pairs and 10 synthetic clusters (N=20..1000, the largest EmulNet admits: healthy, drop, multi-failure,
 EmulNet-buffer overflow, signed-char addresses, updateMyPos quirk regimes).
 """
 import numpy as np
@@ -43,8 +43,8 @@ def test_oracle_matches_reference_large(name, tmp_path):
 
 
 def test_fixture_inventory():
-    # 3 testcases x (8x3 seed grid + the survey's 42/7 pair) + 9 synthetic clusters
-    assert len(ALL) == 3 * 25 + 9
+    # 3 testcases x (8x3 seed grid + the survey's 42/7 pair) + 10 synthetic clusters
+    assert len(ALL) == 3 * 25 + 10
     for name in ALL:
         m = load_case(name)
         assert m["ticks"] == 700 and m["dbg"].startswith(b"131\n")
