@@ -56,6 +56,7 @@ struct gm_ctx {
   hipEvent_t e0 = nullptr, e1 = nullptr;
   std::vector<void *> allocs;
   std::vector<int32_t> failed_h;
+  std::vector<int32_t> fail_t;  // last tick a failed node ran (join ramp: its inGroup is frozen there)
   // FAITHFUL
   FState f{};
   size_t f_smem = 0;
@@ -277,11 +278,17 @@ static int create_scaled(gm_ctx *c) {
   // converged start (cold or warm, gm_config.init_mode); padding columns absent
   const bool warm = c->cfg.init_mode == 1;
   const int t0 = warm ? c->cfg.init_t0 : 0;
-  if (c->cfg.init_mode < 0 || c->cfg.init_mode > 1 || (warm && (t0 < 5 || t0 > GM_T_LIMIT / 2))) return GM_EINVAL;
+  // join ramp (init_mode 2): one context, no keyed drops (a joiner must learn its own
+  // entry from the introducer's list, else updateMyPos's quirk path, MP1Node.cpp:316)
+  const bool ramp = c->cfg.init_mode == 2;
+  if (c->cfg.init_mode < 0 || c->cfg.init_mode > 2 || (warm && (t0 < 5 || t0 > GM_T_LIMIT / 2))) return GM_EINVAL;
+  if (ramp && (s.sharded || c->cfg.drop_pct > 0)) return GM_EUNSUPPORTED;
+  s.ramp = ramp ? 1 : 0;
+  s.intro_until = 0x7FFFFFFF;
   HIPCHECK(hipMemset(s.msg, 0, sizeof(uint8_t) * 2 * cells));
   for (int p = 0; p < 2; p++) HIPCHECK(hipMemset(s.inbox_cnt[p], 0, sizeof(int32_t) * n));
   HIPCHECK(hipMemset(s.failed, 0, sizeof(int32_t) * n));
-  HIPCHECK(gm_launch_init(s, warm ? 1 : 0, t0, c->cfg.init_seed, c->stream));
+  HIPCHECK(gm_launch_init(s, ramp ? 2 : warm ? 1 : 0, t0, c->cfg.init_seed, c->stream));
   HIPCHECK(hipStreamSynchronize(c->stream));
   HIPCHECK(hipMemset(s.bcnt, 0, sizeof(uint32_t) * (size_t)n * s.nb));
   HIPCHECK(hipMemset(s.ev_spill_cnt, 0, sizeof(uint32_t)));
@@ -384,6 +391,7 @@ extern "C" int gm_create(const gm_config *cfg, gm_ctx **out) {
   c->cfg = *cfg;
   c->n = cfg->n;
   c->failed_h.assign(cfg->n, 0);
+  c->fail_t.assign(cfg->n, 0x7FFFFFFF);
   int rc = GM_OK;
   if (hipSetDevice(cfg->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&c->e0) != hipSuccess || hipEventCreate(&c->e1) != hipSuccess ||
@@ -467,6 +475,16 @@ static int tick_sharded(gm_ctx *c);
 static int tick_scaled(gm_ctx *c) {
   if (c->t > GM_T_LIMIT) return GM_ERANGE;
   if (c->s.sharded) return tick_sharded(c);
+  if (c->s.ramp) {  // nodeStart of this tick's starters clears bFailed (MP1Node.cpp:108)
+    const int j0 = 4 * c->t, j1 = std::min(c->n, 4 * c->t + 4);
+    for (int j = j0; j < j1; j++)
+      if (c->failed_h[j]) {
+        c->failed_h[j] = 0;
+        c->fail_t[j] = 0x7FFFFFFF;
+        HIPCHECK(hipMemcpyAsync(c->s.failed + j, c->failed_h.data() + j, sizeof(int32_t), hipMemcpyHostToDevice,
+                                c->stream));
+      }
+  }
   const int t_send = c->t - 1;
   const bool drop = c->cfg.drop_pct > 0 && t_send >= c->cfg.drop_from && t_send < c->cfg.drop_to;
   hipEvent_t k0 = nullptr, k1 = nullptr;
@@ -579,7 +597,10 @@ extern "C" int gm_set_failed(gm_ctx *c, const int32_t *idx, int32_t n) {
   if (!c || (n > 0 && !idx)) return GM_EINVAL;
   for (int k = 0; k < n; k++) {
     if (idx[k] < 0 || idx[k] >= c->n) return GM_EINVAL;
+    if (!c->failed_h[idx[k]]) c->fail_t[idx[k]] = c->t - 1;
     c->failed_h[idx[k]] = 1;
+    // join ramp: the introducer's last tick bounds who gets a JOINREP
+    if (idx[k] == 0 && c->cfg.mode == GM_MODE_SCALED && c->s.ramp) c->s.intro_until = std::min(c->s.intro_until, c->t - 1);
   }
   int32_t *dst = c->cfg.mode == GM_MODE_FAITHFUL ? c->f.failed : c->cfg.mode == GM_MODE_SCALED ? c->s.failed : c->p.failed;
   const bool part = c->cfg.mode == GM_MODE_PARTIAL;  // a row shard holds its own nodes' flags only
@@ -765,7 +786,7 @@ static int read_table_row(gm_ctx *c, int r, std::vector<int32_t> &hb, std::vecto
   ts.resize(w);
   for (int j = 0; j < w; j++) {  // cells are relative to the row's last written tick
     const uint32_t e = row[j];
-    hb[j] = e == 0 ? -1 : 2 * wt - 255 + (int32_t)S_H(e);
+    hb[j] = e == 0 ? -1 : 2 * wt - 255 + (int32_t)S_H(e) - s_hbase(s.ramp, s.c0 + j);
     ts[j] = e == 0 ? -1 : wt - (int32_t)S_AGE(e);
   }
   return GM_OK;
@@ -799,6 +820,14 @@ extern "C" int gm_read_nodes(gm_ctx *c, int32_t *st4) {
     const bool part = c->cfg.mode == GM_MODE_PARTIAL;
     std::fill(a.begin(), a.end(), 1);
     std::fill(b.begin(), b.end(), 1);
+    if (!part && c->s.ramp) {  // join ramp: started (inited) / in the group as of the last tick
+      const int t = c->t - 1;
+      for (int i = 0; i < n; i++) {
+        a[i] = t >= s_start(i);
+        // JOINREP is processed at start+2 only by a node still running then
+        b[i] = i == 0 ? a[i] : s_ingroup(1, c->s.intro_until, i, t) && c->fail_t[i] >= s_start(i) + 2;
+      }
+    }
     HIPCHECK(hipMemcpy(f.data(), part ? c->p.failed : c->s.failed, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
     HIPCHECK(hipMemcpy(h.data(), part ? c->p.hbctr : c->s.hbctr, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
   }

@@ -17,6 +17,11 @@
 // at tick t is 2t-1 (h = 254); h falls by 2 per tick of heartbeat lag, and a present
 // entry lagging more than ~126 ticks sets GM_ERR_LAG instead of wrapping.
 #define S_CELL(h, age) (((h) << 5) | (age))
+__host__ __device__ inline int s_start(int j) { return j >> 2; }  // (int)(0.25 * j) for j >= 0
+__host__ __device__ inline int s_hbase(int ramp, int j) { return (ramp && j > 0) ? 2 * (s_start(j) + 1) : 0; }
+__host__ __device__ inline bool s_ingroup(int ramp, int intro_until, int r, int t) {
+  return !ramp || r == 0 || (t >= s_start(r) + 2 && s_start(r) + 1 <= intro_until);
+}
 #define S_H(c) ((c) >> 5)
 #define S_AGE(c) ((c) & 31u)
 // payload cell (8 bits): h of a fresh entry re-based to the receiving tick (h - 2 >= 1),
@@ -62,6 +67,13 @@ struct SState {
   // rehearse the sharded protocol + RCCL on one GPU; see gm_s_draw / gm_s_accept)
   int shard_rank, shard_count;
   int sharded;
+  // ---- join ramp (gm_config.init_mode 2, single context): node j starts at tick j/4
+  // (Application.cpp:130, STEP_RATE 0.25) and is in the group from tick j/4 + 2 if the
+  // introducer (node 0) answered its JOINREQ at j/4 + 1 (ran that tick: <= intro_until).
+  // A column's heartbeats are stored offset by s_hbase(j) = 2(j/4 + 1) (0 for j = 0), so
+  // every live node's own heartbeat still reads 2t-1 and the narrow cell applies.
+  int ramp;
+  int intro_until;
   int32_t *xcnt;             // bound exchange buffer [shard_count][n][2]: (present, numfailed) per shard
   int32_t *status;           // bound exchange buffer [n][D]: resolved draws, MAX-allreduced
   int32_t *acc;              // [n][8]: targets so far, g[5], numpot, size

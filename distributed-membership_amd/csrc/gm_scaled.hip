@@ -65,7 +65,7 @@ struct RowMeta {
 };
 
 template <int B>
-__device__ __forceinline__ RowMeta<B> row_meta(const SState &s, int r, int par) {
+__device__ __forceinline__ RowMeta<B> row_meta(const SState &s, int r, int par, int t) {
   RowMeta<B> m;
   m.k = -1;
   if (r < s.n) {
@@ -75,7 +75,7 @@ __device__ __forceinline__ RowMeta<B> row_meta(const SState &s, int r, int par) 
     m.snd[0] = a.x; m.snd[1] = a.y; m.snd[2] = a.z; m.snd[3] = a.w;
     m.snd[4] = b.x; m.snd[5] = b.y; m.snd[6] = b.z; m.snd[7] = b.w;
     const int k = s.inbox_cnt[par][r];
-    m.k = s.failed[r] ? -1 : k;
+    m.k = (s.failed[r] || !s_ingroup(s.ramp, s.intro_until, r, t)) ? -1 : k;  // not in the group: untouched
   }
   return m;
 }
@@ -121,7 +121,7 @@ __global__ __launch_bounds__(256) void gm_s_band(SState s, int t, int drop_pct) 
   const __amdgpu_buffer_rsrc_t prs = gm_rsrc(s.msg + slab * 2 * B, (uint32_t)(s.n * B * 2));
   const uint32_t toff = (uint32_t)(r * B + li * Q) * 2;            // r >= n: out of range -> zeros, dropped
   const uint32_t poff = (uint32_t)((par ^ 1) * B + li * Q);        // + sender * 2B
-  const RowMeta<B> meta = row_meta<B>(s, r, par);
+  const RowMeta<B> meta = row_meta<B>(s, r, par, t);
   int k = meta.k;
   if (k > S_KMAX) {
     if (li == 0) atomicOr(s.err, GM_ERR_INBOX);
@@ -207,6 +207,14 @@ __global__ __launch_bounds__(256) void gm_s_band(SState s, int t, int drop_pct) 
 #pragma unroll
       for (int i = 0; i < 8; i++) key[i] = pk(kk[2 * i] | (kk[2 * i + 1] << 16));
     }
+    if (s.ramp && r == 0) {  // the introducer takes the JOINREQs of the nodes that started at t-1:
+      // entry {hb 0, ts t} = stored heartbeat 2t (offset 2(t-1+1)) = h 255 (MP1Node.cpp:226-251)
+#pragma unroll
+      for (int q = 0; q < Q; q++) {
+        const int c = s.c0 + colb + q;
+        if (c >= 1 && c < s.n && s_start(c) == t - 1) key[q >> 1] = pk(unpk(key[q >> 1]) | (255u << (16 * (q & 1))));
+      }
+    }
     // merge: re-base the cell to tick t (h -= 2, age += 1; absent stays 0), then max
     // with the delivered key (insert if absent; raise hb and stamp ts = t if newer)
     const uint32_t tw[8] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y, tb.z, tb.w};
@@ -218,7 +226,7 @@ __global__ __launch_bounds__(256) void gm_s_band(SState s, int t, int drop_pct) 
     if (selfc >= 0 && selfc < Q) {  // updateMyPos + heartbeat++ + myPos->setheartbeat(heartbeat++)
       const int hb = s.hbctr[r] + 1;
       s.hbctr[r] = hb + 1;
-      const int h = 255 - (2 * t - hb);
+      const int h = 255 - (2 * t - (hb + s_hbase(s.ramp, r)));
       if (h < 3 || h > 255) atomicOr(s.err, GM_ERR_LAG);
 #pragma unroll
       for (int i = 0; i < 8; i++) {
@@ -484,7 +492,7 @@ __global__ __launch_bounds__(256) void gm_s_pick(SState s, int t) {
   int32_t *stat = s.rowstat + (size_t)r * 4;
   const int k = s.inbox_cnt[par][r];
   if (lane == 0) s.inbox_cnt[par][r] = 0;  // consumed by gm_s_band; the append target of tick t+2
-  if (s.failed[r]) {
+  if (s.failed[r] || !s_ingroup(s.ramp, s.intro_until, r, t)) {
     if (lane == 0) stat[0] = stat[1] = stat[2] = stat[3] = 0;
     return;
   }
@@ -493,7 +501,16 @@ __global__ __launch_bounds__(256) void gm_s_pick(SState s, int t) {
   const int numpot = (int)size - 1 - (int)numfailed;  // numfailed counts removed entries too (MP1Node.cpp:463)
   const int target = min(GM_FANOUT, numpot);
   int n = 0, g0 = -1, g1 = -1, g2 = -1, g3 = -1, g4 = -1;
-  if (numpot > 0) {
+  if (s.ramp && r == 0) {  // gossipnodes = newNodes first (MP1Node.cpp:458): this tick's joiners, ascending id
+    for (int c = max(1, 4 * (t - 1)); c < min(s.n, 4 * t); c++) {
+      if (n == 0) g0 = c;
+      else if (n == 1) g1 = c;
+      else if (n == 2) g2 = c;
+      else g3 = c;
+      n++;
+    }
+  }
+  if (numpot > 0 && n < target) {
     const uint32_t thr = (0u - size) % size;  // Lemire rejection threshold (uniform_int_dist.h)
     GmLazyMT mt;
     bool done = false;
@@ -720,11 +737,15 @@ __global__ __launch_bounds__(256) void gm_s_accept(SState s, int t, int D) {
 // t0-a}, a = splitmix64(seed ^ r<<32 ^ c) % 4 -- values as if the cluster had been
 // gossiping, so the first ticks carry no mass-staleness transient. Padding absent.
 // Cells are encoded relative to tick t0 (S_CELL: h = 255 - (2*t0 - hb), age = t0 - ts).
+// Join ramp (warm = 2): nobody in any list but the introducer's own entry {hb 0, ts 0}
+// (nodeStart of node 0 at tick 0, MP1Node.cpp:126-140); state as of tick 0.
 __global__ void gm_s_init(SState s, int warm, int t0, uint64_t seed) {
   const int r = blockIdx.x;
   for (int j = threadIdx.x; j < s.wp; j += blockDim.x) {
     uint32_t e = 0;  // absent
-    if (j < s.w) {
+    if (j < s.w && warm == 2) {
+      if (r == 0 && s.c0 + j == 0) e = S_CELL(255u, 0u);
+    } else if (j < s.w) {
       const int c = s.c0 + j;
       if (!warm) e = S_CELL(255u, 0u);  // hb 0 = 2*t0 at t0 = 0
       else if (c == r) e = S_CELL(254u, 0u);
@@ -736,7 +757,7 @@ __global__ void gm_s_init(SState s, int warm, int t0, uint64_t seed) {
     s.table[((size_t)(j / s.band) * s.n + r) * s.band + j % s.band] = (uint16_t)e;
   }
   if (threadIdx.x == 0) {
-    s.hbctr[r] = warm ? 2 * t0 : 0;
+    s.hbctr[r] = warm == 1 ? 2 * t0 : 0;
     s.wtick[r] = t0;
   }
 }

@@ -92,7 +92,11 @@ typedef struct gm_config {
   /* SCALED initial state: 0 = cold converged start (every cell {hb 0, ts 0},
    * first tick 1); 1 = warm converged start at t0: own entry {2*t0-1, t0},
    * others {2*(t0-1-a)-1, t0-a} with a = splitmix64(init_seed, r, c) % 4,
-   * heartbeat counters 2*t0, first tick t0+1 (no mass-staleness transient) */
+   * heartbeat counters 2*t0, first tick t0+1 (no mass-staleness transient);
+   * 2 = join ramp (one context, no drops): node i starts at tick (int)(0.25*i)
+   * (Application.cpp:130), JOINREQ -> introducer -> JOINREP + newNodes-first gossip
+   * (MP1Node.cpp:126-163,226-251) over the unbounded network; state as of tick 0
+   * (the introducer's own entry), first tick 1 */
   int32_t init_mode;
   int32_t init_t0;
   uint64_t init_seed;

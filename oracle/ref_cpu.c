@@ -204,6 +204,8 @@ struct oc_ctx {
   oc_event *ev;
   size_t nev, evcap;
   int32_t *crash;
+  /* SCALED join ramp (init_mode 2): the last tick the introducer ran */
+  int intro_last;
 };
 
 static int is_scaled(const oc_ctx *c) { return c->cfg.mode == OC_SCALED; }
@@ -420,7 +422,7 @@ static void node_loop(oc_ctx *c, int idx) {
         entry e = {m->id, m->port, m->hb, c->t};
         newn[n_new++] = e;
       }
-      en_send(c, nd->id, m->id, JOINREP, 0, 0, 0, JOINREP_SIZE);
+      if (!is_scaled(c)) en_send(c, nd->id, m->id, JOINREP, 0, 0, 0, JOINREP_SIZE);
     } else if (m->type == JOINREP) {
       nd->in_group = 1;
     } else if (m->type == LIST) {
@@ -446,7 +448,8 @@ static void node_start(oc_ctx *c, int idx) {
     nd->in_group = 1;
   } else {
     log_line(c, nd->id, "Trying to join...");
-    en_send(c, nd->id, 1, JOINREQ, nd->id, 0, nd->heartbeat, LIST_SIZE);
+    /* SCALED: the introducer takes the JOINREQs of tick t-1 starters in mp1_run */
+    if (!is_scaled(c)) en_send(c, nd->id, 1, JOINREQ, nd->id, 0, nd->heartbeat, LIST_SIZE);
   }
 }
 
@@ -501,10 +504,31 @@ static void mp1_run(oc_ctx *c) {
     return;
   }
   c->nev = 0;
+  const int ramp = c->cfg.init_mode == 2;
   for (int i = c->n - 1; i >= 0; i--) {
-    if (c->nodes[i].failed) continue;
+    const int start = (int)(0.25 * i); /* Application.cpp:130,143 (STEP_RATE 0.25) */
+    if (ramp && t == start) {
+      node_start(c, i);
+      if (i == 0) c->intro_last = t;
+      continue;
+    }
+    if ((ramp && t < start) || c->nodes[i].failed) continue;
     scaled_recv(c, i);
+    if (ramp) {
+      node *nd = &c->nodes[i];
+      if (i == 0) { /* JOINREQs of the nodes that started at t-1, ascending id (unbounded network) */
+        for (int j = 1; j < c->n; j++) {
+          if ((int)(0.25 * j) != t - 1) continue;
+          msg m = {LIST_SIZE, j + 1, 1, JOINREQ, j + 1, 0, 0};
+          mv_push(&nd->q, &m);
+        }
+      } else if (t == start + 2 && c->intro_last >= start + 1) { /* the introducer answered at start+1 */
+        msg m = {JOINREP_SIZE, 1, i + 1, JOINREP, 0, 0, 0};
+        mv_push(&nd->q, &m);
+      }
+    }
     node_loop(c, i);
+    if (ramp && i == 0) c->intro_last = t;
   }
   qsort(c->ev, c->nev, sizeof(oc_event), ev_canon);
   snap *ts = c->snaps; c->snaps = c->snaps_next; c->snaps_next = ts;
@@ -564,6 +588,7 @@ int oc_crash_set(int n, int count, uint64_t seed, int32_t *out) {
 oc_ctx *oc_create(const oc_config *cfg) {
   if (cfg->n <= 0) return NULL;
   if (cfg->mode == OC_SCALED && cfg->init_mode == 1 && cfg->init_t0 < 5) return NULL; /* hb >= 0 needs t0 >= 5 */
+  if (cfg->mode == OC_SCALED && cfg->init_mode == 2 && cfg->drop_pct > 0) return NULL; /* ramp: no keyed drops */
   if (cfg->mode == OC_FAITHFUL && cfg->n > MAX_NODES) return NULL; /* EmulNet.cpp:108 assert */
   oc_ctx *c = (oc_ctx *)calloc(1, sizeof(oc_ctx));
   c->cfg = *cfg;
@@ -577,10 +602,17 @@ oc_ctx *oc_create(const oc_config *cfg) {
     oc_srand(&c->s1, cfg->time_seed); /* srand(time(NULL)), Application.cpp:50 and :96 */
     c->t = 0;
   } else {
-    const int warm = cfg->init_mode == 1;
+    const int warm = cfg->init_mode == 1, ramp = cfg->init_mode == 2;
     const int t0 = warm ? cfg->init_t0 : 0;
+    c->intro_last = -1;
     for (int i = 0; i < c->n; i++) {
       node *nd = &c->nodes[i];
+      if (ramp) { /* join ramp: nobody started, empty lists (nodeStart at (int)(0.25 i)) */
+        nd->list.v = (entry *)malloc(sizeof(entry) * (size_t)c->n);
+        nd->list.cap = c->n;
+        nd->list.n = 0;
+        continue;
+      }
       nd->inited = nd->in_group = 1;
       nd->heartbeat = warm ? 2 * t0 : 0;
       nd->list.v = (entry *)malloc(sizeof(entry) * (size_t)c->n);
@@ -615,7 +647,7 @@ oc_ctx *oc_create(const oc_config *cfg) {
       oc_destroy(c);
       return NULL;
     }
-    c->t = t0 + 1; /* converged state is "as of tick t0" */
+    c->t = ramp ? 0 : t0 + 1; /* converged state is "as of tick t0"; the ramp starts at tick 0 */
   }
   return c;
 }

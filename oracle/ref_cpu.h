@@ -50,7 +50,7 @@ typedef struct oc_config {
   int drop_pct;        /* per-entry drop percentage in SCALED mode */
   int drop_from, drop_to; /* drops apply to sends at ticks in [drop_from, drop_to) */
   uint64_t drop_seed;
-  int init_mode;       /* 0 cold converged start, 1 warm converged start at init_t0 (gm_abi.h) */
+  int init_mode;       /* 0 cold converged start, 1 warm converged start at init_t0, 2 join ramp (gm_abi.h) */
   int init_t0;
   uint64_t init_seed;
 } oc_config;

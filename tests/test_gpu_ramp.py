@@ -1,0 +1,67 @@
+"""SCALED join ramp: the full membership lifecycle at scale
+instead of a converged start. Node i starts at tick (int)(0.25 i) (Application.cpp:130),
+sends JOINREQ to the introducer, which adds it (hb 0), gossips to this tick's joiners
+first (newNodes, MP1Node.cpp:458) and answers with JOINREP (MP1Node.cpp:226-251); the
+joiner is in the group two ticks after its start. The HIP band/pick kernels (narrow
+cells with a per-column heartbeat offset) against the oracle (oracle/ref_cpu.c SCALED,
+init_mode 2), tick by tick: every table, node state (inited / inGroup / failed /
+heartbeat) and the join/remove event set -- through the ramp, a crash set that hits
+nodes before they start (nodeStart revives them, MP1Node.cpp:108), and the introducer
+crashing mid-ramp (later starters never join)."""
+import pytest
+
+import oracle_py
+from golden_util import digest64
+from membership import GM_MODE_SCALED, Simulator, crash_set
+
+pytestmark = pytest.mark.gpu
+
+
+def seed_with(n, count, want):
+    """a crash seed whose set contains `want` (node 0: the introducer)"""
+    for seed in range(1, 10000):
+        if want in set(crash_set(n, count, seed).tolist()):
+            return seed
+    raise AssertionError("no seed")
+
+
+def run_ramp(n, ticks, crash_tick=-1, crash_count=0, crash_seed=42, band=0):
+    ora = oracle_py.Oracle(n, oracle_py.OC_SCALED, rd_seed=7, crash_tick=crash_tick, crash_count=crash_count,
+                           crash_seed=crash_seed, init_mode=2)
+    sim = Simulator(n, GM_MODE_SCALED, rd_seed=7, init_mode=2, band=band)
+    crash = crash_set(n, crash_count, crash_seed)
+    ora.tick()  # tick 0: nodeStart of nodes 0-3 (the GPU context starts as of tick 0)
+    assert sim.time == ora.time == 1
+    assert digest64(sim.dump_tables()) == digest64(ora.dump()), "tick 0 state differs"
+    joins = removes = 0
+    for _ in range(ticks):
+        t = sim.time
+        ora.tick()
+        sim.tick()
+        if t == crash_tick:
+            sim.set_failed(crash)
+        ev = sim.drain_events()
+        assert ev == ora.events(), f"events differ at tick {t}"
+        joins += sum(e[2] == 1 for e in ev)
+        removes += sum(e[2] == 2 for e in ev)
+        assert digest64(sim.dump_tables()) == digest64(ora.dump()), f"tables differ at tick {t}"
+    assert sim.tick_stats()["err"] == 0
+    return joins, removes
+
+
+@pytest.mark.parametrize("n,band", [(64, 64), (300, 128), (1100, 0)])
+def test_ramp_matches_oracle(n, band):
+    joins, _ = run_ramp(n, n // 4 + 30, band=band)
+    assert joins >= n * (n - 1)  # everyone learned everyone (plus re-joins)
+
+
+def test_ramp_crash_before_start_and_removals():
+    # crash at tick 20 of a 400-node ramp (starts run to tick 99): crashed starters revive
+    joins, removes = run_ramp(400, 140, crash_tick=20, crash_count=40)
+    assert removes > 0
+
+
+def test_ramp_introducer_crash():
+    n, cnt = 256, 8
+    joins, removes = run_ramp(n, 110, crash_tick=30, crash_count=cnt, crash_seed=seed_with(n, cnt, 0))
+    assert removes > 0
