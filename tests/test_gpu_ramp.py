@@ -65,3 +65,32 @@ def test_ramp_introducer_crash():
     n, cnt = 256, 8
     joins, removes = run_ramp(n, 110, crash_tick=30, crash_count=cnt, crash_seed=seed_with(n, cnt, 0))
     assert removes > 0
+
+
+def test_ramp_at_scale_converges():
+    """N = 16,384: the whole 4,096-tick ramp on the GPU (no oracle at this size; size-
+    independent properties instead): every node joins, every live node ends up holding
+    every node exactly once (n entries), each join event is logged once per (observer,
+    subject) pair and nobody is removed in a crash-free run."""
+    import numpy as np
+    n = 16384
+    sim = Simulator(n, GM_MODE_SCALED, rd_seed=7, init_mode=2)
+    joins = removes = 0
+    last = n // 4 + 40
+    while sim.time <= last:
+        sim.tick()
+        if sim.time % 256 == 0 or sim.time > last:
+            ev = sim.drain_events()
+            joins += sum(e[2] == 1 for e in ev)
+            removes += sum(e[2] == 2 for e in ev)
+        else:
+            joins += sim.event_total()  # join+remove records of the last tick
+    st = sim.tick_stats()
+    assert st["err"] == 0 and st["live"] == n
+    nodes = sim.read_nodes()
+    assert (nodes[:, 0] == 1).all() and (nodes[:, 1] == 1).all()
+    for r in (0, 1, n // 2, n - 1):  # spot rows: everyone present
+        hb, ts = sim.read_row(r)
+        assert (hb >= 0).all(), r
+    assert removes == 0
+    assert joins == n * n - 1  # everyone learns everyone (incl. itself); the introducer's own entry is not a join
