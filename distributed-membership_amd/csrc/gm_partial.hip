@@ -101,13 +101,9 @@ template <int H>
 __device__ __forceinline__ int p_insert(uint32_t *tid, uint32_t *thb, uint32_t id, uint32_t idw, uint32_t hb) {
   constexpr int LOGH = H == 512 ? 9 : 10;
   uint32_t h = (id * 0x9E3779B1u) >> (32 - LOGH);
-  for (;;) {
-    uint32_t cur = tid[h];
-    if (cur == 0) {
-      cur = atomicCAS(&tid[h], 0u, idw);
-      if (cur == 0) break;
-    }
-    if ((cur & P_IDMASK) == id) break;
+  for (;;) {  // claim-or-compare in one LDS op
+    const uint32_t cur = atomicCAS(&tid[h], 0u, idw);
+    if (cur == 0 || (cur & P_IDMASK) == id) break;
     h = (h + 1) & (H - 1);
   }
   atomicMax(&thb[h], hb);
@@ -123,11 +119,33 @@ __device__ __forceinline__ int p_owner(const PState &s, int d) {
   return g;
 }
 
+// A node's independent loads, issued together before any branch on them (one memory
+// round trip instead of a chain): crash flag, inbox count, own list, inbox row, S2
+// outputs, heartbeat counter. `nin` = inbox lanes to fetch (the kernel's list bound).
+struct PPre {
+  int failed, k, hbctr;
+  uint64_t own;
+  int sv;
+  uint32_t raw0;
+};
+__device__ __forceinline__ PPre p_preload(const PState &s, int t, const uint32_t *mtraw, int li, int lane, int nin) {
+  const int par = t & 1, V = s.V;
+  PPre p;
+  p.failed = s.failed[li];
+  p.k = s.inbox_cnt[par][li];
+  p.hbctr = s.hbctr[li];
+  p.own = lane < V ? s.lists[((size_t)(par ^ 1) * s.rows + li) * V + lane] : 0ull;
+  p.sv = lane < nin ? s.inbox[par][(size_t)li * P_KMAX + lane] : 0;
+  p.raw0 = lane < 16 ? mtraw[(size_t)li * 16 + lane] : 0u;
+  return p;
+}
+
 // One node's tick on one wave. li: the node's local row (global index n0 + li);
-// k: lists queued for it this tick.
+// pre.k: lists queued for it this tick.
 template <int H, bool BIG>
-__device__ __forceinline__ void p_node(const PState &s, int t, const uint32_t *mtraw, int li, int k, int lane,
-                                       unsigned char *base, int chunk, int r0) {
+__device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, int li, int lane, unsigned char *base,
+                                       int chunk, int r0) {
+  int k = pre.k;
   const int i = s.n0 + li;  // global node index (ids, keys, seeds, targets)
   constexpr int TS = H / 64;                          // table slots per lane
   constexpr int KK = BIG ? P_KP : P_KSMALL;           // lists merged at most
@@ -149,11 +167,11 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const uint32_t *m
     if (lane == 0) atomicOr(s.err, GM_ERR_INBOX);
     k = P_KMAX;
   }
-  // ---- 1. loads
-  const uint64_t own = lane < V ? prev[(size_t)li * V + lane] : 0ull;
-  int sv = lane < k ? s.inbox[par][(size_t)li * P_KMAX + lane] : 0x7FFFFFFF;  // list rows
-  const uint32_t raw0 = lane < 16 ? mtraw[(size_t)li * 16 + lane] : 0u;
-  const int hbnew = s.hbctr[li] + 1;
+  // ---- 1. loads (the independent ones arrived with `pre`)
+  const uint64_t own = pre.own;
+  int sv = lane < k ? pre.sv : 0x7FFFFFFF;  // list rows
+  const uint32_t raw0 = pre.raw0;
+  const int hbnew = pre.hbctr + 1;
   // global sender index of each row (drop keys, the lowest-sender rule)
   int sg = lane < k ? (sv < s.nloc ? s.n0 + sv : s.rsrc[par ^ 1][sv - s.nloc]) : 0x7FFFFFFF;
   {  // clear the table (both word arrays are contiguous)
@@ -178,15 +196,19 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const uint32_t *m
   const int kk = min(k, KK);
   const int per = 64 / V, l = lane % V, jo = lane / V;
   uint64_t dv[NSTEP];
-  int dsn[NSTEP];
 #pragma unroll
   for (int st = 0; st < NSTEP; st++) {
     const int j = st * per + jo;
     const bool ok = jo < per && j < kk;
     const int sn = __shfl(sv, ok ? j : 0, 64);
-    dsn[st] = __shfl(sg, ok ? j : 0, 64);
     dv[st] = ok ? prev[(size_t)sn * V + l] : 0ull;
   }
+  // drop keys: one (t_send, src, dst) hash per delivered list, lane j for list j
+  const bool dropping = s.drop_pct >= 0;
+  uint64_t pairv = 0;
+  if (dropping)
+    pairv = gm_mix64(s.drop_seed ^ ((uint64_t)(uint32_t)(t - 1) << 48) ^ ((uint64_t)(uint32_t)sg << 24) ^
+                     (uint64_t)(uint32_t)i);
   p_wsync();
   // ---- 2. merge: own entries first (they carry P_OWN), then the delivered lists
   int hslot = -1;
@@ -198,15 +220,15 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const uint32_t *m
   p_wsync();
   {
     const uint32_t tfresh = (uint32_t)max(0, 2 * t - 11);  // hb >= 2t-11 <=> (t-1) - (hb+1)/2 < TFAIL
-    const bool dropping = s.drop_pct >= 0;
 #pragma unroll
     for (int st = 0; st < NSTEP; st++) {
       const uint64_t e = dv[st];
       bool take = e != 0 && (uint32_t)e >= tfresh;
       const uint32_t id = (uint32_t)(e >> 32);
       if (dropping && __ballot(take)) {  // per-entry drops keyed by (t_send, src, dst, id-1)
-        const uint64_t pair = gm_mix64(s.drop_seed ^ ((uint64_t)(uint32_t)(t - 1) << 48) ^
-                                       ((uint64_t)(uint32_t)dsn[st] << 24) ^ (uint64_t)(uint32_t)i);
+        const int j = min(st * per + jo, 63);
+        const uint32_t plo = __shfl((uint32_t)pairv, j, 64), phi = __shfl((uint32_t)(pairv >> 32), j, 64);
+        const uint64_t pair = ((uint64_t)phi << 32) | plo;
         const uint32_t h = (uint32_t)(gm_mix64(pair + (uint64_t)(id - 1)) >> 32);
         take = take && (int)(h % 100u) >= s.drop_pct;
       }
@@ -529,16 +551,16 @@ __global__ __launch_bounds__(256) void gm_p_tick_small(PState s, int t, const ui
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int li = r0 + blockIdx.x * 4 + wave;
   if (li >= r1) return;  // whole wave; no workgroup barrier in this kernel
-  if (s.failed[li]) {
+  const PPre pre = p_preload(s, t, mtraw, li, lane, P_KSMALL);
+  if (pre.failed) {
     p_frozen(s, t, li, lane);
     return;
   }
-  const int k = s.inbox_cnt[t & 1][li];
-  if (k > P_KSMALL) {  // deferred to gm_p_tick_big
+  if (pre.k > P_KSMALL) {  // deferred to gm_p_tick_big
     if (lane == 0) s.big[r0 + atomicAdd(&s.big_cnt[chunk], 1)] = li;
     return;
   }
-  p_node<P_HS, false>(s, t, mtraw, li, k, lane, p_smem + (size_t)wave * PLds<P_HS>::bytes, chunk, r0);
+  p_node<P_HS, false>(s, t, pre, li, lane, p_smem + (size_t)wave * PLds<P_HS>::bytes, chunk, r0);
 }
 
 // drains the worklist gm_p_tick_small filled (a fixed grid; every wave exits when the list is done)
@@ -548,8 +570,8 @@ __global__ __launch_bounds__(256) void gm_p_tick_big(PState s, int t, const uint
   const int nbig = s.big_cnt[chunk];
   for (int w = blockIdx.x * 4 + wave; w < nbig; w += gridDim.x * 4) {
     const int li = s.big[r0 + w];
-    const int k = s.inbox_cnt[t & 1][li];
-    p_node<P_HB, true>(s, t, mtraw, li, k, lane, p_smem + (size_t)wave * PLds<P_HB>::bytes, chunk, r0);
+    const PPre pre = p_preload(s, t, mtraw, li, lane, P_KMAX);
+    p_node<P_HB, true>(s, t, pre, li, lane, p_smem + (size_t)wave * PLds<P_HB>::bytes, chunk, r0);
   }
 }
 
