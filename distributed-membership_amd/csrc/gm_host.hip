@@ -368,6 +368,10 @@ static int create_partial(gm_ctx *c) {
     TRY(dalloc(c, &p.send_list, (size_t)G * nl * p.V));
     TRY(dalloc(c, &p.recv_hdr, (size_t)std::max(R, 1) * 8));
     TRY(dalloc(c, &p.recv_cnt, (size_t)p.nchunk * G));
+    std::vector<int32_t> b(G + 1);
+    for (int g = 0; g <= G; g++) b[g] = (int32_t)((int64_t)n * g / G);
+    TRY(dalloc(c, &p.shard_n0, G + 1));
+    HIPCHECK(hipMemcpy(p.shard_n0, b.data(), sizeof(int32_t) * (G + 1), hipMemcpyHostToDevice));
   }
   HIPCHECK(hipMemset(p.lists, 0, sizeof(uint64_t) * 2 * p.rows * p.V));
   HIPCHECK(hipMemset(p.failed, 0, sizeof(int32_t) * nl));

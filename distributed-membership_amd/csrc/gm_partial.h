@@ -40,5 +40,6 @@ struct PState {
   uint64_t *send_list;   // [G][nloc][V]: the sender's final list of the tick
   int32_t *recv_hdr;     // [n - nloc][8] received headers (their lists land in rows nloc.. of the tick's parity)
   int32_t *recv_cnt;     // [K][G] records received from each shard, per chunk
+  int32_t *shard_n0;     // [G+1] first node of every row shard (shard_n0[G] = n)
   uint32_t *err;
 };

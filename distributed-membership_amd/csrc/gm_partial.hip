@@ -110,12 +110,12 @@ __device__ __forceinline__ int p_insert(uint32_t *tid, uint32_t *thb, uint32_t i
   return (int)h;
 }
 
-// first node of row shard g (contiguous balanced ranges)
-__device__ __forceinline__ int p_shard_n0(const PState &s, int g) { return (int)((int64_t)s.n * g / s.G); }
+// owning row shard of node d: contiguous balanced ranges [n*g/G, n*(g+1)/G), boundaries
+// in shard_n0[0..G]; a float estimate is off by at most one, two compares fix it
 __device__ __forceinline__ int p_owner(const PState &s, int d) {
-  int g = (int)((int64_t)d * s.G / s.n);
-  while (g + 1 < s.G && p_shard_n0(s, g + 1) <= d) g++;
-  while (g > 0 && p_shard_n0(s, g) > d) g--;
+  int g = min(s.G - 1, max(0, (int)((float)d * (float)s.G / (float)s.n)));
+  if (g + 1 < s.G && s.shard_n0[g + 1] <= d) g++;
+  if (g > 0 && s.shard_n0[g] > d) g--;
   return g;
 }
 
