@@ -364,6 +364,10 @@ static int create_partial(gm_ctx *c) {
     for (hipEvent_t &e : c->p_chev) HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIPCHECK(hipEventCreateWithFlags(&c->p_done, hipEventDisableTiming));
     TRY(dalloc(c, &p.send_cnt, (size_t)p.nchunk * G));
+    TRY(dalloc(c, &p.recmask, std::max(nl, 1)));
+    TRY(dalloc(c, &p.sp_hdr, (size_t)G * nl * 8));
+    TRY(dalloc(c, &p.sp_list, (size_t)G * nl * p.V));
+    TRY(dalloc(c, &p.pack_blk, (size_t)G * (nl / 256 + 2)));
     TRY(dalloc(c, &p.send_hdr, (size_t)G * nl * 8));
     TRY(dalloc(c, &p.send_list, (size_t)G * nl * p.V));
     TRY(dalloc(c, &p.recv_hdr, (size_t)std::max(R, 1) * 8));
@@ -1218,5 +1222,13 @@ extern "C" int gm_partial_loopback_tick(gm_ctx **ctxs, int32_t G) {
     TRY(check_err(ctxs[g]));
     ctxs[g]->t++;
   }
+  return GM_OK;
+}
+
+extern "C" int gm_shard_exchange_bytes(gm_ctx *c, int64_t *bytes) {
+  if (!c || !bytes) return GM_EINVAL;
+  *bytes = 0;
+  if (c->cfg.mode == GM_MODE_PARTIAL)  // received records of the last tick: 32 B header + the V-entry list
+    *bytes = c->p_recv_last * (int64_t)(32 + 8 * c->p.V);
   return GM_OK;
 }

@@ -34,9 +34,16 @@ struct PState {
   int32_t *big;          // [nloc] worklists of nodes with > P_KSMALL lists (big-table kernel), chunk c at rows r0_c..
   int32_t *big_cnt;      // [K]
   // outgoing lists to the other row shards (sharded only): one record per (sender, remote rank)
+  // The tick kernels write a sender's record to shard q at the fixed slot (q, li) of the
+  // sparse buffers (no contended counters) and its shard bitmask to recmask[li]; per
+  // chunk, gm_p_pack_* compact them (counts, scan, copy) into the send buffers.
+  uint32_t *recmask;     // [nloc] shards li has a record for this tick
+  int32_t *sp_hdr;       // [G][nloc][8] sparse records: header
+  uint64_t *sp_list;     // [G][nloc][V] sparse records: list
+  int32_t *pack_blk;     // [G][nloc/256 + 2] per-block record counts, then offsets
   int32_t *send_cnt;     // [K][G] records of chunk c addressed to shard q
   int32_t *send_hdr;     // [G][nloc][8]: sender global index, #targets on that rank, targets (global), 0;
-                         //   chunk c's records to q from slot q*nloc + r0_c on
+                         //   chunk c's records to q packed from slot q*nloc + r0_c on
   uint64_t *send_list;   // [G][nloc][V]: the sender's final list of the tick
   int32_t *recv_hdr;     // [n - nloc][8] received headers (their lists land in rows nloc.. of the tick's parity)
   int32_t *recv_cnt;     // [K][G] records received from each shard, per chunk

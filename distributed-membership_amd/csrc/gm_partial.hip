@@ -498,19 +498,19 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
       else atomicOr(s.err, GM_ERR_INBOX);
     }
   }
+  uint32_t rmask = 0;  // shards this sender has a record for
   if (s.G > 1 && __ballot(lane < ng && owner != s.rank)) {
     bool first = lane < ng && owner != s.rank;
 #pragma unroll
     for (int q = 0; q < GM_FANOUT - 1; q++)
       if (q < lane && __builtin_amdgcn_readlane(owner, q) == owner) first = false;
     uint64_t fm = __ballot(first);
-    // chunk c's records to shard q: slots [q*nloc + r0_c, ...) (at most one per sender of the chunk)
-    const int slot = first ? atomicAdd(&s.send_cnt[chunk * s.G + owner], 1) : 0;
-    while (fm) {
+    while (fm) {  // one record per (sender, shard) at its fixed sparse slot (rr, li)
       const int fl = __builtin_ctzll(fm);
       fm &= fm - 1;
       const int rr = __builtin_amdgcn_readlane(owner, fl);
-      const size_t rec = (size_t)rr * s.nloc + r0 + (size_t)__builtin_amdgcn_readlane(slot, fl);
+      rmask |= 1u << rr;
+      const size_t rec = (size_t)rr * s.nloc + li;
       uint64_t tm = __ballot(lane < ng && owner == rr);
       const int nt = __builtin_popcountll(tm);
       int tv0 = -1, tv1 = -1, tv2 = -1, tv3 = -1, tv4 = -1;
@@ -524,11 +524,12 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
         else tv4 = d;
       }
       if (lane < 8)
-        s.send_hdr[rec * 8 + lane] = lane == 0 ? i : lane == 1 ? nt : lane == 2 ? tv0 : lane == 3 ? tv1
-                                   : lane == 4 ? tv2 : lane == 5 ? tv3 : lane == 6 ? tv4 : 0;
-      if (lane < V) s.send_list[rec * V + lane] = x;
+        s.sp_hdr[rec * 8 + lane] = lane == 0 ? i : lane == 1 ? nt : lane == 2 ? tv0 : lane == 3 ? tv1
+                                 : lane == 4 ? tv2 : lane == 5 ? tv3 : lane == 6 ? tv4 : 0;
+      if (lane < V) s.sp_list[rec * V + lane] = x;
     }
   }
+  if (s.G > 1 && lane == 0) s.recmask[li] = rmask;
   if (lane < 4) s.rowstat[(size_t)li * 4 + lane] = lane == 0 ? kk : lane == 1 ? cnt : lane == 2 ? numfailed : ng;
   if (lane == 0) s.ev_cnt[li] = nj | (nrem << 16);
 }
@@ -541,6 +542,7 @@ __device__ __forceinline__ void p_frozen(const PState &s, int t, int li, int lan
   if (lane == 0) {
     s.inbox_cnt[par][li] = 0;
     s.ev_cnt[li] = 0;
+    if (s.G > 1) s.recmask[li] = 0;
   }
 }
 
@@ -641,6 +643,59 @@ __global__ __launch_bounds__(256) void gm_p_unpack(PState s, int t, int base, in
   }
 }
 
+// ---- row shards: compaction of chunk c's sparse records into the send buffers
+// (per (shard q, block of 256 senders): count; per q: exclusive scan of the block
+// counts -> send_cnt; per block: local scan + copy, one wave per record)
+#define P_PACK 256
+__device__ __forceinline__ int32_t *p_blk_row(const PState &s, int q) {  // [G][nloc/256 + 2]
+  return s.pack_blk + (size_t)q * (s.nloc / P_PACK + 2);
+}
+
+__global__ __launch_bounds__(P_PACK) void gm_p_pack_count(PState s, int c, int r0, int r1, int nbq) {
+  __shared__ int tmp[16];
+  const int q = blockIdx.x / nbq, b = blockIdx.x % nbq;
+  const int li = r0 + b * P_PACK + threadIdx.x;
+  const int f = (q != s.rank && li < r1) ? (int)((s.recmask[li] >> q) & 1u) : 0;
+  const int tot = gm_block_sum(f, tmp);
+  if (threadIdx.x == 0) p_blk_row(s, q)[b] = tot;
+}
+
+__global__ __launch_bounds__(1024) void gm_p_pack_scan(PState s, int c, int nbq) {
+  __shared__ int tmp[16];
+  const int q = blockIdx.x;
+  int32_t *blk = p_blk_row(s, q);
+  int base = 0;
+  for (int b0 = 0; b0 < nbq; b0 += 1024) {
+    const int b = b0 + threadIdx.x;
+    const int v = b < nbq ? blk[b] : 0;
+    int tot;
+    const int ex = gm_block_scan(v, tmp, &tot);
+    if (b < nbq) blk[b] = base + ex;
+    base += tot;
+  }
+  if (threadIdx.x == 0) s.send_cnt[c * s.G + q] = base;
+}
+
+__global__ __launch_bounds__(P_PACK) void gm_p_pack_copy(PState s, int c, int r0, int r1, int nbq) {
+  __shared__ int tmp[16];
+  __shared__ int lst[P_PACK];
+  const int q = blockIdx.x / nbq, b = blockIdx.x % nbq;
+  const int li = r0 + b * P_PACK + threadIdx.x;
+  const int f = (q != s.rank && li < r1) ? (int)((s.recmask[li] >> q) & 1u) : 0;
+  int m;
+  const int pos = gm_block_scan(f, tmp, &m);
+  if (f) lst[pos] = li;
+  __syncthreads();
+  const int base = p_blk_row(s, q)[b];
+  const int V = s.V, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int k = wave; k < m; k += P_PACK / 64) {
+    const size_t src = (size_t)q * s.nloc + lst[k];
+    const size_t dst = (size_t)q * s.nloc + r0 + base + k;
+    if (lane < 4) ((uint2 *)(s.send_hdr + dst * 8))[lane] = ((const uint2 *)(s.sp_hdr + src * 8))[lane];
+    else if (lane < 4 + V) s.send_list[dst * V + lane - 4] = s.sp_list[src * V + lane - 4];
+  }
+}
+
 #define P_BIG_GRID 1024
 
 // S2 precompute for every row + reset of the per-chunk worklists and record counts
@@ -656,6 +711,14 @@ hipError_t gm_launch_partial_chunk(const PState &s, int t, const uint32_t *mtraw
     hipLaunchKernelGGL(gm_p_tick_small, dim3((r1 - r0 + 3) / 4), dim3(256), 4 * PLds<P_HS>::bytes, st, s, t, mtraw, c,
                        r0, r1);
   hipLaunchKernelGGL(gm_p_tick_big, dim3(P_BIG_GRID), dim3(256), 4 * PLds<P_HB>::bytes, st, s, t, mtraw, c, r0);
+  if (s.G > 1 && r1 > r0) {  // pack the chunk's records for the exchange
+    const int nbq = (r1 - r0 + P_PACK - 1) / P_PACK;
+    hipLaunchKernelGGL(gm_p_pack_count, dim3(s.G * nbq), dim3(P_PACK), 0, st, s, c, r0, r1, nbq);
+    hipLaunchKernelGGL(gm_p_pack_scan, dim3(s.G), dim3(1024), 0, st, s, c, nbq);
+    hipLaunchKernelGGL(gm_p_pack_copy, dim3(s.G * nbq), dim3(P_PACK), 0, st, s, c, r0, r1, nbq);
+  } else if (s.G > 1) {
+    (void)hipMemsetAsync(s.send_cnt + (size_t)c * s.G, 0, sizeof(int32_t) * s.G, st);
+  }
   return hipGetLastError();
 }
 

@@ -37,7 +37,8 @@ EXPORTS = ["gm_parse_conf", "gm_create", "gm_destroy", "gm_tick", "gm_sync", "gm
            "gm_set_dropmsg", "gm_drain_events", "gm_event_counts", "gm_msgcount", "gm_read_row", "gm_read_nodes",
            "gm_dump_tables", "gm_tick_stats", "gm_set_timing", "gm_last_kernel_ms", "gm_crash_set", "gm_strerror",
            "gm_comm_unique_id", "gm_comm_init", "gm_shard_layout", "gm_shard_merge", "gm_shard_draw",
-           "gm_shard_accept", "gm_shard_end_tick", "gm_shard_loopback", "gm_partial_loopback_tick"]
+           "gm_shard_accept", "gm_shard_end_tick", "gm_shard_loopback", "gm_partial_loopback_tick",
+           "gm_shard_exchange_bytes"]
 
 _lib = None
 
@@ -79,6 +80,7 @@ def load_library():
         "gm_shard_layout": [ctypes.c_void_p, P(i32), P(i32)],
         "gm_shard_loopback": [P(ctypes.c_void_p), i32, i32, i32],
         "gm_partial_loopback_tick": [P(ctypes.c_void_p), i32],
+        "gm_shard_exchange_bytes": [ctypes.c_void_p, P(ctypes.c_int64)],
         "gm_shard_merge": [ctypes.c_void_p], "gm_shard_draw": [ctypes.c_void_p, i32, i32],
         "gm_shard_accept": [ctypes.c_void_p, i32, P(i32)], "gm_shard_end_tick": [ctypes.c_void_p],
     }
@@ -245,6 +247,11 @@ class Simulator:
     def shard_accept(self, d):
         v = ctypes.c_int32()
         self._call("gm_shard_accept", self.h, d, ctypes.byref(v))
+        return v.value
+
+    def exchange_bytes(self):
+        v = ctypes.c_int64()
+        self._call("gm_shard_exchange_bytes", self.h, ctypes.byref(v))
         return v.value
 
     def shard_end_tick(self):

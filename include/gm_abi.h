@@ -191,6 +191,8 @@ int gm_shard_loopback(gm_ctx **ctxs, int32_t G, int32_t what, int32_t D);
  * next tick reads), then appends the received rows to their targets inboxes.
  * gm_partial_loopback_tick does one such tick for G contexts on one device. */
 int gm_partial_loopback_tick(gm_ctx **ctxs, int32_t G);
+/* bytes this shard received from the other shards in the last tick's exchange */
+int gm_shard_exchange_bytes(gm_ctx *ctx, int64_t *bytes);
 
 /* Crash set of the SCALED fault schedule: `count` node indices, ascending,
  * chosen by a splitmix64-keyed permutation of [0, n) (host fault injection). */
