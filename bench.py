@@ -302,7 +302,9 @@ def main_partial(a):
                    "parallelism": f"row-shard x{world} (RCCL all-to-allv of lists)" if world > 1 else "single GPU"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                      "frac": (achieved / PEAK_HBM_GBPS) if achieved else None, "traffic": None,
-                     "kernel": "gm_p_tick", "kernel_ms": kernel_ms, "alg_bytes_per_launch": b_alg},
+                     "kernel": "gm_p_tick", "kernel_ms": kernel_ms, "alg_bytes_per_launch": b_alg,
+                     "note": "instruction-issue bound, not HBM bound: ~1050 VALU + ~880 SALU instructions per "
+                             "node (PMC, profiles/r01/partial/pmc_summary_n4m.txt; DESIGN.md PARTIAL)"},
     }
     if world > 1:
         out["roofline"]["note"] = "rank 0's local kernels (its n/G nodes)"
