@@ -322,7 +322,7 @@ static int create_partial(gm_ctx *c) {
   if (p.V < 2 || p.V > 32 || p.V > n) return GM_EUNSUPPORTED;
   const int t0 = c->cfg.init_t0;
   if (c->cfg.init_mode != 1 || t0 < 5 || t0 > GM_T_LIMIT / 2) return GM_EINVAL;
-  if (n > (1 << 25) - 1) return GM_EUNSUPPORTED;  // ids live in 25 bits of the LDS table words
+  if (n > (1 << 25) - 1) return GM_EUNSUPPORTED;  // ids live in 25 bits of the LDS table words and wire entries
   const int G = c->cfg.shard_count > 0 ? c->cfg.shard_count : 1;
   const int rank = c->cfg.shard_rank;
   if (rank < 0 || rank >= G || G > n || G > 256) return GM_EINVAL;
@@ -330,7 +330,7 @@ static int create_partial(gm_ctx *c) {
   p.rank = rank;
   p.n0 = (int)((int64_t)n * rank / G);
   p.nloc = (int)((int64_t)n * (rank + 1) / G) - p.n0;
-  p.rows = n;  // nloc own rows + room for one received list per remote sender (n - nloc)
+  p.rows = G > 1 ? p.nloc : n;  // own rows; received lists stay in recv_list (wire format)
   const int nl = p.nloc, R = n - nl;
   p.rd_seed = c->cfg.rd_seed;
   p.view_seed = c->cfg.view_seed;
@@ -371,6 +371,7 @@ static int create_partial(gm_ctx *c) {
     TRY(dalloc(c, &p.send_hdr, (size_t)G * nl * 8));
     TRY(dalloc(c, &p.send_list, (size_t)G * nl * p.V));
     TRY(dalloc(c, &p.recv_hdr, (size_t)std::max(R, 1) * 8));
+    for (int q = 0; q < 2; q++) TRY(dalloc(c, &p.recv_list[q], (size_t)std::max(R, 1) * p.V));
     TRY(dalloc(c, &p.recv_cnt, (size_t)p.nchunk * G));
     std::vector<int32_t> b(G + 1);
     for (int g = 0; g <= G; g++) b[g] = (int32_t)((int64_t)n * g / G);
@@ -1156,10 +1157,10 @@ static int partial_exchange_chunk(gm_ctx *c, int ch, int64_t *roff) {
     off += (size_t)rc[q];
   }
   if (off > (size_t)(p.n - nl)) return GM_ESTATE;
-  uint64_t *rows_in = p.lists + ((size_t)(c->t & 1) * p.rows + nl) * V;
   NCCLCHECK(ncclAllToAllv(p.send_hdr, hs.data(), hsd.data(), p.recv_hdr, hr.data(), hrd.data(), ncclInt32, c->comm,
                           cs));
-  NCCLCHECK(ncclAllToAllv(p.send_list, ls.data(), lsd.data(), rows_in, lr.data(), lrd.data(), ncclUint64, c->comm, cs));
+  NCCLCHECK(ncclAllToAllv(p.send_list, ls.data(), lsd.data(), p.recv_list[c->t & 1], lr.data(), lrd.data(), ncclUint32, c->comm,
+                          cs));
   HIPCHECK(gm_launch_partial_unpack(p, c->t, (int)*roff, (int)(off - (size_t)*roff), cs));
   *roff = (int64_t)off;
   return GM_OK;
@@ -1209,9 +1210,8 @@ extern "C" int gm_partial_loopback_tick(gm_ctx **ctxs, int32_t G) {
         if (cnt > (size_t)sg.nloc || roff[q] + cnt > (size_t)(dq.n - dq.nloc)) return GM_ESTATE;
         HIPCHECK(hipMemcpyAsync(dq.recv_hdr + roff[q] * 8, sg.send_hdr + ((size_t)q * sg.nloc + r0) * 8,
                                 sizeof(int32_t) * 8 * cnt, hipMemcpyDeviceToDevice, st));
-        HIPCHECK(hipMemcpyAsync(dq.lists + ((size_t)(ctxs[q]->t & 1) * dq.rows + dq.nloc + roff[q]) * V,
-                                sg.send_list + ((size_t)q * sg.nloc + r0) * V, sizeof(uint64_t) * V * cnt,
-                                hipMemcpyDeviceToDevice, st));
+        HIPCHECK(hipMemcpyAsync(dq.recv_list[ctxs[q]->t & 1] + roff[q] * V, sg.send_list + ((size_t)q * sg.nloc + r0) * V,
+                                sizeof(uint32_t) * V * cnt, hipMemcpyDeviceToDevice, st));
         roff[q] += cnt;
       }
       HIPCHECK(gm_launch_partial_unpack(dq, ctxs[q]->t, (int)base, (int)(roff[q] - base), st));
@@ -1229,6 +1229,6 @@ extern "C" int gm_shard_exchange_bytes(gm_ctx *c, int64_t *bytes) {
   if (!c || !bytes) return GM_EINVAL;
   *bytes = 0;
   if (c->cfg.mode == GM_MODE_PARTIAL)  // received records of the last tick: 32 B header + the V-entry list
-    *bytes = c->p_recv_last * (int64_t)(32 + 8 * c->p.V);
+    *bytes = c->p_recv_last * (int64_t)(32 + 4 * c->p.V);
   return GM_OK;
 }

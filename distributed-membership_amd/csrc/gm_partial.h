@@ -10,6 +10,9 @@
 #define P_KMAX 64        // inbox capacity (lists queued per receiver per tick)
 #define P_EV_ADD 1u
 #define P_EV_REMOVE 2u
+// Wire entry of an exchanged list: id | (2t-1 - hb) << 25, only entries fresh at the
+// sender's tick t (the receiver drops the others anyway), 0 = none: 4 bytes instead of 8.
+#define P_WIRE_IDBITS 25
 
 struct PState {
   int n;                 // nodes of the whole cluster
@@ -17,13 +20,13 @@ struct PState {
   // row shard (multi-GPU S-C): this context owns nodes [n0, n0 + nloc); local row li = i - n0.
   // Single context: n0 = 0, nloc = n, G = 1.
   int n0, nloc, G, rank;
-  int rows;              // list rows per parity: nloc own rows + (n - nloc) rows of received remote lists
+  int rows;              // list rows per parity (= nloc: received lists stay in recv_list, wire format)
   int nchunk;            // K: the node ticks run in K row chunks; a shard ships chunk c's records while c+1 runs
   int drop_pct;          // per-entry drop percentage for this tick's deliveries (-1: none)
   uint64_t rd_seed, view_seed, drop_seed;
   uint64_t *lists;       // [2][rows][V] entries (id << 32 | hb), 0 = empty, sorted by id; parity t&1 written at tick t
   int32_t *inbox_cnt[2]; // [nloc] lists queued for each receiver, by delivery-tick parity
-  int32_t *inbox[2];     // [nloc][P_KMAX] list rows of the senders (local row, or nloc + received record)
+  int32_t *inbox[2];     // [nloc][P_KMAX] senders: local row li, or nloc + j for received record j
   int32_t *rsrc[2];      // [n - nloc] global sender index of each received list row, by parity
   int32_t *hbctr;        // [nloc] heartbeat counter
   int32_t *failed;       // [nloc]
@@ -39,13 +42,15 @@ struct PState {
   // chunk, gm_p_pack_* compact them (counts, scan, copy) into the send buffers.
   uint32_t *recmask;     // [nloc] shards li has a record for this tick
   int32_t *sp_hdr;       // [G][nloc][8] sparse records: header
-  uint64_t *sp_list;     // [G][nloc][V] sparse records: list
+  uint32_t *sp_list;     // [G][nloc][V] sparse records: list, wire entries (see P_WIRE below)
   int32_t *pack_blk;     // [G][nloc/256 + 2] per-block record counts, then offsets
   int32_t *send_cnt;     // [K][G] records of chunk c addressed to shard q
   int32_t *send_hdr;     // [G][nloc][8]: sender global index, #targets on that rank, targets (global), 0;
                          //   chunk c's records to q packed from slot q*nloc + r0_c on
-  uint64_t *send_list;   // [G][nloc][V]: the sender's final list of the tick
-  int32_t *recv_hdr;     // [n - nloc][8] received headers (their lists land in rows nloc.. of the tick's parity)
+  uint32_t *send_list;   // [G][nloc][V]: the sender's fresh entries of the tick, wire format
+  int32_t *recv_hdr;     // [n - nloc][8] received headers
+  uint32_t *recv_list[2]; // [n - nloc][V] received lists (wire format), by the parity of the tick that
+                         //   sent them; the next tick's kernels decode them in place
   int32_t *recv_cnt;     // [K][G] records received from each shard, per chunk
   int32_t *shard_n0;     // [G+1] first node of every row shard (shard_n0[G] = n)
   uint32_t *err;

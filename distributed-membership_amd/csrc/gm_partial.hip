@@ -201,7 +201,14 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
     const int j = st * per + jo;
     const bool ok = jo < per && j < kk;
     const int sn = __shfl(sv, ok ? j : 0, 64);
-    dv[st] = ok ? prev[(size_t)sn * V + l] : 0ull;
+    uint64_t e = 0;
+    if (ok && sn < s.nloc) {
+      e = prev[(size_t)sn * V + l];
+    } else if (ok) {  // a list another shard sent at t-1: wire entry id | (2(t-1)-1 - hb) << 25
+      const uint32_t w = s.recv_list[par ^ 1][(size_t)(sn - s.nloc) * V + l];
+      if (w) e = ((uint64_t)(w & ((1u << P_WIRE_IDBITS) - 1)) << 32) | (uint32_t)(2 * t - 3 - (int)(w >> P_WIRE_IDBITS));
+    }
+    dv[st] = e;
   }
   // drop keys: one (t_send, src, dst) hash per delivered list, lane j for list j
   const bool dropping = s.drop_pct >= 0;
@@ -526,7 +533,11 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
       if (lane < 8)
         s.sp_hdr[rec * 8 + lane] = lane == 0 ? i : lane == 1 ? nt : lane == 2 ? tv0 : lane == 3 ? tv1
                                  : lane == 4 ? tv2 : lane == 5 ? tv3 : lane == 6 ? tv4 : 0;
-      if (lane < V) s.sp_list[rec * V + lane] = x;
+      if (lane < V) {  // wire entry: fresh entries only, heartbeat as distance from this tick's 2t-1
+        const uint32_t hb = (uint32_t)x;
+        const bool fresh = lane < cnt && p_age(t, hb) < GM_TFAIL;
+        s.sp_list[rec * V + lane] = fresh ? ((uint32_t)(x >> 32) | ((uint32_t)(2 * t - 1) - hb) << P_WIRE_IDBITS) : 0u;
+      }
     }
   }
   if (s.G > 1 && lane == 0) s.recmask[li] = rmask;
@@ -692,7 +703,7 @@ __global__ __launch_bounds__(P_PACK) void gm_p_pack_copy(PState s, int c, int r0
     const size_t src = (size_t)q * s.nloc + lst[k];
     const size_t dst = (size_t)q * s.nloc + r0 + base + k;
     if (lane < 4) ((uint2 *)(s.send_hdr + dst * 8))[lane] = ((const uint2 *)(s.sp_hdr + src * 8))[lane];
-    else if (lane < 4 + V) s.send_list[dst * V + lane - 4] = s.sp_list[src * V + lane - 4];
+    else if (lane < 4 + V) s.send_list[dst * V + lane - 4] = s.sp_list[src * V + lane - 4];  // wire entries
   }
 }
 
