@@ -1129,9 +1129,9 @@ static int tick_sharded(gm_ctx *c) {
 // ------------------------------------------------------------ PARTIAL row shards
 // After the local kernels of tick t every shard holds, per remote shard q, the
 // records its nodes address to q (header + list). All-to-all of the record counts,
-// then all-to-allv of the headers and of the lists, which land directly in rows
-// nloc.. of parity t&1 (where tick t+1 reads its senders' lists); gm_p_unpack
-// appends each received row to its targets' inboxes.
+// then all-to-allv of the headers and of the lists (wire format), which land in
+// recv_list[t&1] (where tick t+1 reads its senders' lists); gm_p_unpack appends
+// each received record to its targets' inboxes.
 static int partial_exchange_chunk(gm_ctx *c, int ch, int64_t *roff) {
   PState &p = c->p;
   const int G = p.G, V = p.V, nl = p.nloc;

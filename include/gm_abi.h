@@ -187,8 +187,8 @@ int gm_shard_loopback(gm_ctx **ctxs, int32_t G, int32_t what, int32_t D);
  * range; gm_read_nodes / gm_dump_tables / gm_drain_events / gm_tick_stats report
  * its own nodes, with global indices). With RCCL attached (gm_comm_init) gm_tick
  * runs the local kernels, then ncclAllToAll of per-shard record counts and two
- * ncclAllToAllv (record headers; the V-entry lists, straight into the rows the
- * next tick reads), then appends the received rows to their targets inboxes.
+ * ncclAllToAllv (record headers; the lists' fresh entries, 4 bytes each, read in
+ * place by the next tick), then appends the received records to their targets' inboxes.
  * gm_partial_loopback_tick does one such tick for G contexts on one device. */
 int gm_partial_loopback_tick(gm_ctx **ctxs, int32_t G);
 /* bytes this shard received from the other shards in the last tick's exchange */
