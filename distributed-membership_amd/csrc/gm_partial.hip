@@ -286,13 +286,16 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
       alive |= (valid & ~rem) << u;
     }
     int tot;
-    (void)p_excl<TS == 8 ? 4 : 5>(rcount, &removed);
-    const int ro = __builtin_popcount(rown);
-    int rpos = p_excl<TS == 8 ? 4 : 5>(ro, &nrem);
-    if (nrem) {  // REMOVE events of the node's own entries, from the back of its event row
+    removed = nrem = 0;
+    if (__ballot(rcount != 0)) {  // rare: TREMOVE removals in this row
+      (void)p_excl<TS == 8 ? 4 : 5>(rcount, &removed);
+      const int ro = __builtin_popcount(rown);
+      int rpos = p_excl<TS == 8 ? 4 : 5>(ro, &nrem);
+      if (nrem) {  // REMOVE events of the node's own entries, from the back of its event row
 #pragma unroll
-      for (int u = 0; u < TS; u++)
-        if ((rown >> u) & 1) evr[2 * V - 1 - rpos++] = (P_EV_REMOVE << 30) | (w[u] & P_IDMASK);
+        for (int u = 0; u < TS; u++)
+          if ((rown >> u) & 1) evr[2 * V - 1 - rpos++] = (P_EV_REMOVE << 30) | (w[u] & P_IDMASK);
+      }
     }
     int pos = p_excl<TS == 8 ? 4 : 5>(__builtin_popcount(alive), &tot);
     m = tot;

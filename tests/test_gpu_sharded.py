@@ -24,7 +24,8 @@ def merge_dumps(dumps, owners):
     return ("\n".join(out) + "\n").encode()
 
 
-@pytest.mark.parametrize("n,world,drop,warm", [(256, 2, 0, 0), (600, 3, 0, 1), (512, 2, 25, 0), (1100, 4, 10, 1)])
+@pytest.mark.parametrize("n,world,drop,warm", [(256, 2, 0, 0), (600, 3, 0, 1), (512, 2, 25, 0), (1100, 4, 10, 1),
+                                               (2048, 8, 10, 1)])
 def test_shards_match_fused_kernel(n, world, drop, warm):
     kw = dict(rd_seed=7, drop_pct=drop, drop_from=3, drop_to=25, drop_seed=42, init_mode=warm,
               init_t0=6 if warm else 0, init_seed=5)
