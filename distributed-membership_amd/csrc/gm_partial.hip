@@ -55,6 +55,8 @@ __device__ __forceinline__ void p_wsync() {
 }
 
 __device__ __forceinline__ int p_age(int t, uint32_t hb) { return t - (int)((hb + 1u) >> 1); }
+// p_age(t, hb) >= A as one compare: t - floor((hb+1)/2) >= A <=> hb < 2(t-A)+1 (heartbeats < 2^31)
+__device__ __forceinline__ bool p_aged(int t, uint32_t hb, int A) { return (int)hb < 2 * (t - A) + 1; }
 
 // eviction tie-break key (oracle op_evict_key): distinct ids give distinct keys;
 // kseed = mix64(view_seed ^ t) is wave-uniform
@@ -280,7 +282,7 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
 #pragma unroll
     for (int u = 0; u < TS; u++) {  // branch-free: exec-mask traffic is what this kernel spends SALU on
       const uint32_t valid = (w[u] & P_IDMASK) != 0;
-      const uint32_t rem = valid & (uint32_t)(p_age(t, hh[u]) >= GM_TREMOVE);
+      const uint32_t rem = valid & (uint32_t)p_aged(t, hh[u], GM_TREMOVE);
       rcount += (int)rem;
       rown |= (rem & (w[u] >> 31)) << u;
       alive |= (valid & ~rem) << u;
@@ -312,19 +314,25 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
   }
   p_wsync();
   // ---- 4. dense entries e = s*64 + lane; eviction to V
+  // only the first dm = ceil(m / 64) of the DS per-lane slots hold entries (m is wave-uniform):
+  // every per-slot loop below skips the rest with a scalar branch
+  const int dm = (m + 63) >> 6;
   uint32_t dw[DS], dh[DS];
 #pragma unroll
   for (int q = 0; q < DS; q++) {  // DS*64 < H: the reads stay inside the table
-    const int e = q * 64 + lane;
-    const uint32_t a = tid[e], b = thb[e];
-    dw[q] = e < m ? a : 0u;
-    dh[q] = e < m ? b : 0u;
+    dw[q] = dh[q] = 0u;
+    if (q < dm) {
+      const int e = q * 64 + lane;
+      const uint32_t a = tid[e], b = thb[e];
+      dw[q] = e < m ? a : 0u;
+      dh[q] = e < m ? b : 0u;
+    }
   }
   uint32_t keep = 0;
   if (m <= V) {
 #pragma unroll
     for (int q = 0; q < DS; q++)
-      if (dw[q]) keep |= 1u << q;
+      if (q < dm && dw[q]) keep |= 1u << q;
   } else {
     // heartbeat distance from the top (2t-1 = this tick's self heartbeat); alive
     // entries have age < TREMOVE, i.e. distance <= 40 < 64
@@ -333,7 +341,8 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
     p_wsync();
 #pragma unroll
     for (int q = 0; q < DS; q++)  // entries that do not count go to a private trash word
-      atomicAdd((dw[q] && !(dw[q] & P_SELF)) ? &hist[min(max(top - (int)dh[q], 0), 63)] : &tid[H - 64 + lane], 1u);
+      if (q < dm)
+        atomicAdd((dw[q] && !(dw[q] & P_SELF)) ? &hist[min(max(top - (int)dh[q], 0), 63)] : &tid[H - 64 + lane], 1u);
     p_wsync();
     const int need = V - 1;  // self is always kept
     int c = (int)hist[lane];
@@ -346,6 +355,7 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
     uint32_t bucket = 0;
 #pragma unroll
     for (int q = 0; q < DS; q++) {
+      if (q >= dm) continue;
       const int d = min(max(top - (int)dh[q], 0), 63);
       const uint32_t v = dw[q] != 0;
       keep |= (v & (uint32_t)(((dw[q] & P_SELF) != 0) | (d < dcut))) << q;
@@ -361,13 +371,14 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
 #pragma unroll
       for (int q = 0; q < DS; q++) {
         key[q] = ~0ull;
-        if (__ballot((bucket >> q) & 1)) key[q] = ((bucket >> q) & 1) ? p_evict_key(kseed, i, dw[q] & P_IDMASK) : ~0ull;
+        if (q < dm && __ballot((bucket >> q) & 1)) key[q] = ((bucket >> q) & 1) ? p_evict_key(kseed, i, dw[q] & P_IDMASK) : ~0ull;
       }
       p_wsync();
       hist[lane] = 0;
       p_wsync();
 #pragma unroll
-      for (int q = 0; q < DS; q++) atomicAdd(((bucket >> q) & 1) ? &hist[key[q] >> 58] : &tid[H - 64 + lane], 1u);
+      for (int q = 0; q < DS; q++)
+        if (q < dm) atomicAdd(((bucket >> q) & 1) ? &hist[key[q] >> 58] : &tid[H - 64 + lane], 1u);
       p_wsync();
       c = (int)hist[lane];
       inc = p_scan(c, lane);
@@ -379,6 +390,7 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
       uint32_t cand = 0;
 #pragma unroll
       for (int q = 0; q < DS; q++) {
+        if (q >= dm) continue;
         const uint32_t b = (bucket >> q) & 1;
         const int bin = (int)(key[q] >> 58);
         keep |= (b & (uint32_t)(bin < bcut)) << q;
@@ -391,7 +403,7 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
           uint64_t mn = ~0ull;
 #pragma unroll
           for (int q = 0; q < DS; q++)
-            if ((cand >> q) & 1) mn = min(mn, key[q]);
+            if (q < dm && ((cand >> q) & 1)) mn = min(mn, key[q]);
 #pragma unroll
           for (int o = 32; o >= 1; o >>= 1) {
             const uint32_t lo = __shfl_xor((uint32_t)mn, o, 64), hi = __shfl_xor((uint32_t)(mn >> 32), o, 64);
@@ -399,7 +411,7 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
           }
 #pragma unroll
           for (int q = 0; q < DS; q++)
-            if (((cand >> q) & 1) && key[q] == mn) {
+            if (q < dm && ((cand >> q) & 1) && key[q] == mn) {
               keep |= 1u << q;
               cand &= ~(1u << q);
             }
@@ -412,24 +424,26 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
   p_wsync();  // the eviction histogram is dead: it takes the stores of the entries not kept
 #pragma unroll
   for (int q = 0; q < DS; q++) {
+    if (q >= dm) break;
     const bool kq = (keep >> q) & 1;
     const uint64_t bal = __ballot(kq);
     const int p = cnt + p_below(bal);
-    *(kq ? kid + p : hist + lane) = dw[q];
+    // id word rotated left by 2: id << 2 | own << 1 | self (ids < 2^25, bits 25..29 clear),
+    // so the rank below compares whole words
+    *(kq ? kid + p : hist + lane) = __builtin_amdgcn_alignbit(dw[q], dw[q], 30);
     *(kq ? khb + p : hist + lane) = dh[q];
     cnt += __builtin_popcountll(bal);
   }
-  if (lane >= cnt && lane < P_VMAX) kid[lane] = P_IDMASK;  // sentinel ids rank after every real one
+  if (lane >= cnt && lane < P_VMAX) kid[lane] = ~0u;  // sentinels rank after every real entry
   p_wsync();
   {
     const uint32_t mw = lane < cnt ? kid[lane] : 0u, mh = lane < cnt ? khb[lane] : 0u;
-    const uint32_t myid = mw & P_IDMASK;
+    const uint32_t myid = mw >> 2;
     int rank = 0;
 #pragma unroll
-    for (int q = 0; q < P_VMAX / 4; q++) {  // broadcast reads, 4 ids each
+    for (int q = 0; q < P_VMAX / 4; q++) {  // broadcast reads, 4 ids each (ids are distinct)
       const uint4 v = ((const uint4 *)kid)[q];
-      rank += ((v.x & P_IDMASK) < myid) + ((v.y & P_IDMASK) < myid) + ((v.z & P_IDMASK) < myid) +
-              ((v.w & P_IDMASK) < myid);
+      rank += (v.x < mw) + (v.y < mw) + (v.z < mw) + (v.w < mw);
     }
     p_wsync();
     if (lane < cnt) {
@@ -442,10 +456,10 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
   const uint32_t f = lane < cnt ? kid[lane] : 0u;
   if (lane < V) cur[(size_t)li * V + lane] = x;
   // joins (ascending id) from the front of the event row
-  const uint64_t jb = __ballot(lane < cnt && !(f & P_OWN));
+  const uint64_t jb = __ballot(lane < cnt && !(f & 2u));  // rotated P_OWN
   const int nj = __builtin_popcountll(jb);
-  if (lane < cnt && !(f & P_OWN)) evr[p_below(jb)] = (P_EV_ADD << 30) | (uint32_t)(x >> 32);
-  const int numfailed = removed + __builtin_popcountll(__ballot(lane < cnt && p_age(t, (uint32_t)x) >= GM_TFAIL));
+  if (lane < cnt && !(f & 2u)) evr[p_below(jb)] = (P_EV_ADD << 30) | (uint32_t)(x >> 32);
+  const int numfailed = removed + __builtin_popcountll(__ballot(lane < cnt && p_aged(t, (uint32_t)x, GM_TFAIL)));
   // ---- 6. gossip draw over the final list (MP1Node.cpp:449-489), on scalar registers
   const int numpot = cnt - 1 - numfailed;
   const int target = min(GM_FANOUT, numpot);
@@ -484,7 +498,7 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
         const uint64_t e = p_readlane64(x, ixd);
         const int c = (int)(e >> 32) - 1;
         if (c == i) continue;                                    // "me"
-        if (p_age(t, (uint32_t)e) >= GM_TFAIL) continue;          // age >= TFAIL
+        if (p_aged(t, (uint32_t)e, GM_TFAIL)) continue;           // age >= TFAIL
         if ((ng > 0 && g0 == c) || (ng > 1 && g1 == c) || (ng > 2 && g2 == c) || (ng > 3 && g3 == c)) continue;
         if (ng == 0) g0 = c;
         else if (ng == 1) g1 = c;
@@ -538,7 +552,7 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
                                  : lane == 4 ? tv2 : lane == 5 ? tv3 : lane == 6 ? tv4 : 0;
       if (lane < V) {  // wire entry: fresh entries only, heartbeat as distance from this tick's 2t-1
         const uint32_t hb = (uint32_t)x;
-        const bool fresh = lane < cnt && p_age(t, hb) < GM_TFAIL;
+        const bool fresh = lane < cnt && !p_aged(t, hb, GM_TFAIL);
         s.sp_list[rec * V + lane] = fresh ? ((uint32_t)(x >> 32) | ((uint32_t)(2 * t - 1) - hb) << P_WIRE_IDBITS) : 0u;
       }
     }
