@@ -282,6 +282,13 @@ def main_partial(a):
     # per delivered list the sender's list (8V B) + its inbox word
     b_alg = n_live * (16 * V + 120) + m_lists * (8 * V + 4)
     achieved = b_alg / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else None
+    traffic = None  # PMC FETCH_SIZE/WRITE_SIZE of the same tick pair (committed passes; N=16M, V=32 only)
+    tpath = os.path.join(REPO, "profiles", f"traffic_sc_n{n}.json")
+    if world == 1 and V == 32 and os.path.exists(tpath):
+        with open(tpath) as f:
+            tj = json.load(f)
+        if tj.get("layout") == "partial-v32":
+            traffic = tj.get("hbm_bytes_per_launch")
     out = {
         "metric": "simulated node-ticks/sec (S-C partial view)",
         "value": n * a.steps / elapsed,
@@ -301,10 +308,11 @@ def main_partial(a):
                    "live": n_live_all, "lists_per_tick": m_lists_all, "max_inbox": st["max_inbox"],
                    "parallelism": f"row-shard x{world} (RCCL all-to-allv of lists)" if world > 1 else "single GPU"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
-                     "frac": (achieved / PEAK_HBM_GBPS) if achieved else None, "traffic": None,
+                     "frac": (achieved / PEAK_HBM_GBPS) if achieved else None, "traffic": traffic,
                      "kernel": "gm_p_tick", "kernel_ms": kernel_ms, "alg_bytes_per_launch": b_alg,
-                     "note": "instruction-issue bound, not HBM bound: ~1050 VALU + ~880 SALU instructions per "
-                             "node (PMC, profiles/r01/partial/pmc_summary_n4m.txt; DESIGN.md PARTIAL)"},
+                     "note": "instruction-issue bound, not HBM bound: ~900 VALU + ~940 SALU instructions per "
+                             "node, both issue ports ~70% busy (PMC, profiles/r01/partial_v2/variants/pmc_base.txt; "
+                             "DESIGN.md PARTIAL)"},
     }
     if world > 1:
         out["roofline"]["note"] = "rank 0's local kernels (its n/G nodes)"
