@@ -460,59 +460,86 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
   const int nj = __builtin_popcountll(jb);
   if (lane < cnt && !(f & 2u)) evr[p_below(jb)] = (P_EV_ADD << 30) | (uint32_t)(x >> 32);
   const int numfailed = removed + __builtin_popcountll(__ballot(lane < cnt && p_aged(t, (uint32_t)x, GM_TFAIL)));
-  // ---- 6. gossip draw over the final list (MP1Node.cpp:449-489), on scalar registers
+  // ---- 6. gossip draw over the final list (MP1Node.cpp:449-489)
   const int numpot = cnt - 1 - numfailed;
   const int target = min(GM_FANOUT, numpot);
-  int ng = 0, g0 = -1, g1 = -1, g2 = -1, g3 = -1, g4 = -1;
+  int ng = 0;
+  uint32_t *gl = hist;  // the chosen targets in draw order (hist is free after the compaction)
   if (numpot > 0) {
     const uint32_t size = (uint32_t)cnt;
     const uint32_t thr = (0u - size) % size;
-    GmLazyMT mt;
-    bool done = false;
-    for (int batch = 0; !done; batch++) {
-      if (batch > (1 << 16)) {
-        if (lane == 0) atomicOr(s.err, GM_ERR_DRAWS);
-        break;
-      }
-      uint32_t raw = raw0;
-      if (batch > 0) {  // outputs past the precomputed 16: lazy generator in the (free) table region
+    {  // the 16 precomputed outputs in parallel, output d on lane d: it is taken iff Lemire
+       // accepts it, the drawn entry is not "me" and not aged, and no earlier such output drew
+       // the same id (that one was taken, or repeated a taken one) -- the reference's loop
+      const uint64_t prod = (uint64_t)raw0 * size;
+      const int ixv = lane < 16 ? (int)(prod >> 32) : 0;
+      const uint32_t elo = __shfl((uint32_t)x, ixv, 64), ehi = __shfl((uint32_t)(x >> 32), ixv, 64);
+      const int c = (int)ehi - 1;
+      const bool ok = lane < 16 && (uint32_t)prod >= thr && c != i && !p_aged(t, elo, GM_TFAIL);
+      const int cv = ok ? c : -2;
+      bool dup = false;
+#pragma unroll
+      for (int q = 0; q < 15; q++) dup |= lane > q && __builtin_amdgcn_readlane(cv, q) == cv;
+      const bool acc = ok && !dup;
+      const uint64_t ab = __ballot(acc);
+      const int rk = p_below(ab);
+      ng = min(__builtin_popcountll(ab), target);
+      gl[acc && rk < target ? rk : 16 + lane] = (uint32_t)c;  // others: trash words past the targets
+    }
+    if (ng < target) {  // rare: more outputs, from the lazy generator in the (free) table region
+      p_wsync();
+      int g0 = -1, g1 = -1, g2 = -1, g3 = -1, g4 = -1;
+      if (ng > 0) g0 = (int)__builtin_amdgcn_readfirstlane(gl[0]);
+      if (ng > 1) g1 = (int)__builtin_amdgcn_readfirstlane(gl[1]);
+      if (ng > 2) g2 = (int)__builtin_amdgcn_readfirstlane(gl[2]);
+      if (ng > 3) g3 = (int)__builtin_amdgcn_readfirstlane(gl[3]);
+      GmLazyMT mt;
+      bool done = false;
+      for (int batch = 1; !done; batch++) {
+        if (batch > (1 << 16)) {
+          if (lane == 0) atomicOr(s.err, GM_ERR_DRAWS);
+          break;
+        }
         if (lane == 0 && batch == 1) {
           mt.seed(tid, gm_rd_seed(s.rd_seed, t, i + 1));
           for (int q = 0; q < 16; q++) (void)mt.next();
         }
-        raw = 0;
+        uint32_t raw = 0;
         for (int q = 0; q < 16; q++) {
           uint32_t o = 0;
           if (lane == 0) o = mt.next();
           o = __builtin_amdgcn_readfirstlane(o);
           if (lane == q) raw = o;
         }
+        const uint64_t prod = (uint64_t)raw * size;
+        const int ix = (int)(prod >> 32);
+        uint64_t mk = __ballot(lane < 16 && (uint32_t)prod >= thr);
+        while (mk && !done) {
+          const int d = __builtin_ctzll(mk);
+          mk &= mk - 1;
+          const int ixd = __builtin_amdgcn_readlane(ix, d);
+          const uint64_t e = p_readlane64(x, ixd);
+          const int c = (int)(e >> 32) - 1;
+          if (c == i) continue;                                    // "me"
+          if (p_aged(t, (uint32_t)e, GM_TFAIL)) continue;           // age >= TFAIL
+          if ((ng > 0 && g0 == c) || (ng > 1 && g1 == c) || (ng > 2 && g2 == c) || (ng > 3 && g3 == c)) continue;
+          if (ng == 0) g0 = c;
+          else if (ng == 1) g1 = c;
+          else if (ng == 2) g2 = c;
+          else if (ng == 3) g3 = c;
+          else g4 = c;
+          ng++;
+          if (ng >= target) done = true;
+        }
       }
-      const uint64_t prod = (uint64_t)raw * size;
-      const int ix = (int)(prod >> 32);
-      uint64_t mk = __ballot(lane < 16 && (uint32_t)prod >= thr);
-      while (mk && !done) {
-        const int d = __builtin_ctzll(mk);
-        mk &= mk - 1;
-        const int ixd = __builtin_amdgcn_readlane(ix, d);
-        const uint64_t e = p_readlane64(x, ixd);
-        const int c = (int)(e >> 32) - 1;
-        if (c == i) continue;                                    // "me"
-        if (p_aged(t, (uint32_t)e, GM_TFAIL)) continue;           // age >= TFAIL
-        if ((ng > 0 && g0 == c) || (ng > 1 && g1 == c) || (ng > 2 && g2 == c) || (ng > 3 && g3 == c)) continue;
-        if (ng == 0) g0 = c;
-        else if (ng == 1) g1 = c;
-        else if (ng == 2) g2 = c;
-        else if (ng == 3) g3 = c;
-        else g4 = c;
-        ng++;
-        if (ng >= target) done = true;
-      }
+      p_wsync();
+      if (lane < ng) gl[lane] = (uint32_t)(lane == 0 ? g0 : lane == 1 ? g1 : lane == 2 ? g2 : lane == 3 ? g3 : g4);
     }
   }
+  p_wsync();
   // ---- sends: one parallel round of inbox appends, one lane per target; targets owned by
   // another row shard get one record per (sender, shard): header + this tick's list
-  const int dst = lane >= ng ? 0 : lane == 0 ? g0 : lane == 1 ? g1 : lane == 2 ? g2 : lane == 3 ? g3 : g4;
+  const int dst = lane < ng ? (int)gl[lane] : 0;
   const int owner = (s.G > 1 && lane < ng) ? p_owner(s, dst) : s.rank;
   if (lane < ng) {
     s.targets[(size_t)li * GM_FANOUT + lane] = dst;
