@@ -437,14 +437,20 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
   if (lane >= cnt && lane < P_VMAX) kid[lane] = ~0u;  // sentinels rank after every real entry
   p_wsync();
   {
-    const uint32_t mw = lane < cnt ? kid[lane] : 0u, mh = lane < cnt ? khb[lane] : 0u;
+    // entry e = lane % 32 on both half-waves; each half compares it against half of the
+    // kept ids (cnt <= P_VMAX = 32), the two partial ranks add across the halves
+    static_assert(P_VMAX == 32, "the id rank splits a wave into two half-waves of P_VMAX lanes");
+    const int e = lane & (P_VMAX - 1);
+    const uint32_t mw = e < cnt ? kid[e] : 0u, mh = e < cnt ? khb[e] : 0u;
     const uint32_t myid = mw >> 2;
     int rank = 0;
+    const uint4 *kv = (const uint4 *)kid + (lane >> 5) * (P_VMAX / 8);
 #pragma unroll
-    for (int q = 0; q < P_VMAX / 4; q++) {  // broadcast reads, 4 ids each (ids are distinct)
-      const uint4 v = ((const uint4 *)kid)[q];
+    for (int q = 0; q < P_VMAX / 8; q++) {  // broadcast reads, 4 ids each (ids are distinct)
+      const uint4 v = kv[q];
       rank += (v.x < mw) + (v.y < mw) + (v.z < mw) + (v.w < mw);
     }
+    rank += __shfl_xor(rank, 32, 64);
     p_wsync();
     if (lane < cnt) {
       fin[rank] = ((uint64_t)myid << 32) | mh;
