@@ -477,15 +477,22 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
     {  // the 16 precomputed outputs in parallel, output d on lane d: it is taken iff Lemire
        // accepts it, the drawn entry is not "me" and not aged, and no earlier such output drew
        // the same id (that one was taken, or repeated a taken one) -- the reference's loop
-      const uint64_t prod = (uint64_t)raw0 * size;
-      const int ixv = lane < 16 ? (int)(prod >> 32) : 0;
+      // every 16-lane group g evaluates all 16 outputs (output d = lane % 16) and tests
+      // d against the earlier outputs q in [4g, 4g + 4); the groups' results are OR-ed
+      const int d = lane & 15, g4 = (lane >> 4) * 4;
+      const uint32_t rawd = __shfl(raw0, d, 64);
+      const uint64_t prod = (uint64_t)rawd * size;
+      const int ixv = (int)(prod >> 32);
       const uint32_t elo = __shfl((uint32_t)x, ixv, 64), ehi = __shfl((uint32_t)(x >> 32), ixv, 64);
       const int c = (int)ehi - 1;
-      const bool ok = lane < 16 && (uint32_t)prod >= thr && c != i && !p_aged(t, elo, GM_TFAIL);
-      const int cv = ok ? c : -2;
-      bool dup = false;
+      const bool okd = (uint32_t)prod >= thr && c != i && !p_aged(t, elo, GM_TFAIL);
+      const int cv = okd ? c : -2;
+      int dup = 0;
 #pragma unroll
-      for (int q = 0; q < 15; q++) dup |= lane > q && __builtin_amdgcn_readlane(cv, q) == cv;
+      for (int j = 0; j < 4; j++) dup |= (g4 + j < d) & (__shfl(cv, g4 + j, 64) == cv);
+      dup |= __shfl_xor(dup, 16, 64);
+      dup |= __shfl_xor(dup, 32, 64);
+      const bool ok = lane < 16 && okd;
       const bool acc = ok && !dup;
       const uint64_t ab = __ballot(acc);
       const int rk = p_below(ab);
