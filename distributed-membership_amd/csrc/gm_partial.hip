@@ -64,13 +64,16 @@ __device__ __forceinline__ uint64_t p_evict_key(uint64_t kseed, int obs, uint32_
   return gm_mix64(kseed ^ (((uint64_t)(uint32_t)obs << 32) | id));
 }
 
-// wave-wide inclusive scan of ints
-__device__ __forceinline__ int p_scan(int v, int lane) {
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(v, o, 64);
-    if (lane >= o) v += y;
-  }
+// wave-wide inclusive scan of ints on DPP: row_shr 1/2/4/8 scans each 16-lane row,
+// row_bcast15 / row_bcast31 carry the row totals upward (lanes a DPP source does not
+// reach keep the identity 0)
+__device__ __forceinline__ int p_scan(int v, int) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);  // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);  // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);  // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);  // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
   return v;
 }
 
