@@ -27,7 +27,8 @@
 //      exact min-selection pick the smallest keys -- no full sort;
 //   5. the <= V kept entries are ranked by id (broadcast LDS compare) = the
 //      id-sorted list, stored as one coalesced row;
-//   6. the gossip draw runs on scalar registers (readlane of the drawn entry).
+//   6. the gossip draw: the 16 precomputed S2 outputs resolved in parallel across
+//      the wave (duplicates by shuffle-compares), the rare rest on scalars.
 // Nodes with more than P_KSMALL delivered lists (Poisson tail, ~1.4 %) do not fit
 // the small table: the small kernel defers them to a worklist that the big
 // kernel (1024-slot table, sender sort for > P_KP lists) drains.
