@@ -494,8 +494,10 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
       int dup = 0;
 #pragma unroll
       for (int j = 0; j < 4; j++) dup |= (g4 + j < d) & (__shfl(cv, g4 + j, 64) == cv);
-      dup |= __shfl_xor(dup, 16, 64);
-      dup |= __shfl_xor(dup, 32, 64);
+      uint64_t db = __ballot(dup);  // OR of the four groups' verdicts, bit d
+      db |= db >> 32;
+      db |= db >> 16;
+      dup = (int)((uint32_t)db >> d) & 1;
       const bool ok = lane < 16 && okd;
       const bool acc = ok && !dup;
       const uint64_t ab = __ballot(acc);
