@@ -33,6 +33,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "distributed-membership_amd"))
 
 PEAK_HBM_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+LAYOUT_SA = "narrow-band"  # profiles/traffic_n65536.json must describe this payload layout
 
 
 class Roctx:
@@ -117,6 +118,7 @@ def main():
         sim.comm_init(comm_unique_id(), 1, 0)
     else:
         sim = Simulator(n, GM_MODE_SCALED, rd_seed=7, device=local, **init)
+    sim.keep_events(0)  # no per-tick staging of join/remove records; the device counts them (gm_event_totals)
     crash = crash_set(n, ncrash, 42)
     while sim.time <= a.prologue:
         t = sim.time
@@ -151,6 +153,15 @@ def main():
     kernel_ms = sim.last_kernel_ms()
     st = sim.tick_stats()
     assert st["err"] == 0, st
+    # self-check of the measured workload (outside the timed window): the window holds the
+    # TREMOVE sweep of the crashed nodes (MP1Node.cpp:429-444) -- every live observer removed
+    # every crashed node exactly once, nothing else was removed or joined (device counters)
+    tot = sim.event_totals()
+    removed_ok = (a.prologue + a.warmup + a.steps >= a.crash_tick + 25 and a.t0 > 0)
+    if removed_ok:
+        c0, wl = sim.shard_layout() if world > 1 else (0, n)  # a column shard counts its own columns
+        crash_here = int(((crash >= c0) & (crash < c0 + wl)).sum())
+        assert tot["removed"] == (n - ncrash) * crash_here and tot["joined"] == 0, (tot, n - ncrash, crash_here)
 
     n_live, m_lists = st["live"], st["lists"]
     W = sim.shard_layout()[1] if world > 1 else n  # this rank's subject columns
@@ -163,14 +174,20 @@ def main():
     # the survey's int32 (hb, ts) formulation of the same work
     b_survey = 16 * n_live * W + 8 * m_lists * W
     achieved = b_alg / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else None
-    traffic = None
+    # DRAM bytes the layout cannot avoid: the cell read + write and the payload write per
+    # live cell, plus ONE read of each sender's payload (its ~5 re-reads are served by the
+    # Infinity Cache while the band is in flight; FETCH_SIZE counts those hits too)
+    dram_est = 6 * n_live * W
+    frac_dram = (dram_est / (kernel_ms * 1e-3) / 1e9 / PEAK_HBM_GBPS) if kernel_ms > 0 else None
+    traffic, traffic_src = None, None
     tpath_ok = world == 1
     tpath = os.path.join(REPO, "profiles", f"traffic_n{n}.json")
     if tpath_ok and os.path.exists(tpath):
         with open(tpath) as f:
             tj = json.load(f)
-        if tj.get("layout") == "narrow-band":
+        if tj.get("layout") == LAYOUT_SA:
             traffic = tj.get("hbm_bytes_per_launch")
+            traffic_src = f"profiles/traffic_n{n}.json ({tj.get('generated', 'r01')}, rocprofv3 --pmc passes by scripts/gpu.sh pmc_sa)"
 
     value = n * a.steps / elapsed
     out = {
@@ -192,9 +209,13 @@ def main():
                    ("column-shard x1 (RCCL, forced)" if a.force_shard else "single GPU")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                      "frac": (achieved / PEAK_HBM_GBPS) if achieved else None, "traffic": traffic,
+                     "traffic_source": traffic_src,
                      "kernel": "gm_s_band", "kernel_ms": kernel_ms,
                      "alg_bytes_per_launch": b_alg, "survey_int32_bytes_per_launch": b_survey,
+                     "dram_bytes_est": dram_est, "frac_dram": frac_dram,
                      "columns_per_gpu": W},
+        "check": {"removed_rank0": tot["removed"], "joined_rank0": tot["joined"], "removed_all_expected":
+                  (n - ncrash) * ncrash if removed_ok else None},
     }
     if rank == 0 and world == 1 and not a.no_cpu:
         sys.path.insert(0, os.path.join(REPO, "tests"))
@@ -238,6 +259,7 @@ def main_partial(a):
     if a.force_shard and world == 1:  # diagnostics: the row-shard exchange with one RCCL rank
         os.environ["GM_FORCE_SHARD"] = "1"
     sim = Simulator(n, GM_MODE_PARTIAL, device=local, shard_rank=rank, shard_count=world, **kw)
+    sim.keep_events(0)  # views churn ~V joins per node and tick: never staged in the bench
     if world > 1 or a.force_shard:
         sim.comm_init(rendezvous_uid(rank, world) if world > 1 else comm_unique_id(), world, rank)
     crash = crash_set(n, ncrash, 42)

@@ -52,8 +52,13 @@ struct gm_ctx {
   int latched = GM_OK;
   bool timing = false;
   int timed_ticks = 0;  // ticks in the current timing window
-  int ktimed = 0;       // band-kernel event pairs recorded in the window
+  int ktimed = 0;       // band-kernel event pairs recorded in the window (ring slots in use: min(ktimed, GM_TEV_RING))
   hipEvent_t e0 = nullptr, e1 = nullptr;
+  // events: the device keeps one tick's records; with keep_events (default) a tick's records
+  // are staged to `pending` before the next tick overwrites them (gm_keep_events)
+  bool keep_events = true;
+  bool undrained = false;      // the device holds the last tick's records, not yet staged
+  uint64_t ev_tot[6] = {0, 0, 0, 0, 0, 0};  // FAITHFUL: cumulative records per kind
   std::vector<void *> allocs;
   std::vector<int32_t> failed_h;
   std::vector<int32_t> fail_t;  // last tick a failed node ran (join ramp: its inGroup is frozen there)
@@ -271,6 +276,7 @@ static int create_scaled(gm_ctx *c) {
   TRY(dalloc(c, &s.ev_band, (size_t)n * s.nb * s.evs));
   TRY(dalloc(c, &s.ev_spill, s.ev_spill_cap));
   TRY(dalloc(c, &s.ev_spill_cnt, 1));
+  TRY(dalloc(c, &s.evcum, (size_t)n * s.nb));
   TRY(dalloc(c, &s.mtraw, (size_t)n * S_MT_RAW));
   TRY(dalloc(c, &s.rowstat, (size_t)n * 4));
   TRY(dalloc(c, &s.targets, (size_t)n * GM_FANOUT));
@@ -292,6 +298,7 @@ static int create_scaled(gm_ctx *c) {
   HIPCHECK(hipStreamSynchronize(c->stream));
   HIPCHECK(hipMemset(s.bcnt, 0, sizeof(uint32_t) * (size_t)n * s.nb));
   HIPCHECK(hipMemset(s.ev_spill_cnt, 0, sizeof(uint32_t)));
+  HIPCHECK(hipMemset(s.evcum, 0, sizeof(uint64_t) * (size_t)n * s.nb));
   HIPCHECK(hipMemset(s.rowstat, 0, sizeof(int32_t) * n * 4));
   HIPCHECK(hipMemset(s.err, 0, sizeof(uint32_t)));
   if (s.sharded) {
@@ -455,6 +462,12 @@ static bool ev_order(const FEvent &a, const FEvent &b) {
 
 static int tick_faithful(gm_ctx *c) {
   if (c->t >= F_MAX_TIME) return GM_ERANGE;  // EmulNet.cpp:109 assert(time < MAX_TIME)
+  // nodeStart of this tick's starters resets bFailed on the device (MP1Node.cpp:108-116); mirror it
+  for (int i = 0; i < c->n; i++)
+    if ((int)(0.25 * i) == c->t && c->failed_h[i]) {
+      c->failed_h[i] = 0;
+      c->fail_t[i] = 0x7FFFFFFF;
+    }
   FState st = c->f;
   st.drop_pct_now = c->dropmsg ? (int)(c->cfg.drop_prob * 100) : -1;  // EmulNet.cpp:92
   hipLaunchKernelGGL(gm_f_recv, dim3(1), dim3(1024), 0, c->stream, st, c->t);
@@ -474,12 +487,39 @@ static int tick_faithful(gm_ctx *c) {
     HIPCHECK(hipMemsetAsync(c->f.ev_count, 0, sizeof(unsigned long long), c->stream));
     HIPCHECK(hipStreamSynchronize(c->stream));
     std::sort(ev.begin(), ev.end(), ev_order);
-    for (const FEvent &e : ev) c->pending.push_back(gm_event{e.t, e.logger, e.kind, e.subject});
+    for (const FEvent &e : ev) {
+      c->pending.push_back(gm_event{e.t, e.logger, e.kind, e.subject});
+      if (e.kind > 0 && e.kind < 6) c->ev_tot[e.kind]++;
+    }
   }
   return check_err(c);
 }
 
 static int tick_sharded(gm_ctx *c);
+static int before_tick_events(gm_ctx *c);
+
+// Tick-kernel timing: a ring of GM_TEV_RING event pairs on the context stream; a slot
+// is folded into kernel_ms_sum when it is reused (its tick finished long before).
+#define GM_TEV_RING 64
+static int timing_slot(gm_ctx *c, hipEvent_t *k0, hipEvent_t *k1) {
+  if (c->timed_ticks == 0) HIPCHECK(hipEventRecord(c->e0, c->stream));
+  while (c->tev.size() < 2 * (size_t)GM_TEV_RING) {
+    hipEvent_t e;
+    HIPCHECK(hipEventCreate(&e));
+    c->tev.push_back(e);
+  }
+  const int slot = c->ktimed % GM_TEV_RING;
+  if (c->ktimed >= GM_TEV_RING) {
+    float x = 0;
+    HIPCHECK(hipEventSynchronize(c->tev[2 * slot + 1]));
+    HIPCHECK(hipEventElapsedTime(&x, c->tev[2 * slot], c->tev[2 * slot + 1]));
+    c->kernel_ms_sum += x;
+  }
+  *k0 = c->tev[2 * slot];
+  *k1 = c->tev[2 * slot + 1];
+  c->ktimed++;
+  return GM_OK;
+}
 
 static int tick_scaled(gm_ctx *c) {
   if (c->t > GM_T_LIMIT) return GM_ERANGE;
@@ -497,17 +537,7 @@ static int tick_scaled(gm_ctx *c) {
   const int t_send = c->t - 1;
   const bool drop = c->cfg.drop_pct > 0 && t_send >= c->cfg.drop_from && t_send < c->cfg.drop_to;
   hipEvent_t k0 = nullptr, k1 = nullptr;
-  if (c->timing) {
-    if (c->timed_ticks == 0) HIPCHECK(hipEventRecord(c->e0, c->stream));
-    while (c->tev.size() < 2 * (size_t)(c->ktimed + 1)) {
-      hipEvent_t e;
-      HIPCHECK(hipEventCreate(&e));
-      c->tev.push_back(e);
-    }
-    k0 = c->tev[2 * c->ktimed];
-    k1 = c->tev[2 * c->ktimed + 1];
-    c->ktimed++;
-  }
+  if (c->timing) TRY(timing_slot(c, &k0, &k1));
   HIPCHECK(gm_launch_tick(c->s, c->t, drop ? c->cfg.drop_pct : -1, c->nt, c->stream, k0, k1, true));
   if (c->timing) {
     HIPCHECK(hipEventRecord(c->e1, c->stream));
@@ -526,17 +556,7 @@ static int tick_partial(gm_ctx *c) {
   PState st = c->p;
   st.drop_pct = drop ? c->cfg.drop_pct : -1;
   hipEvent_t k0 = nullptr, k1 = nullptr;
-  if (c->timing) {
-    if (c->timed_ticks == 0) HIPCHECK(hipEventRecord(c->e0, c->stream));
-    while (c->tev.size() < 2 * (size_t)(c->ktimed + 1)) {
-      hipEvent_t e;
-      HIPCHECK(hipEventCreate(&e));
-      c->tev.push_back(e);
-    }
-    k0 = c->tev[2 * c->ktimed];
-    k1 = c->tev[2 * c->ktimed + 1];
-    c->ktimed++;
-  }
+  if (c->timing) TRY(timing_slot(c, &k0, &k1));
   if (!c->p_sharded) {
     HIPCHECK(gm_launch_partial_tick(st, c->t, c->p_mtraw, c->stream, k0, k1));
   } else {
@@ -568,9 +588,13 @@ static int tick_partial(gm_ctx *c) {
 extern "C" int gm_tick(gm_ctx *c) {
   if (!c) return GM_EINVAL;
   if (c->latched != GM_OK) return c->latched;
+  TRY(before_tick_events(c));
   int rc = c->cfg.mode == GM_MODE_FAITHFUL ? tick_faithful(c) : c->cfg.mode == GM_MODE_SCALED ? tick_scaled(c)
                                                                                              : tick_partial(c);
-  if (rc == GM_OK) c->t++;
+  if (rc == GM_OK) {
+    c->t++;
+    c->undrained = c->cfg.mode != GM_MODE_FAITHFUL;
+  }
   return rc;
 }
 
@@ -603,9 +627,10 @@ extern "C" int gm_rand(gm_ctx *c, int32_t *out) {
 }
 
 extern "C" int gm_set_failed(gm_ctx *c, const int32_t *idx, int32_t n) {
-  if (!c || (n > 0 && !idx)) return GM_EINVAL;
-  for (int k = 0; k < n; k++) {
+  if (!c || n < 0 || (n > 0 && !idx)) return GM_EINVAL;
+  for (int k = 0; k < n; k++)  // validate everything before any state changes
     if (idx[k] < 0 || idx[k] >= c->n) return GM_EINVAL;
+  for (int k = 0; k < n; k++) {
     if (!c->failed_h[idx[k]]) c->fail_t[idx[k]] = c->t - 1;
     c->failed_h[idx[k]] = 1;
     // join ramp: the introducer's last tick bounds who gets a JOINREP
@@ -654,18 +679,12 @@ static int drain_scaled(gm_ctx *c, std::vector<gm_event> &out) {
     HIPCHECK(hipMemcpy(sp.data(), s.ev_spill, sizeof(uint64_t) * nsp, hipMemcpyDeviceToHost));
     for (uint64_t v : sp) push((int)(v >> 32), (uint32_t)v);
   }
-  // canonical SCALED order: loggers descending; joins ascending id, then removals descending id
-  std::sort(out.begin(), out.end(), [](const gm_event &a, const gm_event &b) {
-    if (a.logger != b.logger) return a.logger > b.logger;
-    if (a.kind != b.kind) return a.kind < b.kind;
-    return a.kind == GM_EV_JOINED ? a.subject < b.subject : a.subject > b.subject;
-  });
   return GM_OK;
 }
 
-static void sort_canonical(std::vector<gm_event> &out) {
+static void sort_canonical(std::vector<gm_event>::iterator b, std::vector<gm_event>::iterator e) {
   // canonical order of the build-defined modes: loggers descending; joins ascending id, then removals descending id
-  std::sort(out.begin(), out.end(), [](const gm_event &a, const gm_event &b) {
+  std::sort(b, e, [](const gm_event &a, const gm_event &b) {
     if (a.logger != b.logger) return a.logger > b.logger;
     if (a.kind != b.kind) return a.kind < b.kind;
     return a.kind == GM_EV_JOINED ? a.subject < b.subject : a.subject > b.subject;
@@ -693,19 +712,38 @@ static int drain_partial(gm_ctx *c, std::vector<gm_event> &out) {
                              (int32_t)(rec & 0x3FFFFFFFu)});
     }
   }
-  sort_canonical(out);
+  return GM_OK;
+}
+
+// SCALED / PARTIAL: move the last tick's device records (one tick's worth is kept on the
+// device, overwritten by the next tick) to the host list, in canonical order.
+static int stage_events(gm_ctx *c) {
+  if (!c->undrained) return GM_OK;
+  c->undrained = false;
+  const size_t first = c->pending.size();
+  if (c->cfg.mode == GM_MODE_SCALED) TRY(drain_scaled(c, c->pending));
+  else if (c->cfg.mode == GM_MODE_PARTIAL) TRY(drain_partial(c, c->pending));
+  sort_canonical(c->pending.begin() + first, c->pending.end());
+  return GM_OK;
+}
+
+// Before a tick overwrites the device records: stage them (keep_events) or drop them.
+static int before_tick_events(gm_ctx *c) {
+  if (c->cfg.mode == GM_MODE_FAITHFUL) return GM_OK;
+  if (c->keep_events) return stage_events(c);
+  c->undrained = false;
+  return GM_OK;
+}
+
+extern "C" int gm_keep_events(gm_ctx *c, int32_t on) {
+  if (!c) return GM_EINVAL;
+  c->keep_events = on != 0;
   return GM_OK;
 }
 
 extern "C" int gm_drain_events(gm_ctx *c, gm_event *out, size_t cap, size_t *n) {
   if (!c || !n) return GM_EINVAL;
-  if (c->cfg.mode == GM_MODE_SCALED) {
-    c->pending.clear();
-    TRY(drain_scaled(c, c->pending));
-  } else if (c->cfg.mode == GM_MODE_PARTIAL) {
-    c->pending.clear();
-    TRY(drain_partial(c, c->pending));
-  }
+  TRY(stage_events(c));
   *n = c->pending.size();
   if (c->pending.size() > cap) return GM_ERANGE;
   if (!c->pending.empty()) memcpy(out, c->pending.data(), sizeof(gm_event) * c->pending.size());
@@ -728,10 +766,35 @@ extern "C" int gm_event_counts(gm_ctx *c, uint64_t counts[6]) {
     std::vector<int32_t> cnt(c->p.nloc);
     HIPCHECK(hipMemcpyAsync(cnt.data(), c->p.ev_cnt, sizeof(int32_t) * c->p.nloc, hipMemcpyDeviceToHost, c->stream));
     HIPCHECK(hipStreamSynchronize(c->stream));
-    for (int32_t v : cnt) counts[0] += (uint64_t)(v & 0xFFFF) + (uint64_t)(v >> 16);
+    for (int32_t v : cnt) {
+      counts[GM_EV_JOINED] += (uint64_t)(v & 0xFFFF);
+      counts[GM_EV_REMOVED] += (uint64_t)(v >> 16);
+    }
+    counts[0] = counts[GM_EV_JOINED] + counts[GM_EV_REMOVED];
   } else {
     for (const gm_event &e : c->pending) counts[e.kind]++;
   }
+  return GM_OK;
+}
+
+extern "C" int gm_event_totals(gm_ctx *c, uint64_t totals[6]) {
+  if (!c || !totals) return GM_EINVAL;
+  for (int k = 0; k < 6; k++) totals[k] = c->ev_tot[k];
+  if (c->cfg.mode == GM_MODE_PARTIAL) return GM_EUNSUPPORTED;
+  if (c->cfg.mode == GM_MODE_SCALED) {
+    std::vector<uint64_t> cum((size_t)c->n * c->s.nb);
+    HIPCHECK(hipMemcpyAsync(cum.data(), c->s.evcum, sizeof(uint64_t) * cum.size(), hipMemcpyDeviceToHost, c->stream));
+    HIPCHECK(hipStreamSynchronize(c->stream));
+    uint64_t j = 0, r = 0;
+    for (uint64_t v : cum) {
+      j += (uint32_t)v;
+      r += v >> 32;
+    }
+    totals[GM_EV_JOINED] = j;
+    totals[GM_EV_REMOVED] = r;
+  }
+  totals[0] = 0;
+  for (int k = 1; k < 6; k++) totals[0] += totals[k];
   return GM_OK;
 }
 
@@ -812,6 +875,18 @@ extern "C" int gm_read_row(gm_ctx *c, int32_t r, int32_t c0, int32_t len, int32_
     hb[j] = rh[c0 + j];
     ts[j] = rt[c0 + j];
   }
+  return GM_OK;
+}
+
+extern "C" int gm_read_views(gm_ctx *c, int32_t r0, int32_t count, uint64_t *out) {
+  if (!c || count < 0 || (count > 0 && !out)) return GM_EINVAL;
+  if (c->cfg.mode != GM_MODE_PARTIAL) return GM_EUNSUPPORTED;
+  const PState &p = c->p;
+  if (r0 < p.n0 || r0 + (int64_t)count > (int64_t)p.n0 + p.nloc) return GM_EINVAL;  // this shard's nodes only
+  HIPCHECK(hipStreamSynchronize(c->stream));
+  if (count)
+    HIPCHECK(hipMemcpy(out, p.lists + ((size_t)((c->t - 1) & 1) * p.rows + (r0 - p.n0)) * p.V,
+                       sizeof(uint64_t) * p.V * (size_t)count, hipMemcpyDeviceToHost));
   return GM_OK;
 }
 
@@ -945,10 +1020,11 @@ extern "C" int gm_last_kernel_ms(gm_ctx *c, float *ms) {
     return GM_OK;
   }
   HIPCHECK(hipEventSynchronize(c->e1));
-  double sum = 0;
-  for (int i = 0; i < c->ktimed; i++) {
+  double sum = c->kernel_ms_sum;  // folded ring slots + the pairs still in the ring
+  for (int k = std::max(0, c->ktimed - GM_TEV_RING); k < c->ktimed; k++) {
+    const int slot = k % GM_TEV_RING;
     float x = 0;
-    HIPCHECK(hipEventElapsedTime(&x, c->tev[2 * i], c->tev[2 * i + 1]));
+    HIPCHECK(hipEventElapsedTime(&x, c->tev[2 * slot], c->tev[2 * slot + 1]));
     sum += x;
   }
   *ms = c->ktimed ? (float)(sum / c->ktimed) : 0.f;
@@ -988,6 +1064,7 @@ extern "C" int gm_crash_set(int32_t n, int32_t count, uint64_t seed, int32_t *ou
 
 #define GM_D_FIRST S_MT_RAW  // S2 outputs per row in the first round (steady state needs ~5-6)
 #define GM_D_MORE 64          // S2 outputs per row in later rounds (transients with many stale entries)
+#define GM_MAX_ROUNDS 4096    // draw rounds per sharded tick (16 + 64 * 4096 S2 outputs per row)
 
 extern "C" int gm_comm_unique_id(uint8_t *out128) {
   if (!out128) return GM_EINVAL;
@@ -1031,6 +1108,7 @@ static int shard_ready(gm_ctx *c) {
 
 extern "C" int gm_shard_merge(gm_ctx *c) {
   TRY(shard_ready(c));
+  TRY(before_tick_events(c));
   const int t_send = c->t - 1;
   const bool drop = c->cfg.drop_pct > 0 && t_send >= c->cfg.drop_from && t_send < c->cfg.drop_to;
   HIPCHECK(hipMemsetAsync(c->s.xcnt + (size_t)c->s.shard_rank * c->n * 2, 0, sizeof(int32_t) * 2 * (size_t)c->n,
@@ -1068,6 +1146,7 @@ extern "C" int gm_shard_end_tick(gm_ctx *c) {
     c->timed_ticks++;
   }
   c->t++;
+  c->undrained = true;
   return GM_OK;
 }
 
@@ -1118,7 +1197,12 @@ static int tick_sharded(gm_ctx *c) {
     int32_t pend = 0;
     TRY(gm_shard_accept(c, D, &pend));
     if (pend == 0) break;
-    round++;
+    if (++round > GM_MAX_ROUNDS) {  // a row that never finds its targets: same guard as gm_s_pick
+      uint32_t e = GM_ERR_DRAWS;
+      HIPCHECK(hipMemcpy(c->s.err, &e, sizeof e, hipMemcpyHostToDevice));
+      c->latched = GM_ERANGE;
+      return c->latched;
+    }
     D = GM_D_MORE;
   }
   c->t--;  // gm_tick advances globaltime
@@ -1178,6 +1262,7 @@ extern "C" int gm_partial_loopback_tick(gm_ctx **ctxs, int32_t G) {
       return GM_EINVAL;
     if (c->latched != GM_OK) return c->latched;
   }
+  for (int g = 0; g < G; g++) TRY(before_tick_events(ctxs[g]));
   for (int g = 0; g < G; g++) {
     gm_ctx *c = ctxs[g];
     const int t_send = c->t - 1;
@@ -1221,6 +1306,7 @@ extern "C" int gm_partial_loopback_tick(gm_ctx **ctxs, int32_t G) {
     HIPCHECK(hipStreamSynchronize(ctxs[g]->stream));
     TRY(check_err(ctxs[g]));
     ctxs[g]->t++;
+    ctxs[g]->undrained = true;
   }
   return GM_OK;
 }

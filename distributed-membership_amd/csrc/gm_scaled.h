@@ -59,7 +59,8 @@ struct SState {
   uint32_t *ev_band;       // [n][nb][evs] kind<<30 | subject id
   uint64_t *ev_spill;      // overflow: (logger<<32) | kind<<30 | subject id
   uint32_t *ev_spill_cnt;
-  uint32_t *mtraw;         // [n][S_MT_RAW] first mt19937 outputs of each row's S2 stream this tick
+  uint64_t *evcum;         // [n][nb] cumulative events since create: joins | removals << 32 (single writer per cell)
+  uint32_t *mtraw;        // [n][S_MT_RAW] first mt19937 outputs of each row's S2 stream this tick
   int32_t *rowstat;        // [n][4]: lists delivered, present, numfailed, targets chosen
   int32_t *targets;        // [n][GM_FANOUT]
   uint32_t *err;

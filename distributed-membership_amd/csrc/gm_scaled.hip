@@ -312,6 +312,11 @@ __global__ __launch_bounds__(256) void gm_s_band(SState s, int t, int drop_pct) 
       if (li >= o) x += y;
     }
     tot = __shfl(x, sub * LPR + LPR - 1, 64);
+    // cumulative (joins, removals) of this (row, band): ADD kinds are 01, REMOVE kinds 10
+    int jr = __builtin_popcount(evk & 0x55555555u) | (__builtin_popcount(evk & 0xAAAAAAAAu) << 16);
+#pragma unroll
+    for (int o = LPR / 2; o >= 1; o >>= 1) jr += __shfl_xor(jr, o, 64);
+    if (live && li == 0 && jr) s.evcum[(size_t)r * s.nb + band] += (uint64_t)(jr & 0xFFFF) | ((uint64_t)(jr >> 16) << 32);
   }
   const int E = s.evs;
   uint32_t sbase = 0;  // one spill-ring reservation per (row, band) that overflows its slots

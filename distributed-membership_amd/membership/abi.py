@@ -38,7 +38,7 @@ EXPORTS = ["gm_parse_conf", "gm_create", "gm_destroy", "gm_tick", "gm_sync", "gm
            "gm_dump_tables", "gm_tick_stats", "gm_set_timing", "gm_last_kernel_ms", "gm_crash_set", "gm_strerror",
            "gm_comm_unique_id", "gm_comm_init", "gm_shard_layout", "gm_shard_merge", "gm_shard_draw",
            "gm_shard_accept", "gm_shard_end_tick", "gm_shard_loopback", "gm_partial_loopback_tick",
-           "gm_shard_exchange_bytes"]
+           "gm_shard_exchange_bytes", "gm_keep_events", "gm_event_totals", "gm_read_views"]
 
 _lib = None
 
@@ -67,7 +67,8 @@ def load_library():
         "gm_time": [ctypes.c_void_p, P(i32)], "gm_rand": [ctypes.c_void_p, P(i32)],
         "gm_set_failed": [ctypes.c_void_p, P(i32), i32], "gm_set_dropmsg": [ctypes.c_void_p, i32],
         "gm_drain_events": [ctypes.c_void_p, P(GmEvent), sz, P(sz)],
-        "gm_event_counts": [ctypes.c_void_p, P(u64)],
+        "gm_event_counts": [ctypes.c_void_p, P(u64)], "gm_event_totals": [ctypes.c_void_p, P(u64)],
+        "gm_keep_events": [ctypes.c_void_p, i32], "gm_read_views": [ctypes.c_void_p, i32, i32, P(u64)],
         "gm_msgcount": [ctypes.c_void_p, i32, P(i32), P(i32)],
         "gm_read_row": [ctypes.c_void_p, i32, i32, i32, P(i32), P(i32)],
         "gm_read_nodes": [ctypes.c_void_p, P(i32)],
@@ -183,10 +184,44 @@ class Simulator:
         self._call("gm_drain_events", self.h, buf, n.value, ctypes.byref(n))
         return [(e.t, e.logger, e.kind, e.subject) for e in buf[:n.value]]
 
+    def drain_events_np(self):
+        """gm_drain_events into an int32 array [n, 4] of (t, logger, kind, subject)."""
+        n = ctypes.c_size_t()
+        rc = self.lib.gm_drain_events(self.h, None, 0, ctypes.byref(n))
+        if rc == GM_OK:
+            return np.zeros((0, 4), dtype=np.int32)
+        if rc != GM_ERANGE:
+            raise GmError(rc, "gm_drain_events")
+        buf = np.empty((n.value, 4), dtype=np.int32)
+        self._call("gm_drain_events", self.h, buf.ctypes.data_as(ctypes.POINTER(GmEvent)), n.value, ctypes.byref(n))
+        return buf[:n.value]
+
+    def keep_events(self, on):
+        self._call("gm_keep_events", self.h, 1 if on else 0)
+
     def event_total(self):
         c = (ctypes.c_uint64 * 6)()
         self._call("gm_event_counts", self.h, c)
         return int(c[0])
+
+    def event_counts(self):
+        """Records of the last tick: [total, joined, removed, ...] (per kind where the mode has it)."""
+        c = (ctypes.c_uint64 * 6)()
+        self._call("gm_event_counts", self.h, c)
+        return [int(x) for x in c]
+
+    def event_totals(self):
+        """Records since gm_create: {kind: count} (FAITHFUL, SCALED)."""
+        c = (ctypes.c_uint64 * 6)()
+        self._call("gm_event_totals", self.h, c)
+        return {"total": int(c[0]), "joined": int(c[GM_EV_JOINED]), "removed": int(c[GM_EV_REMOVED])}
+
+    def read_views(self, r0, count):
+        """PARTIAL: raw views (id << 32 | hb, 0 = empty) of nodes [r0, r0 + count), uint64 [count, V]."""
+        v = self.cfg.view or 32
+        out = np.zeros((count, v), dtype=np.uint64)
+        self._call("gm_read_views", self.h, r0, count, _ptr(out, ctypes.c_uint64))
+        return out
 
     def msgcount(self, t):
         sent = np.zeros((self.n, t), dtype=np.int32)

@@ -101,7 +101,7 @@ typedef struct gm_config {
   int32_t init_t0;
   uint64_t init_seed;
   int32_t band;            /* SCALED columns per band of the tick kernel (64/128/256/512; 0 = auto) */
-  int32_t view;            /* PARTIAL view capacity V (2..64; 0 = 32) */
+  int32_t view;            /* PARTIAL view capacity V (2..32; 0 = 32) */
   uint64_t view_seed;      /* PARTIAL initial views and eviction tie-break */
   int32_t reserved[2];
 } gm_config;
@@ -137,10 +137,22 @@ int gm_set_dropmsg(gm_ctx *ctx, int32_t on);
 /* Drain every event produced since the last drain, in reference log order
  * (ticks ascending; node phase i descending; per node: start line or joins in
  * dequeue order, then removals by descending id, then @@time). If cap is too
- * small, *n receives the number pending and GM_ERANGE is returned (nothing drained). */
+ * small, *n receives the number pending and GM_ERANGE is returned (nothing drained).
+ * SCALED / PARTIAL keep one tick's records on the device; with event keeping on
+ * (the default) gm_tick first stages the previous tick's undrained records to host
+ * memory (a readback per tick), so nothing is lost between drains. */
 int gm_drain_events(gm_ctx *ctx, gm_event *out, size_t cap, size_t *n);
-/* number of events produced in the last tick, per kind (SCALED bench telemetry) */
+/* on = 1 (default): keep every tick's records until drained. on = 0 (benchmarks):
+ * a tick overwrites the previous tick's undrained records (no per-tick readback);
+ * gm_drain_events then returns the last tick's records only. */
+int gm_keep_events(gm_ctx *ctx, int32_t on);
+/* counts[0] = records produced in the last tick (SCALED / PARTIAL telemetry; PARTIAL
+ * also splits them per kind in counts[kind]; FAITHFUL: records pending per kind) */
 int gm_event_counts(gm_ctx *ctx, uint64_t counts[6]);
+/* totals[k] = records of kind k produced since gm_create, totals[0] = their sum,
+ * independent of draining (FAITHFUL, SCALED; SCALED counts on the device, per (row,
+ * band) cell). PARTIAL: GM_EUNSUPPORTED (views churn ~V joins per node and tick). */
+int gm_event_totals(gm_ctx *ctx, uint64_t totals[6]);
 
 /* sent/recv message counts per node id 1..n for ticks [0, t): out arrays [n][t] */
 int gm_msgcount(gm_ctx *ctx, int32_t t, int32_t *sent, int32_t *recv);
@@ -148,6 +160,9 @@ int gm_msgcount(gm_ctx *ctx, int32_t t, int32_t *sent, int32_t *recv);
 /* Dense readback of observer row r: hb/ts per subject column (absent -> -1),
  * columns [c0, c0+len) of this context's shard (c0 relative to the shard start). */
 int gm_read_row(gm_ctx *ctx, int32_t r, int32_t c0, int32_t len, int32_t *hb, int32_t *ts);
+/* PARTIAL: the raw V-entry views (id << 32 | hb, 0 = empty, ascending id) of nodes
+ * [r0, r0 + count) as of the last tick, [count][V]; a row shard reads its own nodes. */
+int gm_read_views(gm_ctx *ctx, int32_t r0, int32_t count, uint64_t *out);
 /* node state: inited, inGroup, bFailed, heartbeat counter (4 int32 per node) */
 int gm_read_nodes(gm_ctx *ctx, int32_t *state4);
 /* Render the membership lists of every node in the parity dump format

@@ -1,21 +1,44 @@
 #!/usr/bin/env python3
 """Turn rocprofv3 FETCH_SIZE / WRITE_SIZE passes into per-launch HBM bytes of the
-tick kernel (profiles/traffic_n<N>.json, read by bench.py as roofline.traffic).
+tick kernel(s) (profiles/traffic_*.json, read by bench.py as roofline.traffic).
 
 Corrections per MI355X_MICROARCH.md §HBM (gfx950): FETCH_SIZE (KiB) reports half
 the bytes of a wide (16 B/lane) coalesced streaming read -> x2; WRITE_SIZE (KiB)
 is exact for 16 B/lane stores. Steady-state launches only: the median of the last
-`--last` dispatches (the prologue's converged-start transient is excluded)."""
+`--last` dispatches of each matching kernel name (the prologue is excluded); when
+`--kernel` matches several kernels (gm_p_tick_small + gm_p_tick_big), their
+per-launch medians are summed (one tick launches each once).
+
+`--fetch` / `--write` take a counter_collection CSV or the rocprofv3 output
+directory holding one (searched recursively)."""
 import argparse
 import csv
+import glob
 import json
+import os
 import statistics
+import time
+
+
+def csv_of(path):
+    if os.path.isfile(path):
+        return path
+    hits = sorted(glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True))
+    if not hits:
+        raise SystemExit(f"no counter_collection.csv under {path}")
+    return hits[-1]
 
 
 def per_launch(path, counter, kernel, last):
-    rows = [r for r in csv.DictReader(open(path)) if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter]
-    vals = [float(r["Counter_Value"]) for r in rows][-last:]
-    return statistics.median(vals), len(rows)
+    per = {}
+    for r in csv.DictReader(open(csv_of(path))):
+        if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            name = r["Kernel_Name"].split("(")[0]
+            per.setdefault(name, []).append(float(r["Counter_Value"]))
+    if not per:
+        raise SystemExit(f"no {counter} rows for {kernel} in {path}")
+    tot = sum(statistics.median(v[-last:]) for v in per.values())
+    return tot, {k: len(v) for k, v in per.items()}
 
 
 def main():
@@ -25,7 +48,7 @@ def main():
     p.add_argument("--n", type=int, default=65536)
     p.add_argument("--kernel", default="gm_s_band")
     p.add_argument("--layout", default="narrow-band")
-    p.add_argument("--last", type=int, default=6)
+    p.add_argument("--last", type=int, default=4)
     p.add_argument("--out", required=True)
     a = p.parse_args()
     f, nf = per_launch(a.fetch, "FETCH_SIZE", a.kernel, a.last)
@@ -34,7 +57,9 @@ def main():
     write_b = w * 1024
     out = {"kernel": a.kernel, "layout": a.layout, "n": a.n, "fetch_size_kib_raw": f, "write_size_kib_raw": w,
            "fetch_bytes_corrected": fetch_b, "write_bytes": write_b, "hbm_bytes_per_launch": fetch_b + write_b,
-           "launches_seen": [nf, nw], "note": "FETCH_SIZE x2 (gfx950 16B/lane streaming-read correction); FETCH_SIZE counts L2 misses, "
+           "launches_seen": {"fetch": nf, "write": nw}, "generated": time.strftime("%Y-%m-%dT%H:%M:%S"),
+           "source": {"fetch": os.path.relpath(csv_of(a.fetch)), "write": os.path.relpath(csv_of(a.write))},
+           "note": "FETCH_SIZE x2 (gfx950 16B/lane streaming-read correction); FETCH_SIZE counts L2 misses, "
                    "Infinity-Cache hits included (MI355X_MICROARCH.md), so re-reads served by the cache still count"}
     with open(a.out, "w") as fh:
         json.dump(out, fh, indent=1)

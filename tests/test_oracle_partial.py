@@ -32,3 +32,17 @@ def oracle_digest(c):
 @pytest.mark.parametrize("c", CASES, ids=[f"n{c['n']}_v{c['v']}_drop{c['drop_pct']}" for c in CASES])
 def test_partial_oracle_digest(c):
     assert oracle_digest(c) == c["sha256"]
+
+
+def test_sc_regime_has_no_removals():
+    """Pins what test_gpu_baseline_configs asserts at N = 16M on the specification:
+    under the S-C schedule (5 % drops every tick, 1 % crash at tick 10) eviction keeps
+    every view full and fresh, so the TREMOVE sweep never fires; crashed nodes leave
+    the views by eviction."""
+    n = 4000
+    ora = oracle_py.PartialOracle(n, v=32, rd_seed=7, view_seed=5, init_t0=8, init_seed=11, crash_tick=10,
+                                  crash_count=n // 100, crash_seed=42, drop_pct=5, drop_from=0, drop_to=1 << 20,
+                                  drop_seed=42)
+    for _ in range(30):
+        ora.tick()
+        assert all(e[2] == 1 for e in ora.events())
