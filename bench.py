@@ -33,7 +33,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "distributed-membership_amd"))
 
 PEAK_HBM_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
-LAYOUT_SA = "narrow-band"  # profiles/traffic_n65536.json must describe this payload layout
+LAYOUT_SA = "nibble-band"  # profiles/traffic_n65536.json must describe this payload layout
 
 
 class Roctx:
@@ -166,18 +166,18 @@ def main():
     n_live, m_lists = st["live"], st["lists"]
     W = sim.shard_layout()[1] if world > 1 else n  # this rank's subject columns
     # algorithmic bytes of one tick in this layout: per live row and
-    # column 2 B cell read + 2 B cell write + 1 B payload write, plus 1 B per delivered
-    # gossip list (payload read) -- the survey's formulation (read and
-    # write the receiver's row once, read each delivered sender row once per delivery)
-    # in this build's 16-bit cell / 8-bit payload units
-    b_alg = (5 * n_live + m_lists) * W
+    # column 2 B cell read + 2 B cell write + 0.5 B payload write, plus 0.5 B per
+    # delivered gossip list (payload read) -- the survey's formulation (SURVEY.md §8(d):
+    # read and write the receiver's row once, read each delivered sender row once per
+    # delivery) in this build's 16-bit cell / 4-bit payload units
+    b_alg = (9 * n_live + m_lists) * W // 2
     # the survey's int32 (hb, ts) formulation of the same work
     b_survey = 16 * n_live * W + 8 * m_lists * W
     achieved = b_alg / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else None
     # DRAM bytes the layout cannot avoid: the cell read + write and the payload write per
     # live cell, plus ONE read of each sender's payload (its ~5 re-reads are served by the
     # Infinity Cache while the band is in flight; FETCH_SIZE counts those hits too)
-    dram_est = 6 * n_live * W
+    dram_est = 5 * n_live * W
     frac_dram = (dram_est / (kernel_ms * 1e-3) / 1e9 / PEAK_HBM_GBPS) if kernel_ms > 0 else None
     traffic, traffic_src = None, None
     tpath_ok = world == 1
@@ -201,7 +201,7 @@ def main():
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        "dtype": "u16 cells / u8 payload (integer)",
+        "dtype": "u16 cells / 4-bit payload (integer)",
         "data": "synthetic (converged full-membership table, seeded crash set)",
         "config": {"workload": "S-A: SCALED full membership, 1% crash at tick 10, fanout 5, TFAIL 5, TREMOVE 20",
                    "n": n, "start": f"warm t0={a.t0}" if a.t0 > 0 else "cold", "prologue_to_tick": a.prologue, "crashed": ncrash, "live": n_live,

@@ -263,7 +263,8 @@ static int create_scaled(gm_ctx *c) {
   const size_t cells = (size_t)n * s.wp;
   TRY(dalloc(c, &s.table, cells));
   c->nt = !(getenv("GM_NT") && !atoi(getenv("GM_NT")));  // non-temporal table streams, default on
-  TRY(dalloc(c, &s.msg, 2 * cells));
+  TRY(dalloc(c, &s.msg, cells));        // nibbles: 2 parities x band/2 bytes per (band, row)
+  TRY(dalloc(c, &s.wide, 2 * cells));   // escape bytes: 2 parities x band
   for (int p = 0; p < 2; p++) {
     TRY(dalloc(c, &s.inbox_cnt[p], n));
     TRY(dalloc(c, &s.inbox[p], (size_t)n * S_KMAX));
@@ -291,7 +292,7 @@ static int create_scaled(gm_ctx *c) {
   if (ramp && (s.sharded || c->cfg.drop_pct > 0)) return GM_EUNSUPPORTED;
   s.ramp = ramp ? 1 : 0;
   s.intro_until = 0x7FFFFFFF;
-  HIPCHECK(hipMemset(s.msg, 0, sizeof(uint8_t) * 2 * cells));
+  HIPCHECK(hipMemset(s.msg, 0, sizeof(uint8_t) * cells));
   for (int p = 0; p < 2; p++) HIPCHECK(hipMemset(s.inbox_cnt[p], 0, sizeof(int32_t) * n));
   HIPCHECK(hipMemset(s.failed, 0, sizeof(int32_t) * n));
   HIPCHECK(gm_launch_init(s, ramp ? 2 : warm ? 1 : 0, t0, c->cfg.init_seed, c->stream));

@@ -24,8 +24,14 @@ __host__ __device__ inline bool s_ingroup(int ramp, int intro_until, int r, int 
 }
 #define S_H(c) ((c) >> 5)
 #define S_AGE(c) ((c) & 31u)
-// payload cell (8 bits): h of a fresh entry re-based to the receiving tick (h - 2 >= 1),
-// 0 = not sent.
+// payload (sendMemberList's fresh entries, re-based to the receiving tick: h' = h - 2):
+// one NIBBLE per cell, 0 = not sent, n in [1, 14] = h' = 224 + 2n (the even values
+// [226, 252]: heartbeat lag <= 13 ticks -- every value of a warm, steady cluster), 15 =
+// escape: the byte h' is in the wide plane (odd h' of cold-start / JOINREQ entries, or a
+// larger lag). Larger nibble = larger h' = newer, so the merge maxes nibbles directly.
+#define S_NIB_BASE 224u
+#define S_NIB_ESC 15u
+#define S_NIB_H(n) (S_NIB_BASE + 2u * (n))
 
 #define S_EV_ADD 1u
 #define S_EV_REMOVE 2u
@@ -48,7 +54,8 @@ struct SState {
   // Band-tiled layout: cell (r, c) of band b = c / band lives at ((b * n + r) * band + c % band),
   // so one band of all rows is one contiguous slab (the unit gm_s_band sweeps).
   uint16_t *table;         // [nb][n][band] S_CELL
-  uint8_t *msg;            // [nb][n][2][band] gossip payload cells, both tick parities of a (band, row) adjacent
+  uint8_t *msg;            // [nb][n][2][band/2] gossip payload nibbles, both tick parities of a (band, row) adjacent
+  uint8_t *wide;           // [nb][n][2][band] escaped payload bytes (written / read only where the nibble is 15)
   int32_t *wtick;          // [n] tick each row's cells are relative to (last written)
   int32_t *inbox_cnt[2];   // [n] lists queued for each receiver, by delivery-tick parity
   int32_t *inbox[2];       // [n][S_KMAX] sender rows

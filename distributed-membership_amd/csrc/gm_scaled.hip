@@ -36,6 +36,7 @@
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint8_t u8x16 __attribute__((ext_vector_type(16)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 // ------------------------------------------------------------------ gm_s_mtgen
 __global__ __launch_bounds__(256) void gm_s_mtgen(SState s, int t) {
@@ -100,6 +101,33 @@ __device__ __forceinline__ uint32_t unpk(u16x2 v) { return __builtin_bit_cast(ui
 __device__ __forceinline__ u16x2 bytes01(uint32_t w) { return pk(__builtin_amdgcn_perm(0u, w, 0x0c010c00u)); }
 __device__ __forceinline__ u16x2 bytes23(uint32_t w) { return pk(__builtin_amdgcn_perm(0u, w, 0x0c030c02u)); }
 
+// Payload nibbles (gm_scaled.h S_NIB_*): dword w of a lane's 8-byte slice holds cells
+// 8w..8w+7; cell 8w+2k sits in nibble 3-k of the low u16, cell 8w+2k+1 in nibble 3-k
+// of the high u16. So v_pk_max_u16 of the dword shifted left by 4k leaves, in the top
+// nibble of each u16, the max over lists of cells (8w+2k, 8w+2k+1) -- the table word
+// 4w+k: max() of u16 lanes is decided by the top nibble whatever the bits below it.
+__device__ __forceinline__ void nib_max(u16x2 acc[8], uint32_t x0, uint32_t x1) {
+  const u16x2 a = pk(x0), b = pk(x1);
+  acc[0] = __builtin_elementwise_max(acc[0], a);
+  acc[1] = __builtin_elementwise_max(acc[1], a << (u16x2)(4));
+  acc[2] = __builtin_elementwise_max(acc[2], a << (u16x2)(8));
+  acc[3] = __builtin_elementwise_max(acc[3], a << (u16x2)(12));
+  acc[4] = __builtin_elementwise_max(acc[4], b);
+  acc[5] = __builtin_elementwise_max(acc[5], b << (u16x2)(4));
+  acc[6] = __builtin_elementwise_max(acc[6], b << (u16x2)(8));
+  acc[7] = __builtin_elementwise_max(acc[7], b << (u16x2)(12));
+}
+// nibble of lane cell q (0..15) in a lane slice (x0, x1)
+__device__ __forceinline__ uint32_t nib_of(uint32_t x0, uint32_t x1, int q) {
+  const uint32_t x = q < 8 ? x0 : x1;
+  const int c = q & 7;
+  return (x >> (16 * (c & 1) + 4 * (3 - (c >> 1)))) & 15u;
+}
+// payload value of a delivered cell: h' from its nibble, or from the wide plane on escape
+__device__ __forceinline__ uint32_t nib_value(uint32_t nb, const uint8_t *wide_cell) {
+  return nb == S_NIB_ESC ? (uint32_t)*wide_cell : nb ? S_NIB_H(nb) : 0u;
+}
+
 template <int B, bool DROP>
 __global__ __launch_bounds__(256) void gm_s_band(SState s, int t, int drop_pct) {
   constexpr int LPR = B / S_COLS_PER_LANE;  // lanes per row
@@ -116,11 +144,13 @@ __global__ __launch_bounds__(256) void gm_s_band(SState s, int t, int drop_pct) 
   const int r = (u - band * U) * RPW + sub;
   const int colb = band * B + li * Q;  // shard-local column of this lane's first cell
   const size_t slab = (size_t)band * s.n;
-  // this band's slabs: table [n][B] cells, payload [n][2][B] bytes (32-bit offsets)
+  // this band's slabs: table [n][B] cells, payload nibbles [n][2][B/2] bytes (32-bit offsets)
   const __amdgpu_buffer_rsrc_t trs = gm_rsrc(s.table + slab * B, (uint32_t)(s.n * B * 2));
-  const __amdgpu_buffer_rsrc_t prs = gm_rsrc(s.msg + slab * 2 * B, (uint32_t)(s.n * B * 2));
+  const __amdgpu_buffer_rsrc_t prs = gm_rsrc(s.msg + slab * B, (uint32_t)(s.n * B));
   const uint32_t toff = (uint32_t)(r * B + li * Q) * 2;            // r >= n: out of range -> zeros, dropped
-  const uint32_t poff = (uint32_t)((par ^ 1) * B + li * Q);        // + sender * 2B
+  const uint32_t poff = (uint32_t)((par ^ 1) * (B / 2) + li * 8);  // + sender * B
+  // escape plane of this band: [n][2][B] bytes, cell (sender, parity, column)
+  const uint8_t *wsrc = s.wide + slab * 2 * B + (size_t)(par ^ 1) * B + li * Q;
   const RowMeta<B> meta = row_meta<B>(s, r, par, t);
   int k = meta.k;
   if (k > S_KMAX) {
@@ -132,10 +162,10 @@ __global__ __launch_bounds__(256) void gm_s_band(SState s, int t, int drop_pct) 
   // once; slots j >= k read out of range (zeros = "not sent"), so no branches
   const u32x4 ta = __builtin_amdgcn_raw_buffer_load_b128(trs, toff, 0, GM_AUX_NT);
   const u32x4 tb = __builtin_amdgcn_raw_buffer_load_b128(trs, toff + 16, 0, GM_AUX_NT);
-  u32x4 m[S_SB];
+  u32x2 m[S_SB];
 #pragma unroll
   for (int j = 0; j < S_SB; j++)
-    m[j] = __builtin_amdgcn_raw_buffer_load_b128(prs, (!DROP && j < k) ? poff + (uint32_t)meta.snd[j] * (2 * B) : GM_OOB, 0, 0);
+    m[j] = __builtin_amdgcn_raw_buffer_load_b64(prs, (!DROP && j < k) ? poff + (uint32_t)meta.snd[j] * B : GM_OOB, 0, 0);
   // lists to merge in this wave (uniform loop bound)
   int kw = 0;
   {
@@ -145,44 +175,51 @@ __global__ __launch_bounds__(256) void gm_s_band(SState s, int t, int drop_pct) 
   }
   int npres = 0, nfail = 0, nev = 0;
   uint32_t evk = 0;  // 2 bits per cell: event kind
+  bool esc_out = false;  // this lane sends a value only the wide plane can carry
+  uint32_t pw[8];        // payload h' per cell pair (u16 halves), 0 = not sent
   if (live) {
-    // merge key per cell = the largest delivered payload h (0 = nothing delivered).
-    // Bytewise max of packed payload words: as u16 lanes, max() is decided by the high
-    // byte, so odd bytes are maxed on the raw words and even bytes on the words
-    // shifted up by 8 within each u16 (3 packed ops per 4 cells per list).
-    u16x2 key[8];
+    // merge key per cell = the largest delivered payload h' (0 = nothing delivered), as
+    // key5 = h' << 5 (the cell with age 0) in the u16 halves of each table word
     const int32_t *ib = s.inbox[par] + (size_t)r * S_KMAX;
+    u16x2 key5[8];
     if (!DROP) {
-      u16x2 ko[4], ke[4];
+      u16x2 acc[8];
 #pragma unroll
-      for (int i = 0; i < 4; i++) ko[i] = ke[i] = (u16x2)(0);
+      for (int i = 0; i < 8; i++) acc[i] = (u16x2)(0);
 #pragma unroll
-      for (int j = 0; j < S_SB; j++) {
-        if (j < kw) {
-          const uint32_t w[4] = {m[j].x, m[j].y, m[j].z, m[j].w};
+      for (int j = 0; j < S_SB; j++)
+        if (j < kw) nib_max(acc, m[j].x, m[j].y);
+      for (int j = S_SB; j < k; j++) {  // rare: more lists than prefetched ids
+        const u32x2 mm = __builtin_amdgcn_raw_buffer_load_b64(prs, poff + (uint32_t)ib[j] * B, 0, 0);
+        nib_max(acc, mm.x, mm.y);
+      }
+      u16x2 nmax = (u16x2)(0);
 #pragma unroll
-          for (int i = 0; i < 4; i++) {
-            ko[i] = __builtin_elementwise_max(ko[i], pk(w[i]));
-            ke[i] = __builtin_elementwise_max(ke[i], pk(w[i]) << (u16x2)(8));
+      for (int i = 0; i < 8; i++) {
+        const u16x2 nb = acc[i] >> (u16x2)(12);
+        nmax = __builtin_elementwise_max(nmax, nb);
+        // h' = 224 + 2n for n >= 1: key5 = 7168 + 64 n, 0 for n = 0
+        key5[i] = (nb << (u16x2)(6)) + __builtin_elementwise_min(nb, (u16x2)(1)) * (u16x2)(S_NIB_BASE << 5);
+      }
+      if (__builtin_elementwise_max(nmax.x, nmax.y) == S_NIB_ESC) {
+        // rare (cold start, JOINREQ entries, lag > 13 ticks): some list escaped a cell of
+        // this lane; the exact key of those cells = max over the lists' decoded values
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+          const u16x2 nb = acc[i] >> (u16x2)(12);
+#pragma unroll
+          for (int h = 0; h < 2; h++) {
+            if (nb[h] != S_NIB_ESC) continue;
+            const int q = 2 * i + h;
+            uint32_t kv = 0;
+            for (int j = 0; j < k; j++) {  // reloads (no dynamic register indexing: no scratch)
+              const int sn = ib[j];
+              const u32x2 mm = __builtin_amdgcn_raw_buffer_load_b64(prs, poff + (uint32_t)sn * B, 0, 0);
+              kv = max(kv, nib_value(nib_of(mm.x, mm.y, q), wsrc + (size_t)sn * 2 * B + q));
+            }
+            key5[i][h] = (uint16_t)(kv << 5);
           }
         }
-      }
-      for (int j = S_SB; j < k; j++) {  // rare: more lists than prefetched ids
-        const u32x4 mm = __builtin_amdgcn_raw_buffer_load_b128(prs, poff + (uint32_t)ib[j] * (2 * B), 0, 0);
-        const uint32_t w[4] = {mm.x, mm.y, mm.z, mm.w};
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-          ko[i] = __builtin_elementwise_max(ko[i], pk(w[i]));
-          ke[i] = __builtin_elementwise_max(ke[i], pk(w[i]) << (u16x2)(8));
-        }
-      }
-      // cells 4i..4i+3 live in bytes 0..3 of word i: even cells in ke's high bytes,
-      // odd cells in ko's high bytes; key pairs = (cell 4i, 4i+1), (4i+2, 4i+3)
-#pragma unroll
-      for (int i = 0; i < 4; i++) {
-        const uint32_t e = unpk(ke[i]), o = unpk(ko[i]);
-        key[2 * i] = pk(__builtin_amdgcn_perm(o, e, 0x0c050c01u));      // [e.byte1, o.byte1]
-        key[2 * i + 1] = pk(__builtin_amdgcn_perm(o, e, 0x0c070c03u));  // [e.byte3, o.byte3]
       }
     } else {
       // per-entry drops keyed by (t_send, src, dst, global column) -- SCALED regime
@@ -191,28 +228,28 @@ __global__ __launch_bounds__(256) void gm_s_band(SState s, int t, int drop_pct) 
       for (int q = 0; q < Q; q++) kk[q] = 0;
       for (int j = 0; j < k; j++) {
         const int sn = ib[j];
-        const u32x4 mv = __builtin_amdgcn_raw_buffer_load_b128(prs, poff + (uint32_t)sn * (2 * B), 0, 0);
-        const uint32_t w[4] = {mv.x, mv.y, mv.z, mv.w};
+        const u32x2 mv = __builtin_amdgcn_raw_buffer_load_b64(prs, poff + (uint32_t)sn * B, 0, 0);
+        if (!(mv.x | mv.y)) continue;
         const uint64_t pair = gm_mix64(s.drop_seed ^ ((uint64_t)(uint32_t)(t - 1) << 48) ^
                                        ((uint64_t)(uint32_t)sn << 24) ^ (uint64_t)(uint32_t)r);
 #pragma unroll
         for (int q = 0; q < Q; q++) {
-          const uint32_t pv = (w[q >> 2] >> (8 * (q & 3))) & 0xFFu;
-          if (!pv) continue;
+          const uint32_t nb = nib_of(mv.x, mv.y, q);
+          if (!nb) continue;
           const uint32_t h = (uint32_t)(gm_mix64(pair + (uint64_t)(s.c0 + colb + q)) >> 32);
           if ((int)(h % 100u) < drop_pct) continue;
-          kk[q] = kk[q] > pv ? kk[q] : pv;
+          kk[q] = max(kk[q], nib_value(nb, wsrc + (size_t)sn * 2 * B + q));
         }
       }
 #pragma unroll
-      for (int i = 0; i < 8; i++) key[i] = pk(kk[2 * i] | (kk[2 * i + 1] << 16));
+      for (int i = 0; i < 8; i++) key5[i] = pk((kk[2 * i] << 5) | (kk[2 * i + 1] << 21));
     }
     if (s.ramp && r == 0) {  // the introducer takes the JOINREQs of the nodes that started at t-1:
       // entry {hb 0, ts t} = stored heartbeat 2t (offset 2(t-1+1)) = h 255 (MP1Node.cpp:226-251)
 #pragma unroll
       for (int q = 0; q < Q; q++) {
         const int c = s.c0 + colb + q;
-        if (c >= 1 && c < s.n && s_start(c) == t - 1) key[q >> 1] = pk(unpk(key[q >> 1]) | (255u << (16 * (q & 1))));
+        if (c >= 1 && c < s.n && s_start(c) == t - 1) key5[q >> 1][q & 1] = (uint16_t)(255u << 5);
       }
     }
     // merge: re-base the cell to tick t (h -= 2, age += 1; absent stays 0), then max
@@ -221,7 +258,7 @@ __global__ __launch_bounds__(256) void gm_s_band(SState s, int t, int drop_pct) 
     u16x2 mm[8];
 #pragma unroll
     for (int i = 0; i < 8; i++)
-      mm[i] = __builtin_elementwise_max(__builtin_elementwise_sub_sat(pk(tw[i]), (u16x2)(63)), key[i] << (u16x2)(5));
+      mm[i] = __builtin_elementwise_max(__builtin_elementwise_sub_sat(pk(tw[i]), (u16x2)(63)), key5[i]);
     const int selfc = (r >= s.c0 && r < s.c0 + s.w) ? r - s.c0 - colb : -1;
     if (selfc >= 0 && selfc < Q) {  // updateMyPos + heartbeat++ + myPos->setheartbeat(heartbeat++)
       const int hb = s.hbctr[r] + 1;
@@ -240,8 +277,8 @@ __global__ __launch_bounds__(256) void gm_s_band(SState s, int t, int drop_pct) 
     }
     // sweep (MP1Node.cpp:426-444), one packed pass: age >= TFAIL counts toward numfailed,
     // age >= TREMOVE removes; fresh entries (age < TFAIL) form the payload sent at tick t
-    u16x2 np2 = (u16x2)(0), nf2 = (u16x2)(0), evany = (u16x2)(0), lagmin = (u16x2)(0xFFFF);
-    uint32_t cw[8], pw[8];
+    u16x2 np2 = (u16x2)(0), nf2 = (u16x2)(0), evany = (u16x2)(0), lagmin = (u16x2)(0xFFFF), bad = (u16x2)(0);
+    uint32_t cw[8], nw[2] = {0u, 0u};
 #pragma unroll
     for (int i = 0; i < 8; i++) {
       const u16x2 v = mm[i];
@@ -252,13 +289,23 @@ __global__ __launch_bounds__(256) void gm_s_band(SState s, int t, int drop_pct) 
       nf2 += stale;
       np2 += __builtin_elementwise_min(v2, (u16x2)(1));
       // h - 2 for fresh cells; stale ones subtract >= 257 and saturate to 0 (not sent)
-      pw[i] = unpk(__builtin_elementwise_sub_sat(v >> (u16x2)(5), stale * (u16x2)(255) + (u16x2)(2)));
+      const u16x2 p2 = __builtin_elementwise_sub_sat(v >> (u16x2)(5), stale * (u16x2)(255) + (u16x2)(2));
+      pw[i] = unpk(p2);
+      // nibble: n = (h' - 224) / 2 for even h' in [226, 252]; other sent values escape (15)
+      const u16x2 nz = __builtin_elementwise_min(p2, (u16x2)(1));
+      const u16x2 n0 = (__builtin_elementwise_sub_sat(p2, (u16x2)(S_NIB_BASE + 2)) >> (u16x2)(1)) + nz;
+      const u16x2 re = n0 * (u16x2)(2) + (u16x2)(S_NIB_BASE);  // re-encoded value
+      const u16x2 b = __builtin_elementwise_min(re ^ p2, (u16x2)(1)) * nz;
+      bad |= b;
+      const u16x2 nib = __builtin_elementwise_max(n0, b * (u16x2)(S_NIB_ESC));
+      nw[i >> 2] += unpk(nib << (u16x2)(4 * (3 - (i & 3))));
       // joins: absent before, present after the merge; removals: gone
       evany |= __builtin_elementwise_sub_sat(__builtin_elementwise_min(v, (u16x2)(1)),
                                              __builtin_elementwise_min(pk(tw[i]), (u16x2)(1))) | gone;
       lagmin = __builtin_elementwise_min(lagmin, v2 - (u16x2)(32));  // present with h <= 2
       cw[i] = unpk(v2);
     }
+    esc_out = unpk(bad) != 0;
     nfail = (int)nf2.x + (int)nf2.y;
     npres = (int)np2.x + (int)np2.y;
     if (__builtin_elementwise_min(lagmin.x, lagmin.y) < 64) atomicOr(s.err, GM_ERR_LAG);
@@ -273,12 +320,16 @@ __global__ __launch_bounds__(256) void gm_s_band(SState s, int t, int drop_pct) 
       }
       nev = __builtin_popcount((evk | (evk >> 1)) & 0x55555555u);
     }
-    const u32x4 na = {cw[0], cw[1], cw[2], cw[3]}, nb = {cw[4], cw[5], cw[6], cw[7]};
+    const u32x4 na = {cw[0], cw[1], cw[2], cw[3]}, nb4 = {cw[4], cw[5], cw[6], cw[7]};
     __builtin_amdgcn_raw_buffer_store_b128(na, trs, toff, 0, GM_AUX_NT);
-    __builtin_amdgcn_raw_buffer_store_b128(nb, trs, toff + 16, 0, GM_AUX_NT);
-    const u32x4 ov = {__builtin_amdgcn_perm(pw[1], pw[0], 0x06040200u), __builtin_amdgcn_perm(pw[3], pw[2], 0x06040200u),
-                      __builtin_amdgcn_perm(pw[5], pw[4], 0x06040200u), __builtin_amdgcn_perm(pw[7], pw[6], 0x06040200u)};
-    __builtin_amdgcn_raw_buffer_store_b128(ov, prs, (uint32_t)(r * 2 * B + par * B + li * Q), 0, GM_AUX_NT);
+    __builtin_amdgcn_raw_buffer_store_b128(nb4, trs, toff + 16, 0, GM_AUX_NT);
+    const u32x2 ov = {nw[0], nw[1]};
+    __builtin_amdgcn_raw_buffer_store_b64(ov, prs, (uint32_t)(r * B + par * (B / 2) + li * 8), 0, GM_AUX_NT);
+    if (esc_out) {  // rare: the lane's 16 payload bytes into the escape plane (read where the nibble is 15)
+      const u32x4 wv = {__builtin_amdgcn_perm(pw[1], pw[0], 0x06040200u), __builtin_amdgcn_perm(pw[3], pw[2], 0x06040200u),
+                        __builtin_amdgcn_perm(pw[5], pw[4], 0x06040200u), __builtin_amdgcn_perm(pw[7], pw[6], 0x06040200u)};
+      *(u32x4 *)(s.wide + slab * 2 * B + (size_t)r * 2 * B + (size_t)par * B + li * Q) = wv;
+    }
     if (band == 0 && li == 0) s.wtick[r] = t;
   }
   // present cells per 64-column chunk (4 lanes) for the draw's rank-select, gathered

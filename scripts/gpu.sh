@@ -27,7 +27,7 @@ PT="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
 
 run_step() {
   case "$1" in
-    tests) timeout -k 10 900 $PT tests -m gpu --durations 15 ${PYTEST_ARGS:-} > $O/gpu_tests.txt 2>&1 ;;
+    tests) timeout -k 10 900 $PT ${TESTS:-tests} -m gpu --durations 15 > $O/gpu_tests.txt 2>&1 ;;
     smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 ;;
     sa) timeout -k 10 300 python -u bench.py ${BENCH_ARGS:-} > $O/bench_sa.json 2> $O/bench_sa.err ;;
     sc) timeout -k 10 400 python -u bench.py --scenario S-C ${BENCH_ARGS:-} > $O/bench_sc.json 2> $O/bench_sc.err ;;
@@ -42,7 +42,7 @@ run_step() {
             timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/pmc_sa_write -o p -- \
               python3 bench.py --no-cpu --steps 5 --warmup 1 > $O/pmc_sa_write.log 2>&1 &&
             python3 scripts/pmc_traffic.py --kernel gm_s_band --fetch $O/pmc_sa_fetch --write $O/pmc_sa_write \
-              --layout narrow-band --out $O/traffic_n65536.json > $O/pmc_sa.txt 2>&1 ;;
+              --layout nibble-band --out $O/traffic_n65536.json > $O/pmc_sa.txt 2>&1 ;;
     pmc_sc) timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/pmc_sc_fetch -o p -- \
               python3 bench.py --scenario S-C --no-cpu --steps 3 --warmup 1 > $O/pmc_sc_fetch.log 2>&1 &&
             timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/pmc_sc_write -o p -- \

@@ -75,16 +75,12 @@ def test_ramp_at_scale_converges():
     import numpy as np
     n = 16384
     sim = Simulator(n, GM_MODE_SCALED, rd_seed=7, init_mode=2)
-    joins = removes = 0
+    sim.keep_events(0)  # n^2 join records: counted on the device (gm_event_totals), not staged
     last = n // 4 + 40
     while sim.time <= last:
         sim.tick()
-        if sim.time % 256 == 0 or sim.time > last:
-            ev = sim.drain_events()
-            joins += sum(e[2] == 1 for e in ev)
-            removes += sum(e[2] == 2 for e in ev)
-        else:
-            joins += sim.event_total()  # join+remove records of the last tick
+    tot = sim.event_totals()
+    joins, removes = tot["joined"], tot["removed"]
     st = sim.tick_stats()
     assert st["err"] == 0 and st["live"] == n
     nodes = sim.read_nodes()

@@ -98,3 +98,42 @@ def test_scaled_invariants_large(warm):
         assert np.all(hb[crashed] == -1)
         assert np.all(hb[~crashed] >= 0)
         assert np.all(sim.time - 1 - ts[~crashed] < 20)  # present => younger than TREMOVE
+
+
+def _escaped_sends(dump, t):
+    """Fresh entries of live rows whose payload value h' = 253 - 2t + hb falls outside the
+    nibble range (h' < 226): sent through the escape plane at tick t (gm_scaled.h S_NIB_*)."""
+    esc = 0
+    for line in dump.decode().splitlines():
+        f = line.split()
+        if int(f[4]):
+            continue
+        for x in f[7:]:
+            _, hb, ts = map(int, x.split(":"))
+            esc += t - ts < 5 and 2 * t - hb > 27
+    return esc
+
+
+def test_scaled_escaped_payloads_match_oracle():
+    # 80 % loss for ticks 6..23 lets fresh entries carry heartbeats more than 13 ticks old;
+    # after the window the loss-free merge (nibble max + escape plane) must take them exactly
+    n = 600
+    kw = dict(rd_seed=7, drop_pct=80, drop_from=6, drop_to=24, drop_seed=42, init_mode=1, init_t0=5, init_seed=43)
+    ora = oracle_py.Oracle(n, oracle_py.OC_SCALED, crash_tick=9, crash_count=6, crash_seed=42, **kw)
+    sim = Simulator(n, GM_MODE_SCALED, **kw)
+    crash = crash_set(n, 6, 42)
+    kinds = {GM_EV_JOINED: 1, GM_EV_REMOVED: 2}
+    esc_after_window = 0
+    for _ in range(36):
+        t = sim.time
+        ora.tick()
+        sim.tick()
+        if t == 9:
+            sim.set_failed(crash)
+        assert [(e[0], e[1], kinds[e[2]], e[3]) for e in sim.drain_events()] == ora.events(), f"events t={t}"
+        d = ora.dump()
+        assert digest64(sim.dump_tables()) == digest64(d), f"tables differ at tick {t}"
+        if t >= 24:
+            esc_after_window += _escaped_sends(d, t)
+    assert esc_after_window > 0  # the escape plane really carried loss-free deliveries
+    assert sim.tick_stats()["err"] == 0
