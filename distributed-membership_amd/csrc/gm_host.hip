@@ -1186,15 +1186,34 @@ extern "C" int gm_shard_loopback(gm_ctx **ctxs, int32_t G, int32_t what, int32_t
   return GM_OK;
 }
 
+// Diagnostics: one column shard alone on a device (no RCCL, no peers): the all-gather of
+// per-row counts mirrors this shard's counts into every peer slot and the draw kernel
+// resolves draws landing in peer columns as fresh column ix (SState.stub) -- a symmetric
+// stand-in with the real kernels at the true shard shape (scripts/shard_profile.py --sb).
+extern "C" int gm_shard_stub(gm_ctx *c, int32_t on) {
+  if (!c || c->cfg.mode != GM_MODE_SCALED || !c->s.sharded) return GM_EINVAL;
+  c->s.stub = on ? 1 : 0;
+  return GM_OK;
+}
+
 static int tick_sharded(gm_ctx *c) {
-  if (!c->comm) return GM_EUNSUPPORTED;  // multi-GPU ticks need gm_comm_init (or the phase API + loopback)
+  if (!c->comm && !c->s.stub) return GM_EUNSUPPORTED;  // multi-GPU ticks need gm_comm_init (or the phase API + loopback)
   const size_t n = (size_t)c->n;
   TRY(gm_shard_merge(c));
-  NCCLCHECK(ncclAllGather(c->s.xcnt + (size_t)c->s.shard_rank * n * 2, c->s.xcnt, n * 2, ncclInt32, c->comm, c->stream));
+  if (c->s.stub) {
+    for (int g = 0; g < c->s.shard_count; g++)
+      if (g != c->s.shard_rank)
+        HIPCHECK(hipMemcpyAsync(c->s.xcnt + (size_t)g * n * 2, c->s.xcnt + (size_t)c->s.shard_rank * n * 2,
+                                sizeof(int32_t) * n * 2, hipMemcpyDeviceToDevice, c->stream));
+  } else {
+    NCCLCHECK(ncclAllGather(c->s.xcnt + (size_t)c->s.shard_rank * n * 2, c->s.xcnt, n * 2, ncclInt32, c->comm,
+                            c->stream));
+  }
   int round = 0, D = GM_D_FIRST;
   for (;;) {
     TRY(gm_shard_draw(c, round, D));
-    NCCLCHECK(ncclAllReduce(c->s.status, c->s.status, n * D, ncclInt32, ncclMax, c->comm, c->stream));
+    if (!c->s.stub)
+      NCCLCHECK(ncclAllReduce(c->s.status, c->s.status, n * D, ncclInt32, ncclMax, c->comm, c->stream));
     int32_t pend = 0;
     TRY(gm_shard_accept(c, D, &pend));
     if (pend == 0) break;

@@ -75,6 +75,8 @@ struct SState {
   // rehearse the sharded protocol + RCCL on one GPU; see gm_s_draw / gm_s_accept)
   int shard_rank, shard_count;
   int sharded;
+  int stub;                // diagnostics (gm_shard_stub): one shard alone on a device; draws landing in
+                           // other shards' columns resolve to fresh column ix (a symmetric stand-in)
   // ---- join ramp (gm_config.init_mode 2, single context): node j starts at tick j/4
   // (Application.cpp:130, STEP_RATE 0.25) and is in the group from tick j/4 + 2 if the
   // introducer (node 0) answered its JOINREQ at j/4 + 1 (ran that tick: <= intro_until).

@@ -710,7 +710,7 @@ __global__ __launch_bounds__(256) void gm_s_draw(SState s, int t, int round, int
     const bool ok = lane < cnt && (uint32_t)prod >= thr;
     const uint32_t ix = (uint32_t)(prod >> 32);
     const bool mine = ok && ix >= own_lo && ix < own_lo + own_cnt;
-    int32_t val = ok ? -1 : -2;
+    int32_t val = ok ? (s.stub ? (int32_t)((ix % (uint32_t)s.n) << 1) | 1 : -1) : -2;
     uint64_t m = __ballot(mine);
     if (m && !have_pre) {
       uint32_t osz, onf;

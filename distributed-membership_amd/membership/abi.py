@@ -38,7 +38,7 @@ EXPORTS = ["gm_parse_conf", "gm_create", "gm_destroy", "gm_tick", "gm_sync", "gm
            "gm_dump_tables", "gm_tick_stats", "gm_set_timing", "gm_last_kernel_ms", "gm_crash_set", "gm_strerror",
            "gm_comm_unique_id", "gm_comm_init", "gm_shard_layout", "gm_shard_merge", "gm_shard_draw",
            "gm_shard_accept", "gm_shard_end_tick", "gm_shard_loopback", "gm_partial_loopback_tick",
-           "gm_shard_exchange_bytes", "gm_keep_events", "gm_event_totals", "gm_read_views"]
+           "gm_shard_exchange_bytes", "gm_keep_events", "gm_event_totals", "gm_read_views", "gm_shard_stub"]
 
 _lib = None
 
@@ -68,7 +68,7 @@ def load_library():
         "gm_set_failed": [ctypes.c_void_p, P(i32), i32], "gm_set_dropmsg": [ctypes.c_void_p, i32],
         "gm_drain_events": [ctypes.c_void_p, P(GmEvent), sz, P(sz)],
         "gm_event_counts": [ctypes.c_void_p, P(u64)], "gm_event_totals": [ctypes.c_void_p, P(u64)],
-        "gm_keep_events": [ctypes.c_void_p, i32], "gm_read_views": [ctypes.c_void_p, i32, i32, P(u64)],
+        "gm_keep_events": [ctypes.c_void_p, i32], "gm_shard_stub": [ctypes.c_void_p, i32], "gm_read_views": [ctypes.c_void_p, i32, i32, P(u64)],
         "gm_msgcount": [ctypes.c_void_p, i32, P(i32), P(i32)],
         "gm_read_row": [ctypes.c_void_p, i32, i32, i32, P(i32), P(i32)],
         "gm_read_nodes": [ctypes.c_void_p, P(i32)],
@@ -288,6 +288,10 @@ class Simulator:
         v = ctypes.c_int64()
         self._call("gm_shard_exchange_bytes", self.h, ctypes.byref(v))
         return v.value
+
+    def shard_stub(self, on):
+        """Diagnostics: tick this column shard alone on its device (gm_shard_stub)."""
+        self._call("gm_shard_stub", self.h, 1 if on else 0)
 
     def shard_end_tick(self):
         self._call("gm_shard_end_tick", self.h)

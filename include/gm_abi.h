@@ -196,6 +196,10 @@ int gm_shard_accept(gm_ctx *ctx, int32_t D, int32_t *npending);
 int gm_shard_end_tick(gm_ctx *ctx);
 /* what = 0: all-gather the per-row counts; what = 1: MAX-allreduce the first n*D draws */
 int gm_shard_loopback(gm_ctx **ctxs, int32_t G, int32_t what, int32_t D);
+/* Diagnostics: tick ONE column shard alone on a device (no RCCL): peers' per-row counts
+ * mirror this shard's and draws landing in peer columns resolve to fresh column ix --
+ * the real kernels at the true shard shape, for measurement only (not a simulation). */
+int gm_shard_stub(gm_ctx *ctx, int32_t on);
 
 /* ---- PARTIAL row sharding (scenario S-C multi-GPU). A PARTIAL context with
  * shard_count = G > 1 owns nodes [n*g/G, n*(g+1)/G) (gm_shard_layout returns the

@@ -37,14 +37,56 @@ def serial_tick(sims):
     return rnd + 1
 
 
+def one_shard(a):
+    """--sb: ONE rank-g column shard of the S-B cluster (N = 262,144, G = 8: 262,144 rows x
+    32,768 columns) alone on this device, ticked by gm_tick in gm_shard_stub mode (peers'
+    counts mirrored, peer-column draws resolved as fresh column ix): the real merge / draw /
+    accept kernels at the true shard shape, without the collectives. Prints one JSON line."""
+    import json
+    n, g, rank = a.cluster or 262144, a.shards, a.rank
+    sim = Simulator(n, GM_MODE_SCALED, rd_seed=7, shard_rank=rank, shard_count=g, init_mode=1, init_t0=8, init_seed=11)
+    sim.keep_events(0)
+    sim.shard_stub(1)
+    crash = crash_set(n, n // 100, 42)
+    while sim.time <= a.prologue:
+        t = sim.time
+        sim.tick()
+        if t == 10:
+            sim.set_failed(crash)
+    for _ in range(3):
+        sim.tick()
+    sim.sync()
+    sim.set_timing(1)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        sim.tick()
+    sim.sync()
+    dt = (time.perf_counter() - t0) / a.steps
+    band_ms = sim.last_kernel_ms()
+    st = sim.tick_stats()
+    c0, w = sim.shard_layout()
+    b_alg = (9 * st["live"] + st["lists"]) * w // 2
+    out = {"what": "one S-B column shard alone on one MI355X (gm_shard_stub: collectives replaced by local stand-ins)",
+           "n": n, "shards": g, "rank": rank, "columns": w, "ms_per_tick": dt * 1e3, "band_kernel_ms": band_ms,
+           "other_kernels_ms": dt * 1e3 - band_ms, "live": st["live"], "lists": st["lists"], "err": st["err"],
+           "band_alg_bytes": b_alg, "band_achieved_gbps": b_alg / (band_ms * 1e-3) / 1e9 if band_ms > 0 else None,
+           "node_ticks_per_s_if_8_such_gpus": n / (dt if dt > 0 else 1)}
+    print(json.dumps(out), flush=True)
+
+
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--cluster", type=int, default=65536)
+    p.add_argument("--cluster", type=int, default=0)
     p.add_argument("--shards", type=int, default=8)
+    p.add_argument("--rank", type=int, default=3)
     p.add_argument("--prologue", type=int, default=25)
     p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--sb", action="store_true", help="one S-B shard alone on the device (gm_shard_stub)")
     a = p.parse_args()
     load_library()
+    if a.sb:
+        return one_shard(a)
+    a.cluster = a.cluster or 65536
     n, g = a.cluster, a.shards
     sims = [Simulator(n, GM_MODE_SCALED, rd_seed=7, shard_rank=r, shard_count=g, init_mode=1, init_t0=8, init_seed=11)
             for r in range(g)]
