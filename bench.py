@@ -157,7 +157,7 @@ def main():
     # TREMOVE sweep of the crashed nodes (MP1Node.cpp:429-444) -- every live observer removed
     # every crashed node exactly once, nothing else was removed or joined (device counters)
     tot = sim.event_totals()
-    removed_ok = (a.prologue + a.warmup + a.steps >= a.crash_tick + 25 and a.t0 > 0)
+    removed_ok = (a.prologue + a.warmup + a.steps >= a.crash_tick + 38 and a.t0 > 0)  # last removals ~tick 42
     if removed_ok:
         c0, wl = sim.shard_layout() if world > 1 else (0, n)  # a column shard counts its own columns
         crash_here = int(((crash >= c0) & (crash < c0 + wl)).sum())

@@ -263,6 +263,7 @@ static int create_scaled(gm_ctx *c) {
   const size_t cells = (size_t)n * s.wp;
   TRY(dalloc(c, &s.table, cells));
   c->nt = !(getenv("GM_NT") && !atoi(getenv("GM_NT")));  // non-temporal table streams, default on
+  s.pipe_waves = getenv("GM_BAND_PIPE") ? std::max(0, atoi(getenv("GM_BAND_PIPE"))) : 0;
   TRY(dalloc(c, &s.msg, cells));        // nibbles: 2 parities x band/2 bytes per (band, row)
   TRY(dalloc(c, &s.wide, 2 * cells));   // escape bytes: 2 parities x band
   for (int p = 0; p < 2; p++) {
@@ -285,13 +286,19 @@ static int create_scaled(gm_ctx *c) {
   // converged start (cold or warm, gm_config.init_mode); padding columns absent
   const bool warm = c->cfg.init_mode == 1;
   const int t0 = warm ? c->cfg.init_t0 : 0;
-  // join ramp (init_mode 2): one context, no keyed drops (a joiner must learn its own
-  // entry from the introducer's list, else updateMyPos's quirk path, MP1Node.cpp:316)
+  // join ramp (init_mode 2): one context; with keyed drops a joiner can miss its own entry
+  // and take updateMyPos's quirk path (MP1Node.cpp:316), handled in gm_s_band
   const bool ramp = c->cfg.init_mode == 2;
   if (c->cfg.init_mode < 0 || c->cfg.init_mode > 2 || (warm && (t0 < 5 || t0 > GM_T_LIMIT / 2))) return GM_EINVAL;
-  if (ramp && (s.sharded || c->cfg.drop_pct > 0)) return GM_EUNSUPPORTED;
+  if (ramp && s.sharded) return GM_EUNSUPPORTED;
   s.ramp = ramp ? 1 : 0;
   s.intro_until = 0x7FFFFFFF;
+  if (ramp) {
+    TRY(dalloc(c, &s.mecol, n));
+    TRY(dalloc(c, &s.selfadd, S_SELFADD_CAP));
+    TRY(dalloc(c, &s.selfadd_cnt, 1));
+    HIPCHECK(hipMemset(s.selfadd_cnt, 0, sizeof(uint32_t)));
+  }
   HIPCHECK(hipMemset(s.msg, 0, sizeof(uint8_t) * cells));
   for (int p = 0; p < 2; p++) HIPCHECK(hipMemset(s.inbox_cnt[p], 0, sizeof(int32_t) * n));
   HIPCHECK(hipMemset(s.failed, 0, sizeof(int32_t) * n));

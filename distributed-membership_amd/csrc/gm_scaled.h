@@ -7,6 +7,7 @@
 #define S_ROW_ALIGN 512          // padded row width granule (a multiple of every band width)
 #define S_SB 8                   // sender ids prefetched per row; payload loads in flight per lane
 #define S_MT_RAW 16              // mt19937 outputs precomputed per row and tick (gm_s_mtgen)
+#define S_SELFADD_CAP 65536      // join ramp: self appends verified per tick (gm_s_selfcheck)
 
 // SCALED cell (16 bits), relative to the tick w the row was last written at:
 //   h = 255 - (2w - hb) (8 bits, the heartbeat; larger = newer), age = w - ts (5 bits);
@@ -75,6 +76,7 @@ struct SState {
   // rehearse the sharded protocol + RCCL on one GPU; see gm_s_draw / gm_s_accept)
   int shard_rank, shard_count;
   int sharded;
+  int pipe_waves;          // > 0: the software-pipelined band kernel with this many waves (env GM_BAND_PIPE)
   int stub;                // diagnostics (gm_shard_stub): one shard alone on a device; draws landing in
                            // other shards' columns resolve to fresh column ix (a symmetric stand-in)
   // ---- join ramp (gm_config.init_mode 2, single context): node j starts at tick j/4
@@ -84,6 +86,9 @@ struct SState {
   // every live node's own heartbeat still reads 2t-1 and the narrow cell applies.
   int ramp;
   int intro_until;
+  int32_t *mecol;            // [n] ramp: myPos's column this tick (self, or the updateMyPos quirk's target)
+  int32_t *selfadd;          // [S_SELFADD_CAP] ramp: rows that appended their own entry this tick
+  uint32_t *selfadd_cnt;
   int32_t *xcnt;             // bound exchange buffer [shard_count][n][2]: (present, numfailed) per shard
   int32_t *status;           // bound exchange buffer [n][D]: resolved draws, MAX-allreduced
   int32_t *acc;              // [n][8]: targets so far, g[5], numpot, size

@@ -98,8 +98,13 @@ typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ u16x2 pk(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
 __device__ __forceinline__ uint32_t unpk(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
 // payload bytes 0,1 / 2,3 of a dword, zero-extended into the two halves
-__device__ __forceinline__ u16x2 bytes01(uint32_t w) { return pk(__builtin_amdgcn_perm(0u, w, 0x0c010c00u)); }
-__device__ __forceinline__ u16x2 bytes23(uint32_t w) { return pk(__builtin_amdgcn_perm(0u, w, 0x0c030c02u)); }
+// min(x, 1) per u16 half as ONE v_pk_min_u16: written as plain vector min the compiler
+// lowers it to a compare + select per half (5 instructions instead of 1)
+__device__ __forceinline__ u16x2 pmin1(u16x2 a) {
+  uint32_t r;
+  asm("v_pk_min_u16 %0, %1, 1 op_sel_hi:[1,0]" : "=v"(r) : "v"(unpk(a)));
+  return pk(r);
+}
 
 // Payload nibbles (gm_scaled.h S_NIB_*): dword w of a lane's 8-byte slice holds cells
 // 8w..8w+7; cell 8w+2k sits in nibble 3-k of the low u16, cell 8w+2k+1 in nibble 3-k
@@ -128,44 +133,80 @@ __device__ __forceinline__ uint32_t nib_value(uint32_t nb, const uint8_t *wide_c
   return nb == S_NIB_ESC ? (uint32_t)*wide_cell : nb ? S_NIB_H(nb) : 0u;
 }
 
+// One work unit of the band sweep: unit u = (band u / U, rows [(u % U) * RPW, +RPW)).
+// unit_load issues the row metadata and the table slice; unit_gather the payload slices
+// (needs the sender ids); unit_finish merges, sweeps, stores and records the counts.
+template <int B>
+struct UnitIn {
+  int band, r, k;  // k: lists delivered to this lane's row, -1 = not merged (crashed / absent / not in the group)
+  int snd[S_SB];
+  u32x4 ta, tb;    // the row's 16 cells of this lane (as loaded)
+};
+
+template <int B>
+__device__ __forceinline__ void unit_load(const SState &s, int t, int u, UnitIn<B> &in) {
+  constexpr int LPR = B / S_COLS_PER_LANE, RPW = 64 / LPR, Q = S_COLS_PER_LANE;
+  const int lane = threadIdx.x & 63;
+  const int sub = lane / LPR, li = lane % LPR;
+  const int U = (s.n + RPW - 1) / RPW;  // units per band
+  in.band = u / U;
+  in.r = (u - in.band * U) * RPW + sub;
+  const size_t slab = (size_t)in.band * s.n;
+  const __amdgpu_buffer_rsrc_t trs = gm_rsrc(s.table + slab * B, (uint32_t)(s.n * B * 2));
+  const uint32_t toff = (uint32_t)(in.r * B + li * Q) * 2;  // r >= n: out of range -> zeros, dropped
+  const RowMeta<B> meta = row_meta<B>(s, in.r, t & 1, t);
+#pragma unroll
+  for (int j = 0; j < S_SB; j++) in.snd[j] = meta.snd[j];
+  in.k = meta.k;
+  // the table slice is independent of the metadata: both in flight together
+  in.ta = __builtin_amdgcn_raw_buffer_load_b128(trs, toff, 0, GM_AUX_NT);
+  in.tb = __builtin_amdgcn_raw_buffer_load_b128(trs, toff + 16, 0, GM_AUX_NT);
+}
+
+// every payload slice at once; slots j >= k read out of range (zeros = "not sent")
 template <int B, bool DROP>
-__global__ __launch_bounds__(256) void gm_s_band(SState s, int t, int drop_pct) {
+__device__ __forceinline__ void unit_gather(const SState &s, int t, const UnitIn<B> &in, u32x2 m[S_SB]) {
+  constexpr int LPR = B / S_COLS_PER_LANE;
+  const int li = (threadIdx.x & 63) % LPR;
+  const __amdgpu_buffer_rsrc_t prs = gm_rsrc(s.msg + (size_t)in.band * s.n * B, (uint32_t)(s.n * B));
+  const uint32_t poff = (uint32_t)(((t & 1) ^ 1) * (B / 2) + li * 8);  // + sender * B
+  const int k = min(in.k, S_KMAX);
+#pragma unroll
+  for (int j = 0; j < S_SB; j++)
+    m[j] = __builtin_amdgcn_raw_buffer_load_b64(prs, (!DROP && j < k) ? poff + (uint32_t)in.snd[j] * B : GM_OOB, 0, 0);
+}
+
+template <int B, bool DROP>
+__device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct, const UnitIn<B> &in,
+                                            const u32x2 m[S_SB]) {
   constexpr int LPR = B / S_COLS_PER_LANE;  // lanes per row
   constexpr int RPW = 64 / LPR;             // rows per wave
   constexpr int Q = S_COLS_PER_LANE;        // cells per lane (8 packed pairs)
   const int lane = threadIdx.x & 63;
   const int par = t & 1;
   const int sub = lane / LPR, li = lane % LPR;
-  const int U = (s.n + RPW - 1) / RPW;  // units per band
-  // wave-uniform unit index (scalar registers: the band / row split stays on the SALU)
-  const int u = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
-  if (u >= U * s.nb) return;  // whole wave
-  const int band = u / U;
-  const int r = (u - band * U) * RPW + sub;
+  const int band = in.band, r = in.r;
   const int colb = band * B + li * Q;  // shard-local column of this lane's first cell
   const size_t slab = (size_t)band * s.n;
   // this band's slabs: table [n][B] cells, payload nibbles [n][2][B/2] bytes (32-bit offsets)
   const __amdgpu_buffer_rsrc_t trs = gm_rsrc(s.table + slab * B, (uint32_t)(s.n * B * 2));
   const __amdgpu_buffer_rsrc_t prs = gm_rsrc(s.msg + slab * B, (uint32_t)(s.n * B));
-  const uint32_t toff = (uint32_t)(r * B + li * Q) * 2;            // r >= n: out of range -> zeros, dropped
+  const uint32_t toff = (uint32_t)(r * B + li * Q) * 2;
   const uint32_t poff = (uint32_t)((par ^ 1) * (B / 2) + li * 8);  // + sender * B
   // escape plane of this band: [n][2][B] bytes, cell (sender, parity, column)
   const uint8_t *wsrc = s.wide + slab * 2 * B + (size_t)(par ^ 1) * B + li * Q;
-  const RowMeta<B> meta = row_meta<B>(s, r, par, t);
-  int k = meta.k;
+  int k = in.k;
   if (k > S_KMAX) {
     if (li == 0) atomicOr(s.err, GM_ERR_INBOX);
     k = S_KMAX;
   }
   const bool live = k >= 0;
-  // issue the table slice (independent of the metadata) and every payload slice at
-  // once; slots j >= k read out of range (zeros = "not sent"), so no branches
-  const u32x4 ta = __builtin_amdgcn_raw_buffer_load_b128(trs, toff, 0, GM_AUX_NT);
-  const u32x4 tb = __builtin_amdgcn_raw_buffer_load_b128(trs, toff + 16, 0, GM_AUX_NT);
-  u32x2 m[S_SB];
+  const u32x4 ta = in.ta, tb = in.tb;
+  struct {
+    int snd[S_SB];
+  } meta;
 #pragma unroll
-  for (int j = 0; j < S_SB; j++)
-    m[j] = __builtin_amdgcn_raw_buffer_load_b64(prs, (!DROP && j < k) ? poff + (uint32_t)meta.snd[j] * B : GM_OOB, 0, 0);
+  for (int j = 0; j < S_SB; j++) meta.snd[j] = in.snd[j];
   // lists to merge in this wave (uniform loop bound)
   int kw = 0;
   {
@@ -199,7 +240,7 @@ __global__ __launch_bounds__(256) void gm_s_band(SState s, int t, int drop_pct) 
         const u16x2 nb = acc[i] >> (u16x2)(12);
         nmax = __builtin_elementwise_max(nmax, nb);
         // h' = 224 + 2n for n >= 1: key5 = 7168 + 64 n, 0 for n = 0
-        key5[i] = (nb << (u16x2)(6)) + __builtin_elementwise_min(nb, (u16x2)(1)) * (u16x2)(S_NIB_BASE << 5);
+        key5[i] = pmin1(nb) * (u16x2)(S_NIB_BASE << 5) + (nb << (u16x2)(6));
       }
       if (__builtin_elementwise_max(nmax.x, nmax.y) == S_NIB_ESC) {
         // rare (cold start, JOINREQ entries, lag > 13 ticks): some list escaped a cell of
@@ -260,17 +301,43 @@ __global__ __launch_bounds__(256) void gm_s_band(SState s, int t, int drop_pct) 
     for (int i = 0; i < 8; i++)
       mm[i] = __builtin_elementwise_max(__builtin_elementwise_sub_sat(pk(tw[i]), (u16x2)(63)), key5[i]);
     const int selfc = (r >= s.c0 && r < s.c0 + s.w) ? r - s.c0 - colb : -1;
+    int selfapp = -1;  // lane cell of an appended self entry: no join record (push_back, not logNodeAdd)
     if (selfc >= 0 && selfc < Q) {  // updateMyPos + heartbeat++ + myPos->setheartbeat(heartbeat++)
       const int hb = s.hbctr[r] + 1;
       s.hbctr[r] = hb + 1;
-      const int h = 255 - (2 * t - (hb + s_hbase(s.ramp, r)));
+      // myPos = lower_bound(self) (MP1Node.cpp:308-322): self if present; else, by the `&&` at
+      // :316, the next larger id if one is present -- that entry takes the heartbeat and ts
+      // (the quirk); else self is appended. Nodes of one start tick (ids 4g..4g+3) share this
+      // lane, and the quirk's target is always one of them in practice (gm_s_selfcheck turns
+      // any other case into GM_ERR_SELF)
+      int tq = selfc;
+      uint32_t selfcell = 0;
+#pragma unroll
+      for (int q = 0; q < Q; q++)
+        if (q == selfc) selfcell = (unpk(mm[q >> 1]) >> (16 * (q & 1))) & 0xFFFFu;
+      if (selfcell == 0) {
+        if (!s.ramp) {
+          atomicOr(s.err, GM_ERR_SELF);
+        } else {
+#pragma unroll
+          for (int q = Q - 1; q >= 0; q--)  // smallest present id above self in the group
+            if (q > selfc && q <= (selfc | 3) && ((unpk(mm[q >> 1]) >> (16 * (q & 1))) & 0xFFFFu)) tq = q;
+          if (tq == selfc) {  // appended: verify afterwards that no larger id was present
+            selfapp = selfc;
+            const uint32_t slot = atomicAdd(s.selfadd_cnt, 1u);
+            if (slot < S_SELFADD_CAP) s.selfadd[slot] = r;
+            else atomicOr(s.err, GM_ERR_SELF);
+          }
+        }
+      }
+      if (s.ramp) s.mecol[r] = s.c0 + colb + tq;
+      const int h = 255 - (2 * t - (hb + s_hbase(s.ramp, s.c0 + colb + tq)));
       if (h < 3 || h > 255) atomicOr(s.err, GM_ERR_LAG);
 #pragma unroll
       for (int i = 0; i < 8; i++) {
-        if ((selfc >> 1) != i) continue;
+        if ((tq >> 1) != i) continue;
         uint32_t v = unpk(mm[i]);
-        const int sh = 16 * (selfc & 1);
-        if (((v >> sh) & 0xFFFFu) == 0) atomicOr(s.err, GM_ERR_SELF);
+        const int sh = 16 * (tq & 1);
         v = (v & ~(0xFFFFu << sh)) | ((uint32_t)S_CELL(h, 0) << sh);
         mm[i] = pk(v);
       }
@@ -287,21 +354,22 @@ __global__ __launch_bounds__(256) void gm_s_band(SState s, int t, int drop_pct) 
       const u16x2 gone = (a + (u16x2)(32 - GM_TREMOVE)) >> (u16x2)(5);  // age >= TREMOVE
       const u16x2 v2 = v * ((u16x2)(1) - gone);
       nf2 += stale;
-      np2 += __builtin_elementwise_min(v2, (u16x2)(1));
+      np2 += pmin1(v2);
       // h - 2 for fresh cells; stale ones subtract >= 257 and saturate to 0 (not sent)
       const u16x2 p2 = __builtin_elementwise_sub_sat(v >> (u16x2)(5), stale * (u16x2)(255) + (u16x2)(2));
       pw[i] = unpk(p2);
-      // nibble: n = (h' - 224) / 2 for even h' in [226, 252]; other sent values escape (15)
-      const u16x2 nz = __builtin_elementwise_min(p2, (u16x2)(1));
-      const u16x2 n0 = (__builtin_elementwise_sub_sat(p2, (u16x2)(S_NIB_BASE + 2)) >> (u16x2)(1)) + nz;
-      const u16x2 re = n0 * (u16x2)(2) + (u16x2)(S_NIB_BASE);  // re-encoded value
-      const u16x2 b = __builtin_elementwise_min(re ^ p2, (u16x2)(1)) * nz;
+      // nibble: n = (h' - 224) / 2, valid iff re-encoding gives h' back (even h' in [226, 252]);
+      // the re-encoding is forced to 0 for n = 0, so a sent value that maps to n = 0 escapes
+      // too, while "not sent" (h' = 0) stays 0; escapes carry 15 (the max)
+      const u16x2 n0 = __builtin_elementwise_sub_sat(p2, (u16x2)(S_NIB_BASE)) >> (u16x2)(1);
+      const u16x2 re = (n0 * (u16x2)(2) + (u16x2)(S_NIB_BASE)) * pmin1(n0);
+      const u16x2 b = pmin1(re ^ p2);
       bad |= b;
       const u16x2 nib = __builtin_elementwise_max(n0, b * (u16x2)(S_NIB_ESC));
-      nw[i >> 2] += unpk(nib << (u16x2)(4 * (3 - (i & 3))));
-      // joins: absent before, present after the merge; removals: gone
-      evany |= __builtin_elementwise_sub_sat(__builtin_elementwise_min(v, (u16x2)(1)),
-                                             __builtin_elementwise_min(pk(tw[i]), (u16x2)(1))) | gone;
+      nw[i >> 2] += unpk(nib * (u16x2)(1u << (4 * (3 - (i & 3)))));
+      // joins: absent before, present after the merge (t * 0xFFFF = -t saturates v away unless
+      // t = 0); removals: gone
+      evany |= __builtin_elementwise_sub_sat(v, pk(tw[i]) * (u16x2)(0xFFFF)) | gone;
       lagmin = __builtin_elementwise_min(lagmin, v2 - (u16x2)(32));  // present with h <= 2
       cw[i] = unpk(v2);
     }
@@ -315,7 +383,7 @@ __global__ __launch_bounds__(256) void gm_s_band(SState s, int t, int drop_pct) 
         const uint32_t before = (tw[q >> 1] >> (16 * (q & 1))) & 0xFFFFu;
         const uint32_t merged = (unpk(mm[q >> 1]) >> (16 * (q & 1))) & 0xFFFFu;
         const uint32_t after = (cw[q >> 1] >> (16 * (q & 1))) & 0xFFFFu;
-        const uint32_t ev = merged ? (!before ? S_EV_ADD : !after ? S_EV_REMOVE : 0u) : 0u;
+        const uint32_t ev = merged && q != selfapp ? (!before ? S_EV_ADD : !after ? S_EV_REMOVE : 0u) : 0u;
         evk |= ev << (2 * q);
       }
       nev = __builtin_popcount((evk | (evk >> 1)) & 0x55555555u);
@@ -399,6 +467,85 @@ __global__ __launch_bounds__(256) void gm_s_band(SState s, int t, int drop_pct) 
     if (s.sharded && live)
       atomicAdd((unsigned long long *)(s.xcnt + ((size_t)s.shard_rank * s.n + r) * 2),
                 (unsigned long long)(pf & 0xFFFF) | ((unsigned long long)(pf >> 16) << 32));
+  }
+}
+
+template <int B, bool DROP>
+__global__ __launch_bounds__(256) void gm_s_band(SState s, int t, int drop_pct) {
+  constexpr int RPW = 64 / (B / S_COLS_PER_LANE);
+  const int U = (s.n + RPW - 1) / RPW;
+  // wave-uniform unit index (scalar registers: the band / row split stays on the SALU)
+  const int u = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  if (u >= U * s.nb) return;  // whole wave
+  UnitIn<B> in;
+  unit_load<B>(s, t, u, in);
+  u32x2 m[S_SB];
+  unit_gather<B, DROP>(s, t, in, m);
+  unit_finish<B, DROP>(s, t, drop_pct, in, m);
+}
+
+// Software-pipelined variant (GM_BAND_PIPE=<waves>): a fixed grid of waves strides over the
+// units in band-major rounds; each wave issues the next unit's metadata + table slice
+// before it merges the current one, and its payload gathers right after -- two units in
+// flight per wave instead of one dependent load chain per unit.
+template <int B>
+__global__ __launch_bounds__(256) void gm_s_band_pipe(SState s, int t, int nwaves) {
+  constexpr int RPW = 64 / (B / S_COLS_PER_LANE);
+  const int total = ((s.n + RPW - 1) / RPW) * s.nb;
+  int u = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  if (u >= total) return;
+  UnitIn<B> cur, nxt;
+  u32x2 m[S_SB];
+  unit_load<B>(s, t, u, cur);
+  unit_gather<B, false>(s, t, cur, m);
+  for (;;) {
+    const int un = u + nwaves;
+    const bool more = un < total;  // wave-uniform
+    if (more) unit_load<B>(s, t, un, nxt);
+    unit_finish<B, false>(s, t, -1, cur, m);
+    if (!more) break;
+    unit_gather<B, false>(s, t, nxt, m);
+    cur = nxt;
+    u = un;
+  }
+}
+
+// --------------------------------------------------------------- gm_s_selfcheck
+// Join ramp: rows that appended their own entry this tick (updateMyPos found no self and no
+// larger id of its start group). The reference appends only if NO larger id is present
+// after the merge (lower_bound == end); a larger id of a later group would have taken the
+// quirk path with a heartbeat the narrow cell cannot hold. Verify, one wave per row: no
+// cell above the group is present after the sweep, none was removed by it (events).
+__global__ __launch_bounds__(256) void gm_s_selfcheck(SState s) {
+  const int lane = threadIdx.x & 63;
+  const int nw = gridDim.x * 4;
+  const uint32_t cnt = min(*s.selfadd_cnt, (uint32_t)S_SELFADD_CAP);
+  for (uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6); i < cnt; i += nw) {
+    const int r = s.selfadd[i];
+    const int gend = (r | 3) - s.c0;  // last shard column of the row's start group
+    const int b0 = (gend + 1) / s.band;
+    bool bad = false;
+    for (int b = b0 + 1 + lane; b < s.nb; b += 64) {  // whole bands above: nothing present, no events
+      const uint32_t v = s.bcnt[(size_t)r * s.nb + b];
+      bad |= S_BC_PRES(v) != 0 || S_BC_NEV(v) != 0;
+    }
+    if (b0 < s.nb) {
+      const uint16_t *cells = s.table + ((size_t)b0 * s.n + r) * s.band;
+      for (int j = lane; j < s.band; j += 64)
+        bad |= b0 * s.band + j > gend && cells[j] != 0;
+      const uint32_t v = s.bcnt[(size_t)r * s.nb + b0];
+      const int ne = min((int)S_BC_NEV(v), s.evs);
+      const uint32_t *ev = s.ev_band + ((size_t)r * s.nb + b0) * s.evs;
+      for (int q = lane; q < ne; q += 64) bad |= (int)(ev[q] & 0x3FFFFFFFu) - 1 - s.c0 > gend;
+      if ((int)S_BC_NEV(v) > s.evs) {  // spilled records of this (row, band)
+        const uint32_t ns = min(*s.ev_spill_cnt, s.ev_spill_cap);
+        for (uint32_t q = lane; q < ns; q += 64) {
+          const uint64_t e = s.ev_spill[q];
+          bad |= (int)(e >> 32) == r && (int)((uint32_t)e & 0x3FFFFFFFu) - 1 - s.c0 > gend;
+        }
+      }
+    }
+    if (__ballot(bad) && lane == 0) atomicOr(s.err, GM_ERR_SELF);
   }
 }
 
@@ -554,6 +701,7 @@ __global__ __launch_bounds__(256) void gm_s_pick(SState s, int t) {
   }
   uint32_t size, numfailed;
   gm_row_totals<B>(s, r, lane, pre, size, numfailed);
+  const int me = s.ramp ? s.mecol[r] : r;
   const int numpot = (int)size - 1 - (int)numfailed;  // numfailed counts removed entries too (MP1Node.cpp:463)
   const int target = min(GM_FANOUT, numpot);
   int n = 0, g0 = -1, g1 = -1, g2 = -1, g3 = -1, g4 = -1;
@@ -611,7 +759,7 @@ __global__ __launch_bounds__(256) void gm_s_pick(SState s, int t) {
             continue;
           }
           const int c = s.c0 + col[i];
-          if (c == r) continue;  // "me" (MP1Node.cpp:470)
+          if (c == me) continue;  // "me" = myPos's id (MP1Node.cpp:459-460,470)
           if (!fr[i]) continue;  // age >= TFAIL (MP1Node.cpp:471)
           if ((n > 0 && g0 == c) || (n > 1 && g1 == c) || (n > 2 && g2 == c) || (n > 3 && g3 == c)) continue;
           if (n == 0) g0 = c;
@@ -829,8 +977,14 @@ static hipError_t launch_tick_b(const SState &s, int t, int drop_pct, bool nt, h
   hipLaunchKernelGGL(gm_s_mtgen, dim3((s.n + 255) / 256), dim3(256), 0, st, s, t);
   if (k0) (void)hipEventRecord(k0, st);
   if (drop_pct >= 0) hipLaunchKernelGGL((gm_s_band<B, true>), dim3(nblk), dim3(256), 0, st, s, t, drop_pct);
+  else if (s.pipe_waves > 0)
+    hipLaunchKernelGGL((gm_s_band_pipe<B>), dim3((s.pipe_waves + 3) / 4), dim3(256), 0, st, s, t, 4 * ((s.pipe_waves + 3) / 4));
   else hipLaunchKernelGGL((gm_s_band<B, false>), dim3(nblk), dim3(256), 0, st, s, t, drop_pct);
   if (k1) (void)hipEventRecord(k1, st);
+  if (s.ramp) {
+    hipLaunchKernelGGL(gm_s_selfcheck, dim3(16), dim3(256), 0, st, s);
+    (void)hipMemsetAsync(s.selfadd_cnt, 0, sizeof(uint32_t), st);
+  }
   const size_t smem = sizeof(uint32_t) * 4 * gm_draw_lds_words(s.wp);
   if (pick) hipLaunchKernelGGL((gm_s_pick<B>), dim3((s.n + 3) / 4), dim3(256), smem, st, s, t);
   return hipGetLastError();

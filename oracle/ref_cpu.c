@@ -206,6 +206,8 @@ struct oc_ctx {
   int32_t *crash;
   /* SCALED join ramp (init_mode 2): the last tick the introducer ran */
   int intro_last;
+  /* test telemetry: updateMyPos quirk firings and the largest start-tick gap self -> target */
+  int64_t quirk_n, quirk_maxgap;
 };
 
 static int is_scaled(const oc_ctx *c) { return c->cfg.mode == OC_SCALED; }
@@ -301,6 +303,11 @@ static void en_recv(oc_ctx *c, node *nd) {
 /* MP1Node::updateMyPos (MP1Node.cpp:308-322), including the `&&` quirk at :316 */
 static void update_my_pos(oc_ctx *c, node *nd) {
   int p = lower_bound(&nd->list, nd->id, 0);
+  if (p < nd->list.n && nd->list.v[p].id != nd->id) { /* the quirk fires: myPos = the next larger id */
+    const int64_t gap = (int64_t)(int)(0.25 * (nd->list.v[p].id - 1)) - (int64_t)(int)(0.25 * (nd->id - 1));
+    c->quirk_n++;
+    if (gap > c->quirk_maxgap) c->quirk_maxgap = gap;
+  }
   if (p == nd->list.n || (nd->list.v[p].id != nd->id && nd->list.v[p].port != 0)) {
     entry e = {nd->id, 0, nd->heartbeat, c->t};
     el_push(&nd->list, e);
@@ -588,7 +595,7 @@ int oc_crash_set(int n, int count, uint64_t seed, int32_t *out) {
 oc_ctx *oc_create(const oc_config *cfg) {
   if (cfg->n <= 0) return NULL;
   if (cfg->mode == OC_SCALED && cfg->init_mode == 1 && cfg->init_t0 < 5) return NULL; /* hb >= 0 needs t0 >= 5 */
-  if (cfg->mode == OC_SCALED && cfg->init_mode == 2 && cfg->drop_pct > 0) return NULL; /* ramp: no keyed drops */
+  /* the join ramp with keyed drops runs the updateMyPos quirk path (MP1Node.cpp:316) */
   if (cfg->mode == OC_FAITHFUL && cfg->n > MAX_NODES) return NULL; /* EmulNet.cpp:108 assert */
   oc_ctx *c = (oc_ctx *)calloc(1, sizeof(oc_ctx));
   c->cfg = *cfg;
@@ -1122,4 +1129,11 @@ const char *op_dump(op_ctx *c, size_t *len) {
   }
   *len = c->dump.n;
   return c->dump.p ? c->dump.p : "";
+}
+
+/* test telemetry: [0] = updateMyPos quirk firings so far, [1] = largest start-tick gap
+ * between the node and the entry the quirk rewrote */
+void oc_quirks(const oc_ctx *c, int64_t out[2]) {
+  out[0] = c->quirk_n;
+  out[1] = c->quirk_maxgap;
 }

@@ -77,6 +77,8 @@ size_t oc_events(oc_ctx *c, const oc_event **ev);
 int oc_row(oc_ctx *c, int r, int32_t *hb, int32_t *ts);
 /* node state: inited, inGroup, bFailed, heartbeat counter */
 int oc_node(oc_ctx *c, int r, int32_t *state4);
+/* test telemetry: [0] = updateMyPos quirk firings, [1] = largest start-tick gap self -> target */
+void oc_quirks(const oc_ctx *c, int64_t out[2]);
 /* the crash set the SCALED driver uses (host fault injection) */
 int oc_crash_set(int n, int count, uint64_t seed, int32_t *out);
 

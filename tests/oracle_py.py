@@ -60,6 +60,8 @@ def lib():
         L.oc_events.restype = ctypes.c_size_t
         L.oc_row.argtypes = [ctypes.c_void_p, ctypes.c_int, P(ctypes.c_int32), P(ctypes.c_int32)]
         L.oc_node.argtypes = [ctypes.c_void_p, ctypes.c_int, P(ctypes.c_int32)]
+        L.oc_quirks.argtypes = [ctypes.c_void_p, P(ctypes.c_int64)]
+        L.oc_quirks.restype = None
         L.oc_crash_set.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint64, P(ctypes.c_int32)]
         L.oc_srand.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
         L.oc_rand_next.argtypes = [ctypes.c_void_p]
@@ -121,6 +123,12 @@ class Oracle:
 
     def dump(self):
         return self._buf("oc_dump")
+
+    def quirks(self):
+        """(updateMyPos quirk firings so far, largest start-tick gap self -> rewritten entry)"""
+        out = (ctypes.c_int64 * 2)()
+        self.L.oc_quirks(self.h, out)
+        return int(out[0]), int(out[1])
 
     def dbg(self):
         return self._buf("oc_dbg_log")

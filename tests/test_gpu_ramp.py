@@ -25,10 +25,13 @@ def seed_with(n, count, want):
     raise AssertionError("no seed")
 
 
-def run_ramp(n, ticks, crash_tick=-1, crash_count=0, crash_seed=42, band=0):
+def run_ramp(n, ticks, crash_tick=-1, crash_count=0, crash_seed=42, band=0, drop_pct=0, every=1, ora_out=None):
+    drops = dict(drop_pct=drop_pct, drop_from=0, drop_to=1 << 20, drop_seed=42)
     ora = oracle_py.Oracle(n, oracle_py.OC_SCALED, rd_seed=7, crash_tick=crash_tick, crash_count=crash_count,
-                           crash_seed=crash_seed, init_mode=2)
-    sim = Simulator(n, GM_MODE_SCALED, rd_seed=7, init_mode=2, band=band)
+                           crash_seed=crash_seed, init_mode=2, **drops)
+    sim = Simulator(n, GM_MODE_SCALED, rd_seed=7, init_mode=2, band=band, **drops)
+    if ora_out is not None:
+        ora_out.append(ora)
     crash = crash_set(n, crash_count, crash_seed)
     ora.tick()  # tick 0: nodeStart of nodes 0-3 (the GPU context starts as of tick 0)
     assert sim.time == ora.time == 1
@@ -44,7 +47,9 @@ def run_ramp(n, ticks, crash_tick=-1, crash_count=0, crash_seed=42, band=0):
         assert ev == ora.events(), f"events differ at tick {t}"
         joins += sum(e[2] == 1 for e in ev)
         removes += sum(e[2] == 2 for e in ev)
-        assert digest64(sim.dump_tables()) == digest64(ora.dump()), f"tables differ at tick {t}"
+        if t % every == 0 or sim.time > ticks:
+            assert digest64(sim.dump_tables()) == digest64(ora.dump()), f"tables differ at tick {t}"
+    assert digest64(sim.dump_tables()) == digest64(ora.dump()), "final tables differ"
     assert sim.tick_stats()["err"] == 0
     return joins, removes
 
@@ -90,3 +95,32 @@ def test_ramp_at_scale_converges():
         assert (hb >= 0).all(), r
     assert removes == 0
     assert joins == n * n - 1  # everyone learns everyone (incl. itself); the introducer's own entry is not a join
+
+
+@pytest.mark.parametrize("n,drop,band,every", [(300, 50, 128, 1), (1100, 10, 0, 4)])
+def test_ramp_with_drops_matches_oracle(n, drop, band, every):
+    """Keyed drops during the ramp: joiners miss their own entry in the lists they merge, so
+    updateMyPos (MP1Node.cpp:308-322) takes the `&&` quirk -- the next larger id present takes
+    the heartbeat and timestamp, and that id counts as "me" in the gossip draw (:459-470)."""
+    keep = []
+    joins, _ = run_ramp(n, n // 4 + 30, band=band, drop_pct=drop, every=every, ora_out=keep)
+    fired, gap = keep[0].quirks()
+    assert fired > 0 and gap == 0, (fired, gap)
+    assert joins > 0
+
+
+def test_ramp_with_drops_at_scale():
+    """N = 16,384 ramp under 10 % keyed drops (no oracle at this size): the quirk path never
+    meets a case the narrow cell cannot hold (err stays 0: gm_s_selfcheck, GM_ERR_LAG), and
+    every node ends up in the group."""
+    n = 16384
+    sim = Simulator(n, GM_MODE_SCALED, rd_seed=7, init_mode=2, drop_pct=10, drop_from=0, drop_to=1 << 20,
+                    drop_seed=42)
+    sim.keep_events(0)
+    while sim.time <= n // 4 + 40:
+        sim.tick()
+    st = sim.tick_stats()
+    assert st["err"] == 0 and st["live"] == n
+    nodes = sim.read_nodes()
+    assert (nodes[:, 0] == 1).all() and (nodes[:, 1] == 1).all()
+    assert sim.event_totals()["joined"] >= n * n - 1
