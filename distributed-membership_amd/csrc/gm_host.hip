@@ -24,8 +24,9 @@ __global__ void gm_f_node(FState s, int t);
 __global__ void gm_f_send(FState s, int t);
 hipError_t gm_launch_tick(const SState &s, int t, int drop_pct, bool nt, hipStream_t st, hipEvent_t k0, hipEvent_t k1,
                           bool pick);
-hipError_t gm_launch_draw(const SState &s, int t, int round, int D, hipStream_t st);
-hipError_t gm_launch_accept(const SState &s, int t, int D, hipStream_t st);
+hipError_t gm_launch_draw(const SState &s, int t, int round, int D, int listed, hipStream_t st);
+hipError_t gm_launch_accept(const SState &s, int t, int D, int mode, hipStream_t st);
+hipError_t gm_launch_plist_sort(const SState &s, hipStream_t st);
 hipError_t gm_launch_init(const SState &s, int warm, int t0, uint64_t seed, hipStream_t st);
 hipError_t gm_launch_partial_tick(const PState &s, int t, uint32_t *mtraw, hipStream_t st, hipEvent_t k0,
                                   hipEvent_t k1);
@@ -46,6 +47,9 @@ struct gm_ctx {
   std::vector<hipEvent_t> tev;            // per-tick band-kernel event pairs (single context)
   double kernel_ms_sum = 0;
   bool nt = true;                    // non-temporal table streams (env GM_NT=0 to disable)
+  int shard_sync = -1;               // sharded tick draw rounds: 1 host-driven unbounded loop, 0 bounded
+                                     // stream-ordered, -1 auto (env GM_SHARD_SYNC)
+  int64_t nfailed = 0;               // nodes with failed_h set (gm_set_failed)
   int t = 0;
   int n = 0;
   int dropmsg = 0;
@@ -264,6 +268,7 @@ static int create_scaled(gm_ctx *c) {
   TRY(dalloc(c, &s.table, cells));
   c->nt = !(getenv("GM_NT") && !atoi(getenv("GM_NT")));  // non-temporal table streams, default on
   s.pipe_waves = getenv("GM_BAND_PIPE") ? std::max(0, atoi(getenv("GM_BAND_PIPE"))) : 0;
+  c->shard_sync = getenv("GM_SHARD_SYNC") ? (atoi(getenv("GM_SHARD_SYNC")) ? 1 : 0) : -1;
   TRY(dalloc(c, &s.msg, cells));        // nibbles: 2 parities x band/2 bytes per (band, row)
   TRY(dalloc(c, &s.wide, 2 * cells));   // escape bytes: 2 parities x band
   for (int p = 0; p < 2; p++) {
@@ -273,8 +278,7 @@ static int create_scaled(gm_ctx *c) {
   TRY(dalloc(c, &s.hbctr, n));
   TRY(dalloc(c, &s.wtick, n));
   TRY(dalloc(c, &s.failed, n));
-  TRY(dalloc(c, &s.bcnt, (size_t)n * s.nb));
-  TRY(dalloc(c, &s.ccnt, (size_t)n * (s.wp >> 6)));
+  TRY(dalloc(c, &s.brec, (size_t)n * s.nb));
   TRY(dalloc(c, &s.ev_band, (size_t)n * s.nb * s.evs));
   TRY(dalloc(c, &s.ev_spill, s.ev_spill_cap));
   TRY(dalloc(c, &s.ev_spill_cnt, 1));
@@ -304,7 +308,7 @@ static int create_scaled(gm_ctx *c) {
   HIPCHECK(hipMemset(s.failed, 0, sizeof(int32_t) * n));
   HIPCHECK(gm_launch_init(s, ramp ? 2 : warm ? 1 : 0, t0, c->cfg.init_seed, c->stream));
   HIPCHECK(hipStreamSynchronize(c->stream));
-  HIPCHECK(hipMemset(s.bcnt, 0, sizeof(uint32_t) * (size_t)n * s.nb));
+  HIPCHECK(hipMemset(s.brec, 0, sizeof(uint4) * (size_t)n * s.nb));
   HIPCHECK(hipMemset(s.ev_spill_cnt, 0, sizeof(uint32_t)));
   HIPCHECK(hipMemset(s.evcum, 0, sizeof(uint64_t) * (size_t)n * s.nb));
   HIPCHECK(hipMemset(s.rowstat, 0, sizeof(int32_t) * n * 4));
@@ -316,6 +320,12 @@ static int create_scaled(gm_ctx *c) {
     c->dmax = 64;
     TRY(dalloc(c, &s.xcnt, (size_t)G * n * 2));
     TRY(dalloc(c, &s.status, (size_t)n * c->dmax));
+    // bounded rounds (tick_sharded): round 0 takes every row's first 16 S2 outputs, round 1
+    // the next 64 for up to plist_cap rows left pending -- no host round trip per tick
+    s.plist_cap = std::min(S_PLIST_CAP, std::max(256, n / 16));
+    TRY(dalloc(c, &s.plist, s.plist_cap));
+    TRY(dalloc(c, &s.plist_cnt, 1));
+    TRY(dalloc(c, &s.status1, (size_t)s.plist_cap * c->dmax));
     HIPCHECK(hipMemset(s.pending, 0, sizeof(int32_t) * n));
     HIPCHECK(hipMemset(s.xcnt, 0, sizeof(int32_t) * (size_t)G * n * 2));
   }
@@ -639,6 +649,7 @@ extern "C" int gm_set_failed(gm_ctx *c, const int32_t *idx, int32_t n) {
   for (int k = 0; k < n; k++)  // validate everything before any state changes
     if (idx[k] < 0 || idx[k] >= c->n) return GM_EINVAL;
   for (int k = 0; k < n; k++) {
+    c->nfailed += c->failed_h[idx[k]] == 0;
     if (!c->failed_h[idx[k]]) c->fail_t[idx[k]] = c->t - 1;
     c->failed_h[idx[k]] = 1;
     // join ramp: the introducer's last tick bounds who gets a JOINREP
@@ -658,14 +669,26 @@ extern "C" int gm_set_dropmsg(gm_ctx *c, int32_t on) {
   return GM_OK;
 }
 
+// The S_BC words of the last tick in (row, band) order (the device keeps [band][row] records).
+static int read_bcnt(gm_ctx *c, std::vector<uint32_t> &bc) {
+  const SState &s = c->s;
+  const size_t n = (size_t)c->n, nrb = n * s.nb;
+  std::vector<uint4> rec(nrb);
+  HIPCHECK(hipMemcpyAsync(rec.data(), s.brec, sizeof(uint4) * nrb, hipMemcpyDeviceToHost, c->stream));
+  HIPCHECK(hipStreamSynchronize(c->stream));
+  bc.resize(nrb);
+  for (size_t b = 0; b < (size_t)s.nb; b++)
+    for (size_t r = 0; r < n; r++) bc[r * s.nb + b] = rec[b * n + r].z;
+  return GM_OK;
+}
+
 static int drain_scaled(gm_ctx *c, std::vector<gm_event> &out) {
   const SState &s = c->s;
   const size_t nrb = (size_t)c->n * s.nb;
-  std::vector<uint32_t> bc(nrb);
+  std::vector<uint32_t> bc;
   uint32_t nsp = 0;
-  HIPCHECK(hipMemcpyAsync(bc.data(), s.bcnt, sizeof(uint32_t) * nrb, hipMemcpyDeviceToHost, c->stream));
   HIPCHECK(hipMemcpyAsync(&nsp, s.ev_spill_cnt, sizeof nsp, hipMemcpyDeviceToHost, c->stream));
-  HIPCHECK(hipStreamSynchronize(c->stream));
+  TRY(read_bcnt(c, bc));
   const int t = c->t - 1;
   auto push = [&](int r, uint32_t rec) {
     out.push_back(gm_event{t, r, (int)(rec >> 30) == (int)S_EV_ADD ? GM_EV_JOINED : GM_EV_REMOVED,
@@ -763,10 +786,8 @@ extern "C" int gm_event_counts(gm_ctx *c, uint64_t counts[6]) {
   if (!c || !counts) return GM_EINVAL;
   for (int k = 0; k < 6; k++) counts[k] = 0;
   if (c->cfg.mode == GM_MODE_SCALED) {
-    const size_t nrb = (size_t)c->n * c->s.nb;
-    std::vector<uint32_t> bc(nrb);
-    HIPCHECK(hipMemcpyAsync(bc.data(), c->s.bcnt, sizeof(uint32_t) * nrb, hipMemcpyDeviceToHost, c->stream));
-    HIPCHECK(hipStreamSynchronize(c->stream));
+    std::vector<uint32_t> bc;
+    TRY(read_bcnt(c, bc));
     uint64_t tot = 0;
     for (uint32_t v : bc) tot += S_BC_NEV(v);  // slots + spilled, per (row, band)
     counts[0] = tot;  // join+remove records of the last tick (per-kind split needs a drain)
@@ -1023,10 +1044,6 @@ extern "C" int gm_last_kernel_ms(gm_ctx *c, float *ms) {
   if (!c || !ms) return GM_EINVAL;
   *ms = 0.f;
   if (!c->timing || c->cfg.mode == GM_MODE_FAITHFUL || c->timed_ticks == 0) return GM_OK;
-  if (c->cfg.mode == GM_MODE_SCALED && c->s.sharded) {  // per-tick merge-kernel events, summed at each tick end
-    *ms = (float)(c->kernel_ms_sum / c->timed_ticks);
-    return GM_OK;
-  }
   HIPCHECK(hipEventSynchronize(c->e1));
   double sum = c->kernel_ms_sum;  // folded ring slots + the pairs still in the ring
   for (int k = std::max(0, c->ktimed - GM_TEV_RING); k < c->ktimed; k++) {
@@ -1121,8 +1138,9 @@ extern "C" int gm_shard_merge(gm_ctx *c) {
   const bool drop = c->cfg.drop_pct > 0 && t_send >= c->cfg.drop_from && t_send < c->cfg.drop_to;
   HIPCHECK(hipMemsetAsync(c->s.xcnt + (size_t)c->s.shard_rank * c->n * 2, 0, sizeof(int32_t) * 2 * (size_t)c->n,
                           c->stream));
-  HIPCHECK(gm_launch_tick(c->s, c->t, drop ? c->cfg.drop_pct : -1, c->nt, c->stream, c->timing ? c->k0 : nullptr,
-                          c->timing ? c->k1 : nullptr, false));
+  hipEvent_t k0 = nullptr, k1 = nullptr;
+  if (c->timing) TRY(timing_slot(c, &k0, &k1));
+  HIPCHECK(gm_launch_tick(c->s, c->t, drop ? c->cfg.drop_pct : -1, c->nt, c->stream, k0, k1, false));
   return GM_OK;
 }
 
@@ -1130,7 +1148,7 @@ extern "C" int gm_shard_draw(gm_ctx *c, int32_t round, int32_t D) {
   TRY(shard_ready(c));
   // round 0 covers the precomputed S2 outputs [0, 16), round q >= 1 outputs [16 + 64(q-1), 16 + 64q)
   if (round < 0 || D != (round == 0 ? GM_D_FIRST : GM_D_MORE)) return GM_EINVAL;
-  HIPCHECK(gm_launch_draw(c->s, c->t, round, D, c->stream));
+  HIPCHECK(gm_launch_draw(c->s, c->t, round, D, 0, c->stream));
   return GM_OK;
 }
 
@@ -1138,7 +1156,7 @@ extern "C" int gm_shard_accept(gm_ctx *c, int32_t D, int32_t *npending) {
   TRY(shard_ready(c));
   if (D <= 0 || D > c->dmax || !npending) return GM_EINVAL;
   HIPCHECK(hipMemsetAsync(c->s.npending, 0, sizeof(int32_t), c->stream));
-  HIPCHECK(gm_launch_accept(c->s, c->t, D, c->stream));
+  HIPCHECK(gm_launch_accept(c->s, c->t, D, 0, c->stream));
   HIPCHECK(hipMemcpyAsync(npending, c->s.npending, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
   HIPCHECK(hipStreamSynchronize(c->stream));
   return GM_OK;
@@ -1146,11 +1164,8 @@ extern "C" int gm_shard_accept(gm_ctx *c, int32_t D, int32_t *npending) {
 
 extern "C" int gm_shard_end_tick(gm_ctx *c) {
   TRY(shard_ready(c));
-  if (c->timing) {
-    float ms = 0;
-    HIPCHECK(hipEventSynchronize(c->k1));
-    HIPCHECK(hipEventElapsedTime(&ms, c->k0, c->k1));
-    c->kernel_ms_sum += ms;
+  if (c->timing) {  // band-kernel events are in the timing ring (no host wait here)
+    HIPCHECK(hipEventRecord(c->e1, c->stream));
     c->timed_ticks++;
   }
   c->t++;
@@ -1215,6 +1230,30 @@ static int tick_sharded(gm_ctx *c) {
   } else {
     NCCLCHECK(ncclAllGather(c->s.xcnt + (size_t)c->s.shard_rank * n * 2, c->s.xcnt, n * 2, ncclInt32, c->comm,
                             c->stream));
+  }
+  const int64_t nfailed = c->nfailed;
+  // mass failure or heavy loss leaves many entries stale, so rows need many draws: the
+  // host-driven unbounded loop below (also GM_SHARD_SYNC=1)
+  const bool sync = c->shard_sync == 1 || (c->shard_sync < 0 && (c->cfg.drop_pct >= 30 || 10 * nfailed > (int64_t)n));
+  if (!sync) {
+    // bounded rounds, stream-ordered (no host round trip): round 0 = every row's first 16
+    // S2 outputs; rows left pending go to a list (sorted: identical on every rank) that
+    // round 1 serves with the next 64; a row still short after that sets GM_ERR_DRAWS
+    SState &s = c->s;
+    HIPCHECK(hipMemsetAsync(s.plist_cnt, 0, sizeof(uint32_t), c->stream));
+    HIPCHECK(gm_launch_draw(s, c->t, 0, GM_D_FIRST, 0, c->stream));
+    if (!s.stub)
+      NCCLCHECK(ncclAllReduce(s.status, s.status, n * GM_D_FIRST, ncclInt32, ncclMax, c->comm, c->stream));
+    HIPCHECK(gm_launch_accept(s, c->t, GM_D_FIRST, 1, c->stream));
+    HIPCHECK(gm_launch_plist_sort(s, c->stream));
+    HIPCHECK(gm_launch_draw(s, c->t, 1, GM_D_MORE, 1, c->stream));
+    if (!s.stub)
+      NCCLCHECK(ncclAllReduce(s.status1, s.status1, (size_t)s.plist_cap * GM_D_MORE, ncclInt32, ncclMax, c->comm,
+                              c->stream));
+    HIPCHECK(gm_launch_accept(s, c->t, GM_D_MORE, 2, c->stream));
+    c->t--;  // gm_tick advances globaltime
+    TRY(gm_shard_end_tick(c));
+    return GM_OK;
   }
   int round = 0, D = GM_D_FIRST;
   for (;;) {

@@ -8,6 +8,7 @@
 #define S_SB 8                   // sender ids prefetched per row; payload loads in flight per lane
 #define S_MT_RAW 16              // mt19937 outputs precomputed per row and tick (gm_s_mtgen)
 #define S_SELFADD_CAP 65536      // join ramp: self appends verified per tick (gm_s_selfcheck)
+#define S_PLIST_CAP 4096         // sharded tick: rows a second (bounded) draw round takes
 
 // SCALED cell (16 bits), relative to the tick w the row was last written at:
 //   h = 255 - (2w - hb) (8 bits, the heartbeat; larger = newer), age = w - ts (5 bits);
@@ -38,6 +39,7 @@ __host__ __device__ inline bool s_ingroup(int ramp, int intro_until, int r, int 
 #define S_EV_REMOVE 2u
 
 // bcnt word of one (row, band): present | numfailed << 11 | events << 22 (saturating)
+#include <hip/hip_runtime.h>
 #define S_BC_PRES(v) ((v) & 0x7FFu)
 #define S_BC_FAIL(v) (((v) >> 11) & 0x7FFu)
 #define S_BC_NEV(v) ((v) >> 22)
@@ -62,8 +64,8 @@ struct SState {
   int32_t *inbox[2];       // [n][S_KMAX] sender rows
   int32_t *hbctr;          // [n] MP1Node heartbeat counter (Member::heartbeat)
   int32_t *failed;         // [n] Member::bFailed
-  uint32_t *bcnt;          // [n][nb] per-(row, band) counts after the sweep (S_BC_*)
-  uint8_t *ccnt;           // [nb][n][band/64] present cells per 64-column chunk after the sweep (rank-select)
+  uint4 *brec;             // [nb][n] per-(band, row) record after the sweep: .x/.y = present cells per 64-column
+                           // chunk (band/64 bytes, rank-select), .z = bcnt word (S_BC_*); rows adjacent = whole-line writes
   uint32_t *ev_band;       // [n][nb][evs] kind<<30 | subject id
   uint64_t *ev_spill;      // overflow: (logger<<32) | kind<<30 | subject id
   uint32_t *ev_spill_cnt;
@@ -94,4 +96,8 @@ struct SState {
   int32_t *acc;              // [n][8]: targets so far, g[5], numpot, size
   int32_t *pending;          // [n] rows still drawing
   int32_t *npending;         // rows still drawing after the last accept round
+  int plist_cap;             // bounded rounds: capacity of the pending-row list (<= S_PLIST_CAP)
+  int32_t *plist;            // [plist_cap] rows pending after round 0 (ascending after gm_s_plist_sort)
+  uint32_t *plist_cnt;
+  int32_t *status1;          // bound exchange buffer [plist_cap][GM_D_MORE]: round-1 draws of the listed rows
 };

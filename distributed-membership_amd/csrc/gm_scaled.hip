@@ -401,22 +401,13 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
     if (band == 0 && li == 0) s.wtick[r] = t;
   }
   // present cells per 64-column chunk (4 lanes) for the draw's rank-select, gathered
-  // into the row's first lane and stored as one B/64-byte piece of the band slab
+  // into the row's first lane: bytes 0..B/64-1 of the (band, row) record
   int cc = npres;
   cc += __shfl_xor(cc, 1, 64);
   cc += __shfl_xor(cc, 2, 64);
-  {
-    uint64_t piece = 0;
+  uint64_t piece = 0;
 #pragma unroll
-    for (int c = 0; c < B / 64; c++) piece |= (uint64_t)(__shfl(cc, sub * LPR + 4 * c, 64) & 0xFF) << (8 * c);
-    if (live && li == 0) {
-      uint8_t *dst = s.ccnt + (slab + r) * (B / 64);
-      if (B == 64) *dst = (uint8_t)piece;
-      else if (B == 128) *(uint16_t *)dst = (uint16_t)piece;
-      else if (B == 256) *(uint32_t *)dst = (uint32_t)piece;
-      else *(uint64_t *)dst = piece;
-    }
-  }
+  for (int c = 0; c < B / 64; c++) piece |= (uint64_t)(__shfl(cc, sub * LPR + 4 * c, 64) & 0xFF) << (8 * c);
   // per-row reductions over the row's LPR lanes (aligned lane segments): counts packed
   // as present | numfailed << 16 (each <= B)
   int pf = npres | (nfail << 16);
@@ -460,8 +451,9 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
     }
   }
   if (li == 0 && r < s.n) {
-    s.bcnt[(size_t)r * s.nb + band] =
-        live ? ((uint32_t)(pf & 0xFFFF) | ((uint32_t)(pf >> 16) << 11) | ((uint32_t)min(tot, 1023) << 22)) : 0u;
+    // one 16-byte record per (band, row), consecutive rows adjacent: whole-line writes
+    const uint32_t bc = (uint32_t)(pf & 0xFFFF) | ((uint32_t)(pf >> 16) << 11) | ((uint32_t)min(tot, 1023) << 22);
+    s.brec[slab + r] = live ? make_uint4((uint32_t)piece, (uint32_t)(piece >> 32), bc, 0u) : make_uint4(0u, 0u, 0u, 0u);
     // column shard: this shard's row totals (present, numfailed) for the all-gather,
     // accumulated as one packed 64-bit add per (row, band) into the zeroed slot
     if (s.sharded && live)
@@ -526,14 +518,14 @@ __global__ __launch_bounds__(256) void gm_s_selfcheck(SState s) {
     const int b0 = (gend + 1) / s.band;
     bool bad = false;
     for (int b = b0 + 1 + lane; b < s.nb; b += 64) {  // whole bands above: nothing present, no events
-      const uint32_t v = s.bcnt[(size_t)r * s.nb + b];
+      const uint32_t v = s.brec[(size_t)b * s.n + r].z;
       bad |= S_BC_PRES(v) != 0 || S_BC_NEV(v) != 0;
     }
     if (b0 < s.nb) {
       const uint16_t *cells = s.table + ((size_t)b0 * s.n + r) * s.band;
       for (int j = lane; j < s.band; j += 64)
         bad |= b0 * s.band + j > gend && cells[j] != 0;
-      const uint32_t v = s.bcnt[(size_t)r * s.nb + b0];
+      const uint32_t v = s.brec[(size_t)b0 * s.n + r].z;
       const int ne = min((int)S_BC_NEV(v), s.evs);
       const uint32_t *ev = s.ev_band + ((size_t)r * s.nb + b0) * s.evs;
       for (int q = lane; q < ne; q += 64) bad |= (int)(ev[q] & 0x3FFFFFFFu) - 1 - s.c0 > gend;
@@ -562,11 +554,11 @@ __device__ __forceinline__ void gm_row_totals(const SState &s, int r, int lane, 
   constexpr int CPB = B / 64;  // chunks per band
   const int nb = s.nb, perb = (nb + 63) >> 6;
   const int b0 = min(nb, lane * perb), b1 = min(nb, b0 + perb);
-  const uint32_t *bc = s.bcnt + (size_t)r * nb;
   uint32_t fs = 0, ps = 0;
   for (int b = b0; b < b1; b++) {
-    fs += S_BC_FAIL(bc[b]);
-    ps += S_BC_PRES(bc[b]);
+    const uint32_t v = s.brec[(size_t)b * s.n + r].z;
+    fs += S_BC_FAIL(v);
+    ps += S_BC_PRES(v);
   }
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) fs += __shfl_xor(fs, o, 64);
@@ -581,12 +573,8 @@ __device__ __forceinline__ void gm_row_totals(const SState &s, int r, int lane, 
   if (pre) {
     uint32_t a = x - ps;
     for (int b = b0; b < b1; b++) {
-      const uint8_t *pc = s.ccnt + ((size_t)b * s.n + r) * CPB;
-      uint64_t v;
-      if (CPB == 1) v = *pc;
-      else if (CPB == 2) v = *(const uint16_t *)pc;
-      else if (CPB == 4) v = *(const uint32_t *)pc;
-      else v = *(const uint64_t *)pc;
+      const uint2 pc = *(const uint2 *)&s.brec[(size_t)b * s.n + r];
+      const uint64_t v = (uint64_t)pc.x | ((uint64_t)pc.y << 32);
 #pragma unroll
       for (int c = 0; c < CPB; c++) {
         pre[b * CPB + c] = a;
@@ -800,10 +788,14 @@ __global__ __launch_bounds__(256) void gm_s_pick(SState s, int t) {
 // status[r][d] = -2 for an output Lemire rejects (same on every rank),
 // (global column << 1) | fresh on the owning rank, -1 elsewhere (MAX-allreduced).
 template <int B>
-__global__ __launch_bounds__(256) void gm_s_draw(SState s, int t, int round, int D) {
+__global__ __launch_bounds__(256) void gm_s_draw(SState s, int t, int round, int D, int listed) {
   extern __shared__ __align__(16) uint32_t p_smem[];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int r = blockIdx.x * 4 + wave;
+  // listed: the rows still pending after round 0, in ascending order (gm_s_plist_sort);
+  // their statuses go to status1 by list position
+  const int i = blockIdx.x * 4 + wave;
+  if (listed && i >= (int)min(*s.plist_cnt, (uint32_t)s.plist_cap)) return;
+  const int r = listed ? s.plist[i] : i;
   if (r >= s.n) return;
   uint32_t *pre = p_smem + wave * gm_draw_lds_words(s.wp);
   uint32_t *mts = pre + (s.wp >> 6) + 1;
@@ -844,7 +836,7 @@ __global__ __launch_bounds__(256) void gm_s_draw(SState s, int t, int round, int
   bool have_pre = false;  // this shard's chunk prefix of the row, built on first use
   const uint32_t thr = (0u - size) % size;
   GmLazyMT mt;
-  int32_t *st = s.status + (size_t)r * D;
+  int32_t *st = listed ? s.status1 + (size_t)i * D : s.status + (size_t)r * D;
   for (int d0 = 0; d0 < D; d0 += 64) {
     const int cnt = min(64, D - d0);
     uint32_t raw = 0;
@@ -891,15 +883,20 @@ __global__ __launch_bounds__(256) void gm_s_draw(SState s, int t, int round, int
 // Phase C: with every draw resolved (MAX-allreduced status), run the acceptance loop
 // of MP1Node.cpp:466-489 (skip me, skip stale, skip duplicates) identically on every
 // rank; finished rows enqueue themselves into their targets' inboxes for tick t+1.
-__global__ __launch_bounds__(256) void gm_s_accept(SState s, int t, int D) {
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+// mode 0: every row, statuses by row; rows left pending are counted (npending, host loop).
+// mode 1: every row, and rows left pending are also appended to plist (bounded rounds).
+// mode 2: the plist rows, statuses by list position; a row still pending sets GM_ERR_DRAWS.
+__global__ __launch_bounds__(256) void gm_s_accept(SState s, int t, int D, int mode) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (mode == 2 && i >= (int)min(*s.plist_cnt, (uint32_t)s.plist_cap)) return;
+  const int r = mode == 2 ? s.plist[i] : i;
   if (r >= s.n || !s.pending[r]) return;
   int32_t *acc = s.acc + (size_t)r * 8;
   int n = acc[0];
   const int numpot = acc[6];
   int g[GM_FANOUT];
   for (int q = 0; q < n; q++) g[q] = acc[1 + q];
-  const int32_t *st = s.status + (size_t)r * D;
+  const int32_t *st = mode == 2 ? s.status1 + (size_t)i * D : s.status + (size_t)r * D;
   bool done = false;
   for (int d = 0; d < D && !done; d++) {
     const int32_t v = st[d];
@@ -920,7 +917,15 @@ __global__ __launch_bounds__(256) void gm_s_accept(SState s, int t, int D) {
   for (int q = 0; q < n; q++) acc[1 + q] = g[q];
   acc[0] = n;
   if (!done) {
-    atomicAdd(s.npending, 1);
+    if (mode == 0) {
+      atomicAdd(s.npending, 1);
+    } else if (mode == 1) {
+      const uint32_t slot = atomicAdd(s.plist_cnt, 1u);
+      if (slot < (uint32_t)s.plist_cap) s.plist[slot] = r;
+      else atomicOr(s.err, GM_ERR_DRAWS);  // more rows than the bounded round takes
+    } else {
+      atomicOr(s.err, GM_ERR_DRAWS);  // 16 + 64 draws did not fill the row's targets
+    }
     return;
   }
   s.pending[r] = 0;
@@ -1001,21 +1006,55 @@ hipError_t gm_launch_tick(const SState &s, int t, int drop_pct, bool nt, hipStre
   }
 }
 
-hipError_t gm_launch_draw(const SState &s, int t, int round, int D, hipStream_t st) {
+hipError_t gm_launch_draw(const SState &s, int t, int round, int D, int listed, hipStream_t st) {
   const size_t smem = sizeof(uint32_t) * 4 * gm_draw_lds_words(s.wp);
-  const dim3 grid((s.n + 3) / 4), blk(256);
+  const dim3 grid(((listed ? s.plist_cap : s.n) + 3) / 4), blk(256);
   switch (s.band) {
-    case 64: hipLaunchKernelGGL(gm_s_draw<64>, grid, blk, smem, st, s, t, round, D); break;
-    case 128: hipLaunchKernelGGL(gm_s_draw<128>, grid, blk, smem, st, s, t, round, D); break;
-    case 256: hipLaunchKernelGGL(gm_s_draw<256>, grid, blk, smem, st, s, t, round, D); break;
-    case 512: hipLaunchKernelGGL(gm_s_draw<512>, grid, blk, smem, st, s, t, round, D); break;
+    case 64: hipLaunchKernelGGL(gm_s_draw<64>, grid, blk, smem, st, s, t, round, D, listed); break;
+    case 128: hipLaunchKernelGGL(gm_s_draw<128>, grid, blk, smem, st, s, t, round, D, listed); break;
+    case 256: hipLaunchKernelGGL(gm_s_draw<256>, grid, blk, smem, st, s, t, round, D, listed); break;
+    case 512: hipLaunchKernelGGL(gm_s_draw<512>, grid, blk, smem, st, s, t, round, D, listed); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
 
-hipError_t gm_launch_accept(const SState &s, int t, int D, hipStream_t st) {
-  hipLaunchKernelGGL(gm_s_accept, dim3((s.n + 255) / 256), dim3(256), 0, st, s, t, D);
+hipError_t gm_launch_accept(const SState &s, int t, int D, int mode, hipStream_t st) {
+  const int rows = mode == 2 ? s.plist_cap : s.n;
+  hipLaunchKernelGGL(gm_s_accept, dim3((rows + 255) / 256), dim3(256), 0, st, s, t, D, mode);
+  return hipGetLastError();
+}
+
+// The pending rows of round 0 in ascending order: the list order (= status1 rows) must be
+// the same on every rank, whatever order the atomics appended them in.
+__global__ __launch_bounds__(1024) void gm_s_plist_sort(SState s) {
+  __shared__ int32_t v[S_PLIST_CAP];
+  const int cnt = (int)min(*s.plist_cnt, (uint32_t)s.plist_cap);
+  if (cnt <= 1) return;
+  int m = 1;
+  while (m < cnt) m <<= 1;
+  for (int k = threadIdx.x; k < m; k += blockDim.x) v[k] = k < cnt ? s.plist[k] : 0x7FFFFFFF;
+  __syncthreads();
+  for (int size = 2; size <= m; size <<= 1)
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int k = threadIdx.x; k < m; k += blockDim.x) {
+        const int o = k ^ stride;
+        if (o > k) {
+          const bool up = (k & size) == 0;
+          const int a = v[k], b = v[o];
+          if ((a > b) == up) {
+            v[k] = b;
+            v[o] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  for (int k = threadIdx.x; k < cnt; k += blockDim.x) s.plist[k] = v[k];
+}
+
+hipError_t gm_launch_plist_sort(const SState &s, hipStream_t st) {
+  hipLaunchKernelGGL(gm_s_plist_sort, dim3(1), dim3(1024), 0, st, s);
   return hipGetLastError();
 }
 

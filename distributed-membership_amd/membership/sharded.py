@@ -22,8 +22,9 @@ import os
 
 from .abi import GM_MODE_SCALED, Simulator, comm_unique_id, shard_loopback
 
-D_FIRST = 16  # must match GM_D_FIRST in gm_host.hip
-D_MORE = 64   # must match GM_D_MORE
+D_FIRST = 16        # must match GM_D_FIRST in gm_host.hip
+D_MORE = 64         # must match GM_D_MORE
+MAX_ROUNDS = 4096   # must match GM_MAX_ROUNDS: a row that never fills its targets
 
 
 def loopback_tick(sims):
@@ -41,6 +42,8 @@ def loopback_tick(sims):
             raise RuntimeError(f"shards disagree on pending rows: {pend}")
         if pend[0] == 0:
             break
+        if rnd + 1 > MAX_ROUNDS:
+            raise RuntimeError(f"{pend[0]} rows still drawing after {MAX_ROUNDS} rounds")
         rnd, d = rnd + 1, D_MORE
     for s in sims:
         s.shard_end_tick()

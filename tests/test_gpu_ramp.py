@@ -123,4 +123,7 @@ def test_ramp_with_drops_at_scale():
     assert st["err"] == 0 and st["live"] == n
     nodes = sim.read_nodes()
     assert (nodes[:, 0] == 1).all() and (nodes[:, 1] == 1).all()
-    assert sim.event_totals()["joined"] >= n * n - 1
+    assert sim.event_totals()["joined"] >= n * (n - 1)  # every other node joined (self may be appended, unlogged)
+    for r in (0, 1, n // 2, n - 1):  # spot rows: everyone present
+        hb, ts = sim.read_row(r)
+        assert (hb >= 0).all(), r

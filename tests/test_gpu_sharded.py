@@ -55,19 +55,26 @@ def test_shards_match_fused_kernel(n, world, drop, warm):
         assert st["lists"] == ref.tick_stats()["lists"]
 
 
-@pytest.mark.parametrize("n,drop", [(777, 0), (2048, 20)])
-def test_rccl_single_rank_matches_fused_kernel(n, drop, monkeypatch):
+@pytest.mark.parametrize("n,drop,ncrash,rounds", [(777, 0, 12, "auto"), (2048, 20, 32, "auto"), (777, 0, 12, "sync"),
+                                                  (777, 0, 388, "bounded")])
+def test_rccl_single_rank_matches_fused_kernel(n, drop, ncrash, rounds, monkeypatch):
     """The RCCL-driven sharded tick (gm_tick -> ncclAllGather / ncclAllReduce on the
     context stream) with one forced shard on the one GPU this box has: the exact
-    collective calls the multi-GPU run makes, degenerate only in the rank count."""
+    collective calls the multi-GPU run makes, degenerate only in the rank count.
+    "auto" takes the bounded, stream-ordered draw rounds here; "sync" the host-driven
+    loop; "bounded" with half the cluster crashed forces the bounded path with many rows
+    left pending after round 0, so round 1 (the sorted pending list) does real work."""
     from membership.abi import comm_unique_id
     kw = dict(rd_seed=7, drop_pct=drop, drop_from=3, drop_to=25, drop_seed=42, init_mode=1, init_t0=6, init_seed=5)
     ref = Simulator(n, GM_MODE_SCALED, **kw)
     monkeypatch.setenv("GM_FORCE_SHARD", "1")
+    if rounds != "auto":
+        monkeypatch.setenv("GM_SHARD_SYNC", "1" if rounds == "sync" else "0")
     sh = Simulator(n, GM_MODE_SCALED, shard_rank=0, shard_count=1, **kw)
     monkeypatch.delenv("GM_FORCE_SHARD")
+    monkeypatch.delenv("GM_SHARD_SYNC", raising=False)
     sh.comm_init(comm_unique_id(), 1, 0)
-    crash = crash_set(n, max(2, n // 64), 42)
+    crash = crash_set(n, ncrash, 42)
     for _ in range(32):
         t = ref.time
         ref.tick()
