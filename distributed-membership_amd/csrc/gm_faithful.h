@@ -31,6 +31,7 @@ struct FState {
   FMsg *buf;                   // EmulNet buffer [F_ENBUFFSIZE]
   int32_t *bufsize;
   int32_t *holepos;            // [F_ENBUFFSIZE] scratch
+  int32_t *keys;               // [F_ENBUFFSIZE] scratch: strcmp key of each buffered message's destination
   FMsg *q;                     // this tick's queues, concatenated [F_ENBUFFSIZE]
   int32_t *q_off, *q_cnt;      // [n]
   int32_t *scount;             // sends per node this tick

@@ -45,52 +45,52 @@ __device__ __forceinline__ uint32_t f_strkey(int32_t id) {
 __global__ __launch_bounds__(F_RECV_THREADS) void gm_f_recv(FState s, int t) {
   __shared__ int s_tmp[32];
   FMsg *buf = s.buf;
+  int32_t *key = s.keys;  // strcmp key of every element's destination, moved with the element
   int B = *s.bufsize;
+  for (int j = threadIdx.x; j < B; j += F_RECV_THREADS) key[j] = (int32_t)f_strkey(buf[j].to);
+  __syncthreads();
   int qbase = 0;
   for (int i = 0; i < s.n; i++) {
     if (threadIdx.x == 0) { s.q_off[i] = qbase; s.q_cnt[i] = 0; }
     if (!(t > s.start[i] && !s.failed[i])) continue;  // Application.cpp:130
-    const uint32_t me = f_strkey(i + 1);
+    const int32_t me = (int32_t)f_strkey(i + 1);
     const int L = (B + F_RECV_THREADS - 1) / F_RECV_THREADS;
     const int lo = min(B, (int)threadIdx.x * L), hi = min(B, lo + L);
     int c = 0;
-    for (int j = lo; j < hi; j++) c += f_strkey(buf[j].to) == me;
+    for (int j = lo; j < hi; j++) c += key[j] == me;
     int k;
     int before = gm_block_scan(c, s_tmp, &k);  // matches at index < lo
     if (k == 0) continue;
     const int Bn = B - k;
     // deliver in descending buffer index; tag the matches that sit in the
     // vacated tail [Bn, B) with their 1-based descending rank
-    int r = before;
-    for (int j = lo; j < hi; j++) {
-      if (f_strkey(buf[j].to) == me) {
-        s.q[qbase + (k - 1 - r)] = buf[j];
-        r++;
-      }
-    }
     for (int j = max(lo, Bn); j < hi; j++) s.holepos[j - Bn] = 0;
     __syncthreads();
-    r = before;
-    for (int j = lo; j < hi; j++) {
-      if (f_strkey(buf[j].to) == me) {
-        if (j >= Bn) s.holepos[j - Bn] = k - r;
-        r++;
+    if (c) {
+      int r = before;
+      for (int j = lo; j < hi; j++) {
+        if (key[j] == me) {
+          s.q[qbase + (k - 1 - r)] = buf[j];
+          if (j >= Bn) s.holepos[j - Bn] = k - r;
+          r++;
+        }
       }
     }
     __syncthreads();
     // swap-with-last, closed form: the i-th hole (descending) receives what sits
     // at position B-i when it is processed; if B-i is itself an earlier hole h_m,
     // that is what h_m received from B-m -- follow the chain to an original element
-    r = before;
-    for (int j = lo; j < hi; j++) {
-      if (f_strkey(buf[j].to) == me) {
-        if (j < Bn) {
+    if (c && lo < Bn) {
+      int r = before;
+      for (int j = lo; j < min(hi, Bn); j++) {
+        if (key[j] == me) {
           int x = B - (k - r);
           int guard = 0;
           while (s.holepos[x - Bn] > 0 && ++guard <= k) x = B - s.holepos[x - Bn];
           buf[j] = buf[x];  // x >= Bn: never overwritten in this pass
+          key[j] = key[x];
+          r++;
         }
-        r++;
       }
     }
     __syncthreads();
@@ -364,21 +364,34 @@ __global__ __launch_bounds__(F_SEND_THREADS) void gm_f_send(FState s, int t) {
     if (threadIdx.x == 0) atomicOr(s.err, GM_ERR_DRAWS);
     return;
   }
-  // S1: one glibc rand() draw per ENsend, in send order (EmulNet.cpp:90)
+  // S1: one glibc rand() draw per ENsend, in send order (EmulNet.cpp:90). glibc TYPE_3
+  // keeps rptr 3 words behind fptr (mod 31), both advancing by one per draw; with the
+  // ring rotated so that x[j] is the word fptr reaches at step j of each 31-step round,
+  // step j is x[j] += x[(j + 28) % 31] -- static register indices in a fully unrolled
+  // round, no dynamically indexed (scratch) state on the serial chain.
   if (threadIdx.x == 0) {
-    int32_t st[31];
-    for (int k = 0; k < 31; k++) st[k] = s.s1[k];
-    int f = s.s1[31], r = s.s1[32];
-    for (int o = 0; o < S; o++) {
-      uint32_t v = (uint32_t)st[f] + (uint32_t)st[r];
-      st[f] = (int32_t)v;
-      f = f == 30 ? 0 : f + 1;
-      r = r == 30 ? 0 : r + 1;
-      s.draws[o] = (int32_t)(v >> 1);
+    const int f0 = s.s1[31];
+    uint32_t x[31];
+    for (int j = 0; j < 31; j++) x[j] = (uint32_t)s.s1[(f0 + j) % 31];
+    int o = 0;
+    for (; o + 31 <= S; o += 31) {
+#pragma unroll
+      for (int j = 0; j < 31; j++) {
+        x[j] += x[(j + 28) % 31];
+        s.draws[o + j] = (int32_t)(x[j] >> 1);
+      }
     }
-    for (int k = 0; k < 31; k++) s.s1[k] = st[k];
+#pragma unroll
+    for (int j = 0; j < 31; j++) {
+      if (o + j < S) {
+        x[j] += x[(j + 28) % 31];
+        s.draws[o + j] = (int32_t)(x[j] >> 1);
+      }
+    }
+    for (int j = 0; j < 31; j++) s.s1[(f0 + j) % 31] = (int32_t)x[j];
+    const int f = (f0 + S) % 31;
     s.s1[31] = f;
-    s.s1[32] = r;
+    s.s1[32] = (f + 28) % 31;
   }
   __syncthreads();
   const int B0 = *s.bufsize;

@@ -25,8 +25,8 @@ __global__ void gm_f_send(FState s, int t);
 hipError_t gm_launch_tick(const SState &s, int t, int drop_pct, bool nt, hipStream_t st, hipEvent_t k0, hipEvent_t k1,
                           bool pick);
 hipError_t gm_launch_draw(const SState &s, int t, int round, int D, int listed, hipStream_t st);
-hipError_t gm_launch_accept(const SState &s, int t, int D, int mode, hipStream_t st);
-hipError_t gm_launch_plist_sort(const SState &s, hipStream_t st);
+hipError_t gm_launch_accept(const SState &s, int t, int D, int in_list, int out, hipStream_t st);
+hipError_t gm_launch_plist_sort(const SState &s, int l, hipStream_t st);
 hipError_t gm_launch_init(const SState &s, int warm, int t0, uint64_t seed, hipStream_t st);
 hipError_t gm_launch_partial_tick(const PState &s, int t, uint32_t *mtraw, hipStream_t st, hipEvent_t k0,
                                   hipEvent_t k1);
@@ -37,6 +37,10 @@ hipError_t gm_launch_partial_chunk(const PState &s, int t, const uint32_t *mtraw
 size_t gm_partial_lds_bytes();
 
 #define GM_T_LIMIT 32766  // packed 16-bit hb/ts stay exact: hb <= 2t+1 < 0xFFFF
+#define GM_D_FIRST S_MT_RAW  // S2 outputs per row in the first round (steady state needs ~5-6)
+#define GM_D_MORE 64          // S2 outputs per row in later rounds (transients with many stale entries)
+#define GM_MAX_ROUNDS 4096    // draw rounds per sharded tick (16 + 64 * 4096 S2 outputs per row)
+#define GM_D_LAST 256         // bounded rounds: S2 outputs of round 2 (outputs [80, 336))
 
 struct gm_ctx {
   gm_config cfg;
@@ -188,6 +192,7 @@ static int create_faithful(gm_ctx *c) {
   TRY(dalloc(c, &f.buf, F_ENBUFFSIZE));
   TRY(dalloc(c, &f.bufsize, 1));
   TRY(dalloc(c, &f.holepos, F_ENBUFFSIZE));
+  TRY(dalloc(c, &f.keys, F_ENBUFFSIZE));
   TRY(dalloc(c, &f.q, F_ENBUFFSIZE));
   TRY(dalloc(c, &f.q_off, n));
   TRY(dalloc(c, &f.q_cnt, n));
@@ -233,10 +238,16 @@ static int create_faithful(gm_ctx *c) {
 static int pick_band(const gm_ctx *c, int n, int wp) {
   int b = c->cfg.band;
   if (!b && getenv("GM_BAND")) b = atoi(getenv("GM_BAND"));
-  if (b) return (b == 64 || b == 128 || b == 256 || b == 512) && wp % b == 0 ? b : -1;
-  const double budget = 210e6;
-  for (int cand : {512, 256, 128})
-    if (wp % cand == 0 && 6.0 * n * cand <= budget) return cand;
+  if (b) return (b == 64 || b == 128 || b == 256 || b == 512 || b == 1024) && wp % b == 0 ? b : -1;
+  // Measured (profiles/r02/): the widest band wins -- one row per wave at B = 1024 (no
+  // max over two rows' list counts, half the per-(row, band) bookkeeping per cell), and a
+  // payload gather stays whole lines; B = 128 gathers half a line per row. gm_s_band at
+  // N = 65,536: 4.98 ms (B = 1024), 5.43 (512), 7.42 (128); the S-B shard (N = 262,144,
+  // G = 8): 11.0 / 12.0 / 15.0 ms. Per-band traffic up to ~1.4 GB still keeps the gathered
+  // payload slab (n x B/2 bytes) on-die.
+  const double budget = 1.4e9;
+  for (int cand : {1024, 512, 256, 128})
+    if (wp % cand == 0 && 5.0 * n * cand <= budget) return cand;
   return 64;
 }
 
@@ -322,10 +333,13 @@ static int create_scaled(gm_ctx *c) {
     TRY(dalloc(c, &s.status, (size_t)n * c->dmax));
     // bounded rounds (tick_sharded): round 0 takes every row's first 16 S2 outputs, round 1
     // the next 64 for up to plist_cap rows left pending -- no host round trip per tick
-    s.plist_cap = std::min(S_PLIST_CAP, std::max(256, n / 16));
-    TRY(dalloc(c, &s.plist, s.plist_cap));
-    TRY(dalloc(c, &s.plist_cnt, 1));
-    TRY(dalloc(c, &s.status1, (size_t)s.plist_cap * c->dmax));
+    s.plist_cap[1] = std::min(S_PLIST_CAP, std::max(256, n / 16));  // round 1: 64 more outputs
+    s.plist_cap[2] = 256;                                             // round 2: 256 more outputs
+    for (int l = 1; l <= 2; l++) {
+      TRY(dalloc(c, &s.plist[l], s.plist_cap[l]));
+      TRY(dalloc(c, &s.plist_cnt[l], 1));
+      TRY(dalloc(c, &s.statusl[l], (size_t)s.plist_cap[l] * (l == 1 ? GM_D_MORE : GM_D_LAST)));
+    }
     HIPCHECK(hipMemset(s.pending, 0, sizeof(int32_t) * n));
     HIPCHECK(hipMemset(s.xcnt, 0, sizeof(int32_t) * (size_t)G * n * 2));
   }
@@ -1087,9 +1101,6 @@ extern "C" int gm_crash_set(int32_t n, int32_t count, uint64_t seed, int32_t *ou
     }                                                                                \
   } while (0)
 
-#define GM_D_FIRST S_MT_RAW  // S2 outputs per row in the first round (steady state needs ~5-6)
-#define GM_D_MORE 64          // S2 outputs per row in later rounds (transients with many stale entries)
-#define GM_MAX_ROUNDS 4096    // draw rounds per sharded tick (16 + 64 * 4096 S2 outputs per row)
 
 extern "C" int gm_comm_unique_id(uint8_t *out128) {
   if (!out128) return GM_EINVAL;
@@ -1156,7 +1167,7 @@ extern "C" int gm_shard_accept(gm_ctx *c, int32_t D, int32_t *npending) {
   TRY(shard_ready(c));
   if (D <= 0 || D > c->dmax || !npending) return GM_EINVAL;
   HIPCHECK(hipMemsetAsync(c->s.npending, 0, sizeof(int32_t), c->stream));
-  HIPCHECK(gm_launch_accept(c->s, c->t, D, 0, c->stream));
+  HIPCHECK(gm_launch_accept(c->s, c->t, D, 0, 0, c->stream));
   HIPCHECK(hipMemcpyAsync(npending, c->s.npending, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
   HIPCHECK(hipStreamSynchronize(c->stream));
   return GM_OK;
@@ -1240,17 +1251,29 @@ static int tick_sharded(gm_ctx *c) {
     // S2 outputs; rows left pending go to a list (sorted: identical on every rank) that
     // round 1 serves with the next 64; a row still short after that sets GM_ERR_DRAWS
     SState &s = c->s;
-    HIPCHECK(hipMemsetAsync(s.plist_cnt, 0, sizeof(uint32_t), c->stream));
+    for (int l = 1; l <= 2; l++) HIPCHECK(hipMemsetAsync(s.plist_cnt[l], 0, sizeof(uint32_t), c->stream));
     HIPCHECK(gm_launch_draw(s, c->t, 0, GM_D_FIRST, 0, c->stream));
     if (!s.stub)
       NCCLCHECK(ncclAllReduce(s.status, s.status, n * GM_D_FIRST, ncclInt32, ncclMax, c->comm, c->stream));
-    HIPCHECK(gm_launch_accept(s, c->t, GM_D_FIRST, 1, c->stream));
-    HIPCHECK(gm_launch_plist_sort(s, c->stream));
-    HIPCHECK(gm_launch_draw(s, c->t, 1, GM_D_MORE, 1, c->stream));
-    if (!s.stub)
-      NCCLCHECK(ncclAllReduce(s.status1, s.status1, (size_t)s.plist_cap * GM_D_MORE, ncclInt32, ncclMax, c->comm,
-                              c->stream));
-    HIPCHECK(gm_launch_accept(s, c->t, GM_D_MORE, 2, c->stream));
+    HIPCHECK(gm_launch_accept(s, c->t, GM_D_FIRST, 0, 1, c->stream));
+    for (int l = 1; l <= 2; l++) {  // rounds 1, 2 over the sorted pending lists
+      const int D = l == 1 ? GM_D_MORE : GM_D_LAST;
+      HIPCHECK(gm_launch_plist_sort(s, l, c->stream));
+      HIPCHECK(gm_launch_draw(s, c->t, l, D, l, c->stream));
+      if (!s.stub)
+        NCCLCHECK(ncclAllReduce(s.statusl[l], s.statusl[l], (size_t)s.plist_cap[l] * D, ncclInt32, ncclMax, c->comm,
+                                c->stream));
+      HIPCHECK(gm_launch_accept(s, c->t, D, l, l == 1 ? 2 : -1, c->stream));
+    }
+    if (getenv("GM_DEBUG_ROUNDS")) {  // diagnostics: rows left after round 0, error flags
+      uint32_t pc1 = 0, pc2 = 0, e = 0;
+      HIPCHECK(hipMemcpyAsync(&pc1, s.plist_cnt[1], sizeof pc1, hipMemcpyDeviceToHost, c->stream));
+      HIPCHECK(hipMemcpyAsync(&pc2, s.plist_cnt[2], sizeof pc2, hipMemcpyDeviceToHost, c->stream));
+      HIPCHECK(hipMemcpyAsync(&e, s.err, sizeof e, hipMemcpyDeviceToHost, c->stream));
+      HIPCHECK(hipStreamSynchronize(c->stream));
+      fprintf(stderr, "[gm] t=%d rows pending after round 0: %u (cap %d), after round 1: %u (cap %d), err 0x%x\n", c->t,
+              pc1, s.plist_cap[1], pc2, s.plist_cap[2], e);
+    }
     c->t--;  // gm_tick advances globaltime
     TRY(gm_shard_end_tick(c));
     return GM_OK;
@@ -1262,6 +1285,7 @@ static int tick_sharded(gm_ctx *c) {
       NCCLCHECK(ncclAllReduce(c->s.status, c->s.status, n * D, ncclInt32, ncclMax, c->comm, c->stream));
     int32_t pend = 0;
     TRY(gm_shard_accept(c, D, &pend));
+    if (getenv("GM_DEBUG_ROUNDS")) fprintf(stderr, "[gm] t=%d round %d: %d rows still drawing\n", c->t, round, pend);
     if (pend == 0) break;
     if (++round > GM_MAX_ROUNDS) {  // a row that never finds its targets: same guard as gm_s_pick
       uint32_t e = GM_ERR_DRAWS;

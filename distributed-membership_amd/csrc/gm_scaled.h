@@ -4,7 +4,8 @@
 
 #define S_KMAX 64                // inbox capacity (gossip lists per receiver per tick)
 #define S_COLS_PER_LANE 16       // 32 B of table + 16 B per sender payload per lane and row
-#define S_ROW_ALIGN 512          // padded row width granule (a multiple of every band width)
+#define S_ROW_ALIGN 512          // padded row width granule (a multiple of every band width up to 512)
+#define S_CHUNK(B) ((B) >= 1024 ? 128 : 64)  // columns per rank-select chunk (<= 8 chunks per band)
 #define S_SB 8                   // sender ids prefetched per row; payload loads in flight per lane
 #define S_MT_RAW 16              // mt19937 outputs precomputed per row and tick (gm_s_mtgen)
 #define S_SELFADD_CAP 65536      // join ramp: self appends verified per tick (gm_s_selfcheck)
@@ -96,8 +97,11 @@ struct SState {
   int32_t *acc;              // [n][8]: targets so far, g[5], numpot, size
   int32_t *pending;          // [n] rows still drawing
   int32_t *npending;         // rows still drawing after the last accept round
-  int plist_cap;             // bounded rounds: capacity of the pending-row list (<= S_PLIST_CAP)
-  int32_t *plist;            // [plist_cap] rows pending after round 0 (ascending after gm_s_plist_sort)
-  uint32_t *plist_cnt;
-  int32_t *status1;          // bound exchange buffer [plist_cap][GM_D_MORE]: round-1 draws of the listed rows
+  // bounded rounds (tick_sharded): pending list l = 1, 2 holds the rows left after round l-1
+  // (ascending after gm_s_plist_sort: the same order on every rank); statusl[l] = the bound
+  // exchange buffer [plist_cap[l]][D_l] of round l's draws, by list position. Index 0 unused.
+  int plist_cap[3];
+  int32_t *plist[3];
+  uint32_t *plist_cnt[3];
+  int32_t *statusl[3];
 };

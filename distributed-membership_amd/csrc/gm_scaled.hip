@@ -98,6 +98,14 @@ typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ u16x2 pk(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
 __device__ __forceinline__ uint32_t unpk(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
 // payload bytes 0,1 / 2,3 of a dword, zero-extended into the two halves
+// a += b per u16 half, opaque to the compiler: plain vector adds of the sweep's
+// per-pair counts get re-associated into a tree that keeps every pair's term live
+// (9 VGPR spills at occupancy 8); an in-order chain consumes each term at once
+__device__ __forceinline__ u16x2 padd(u16x2 a, u16x2 b) {
+  uint32_t r;
+  asm("v_pk_add_u16 %0, %1, %2" : "=v"(r) : "v"(unpk(a)), "v"(unpk(b)));
+  return pk(r);
+}
 // min(x, 1) per u16 half as ONE v_pk_min_u16: written as plain vector min the compiler
 // lowers it to a compare + select per half (5 instructions instead of 1)
 __device__ __forceinline__ u16x2 pmin1(u16x2 a) {
@@ -217,7 +225,6 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
   int npres = 0, nfail = 0, nev = 0;
   uint32_t evk = 0;  // 2 bits per cell: event kind
   bool esc_out = false;  // this lane sends a value only the wide plane can carry
-  uint32_t pw[8];        // payload h' per cell pair (u16 halves), 0 = not sent
   if (live) {
     // merge key per cell = the largest delivered payload h' (0 = nothing delivered), as
     // key5 = h' << 5 (the cell with age 0) in the u16 halves of each table word
@@ -353,11 +360,10 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
       const u16x2 stale = (a + (u16x2)(32 - GM_TFAIL)) >> (u16x2)(5);   // age >= TFAIL
       const u16x2 gone = (a + (u16x2)(32 - GM_TREMOVE)) >> (u16x2)(5);  // age >= TREMOVE
       const u16x2 v2 = v * ((u16x2)(1) - gone);
-      nf2 += stale;
-      np2 += pmin1(v2);
+      nf2 = padd(nf2, stale);
+      np2 = padd(np2, pmin1(v2));
       // h - 2 for fresh cells; stale ones subtract >= 257 and saturate to 0 (not sent)
       const u16x2 p2 = __builtin_elementwise_sub_sat(v >> (u16x2)(5), stale * (u16x2)(255) + (u16x2)(2));
-      pw[i] = unpk(p2);
       // nibble: n = (h' - 224) / 2, valid iff re-encoding gives h' back (even h' in [226, 252]);
       // the re-encoding is forced to 0 for n = 0, so a sent value that maps to n = 0 escapes
       // too, while "not sent" (h' = 0) stays 0; escapes carry 15 (the max)
@@ -378,36 +384,49 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
     npres = (int)np2.x + (int)np2.y;
     if (__builtin_elementwise_min(lagmin.x, lagmin.y) < 64) atomicOr(s.err, GM_ERR_LAG);
     if (unpk(evany)) {  // rare: this lane's joins / removals, as 2-bit kinds per cell
+      // the cells as loaded, re-read (still in memory: the stores come below) rather than
+      // kept live through the sweep for this rare path (21 VGPRs: occupancy 5 -> 8)
+      const u32x4 ra = __builtin_amdgcn_raw_buffer_load_b128(trs, toff, 0, 0);
+      const u32x4 rb = __builtin_amdgcn_raw_buffer_load_b128(trs, toff + 16, 0, 0);
+      const uint32_t tb0[8] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
 #pragma unroll
-      for (int q = 0; q < Q; q++) {
-        const uint32_t before = (tw[q >> 1] >> (16 * (q & 1))) & 0xFFFFu;
-        const uint32_t merged = (unpk(mm[q >> 1]) >> (16 * (q & 1))) & 0xFFFFu;
+      for (int q = 0; q < Q; q++) {  // from the loaded and the swept cells only (the merge never deletes:
+        // present before and absent after = removed; a cell inserted this tick has age 0)
+        const uint32_t before = (tb0[q >> 1] >> (16 * (q & 1))) & 0xFFFFu;
         const uint32_t after = (cw[q >> 1] >> (16 * (q & 1))) & 0xFFFFu;
-        const uint32_t ev = merged && q != selfapp ? (!before ? S_EV_ADD : !after ? S_EV_REMOVE : 0u) : 0u;
+        const uint32_t ev = !before ? (after && q != selfapp ? S_EV_ADD : 0u) : (!after ? S_EV_REMOVE : 0u);
         evk |= ev << (2 * q);
       }
       nev = __builtin_popcount((evk | (evk >> 1)) & 0x55555555u);
+    }
+    if (esc_out) {  // rare: the lane's 16 payload bytes h' into the escape plane (read where the nibble is 15)
+      uint32_t pw[8];
+#pragma unroll
+      for (int i = 0; i < 8; i++) {  // removed cells send nothing: the swept cells suffice
+        const u16x2 v = pk(cw[i]);
+        const u16x2 stale = ((v & (u16x2)(31)) + (u16x2)(32 - GM_TFAIL)) >> (u16x2)(5);
+        pw[i] = unpk(__builtin_elementwise_sub_sat(v >> (u16x2)(5), stale * (u16x2)(255) + (u16x2)(2)));
+      }
+      const u32x4 wv = {__builtin_amdgcn_perm(pw[1], pw[0], 0x06040200u), __builtin_amdgcn_perm(pw[3], pw[2], 0x06040200u),
+                        __builtin_amdgcn_perm(pw[5], pw[4], 0x06040200u), __builtin_amdgcn_perm(pw[7], pw[6], 0x06040200u)};
+      *(u32x4 *)(s.wide + slab * 2 * B + (size_t)r * 2 * B + (size_t)par * B + li * Q) = wv;
     }
     const u32x4 na = {cw[0], cw[1], cw[2], cw[3]}, nb4 = {cw[4], cw[5], cw[6], cw[7]};
     __builtin_amdgcn_raw_buffer_store_b128(na, trs, toff, 0, GM_AUX_NT);
     __builtin_amdgcn_raw_buffer_store_b128(nb4, trs, toff + 16, 0, GM_AUX_NT);
     const u32x2 ov = {nw[0], nw[1]};
     __builtin_amdgcn_raw_buffer_store_b64(ov, prs, (uint32_t)(r * B + par * (B / 2) + li * 8), 0, GM_AUX_NT);
-    if (esc_out) {  // rare: the lane's 16 payload bytes into the escape plane (read where the nibble is 15)
-      const u32x4 wv = {__builtin_amdgcn_perm(pw[1], pw[0], 0x06040200u), __builtin_amdgcn_perm(pw[3], pw[2], 0x06040200u),
-                        __builtin_amdgcn_perm(pw[5], pw[4], 0x06040200u), __builtin_amdgcn_perm(pw[7], pw[6], 0x06040200u)};
-      *(u32x4 *)(s.wide + slab * 2 * B + (size_t)r * 2 * B + (size_t)par * B + li * Q) = wv;
-    }
     if (band == 0 && li == 0) s.wtick[r] = t;
   }
   // present cells per 64-column chunk (4 lanes) for the draw's rank-select, gathered
   // into the row's first lane: bytes 0..B/64-1 of the (band, row) record
+  constexpr int CH = S_CHUNK(B), LPC = CH / Q;  // columns / lanes per rank-select chunk
   int cc = npres;
-  cc += __shfl_xor(cc, 1, 64);
-  cc += __shfl_xor(cc, 2, 64);
+#pragma unroll
+  for (int o = 1; o < LPC; o <<= 1) cc += __shfl_xor(cc, o, 64);
   uint64_t piece = 0;
 #pragma unroll
-  for (int c = 0; c < B / 64; c++) piece |= (uint64_t)(__shfl(cc, sub * LPR + 4 * c, 64) & 0xFF) << (8 * c);
+  for (int c = 0; c < B / CH; c++) piece |= (uint64_t)(__shfl(cc, sub * LPR + LPC * c, 64) & 0xFF) << (8 * c);
   // per-row reductions over the row's LPR lanes (aligned lane segments): counts packed
   // as present | numfailed << 16 (each <= B)
   int pf = npres | (nfail << 16);
@@ -544,14 +563,14 @@ __global__ __launch_bounds__(256) void gm_s_selfcheck(SState s) {
 // ------------------------------------------------------- wave-per-row helpers
 // LDS per wave of the draw kernels: chunk prefix [wp/64 + 1] u32, the fallback
 // generator's state [624] u32.
-__host__ __device__ __forceinline__ size_t gm_draw_lds_words(int wp) { return (size_t)(wp >> 6) + 1 + 624; }
+__host__ __device__ __forceinline__ size_t gm_draw_lds_words(int wp) { return (size_t)(wp >> 6) + 1 + 624; }  // >= chunks + 1
 
 // Row r of this shard: numfailed (band counts), size and the chunk prefix
 // pre[c] = present cells in chunks [0, c) (pre[nc] = size), from the chunk counts.
 template <int B>
 __device__ __forceinline__ void gm_row_totals(const SState &s, int r, int lane, uint32_t *pre, uint32_t &size,
                                               uint32_t &nfail) {
-  constexpr int CPB = B / 64;  // chunks per band
+  constexpr int CPB = B / S_CHUNK(B);  // rank-select chunks per band
   const int nb = s.nb, perb = (nb + 63) >> 6;
   const int b0 = min(nb, lane * perb), b1 = min(nb, b0 + perb);
   uint32_t fs = 0, ps = 0;
@@ -595,28 +614,33 @@ __device__ __forceinline__ void gm_row_totals(const SState &s, int r, int lane, 
 template <int B>
 __device__ __forceinline__ void gm_resolve8(const SState &s, int r, const uint32_t *pre, bool act, uint32_t ix, int lane,
                                             int col[8], int fresh[8]) {
+  constexpr int CH = S_CHUNK(B), CPL = CH / 8;  // chunk columns, cells per lane of the 8-lane group
   const int gl = lane & 7;
   int cnt = 0, base = 0;
-  uint32_t en[8];
+  uint32_t en[CPL];
 #pragma unroll
-  for (int v = 0; v < 8; v++) en[v] = 0;
+  for (int v = 0; v < CPL; v++) en[v] = 0;
   uint32_t q = 0;
   if (act) {
-    int lo = 0, hi = (s.wp >> 6) - 1;  // largest chunk with pre[c] <= ix (a non-empty one)
+    int lo = 0, hi = s.wp / CH - 1;  // largest chunk with pre[c] <= ix (a non-empty one)
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
       if (pre[mid] <= ix) lo = mid;
       else hi = mid - 1;
     }
     q = ix - pre[lo];
-    const int col0 = lo * 64 + gl * 8;  // this lane's 8 cells
+    const int col0 = lo * CH + gl * CPL;  // this lane's cells
     base = col0;
-    const uint4 t4 = *(const uint4 *)(s.table + ((size_t)(col0 / B) * s.n + r) * B + (col0 % B));
-    const uint32_t w[4] = {t4.x, t4.y, t4.z, t4.w};
+    const uint16_t *cp = s.table + ((size_t)(col0 / B) * s.n + r) * B + (col0 % B);
 #pragma unroll
-    for (int v = 0; v < 8; v++) en[v] = (w[v >> 1] >> (16 * (v & 1))) & 0xFFFFu;
+    for (int h = 0; h < CPL / 8; h++) {
+      const uint4 t4 = *(const uint4 *)(cp + 8 * h);
+      const uint32_t w[4] = {t4.x, t4.y, t4.z, t4.w};
 #pragma unroll
-    for (int v = 0; v < 8; v++) cnt += en[v] != 0;
+      for (int v = 0; v < 8; v++) en[8 * h + v] = (w[v >> 1] >> (16 * (v & 1))) & 0xFFFFu;
+    }
+#pragma unroll
+    for (int v = 0; v < CPL; v++) cnt += en[v] != 0;
   }
   int x = cnt;
 #pragma unroll
@@ -631,7 +655,7 @@ __device__ __forceinline__ void gm_resolve8(const SState &s, int r, const uint32
     holder = true;
     int need = (int)q - excl;
 #pragma unroll
-    for (int v = 0; v < 8; v++) {
+    for (int v = 0; v < CPL; v++) {
       if (en[v] != 0) {
         if (need == 0) {
           mycol = base + v;
@@ -794,8 +818,8 @@ __global__ __launch_bounds__(256) void gm_s_draw(SState s, int t, int round, int
   // listed: the rows still pending after round 0, in ascending order (gm_s_plist_sort);
   // their statuses go to status1 by list position
   const int i = blockIdx.x * 4 + wave;
-  if (listed && i >= (int)min(*s.plist_cnt, (uint32_t)s.plist_cap)) return;
-  const int r = listed ? s.plist[i] : i;
+  if (listed && i >= (int)min(*s.plist_cnt[listed], (uint32_t)s.plist_cap[listed])) return;
+  const int r = listed ? s.plist[listed][i] : i;
   if (r >= s.n) return;
   uint32_t *pre = p_smem + wave * gm_draw_lds_words(s.wp);
   uint32_t *mts = pre + (s.wp >> 6) + 1;
@@ -836,13 +860,13 @@ __global__ __launch_bounds__(256) void gm_s_draw(SState s, int t, int round, int
   bool have_pre = false;  // this shard's chunk prefix of the row, built on first use
   const uint32_t thr = (0u - size) % size;
   GmLazyMT mt;
-  int32_t *st = listed ? s.status1 + (size_t)i * D : s.status + (size_t)r * D;
+  int32_t *st = listed ? s.statusl[listed] + (size_t)i * D : s.status + (size_t)r * D;
   for (int d0 = 0; d0 < D; d0 += 64) {
     const int cnt = min(64, D - d0);
     uint32_t raw = 0;
     if (round == 0) {
       if (lane < cnt) raw = s.mtraw[(size_t)r * S_MT_RAW + d0 + lane];
-    } else {
+    } else {  // round q >= 1 continues after 16 + 64 (q - 1) outputs (round 2 of the bounded tick: after 80)
       raw = gm_mt_batch(mt, mts, gm_rd_seed(s.rd_seed, t, r + 1), d0 == 0, S_MT_RAW + 64 * (round - 1) + d0, cnt,
                         lane);
     }
@@ -886,17 +910,20 @@ __global__ __launch_bounds__(256) void gm_s_draw(SState s, int t, int round, int
 // mode 0: every row, statuses by row; rows left pending are counted (npending, host loop).
 // mode 1: every row, and rows left pending are also appended to plist (bounded rounds).
 // mode 2: the plist rows, statuses by list position; a row still pending sets GM_ERR_DRAWS.
-__global__ __launch_bounds__(256) void gm_s_accept(SState s, int t, int D, int mode) {
+// in_list 0: every row, statuses by row; 1 / 2: the rows of pending list 1 / 2, statuses by
+// list position. Rows left pending go to: out -1 -> GM_ERR_DRAWS (bounded rounds exhausted),
+// 0 -> the npending count (host-driven loop), 1 / 2 -> pending list 1 / 2 (next bounded round).
+__global__ __launch_bounds__(256) void gm_s_accept(SState s, int t, int D, int in_list, int out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (mode == 2 && i >= (int)min(*s.plist_cnt, (uint32_t)s.plist_cap)) return;
-  const int r = mode == 2 ? s.plist[i] : i;
+  if (in_list && i >= (int)min(*s.plist_cnt[in_list], (uint32_t)s.plist_cap[in_list])) return;
+  const int r = in_list ? s.plist[in_list][i] : i;
   if (r >= s.n || !s.pending[r]) return;
   int32_t *acc = s.acc + (size_t)r * 8;
   int n = acc[0];
   const int numpot = acc[6];
   int g[GM_FANOUT];
   for (int q = 0; q < n; q++) g[q] = acc[1 + q];
-  const int32_t *st = mode == 2 ? s.status1 + (size_t)i * D : s.status + (size_t)r * D;
+  const int32_t *st = in_list ? s.statusl[in_list] + (size_t)i * D : s.status + (size_t)r * D;
   bool done = false;
   for (int d = 0; d < D && !done; d++) {
     const int32_t v = st[d];
@@ -917,14 +944,14 @@ __global__ __launch_bounds__(256) void gm_s_accept(SState s, int t, int D, int m
   for (int q = 0; q < n; q++) acc[1 + q] = g[q];
   acc[0] = n;
   if (!done) {
-    if (mode == 0) {
+    if (out == 0) {
       atomicAdd(s.npending, 1);
-    } else if (mode == 1) {
-      const uint32_t slot = atomicAdd(s.plist_cnt, 1u);
-      if (slot < (uint32_t)s.plist_cap) s.plist[slot] = r;
+    } else if (out > 0) {
+      const uint32_t slot = atomicAdd(s.plist_cnt[out], 1u);
+      if (slot < (uint32_t)s.plist_cap[out]) s.plist[out][slot] = r;
       else atomicOr(s.err, GM_ERR_DRAWS);  // more rows than the bounded round takes
     } else {
-      atomicOr(s.err, GM_ERR_DRAWS);  // 16 + 64 draws did not fill the row's targets
+      atomicOr(s.err, GM_ERR_DRAWS);  // the bounded rounds' draws did not fill the row's targets
     }
     return;
   }
@@ -1002,38 +1029,41 @@ hipError_t gm_launch_tick(const SState &s, int t, int drop_pct, bool nt, hipStre
     case 128: return launch_tick_b<128>(s, t, drop_pct, nt, st, k0, k1, pick);
     case 256: return launch_tick_b<256>(s, t, drop_pct, nt, st, k0, k1, pick);
     case 512: return launch_tick_b<512>(s, t, drop_pct, nt, st, k0, k1, pick);
+    case 1024: return launch_tick_b<1024>(s, t, drop_pct, nt, st, k0, k1, pick);
     default: return hipErrorInvalidValue;
   }
 }
 
 hipError_t gm_launch_draw(const SState &s, int t, int round, int D, int listed, hipStream_t st) {
   const size_t smem = sizeof(uint32_t) * 4 * gm_draw_lds_words(s.wp);
-  const dim3 grid(((listed ? s.plist_cap : s.n) + 3) / 4), blk(256);
+  const dim3 grid(((listed ? s.plist_cap[listed] : s.n) + 3) / 4), blk(256);
   switch (s.band) {
     case 64: hipLaunchKernelGGL(gm_s_draw<64>, grid, blk, smem, st, s, t, round, D, listed); break;
     case 128: hipLaunchKernelGGL(gm_s_draw<128>, grid, blk, smem, st, s, t, round, D, listed); break;
     case 256: hipLaunchKernelGGL(gm_s_draw<256>, grid, blk, smem, st, s, t, round, D, listed); break;
     case 512: hipLaunchKernelGGL(gm_s_draw<512>, grid, blk, smem, st, s, t, round, D, listed); break;
+    case 1024: hipLaunchKernelGGL(gm_s_draw<1024>, grid, blk, smem, st, s, t, round, D, listed); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
 
-hipError_t gm_launch_accept(const SState &s, int t, int D, int mode, hipStream_t st) {
-  const int rows = mode == 2 ? s.plist_cap : s.n;
-  hipLaunchKernelGGL(gm_s_accept, dim3((rows + 255) / 256), dim3(256), 0, st, s, t, D, mode);
+hipError_t gm_launch_accept(const SState &s, int t, int D, int in_list, int out, hipStream_t st) {
+  const int rows = in_list ? s.plist_cap[in_list] : s.n;
+  hipLaunchKernelGGL(gm_s_accept, dim3((rows + 255) / 256), dim3(256), 0, st, s, t, D, in_list, out);
   return hipGetLastError();
 }
 
 // The pending rows of round 0 in ascending order: the list order (= status1 rows) must be
 // the same on every rank, whatever order the atomics appended them in.
-__global__ __launch_bounds__(1024) void gm_s_plist_sort(SState s) {
+__global__ __launch_bounds__(1024) void gm_s_plist_sort(SState s, int l) {
   __shared__ int32_t v[S_PLIST_CAP];
-  const int cnt = (int)min(*s.plist_cnt, (uint32_t)s.plist_cap);
+  int32_t *list = s.plist[l];
+  const int cnt = (int)min(*s.plist_cnt[l], (uint32_t)s.plist_cap[l]);
   if (cnt <= 1) return;
   int m = 1;
   while (m < cnt) m <<= 1;
-  for (int k = threadIdx.x; k < m; k += blockDim.x) v[k] = k < cnt ? s.plist[k] : 0x7FFFFFFF;
+  for (int k = threadIdx.x; k < m; k += blockDim.x) v[k] = k < cnt ? list[k] : 0x7FFFFFFF;
   __syncthreads();
   for (int size = 2; size <= m; size <<= 1)
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
@@ -1050,11 +1080,11 @@ __global__ __launch_bounds__(1024) void gm_s_plist_sort(SState s) {
       }
       __syncthreads();
     }
-  for (int k = threadIdx.x; k < cnt; k += blockDim.x) s.plist[k] = v[k];
+  for (int k = threadIdx.x; k < cnt; k += blockDim.x) list[k] = v[k];
 }
 
-hipError_t gm_launch_plist_sort(const SState &s, hipStream_t st) {
-  hipLaunchKernelGGL(gm_s_plist_sort, dim3(1), dim3(1024), 0, st, s);
+hipError_t gm_launch_plist_sort(const SState &s, int l, hipStream_t st) {
+  hipLaunchKernelGGL(gm_s_plist_sort, dim3(1), dim3(1024), 0, st, s, l);
   return hipGetLastError();
 }
 

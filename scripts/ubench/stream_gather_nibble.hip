@@ -96,5 +96,6 @@ int main() {
   RUN(512, 5, 0); RUN(256, 5, 0); RUN(128, 5, 0);
   RUN(512, 5, 1); RUN(256, 5, 1); RUN(128, 5, 1);
   RUN(512, 8, 1);
+  RUN(1024, 0, 0); RUN(1024, 5, 0); RUN(1024, 5, 1);
   return 0;
 }

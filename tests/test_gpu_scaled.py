@@ -47,7 +47,7 @@ def test_scaled_matches_oracle(n):
     run_pair(n, 40, crash_tick=8, crash_count=max(1, n // 50))
 
 
-@pytest.mark.parametrize("band", [64, 128, 256, 512])
+@pytest.mark.parametrize("band", [64, 128, 256, 512, 1024])
 def test_scaled_every_band_width_matches_oracle(band):
     # the band width changes only the tiling of gm_s_band / the rank-select of gm_s_pick
     run_pair(700, 36, crash_tick=9, crash_count=9, drop_pct=15, drop_from=4, drop_to=22, init_mode=1, init_t0=7,
