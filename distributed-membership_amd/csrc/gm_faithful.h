@@ -5,6 +5,7 @@
 #define F_ENBUFFSIZE 30000  // EmulNet.h:12
 #define F_MAX_NODES 1000    // EmulNet.h:10 (ENsend asserts src <= MAX_NODES)
 #define F_MAX_TIME 3600     // EmulNet.h:11
+#define F_RECV_LDS (160 * 1024)  // gm_f_recv dynamic LDS (the whole CU's)
 
 enum { F_JOINREQ = 0, F_JOINREP = 1, F_LIST = 2 };  // MP1Node.h:30-35
 
@@ -30,8 +31,12 @@ struct FState {
   int32_t *failed, *inited, *ingroup, *hbctr, *started_now;  // [n]
   FMsg *buf;                   // EmulNet buffer [F_ENBUFFSIZE]
   int32_t *bufsize;
-  int32_t *holepos;            // [F_ENBUFFSIZE] scratch
-  int32_t *keys;               // [F_ENBUFFSIZE] scratch: strcmp key of each buffered message's destination
+  uint16_t *holepos;           // [2][F_ENBUFFSIZE] hole ranks + hit positions when they exceed gm_f_recv's LDS
+  uint16_t *qidx;              // [F_ENBUFFSIZE] queue slot -> tick-start buffer index
+  FMsg *buf2;                  // [F_ENBUFFSIZE] the other buffer: gm_f_recvout compacts the survivors into it
+  uint16_t *bkey, *bkey2;      // [F_ENBUFFSIZE] destination key (strcmp prefix) of every buffered message
+  uint16_t *sidx;              // [F_ENBUFFSIZE] survivors' tick-start indices (gm_f_recv -> gm_f_recvout)
+  int32_t *rmeta;              // [2] messages delivered this tick, survivors
   FMsg *q;                     // this tick's queues, concatenated [F_ENBUFFSIZE]
   int32_t *q_off, *q_cnt;      // [n]
   int32_t *scount;             // sends per node this tick
@@ -41,6 +46,11 @@ struct FState {
   int32_t *fcols;              // [n][n] fresh columns ascending
   int32_t *s1;                 // glibc TYPE_3 state: 31 words + fptr + rptr
   int32_t *draws;              // [draw_cap]
+  int32_t *sbase;              // [n] first send ordinal of node i (node-descending order)
+  int32_t *smeta;              // [3] this tick's draw count S (-1: over draw_cap), S1 fptr at tick start, B0
+  int32_t *spre;               // [draw_cap + 1] exclusive prefix count of kept sends
+  uint32_t *s1mat;             // [64][31][32] P_q = R^(q+1), R = one 31-draw round of the S1 register
+  uint32_t *s1vb;              // [draw_cap / 1984 + 2][32] S1 register at every 64th round
   int32_t *sent, *recv;        // [(F_MAX_NODES+1)][tmax]
   FEvent *ev;
   unsigned long long *ev_count;

@@ -21,6 +21,7 @@
 //               sends are ordered node-descending (the node-phase order), each
 //               consumes the next glibc rand() draw of the S1 stream; the
 //               30000 cap is a prefix count over the not-drop-drawn sends.
+#include <type_traits>
 #include "gm_device.h"
 #include "gm_abi.h"
 #include "gm_faithful.h"
@@ -42,66 +43,192 @@ __device__ __forceinline__ uint32_t f_strkey(int32_t id) {
 }
 
 // ---------------------------------------------------------------- recv phase
+// gm_f_recv (one workgroup) walks the receivers ascending on an LDS image of the buffer:
+// one u32 per buffered message, its destination key << 16 | its index in the tick-start
+// buffer (F_ENBUFFSIZE < 2^16; the key -- the strcmp prefix of the destination address,
+// EmulNet.cpp:154 -- of ids 1..n is <= n; it is kept beside the buffer in bkey), message
+// counts per (key, segment of `seg` slots, seg sized from n so the table stays ~24 KB),
+// the receivers' active flags and two k-entry scratch arrays. Per receiver with k messages:
+//   ranks  a DPP scan over the key's segment counts gives every segment's first rank;
+//   scan   waves take the segments holding a match (and those of the vacated tail
+//          [B-k, B)) round-robin; a match stores its position at hit[rank], every tail
+//          slot gets its hole rank (1-based descending, 0 = no match);
+//   fill   one thread per rank: queue slot k-1-rank (descending buffer index = the
+//          reference's dequeue order) gets the message's tick-start index, and a match
+//          below B-k is overwritten in closed form: the hole of descending rank i
+//          receives what sits at B-i when it is processed, i.e. follow the chain
+//          through earlier tail holes to an original element;
+// with one LDS-only barrier after each. gm_f_recvout (many workgroups) then materialises
+// the queues and compacts the survivors into the other buffer. Ranks over the LDS room
+// use the same code on global scratch with full barriers.
+#define F_EL_SLOTS ((F_ENBUFFSIZE + 255) / 256 * 256)  // el[] incl. the b128 overread pad
+#define F_CW_BYTES 24576                               // count table budget
+static_assert(4 * F_EL_SLOTS + F_CW_BYTES + 4 * (F_MAX_NODES + 1) + F_MAX_NODES + 4 * 1024 <= F_RECV_LDS,
+              "gm_f_recv LDS budget");
+
+__device__ __forceinline__ void lds_barrier() {
+  // every wave's LDS traffic done, then the barrier; global stores stay in flight
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+__device__ __forceinline__ int mbcnt(uint64_t m) {  // set bits of m in the lanes below
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+}
+
+__device__ __forceinline__ int wave_incl_scan(int v) {  // DPP: rows by row_shr, then row_bcast
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);
+  return v;
+}
+
 __global__ __launch_bounds__(F_RECV_THREADS) void gm_f_recv(FState s, int t) {
-  __shared__ int s_tmp[32];
-  FMsg *buf = s.buf;
-  int32_t *key = s.keys;  // strcmp key of every element's destination, moved with the element
+  extern __shared__ uint32_t s_lds[];
+  const int n = s.n;
+  // segment size: a multiple of 256 slots, (n + 1) x nseg u16 counts within F_CW_BYTES, nseg <= 128
+  const int seg = max(256, (F_EL_SLOTS / min(128, F_CW_BYTES / 2 / (n + 1)) + 255) & ~255);
+  const int nsw = ((F_EL_SLOTS + seg - 1) / seg + 1) >> 1;  // count words per key (2 segments each)
+  uint32_t *el = s_lds;                                 // [F_EL_SLOTS]
+  uint32_t *cw = s_lds + F_EL_SLOTS;                    // [n + 1][nsw]
+  uint8_t *act = (uint8_t *)(cw + (n + 1) * nsw);       // [n], padded to 4
+  uint16_t *scr = (uint16_t *)(act + ((n + 3) & ~3));   // [2][cap]: hole ranks, hit positions
+  const int cap = (int)((F_RECV_LDS - ((uint8_t *)scr - (uint8_t *)s_lds)) / 4);
   int B = *s.bufsize;
-  for (int j = threadIdx.x; j < B; j += F_RECV_THREADS) key[j] = (int32_t)f_strkey(buf[j].to);
+#ifdef GM_F_PROFILE
+  const uint64_t c0 = wall_clock64();
+  const int B00 = B;
+  uint64_t c1 = 0;
+#endif
+  if (threadIdx.x == 0) *s.ev_count = 0;  // the host copied the last tick's records (mailbox)
+  for (int j = threadIdx.x; j < (n + 1) * nsw; j += F_RECV_THREADS) cw[j] = 0;
+  for (int i = threadIdx.x; i < n; i += F_RECV_THREADS)
+    act[i] = t > s.start[i] && !s.failed[i];  // Application.cpp:130
   __syncthreads();
+  for (int j0 = threadIdx.x; j0 < B; j0 += 8 * F_RECV_THREADS) {
+    uint32_t kk[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int j = j0 + u * F_RECV_THREADS;
+      kk[u] = j < B ? s.bkey[j] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int j = j0 + u * F_RECV_THREADS;
+      if (j >= B) break;
+      el[j] = kk[u] << 16 | (uint32_t)j;
+      const int g = j / seg;
+      atomicAdd(&cw[kk[u] * nsw + (g >> 1)], 1u << (16 * (g & 1)));
+    }
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#ifdef GM_F_PROFILE
+  c1 = wall_clock64();
+#endif
   int qbase = 0;
-  for (int i = 0; i < s.n; i++) {
+  for (int i = 0; i < n; i++) {
     if (threadIdx.x == 0) { s.q_off[i] = qbase; s.q_cnt[i] = 0; }
-    if (!(t > s.start[i] && !s.failed[i])) continue;  // Application.cpp:130
-    const int32_t me = (int32_t)f_strkey(i + 1);
-    const int L = (B + F_RECV_THREADS - 1) / F_RECV_THREADS;
-    const int lo = min(B, (int)threadIdx.x * L), hi = min(B, lo + L);
-    int c = 0;
-    for (int j = lo; j < hi; j++) c += key[j] == me;
-    int k;
-    int before = gm_block_scan(c, s_tmp, &k);  // matches at index < lo
+    if (!act[i]) continue;
+    const uint32_t me = f_strkey(i + 1);
+    // all of this key's messages go to its first active receiver; lane l holds the
+    // counts of segments 2l, 2l+1 and the number of matches in the segments below 2l
+    const uint32_t wd = lane < nsw ? cw[me * nsw + lane] : 0u;
+    const int clo = (int)(wd & 0xFFFFu), chi = (int)(wd >> 16);
+    const int incl = wave_incl_scan(clo + chi);
+    const int k = __builtin_amdgcn_readlane(incl, 63);
     if (k == 0) continue;
+    const int excl = incl - clo - chi;
     const int Bn = B - k;
-    // deliver in descending buffer index; tag the matches that sit in the
-    // vacated tail [Bn, B) with their 1-based descending rank
-    for (int j = max(lo, Bn); j < hi; j++) s.holepos[j - Bn] = 0;
-    __syncthreads();
-    if (c) {
-      int r = before;
-      for (int j = lo; j < hi; j++) {
-        if (key[j] == me) {
-          s.q[qbase + (k - 1 - r)] = buf[j];
-          if (j >= Bn) s.holepos[j - Bn] = k - r;
-          r++;
+    auto walk = [&](auto big_tag) {
+      constexpr bool BIG = decltype(big_tag)::value;
+      uint16_t *hp = BIG ? s.holepos : scr;
+      uint16_t *hit = BIG ? s.holepos + F_ENBUFFSIZE : scr + cap;
+      for (int g = wid; g * seg < B; g += F_RECV_THREADS / 64) {
+        const int l = g >> 1;
+        const int cg = (g & 1) ? __builtin_amdgcn_readlane(chi, l) : __builtin_amdgcn_readlane(clo, l);
+        const int s0 = g * seg, s1 = min(B, s0 + seg);
+        if (cg == 0 && s1 <= Bn) continue;
+        int r = __builtin_amdgcn_readlane(excl, l) + ((g & 1) ? __builtin_amdgcn_readlane(clo, l) : 0);
+        for (int j0 = cg ? s0 : max(s0, Bn & ~255); j0 < s1; j0 += 256) {
+          const int jb = j0 + 4 * lane;
+          const uint4 e4 = *(const uint4 *)&el[jb];
+          const uint32_t e[4] = {e4.x, e4.y, e4.z, e4.w};
+          bool h[4];
+          uint64_t b[4];
+          int rk = r;
+#pragma unroll
+          for (int q = 0; q < 4; q++) {
+            h[q] = jb + q < s1 && (e[q] >> 16) == me;
+            b[q] = __ballot(h[q]);
+            rk += mbcnt(b[q]);
+          }
+#pragma unroll
+          for (int q = 0; q < 4; q++) {
+            const int j = jb + q;
+            if (h[q]) hit[rk] = (uint16_t)j;
+            if (j >= Bn && j < s1) hp[j - Bn] = h[q] ? (uint16_t)(k - rk) : (uint16_t)0;
+            rk += h[q];
+          }
+          r += __popcll(b[0]) + __popcll(b[1]) + __popcll(b[2]) + __popcll(b[3]);
         }
       }
-    }
-    __syncthreads();
-    // swap-with-last, closed form: the i-th hole (descending) receives what sits
-    // at position B-i when it is processed; if B-i is itself an earlier hole h_m,
-    // that is what h_m received from B-m -- follow the chain to an original element
-    if (c && lo < Bn) {
-      int r = before;
-      for (int j = lo; j < min(hi, Bn); j++) {
-        if (key[j] == me) {
-          int x = B - (k - r);
-          int guard = 0;
-          while (s.holepos[x - Bn] > 0 && ++guard <= k) x = B - s.holepos[x - Bn];
-          buf[j] = buf[x];  // x >= Bn: never overwritten in this pass
-          key[j] = key[x];
-          r++;
+      if constexpr (BIG) __syncthreads(); else lds_barrier();
+      for (int rk = threadIdx.x; rk < k; rk += F_RECV_THREADS) {
+        const int j = hit[rk];
+        s.qidx[qbase + (k - 1 - rk)] = (uint16_t)(el[j] & 0xFFFFu);
+        if (j >= Bn) continue;
+        int x = B - (k - rk);
+        for (int guard = 0; guard < k; guard++) {
+          const int hx = hp[x - Bn];
+          if (hx == 0) break;
+          x = B - hx;
+        }
+        const uint32_t mv = el[x];  // x >= Bn, not a match: never overwritten in this pass
+        el[j] = mv;
+        const int gx = x / seg, gj = j / seg;  // the moved message may change segment
+        if (gx != gj) {
+          const uint32_t kx = mv >> 16;
+          atomicSub(&cw[kx * nsw + (gx >> 1)], 1u << (16 * (gx & 1)));
+          atomicAdd(&cw[kx * nsw + (gj >> 1)], 1u << (16 * (gj & 1)));
         }
       }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      s.q_cnt[i] = k;
-      s.recv[(size_t)(i + 1) * s.tmax + t] += k;  // recv_msgs[dst][time] (EmulNet.cpp:172)
-    }
+      if (threadIdx.x < nsw) cw[me * nsw + threadIdx.x] = 0;
+      if (threadIdx.x == 0) s.q_cnt[i] = k;
+      if constexpr (BIG) __syncthreads(); else lds_barrier();
+    };
+    if (k > cap) walk(std::true_type{}); else walk(std::false_type{});
     qbase += k;
     B = Bn;
   }
-  if (threadIdx.x == 0) *s.bufsize = B;
+  for (int j = threadIdx.x; j < B; j += F_RECV_THREADS) s.sidx[j] = (uint16_t)(el[j] & 0xFFFFu);
+  if (threadIdx.x == 0) {
+    s.rmeta[0] = qbase;
+    s.rmeta[1] = B;
+  }
+#ifdef GM_F_PROFILE
+  if (threadIdx.x == 0 && t % 100 == 50)
+    printf("recv t=%d B0=%d q=%d prolog=%llu loop=%llu (x10ns)\n", t, B00, qbase, (unsigned long long)(c1 - c0),
+           (unsigned long long)(wall_clock64() - c1));
+#endif
+}
+
+// queues and survivors (grid-stride over both), recv_msgs counters
+__global__ __launch_bounds__(256) void gm_f_recvout(FState s, int t) {
+  const int Q = s.rmeta[0], B = s.rmeta[1];
+  const int stride = gridDim.x * blockDim.x;
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  for (int p = tid; p < Q; p += stride) s.q[p] = s.buf[s.qidx[p]];
+  for (int j = tid; j < B; j += stride) {
+    const int x = s.sidx[j];
+    s.buf2[j] = s.buf[x];
+    s.bkey2[j] = s.bkey[x];
+  }
+  for (int i = tid; i < s.n; i += stride)
+    s.recv[(size_t)(i + 1) * s.tmax + t] += s.q_cnt[i];  // recv_msgs[dst][time] (EmulNet.cpp:172)
+  if (tid == 0) *s.bufsize = B;
 }
 
 // ---------------------------------------------------------------- node phase
@@ -348,98 +475,174 @@ __global__ __launch_bounds__(F_NODE_THREADS) void gm_f_node(FState s, int t) {
 }
 
 // ---------------------------------------------------------------- send phase
-__global__ __launch_bounds__(F_SEND_THREADS) void gm_f_send(FState s, int t) {
-  __shared__ int s_tmp[32];
-  __shared__ int s_base[1024];
-  __shared__ int s_total;
-  // node-phase order is i descending: exclusive scan of scount over i = n-1..0
-  if (threadIdx.x == 0) {
-    int acc = 0;
-    for (int i = s.n - 1; i >= 0; i--) { s_base[i] = acc; acc += s.scount[i]; }
-    s_total = acc;
+// S1: one glibc rand() draw per ENsend, in send order (EmulNet.cpp:90). glibc TYPE_3 keeps
+// rptr 3 words behind fptr (mod 31), both advancing by one per draw. With the ring rotated
+// so that x[j] is the word fptr reaches at step j of a 31-step round, step j is
+// x[j] += x[(j + 28) % 31] and its draw is x[j] >> 1: a round maps the register vector v
+// linearly (mod 2^32) to v' = R v and its 31 draws are v' >> 1. So round m's draws are
+// (R^(m+1) v0) >> 1, computed in parallel from precomputed powers: the prep kernel steps
+// block states v_(64b) = (R^64)^b v0 serially (one 31x31 product per 1984 draws) and the
+// expansion evaluates round 64b + q as R^(q+1) v_(64b), one output word per lane.
+
+// node-phase order is i descending: exclusive scan of scount over i = n-1..0; S1 block states
+__global__ __launch_bounds__(64) void gm_f_sendprep(FState s) {
+  const int lane = threadIdx.x;
+  int acc = 0;
+  for (int top = s.n - 1; top >= 0; top -= 64) {
+    const int i = top - lane;
+    const int v = i >= 0 ? s.scount[i] : 0;
+    int x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int y = __shfl_up(x, d);
+      if (lane >= d) x += y;
+    }
+    if (i >= 0) s.sbase[i] = acc + x - v;
+    acc += __shfl(x, 63);
   }
-  __syncthreads();
-  const int S = s_total;
+  const int S = acc;
   if (S > s.draw_cap) {
-    if (threadIdx.x == 0) atomicOr(s.err, GM_ERR_DRAWS);
+    if (lane == 0) {
+      atomicOr(s.err, GM_ERR_DRAWS);
+      s.smeta[0] = -1;
+    }
     return;
   }
-  // S1: one glibc rand() draw per ENsend, in send order (EmulNet.cpp:90). glibc TYPE_3
-  // keeps rptr 3 words behind fptr (mod 31), both advancing by one per draw; with the
-  // ring rotated so that x[j] is the word fptr reaches at step j of each 31-step round,
-  // step j is x[j] += x[(j + 28) % 31] -- static register indices in a fully unrolled
-  // round, no dynamically indexed (scratch) state on the serial chain.
-  if (threadIdx.x == 0) {
-    const int f0 = s.s1[31];
-    uint32_t x[31];
-    for (int j = 0; j < 31; j++) x[j] = (uint32_t)s.s1[(f0 + j) % 31];
-    int o = 0;
-    for (; o + 31 <= S; o += 31) {
+  const int f0 = s.s1[31];
+  const int nb = S / 31 / 64 + 1;  // block states the expansion reads (rounds 0 .. S/31)
+  const uint32_t *r64 = s.s1mat + (size_t)63 * 31 * 32;  // R^64 = P_63
+  uint32_t row[31];
 #pragma unroll
-      for (int j = 0; j < 31; j++) {
-        x[j] += x[(j + 28) % 31];
-        s.draws[o + j] = (int32_t)(x[j] >> 1);
-      }
-    }
+  for (int j = 0; j < 31; j++) row[j] = lane < 31 ? r64[lane * 32 + j] : 0u;
+  uint32_t v = lane < 31 ? (uint32_t)s.s1[(f0 + lane) % 31] : 0u;
+  for (int b = 0; b < nb; b++) {
+    if (lane < 32) s.s1vb[(size_t)b * 32 + lane] = v;
+    if (b + 1 < nb) {
+      uint32_t a = 0;
 #pragma unroll
-    for (int j = 0; j < 31; j++) {
-      if (o + j < S) {
-        x[j] += x[(j + 28) % 31];
-        s.draws[o + j] = (int32_t)(x[j] >> 1);
-      }
+      for (int j = 0; j < 31; j++) a += row[j] * (uint32_t)__builtin_amdgcn_readlane((int)v, j);
+      v = a;
     }
-    for (int j = 0; j < 31; j++) s.s1[(f0 + j) % 31] = (int32_t)x[j];
+  }
+  if (lane == 0) {
+    s.smeta[0] = S;
+    s.smeta[1] = f0;
     const int f = (f0 + S) % 31;
     s.s1[31] = f;
     s.s1[32] = (f + 28) % 31;
   }
+}
+
+// the tick's S draws: round m (lanes 0..30 of a half-wave) = P_(m mod 64) v_(64 (m / 64));
+// the rounds holding the last draw write the register back (words j < S mod 31 from round
+// S/31, the rest from round S/31 - 1; none change when S < 31 for j >= S)
+__global__ __launch_bounds__(256) void gm_f_s1expand(FState s) {
+  const int S = s.smeta[0];
+  if (S <= 0) return;
+  const int f0 = s.smeta[1];
+  const int full = S / 31, rem = S % 31;
+  const int k = threadIdx.x & 31;
+  const int hw = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 5), nhw = (int)((gridDim.x * blockDim.x) >> 5);
+  if (k == 31) return;
+  for (int m = hw; m <= full; m += nhw) {
+    const uint4 *P = (const uint4 *)(s.s1mat + ((size_t)(m & 63) * 31 + k) * 32);
+    const uint4 *vb = (const uint4 *)(s.s1vb + (size_t)(m >> 6) * 32);
+    uint32_t a = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const uint4 p = P[j], x = vb[j];
+      a += p.x * x.x + p.y * x.y + p.z * x.z + p.w * x.w;  // word 31 of both is 0
+    }
+    const int o = m * 31 + k;
+    if (o < S) s.draws[o] = (int32_t)(a >> 1);
+    if ((m == full && k < rem) || (m == full - 1 && k >= rem)) s.s1[(f0 + k) % 31] = (int32_t)a;
+  }
+}
+
+// ENsend's drop draw and the 30000 cap (EmulNet.cpp:90-99): exclusive prefix count of the
+// not-drop-drawn sends in send order (pre[o]); a send is buffered at B0 + pre[o] iff kept
+// and pre[o] < room. One workgroup; thread t scans a contiguous run of ordinals.
+__global__ __launch_bounds__(F_SEND_THREADS) void gm_f_sendscan(FState s, int t) {
+  __shared__ int s_tmp[32];
+  const int S = s.smeta[0];
+  if (S < 0) return;  // draw cap exceeded (error latched by gm_f_sendprep)
+  const int pct = s.drop_pct_now;  // (int)(MSG_DROP_PROB*100) while dropmsg, else -1
+  const int L = (S + F_SEND_THREADS - 1) / F_SEND_THREADS;
+  const int o0 = min(S, (int)threadIdx.x * L), o1 = min(S, o0 + L);
+  int c = 0;
+  for (int o = o0; o < o1; o++) c += !(pct >= 0 && (s.draws[o] % 100) < pct);
+  int total;
+  int p = gm_block_scan(c, s_tmp, &total);
+  for (int o = o0; o < o1; o++) {
+    s.spre[o] = p;
+    p += !(pct >= 0 && (s.draws[o] % 100) < pct);
+  }
+  if (threadIdx.x == 0) s.spre[S] = total;
   __syncthreads();
   const int B0 = *s.bufsize;
   const int room = F_ENBUFFSIZE - B0;
-  const int pct = s.drop_pct_now;  // (int)(MSG_DROP_PROB*100) while dropmsg, else -1
-  int kept = 0;                    // not-drop-drawn sends so far
-  for (int base = 0; base < S; base += F_SEND_THREADS) {
-    int o = base + threadIdx.x;
-    int keep = 0;
-    if (o < S) keep = !(pct >= 0 && (s.draws[o] % 100) < pct);
-    int tk;
-    int rk = gm_block_scan(keep, s_tmp, &tk);
-    int before = kept + rk;
-    if (keep && before < room) {
-      // locate the sender: s_base is non-increasing in i; the smallest i with
-      // s_base[i] <= o is the node whose sends contain ordinal o
-      int lo = 0, hi = s.n - 1, i = s.n - 1;
-      while (lo <= hi) {
-        int mid = (lo + hi) >> 1;
-        if (s_base[mid] <= o) { i = mid; hi = mid - 1; } else lo = mid + 1;
-      }
-      int k = o - s_base[i];
-      FMsg m;
-      m.from = i + 1;
-      if (s.started_now[i]) {
-        m.to = 1;
-        m.type = F_JOINREQ;
-        m.subj = i + 1;
-        m.hb = 0;
-      } else if (k < s.jcnt[i]) {
-        m.to = s.jrq[(size_t)i * s.n + k];
-        m.type = F_JOINREP;
-        m.subj = 0;
-        m.hb = 0;
-      } else {
-        int kk = k - s.jcnt[i];
-        int nf = s.fcnt[i];
-        int g = kk / nf, e = kk % nf;
-        int c = s.fcols[(size_t)i * s.n + e];
-        m.to = s.gossip[(size_t)i * s.gstride + g];
-        m.type = F_LIST;
-        m.subj = c + 1;
-        m.hb = (int)gm_hb(s.table[(size_t)i * s.np + c]);
-      }
-      s.buf[B0 + before] = m;
-      atomicAdd(&s.sent[(size_t)(i + 1) * s.tmax + t], 1);  // sent_msgs[src][time]
-    }
-    kept += tk;
+  // sent_msgs[src][time]: node i's buffered sends are its kept ordinals below the cap
+  for (int i = threadIdx.x; i < s.n; i += F_SEND_THREADS) {
+    const int a = s.sbase[i], b = a + s.scount[i];
+    const int k = min(s.spre[b], room) - min(s.spre[a], room);
+    if (k) s.sent[(size_t)(i + 1) * s.tmax + t] += k;
   }
-  if (threadIdx.x == 0) *s.bufsize = B0 + min(kept, room);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    s.smeta[2] = B0;
+    *s.bufsize = B0 + min(total, room);
+  }
+}
+
+// materialise every buffered send (grid-stride over ordinals)
+__global__ __launch_bounds__(256) void gm_f_sendemit(FState s) {
+  __shared__ int s_base[F_MAX_NODES];
+  const int S = s.smeta[0];
+  if (S <= 0) return;
+  const int B0 = s.smeta[2];
+  const int room = F_ENBUFFSIZE - B0;
+  const int pct = s.drop_pct_now;
+  for (int i = threadIdx.x; i < s.n; i += blockDim.x) s_base[i] = s.sbase[i];
+  __syncthreads();
+  for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < S; o += gridDim.x * blockDim.x) {
+    const int before = s.spre[o];
+    if (before >= room || (pct >= 0 && (s.draws[o] % 100) < pct)) continue;
+    // locate the sender: s_base is non-increasing in i; the smallest i with
+    // s_base[i] <= o is the node whose sends contain ordinal o
+    int lo = 0, hi = s.n - 1, i = s.n - 1;
+    while (lo <= hi) {
+      int mid = (lo + hi) >> 1;
+      if (s_base[mid] <= o) { i = mid; hi = mid - 1; } else lo = mid + 1;
+    }
+    int k = o - s_base[i];
+    FMsg m;
+    m.from = i + 1;
+    if (s.started_now[i]) {
+      m.to = 1;
+      m.type = F_JOINREQ;
+      m.subj = i + 1;
+      m.hb = 0;
+    } else if (k < s.jcnt[i]) {
+      m.to = s.jrq[(size_t)i * s.n + k];
+      m.type = F_JOINREP;
+      m.subj = 0;
+      m.hb = 0;
+    } else {
+      int kk = k - s.jcnt[i];
+      int nf = s.fcnt[i];
+      int g = kk / nf, e = kk % nf;
+      int c = s.fcols[(size_t)i * s.n + e];
+      m.to = s.gossip[(size_t)i * s.gstride + g];
+      m.type = F_LIST;
+      m.subj = c + 1;
+      m.hb = (int)gm_hb(s.table[(size_t)i * s.np + c]);
+    }
+    s.buf[B0 + before] = m;
+    uint32_t key = f_strkey(m.to);
+    if (key > (uint32_t)s.n) {  // destinations are node ids 1..n (ENsend asserts them)
+      atomicOr(s.err, GM_ERR_BUFFER);
+      key = s.n;
+    }
+    s.bkey[B0 + before] = (uint16_t)key;
+  }
 }

@@ -20,8 +20,12 @@
 #include "gm_scaled.h"
 
 __global__ void gm_f_recv(FState s, int t);
+__global__ void gm_f_recvout(FState s, int t);
 __global__ void gm_f_node(FState s, int t);
-__global__ void gm_f_send(FState s, int t);
+__global__ void gm_f_sendscan(FState s, int t);
+__global__ void gm_f_sendemit(FState s);
+__global__ void gm_f_sendprep(FState s);
+__global__ void gm_f_s1expand(FState s);
 hipError_t gm_launch_tick(const SState &s, int t, int drop_pct, bool nt, hipStream_t st, hipEvent_t k0, hipEvent_t k1,
                           bool pick);
 hipError_t gm_launch_draw(const SState &s, int t, int round, int D, int listed, hipStream_t st);
@@ -37,6 +41,7 @@ hipError_t gm_launch_partial_chunk(const PState &s, int t, const uint32_t *mtraw
 size_t gm_partial_lds_bytes();
 
 #define GM_T_LIMIT 32766  // packed 16-bit hb/ts stay exact: hb <= 2t+1 < 0xFFFF
+#define GM_F_MAILBOX 512  // FAITHFUL events copied back with the tick's count and error flags  // packed 16-bit hb/ts stay exact: hb <= 2t+1 < 0xFFFF
 #define GM_D_FIRST S_MT_RAW  // S2 outputs per row in the first round (steady state needs ~5-6)
 #define GM_D_MORE 64          // S2 outputs per row in later rounds (transients with many stale entries)
 #define GM_MAX_ROUNDS 4096    // draw rounds per sharded tick (16 + 64 * 4096 S2 outputs per row)
@@ -73,6 +78,7 @@ struct gm_ctx {
   // FAITHFUL
   FState f{};
   size_t f_smem = 0;
+  void *f_mail = nullptr;            // pinned host copy of the FAITHFUL tick mailbox
   std::vector<gm_event> pending;
   // SCALED
   SState s{};
@@ -171,6 +177,32 @@ static void s1_seed(uint32_t seed, int32_t st[33]) {
   st[32] = r;
 }
 
+// P_q = R^(q+1), q = 0..63, rows padded to 32 words: R is one 31-draw round of the S1
+// register in fptr-rotated order, x[j] += x[(j + 28) % 31] for j ascending (gm_f_s1expand)
+static std::vector<uint32_t> s1_round_powers() {
+  uint32_t R[31][31], cur[31][31], nxt[31][31];
+  for (int i = 0; i < 31; i++) {  // column i = the round applied to basis vector e_i
+    uint32_t x[31] = {0};
+    x[i] = 1;
+    for (int j = 0; j < 31; j++) x[j] += x[(j + 28) % 31];
+    for (int k = 0; k < 31; k++) R[k][i] = x[k];
+  }
+  std::vector<uint32_t> P((size_t)64 * 31 * 32, 0u);
+  memcpy(cur, R, sizeof R);
+  for (int q = 0; q < 64; q++) {
+    for (int k = 0; k < 31; k++)
+      for (int j = 0; j < 31; j++) P[((size_t)q * 31 + k) * 32 + j] = cur[k][j];
+    for (int k = 0; k < 31; k++)
+      for (int j = 0; j < 31; j++) {
+        uint32_t a = 0;
+        for (int l = 0; l < 31; l++) a += R[k][l] * cur[l][j];
+        nxt[k][j] = a;
+      }
+    memcpy(cur, nxt, sizeof cur);
+  }
+  return P;
+}
+
 static int create_faithful(gm_ctx *c) {
   const int n = c->n;
   if (n > F_MAX_NODES) return GM_EUNSUPPORTED;  // EmulNet.cpp:108 assert(src <= MAX_NODES)
@@ -191,8 +223,12 @@ static int create_faithful(gm_ctx *c) {
   TRY(dalloc(c, &f.started_now, n));
   TRY(dalloc(c, &f.buf, F_ENBUFFSIZE));
   TRY(dalloc(c, &f.bufsize, 1));
-  TRY(dalloc(c, &f.holepos, F_ENBUFFSIZE));
-  TRY(dalloc(c, &f.keys, F_ENBUFFSIZE));
+  TRY(dalloc(c, &f.holepos, 2 * F_ENBUFFSIZE));
+  TRY(dalloc(c, &f.buf2, F_ENBUFFSIZE));
+  TRY(dalloc(c, &f.bkey, F_ENBUFFSIZE));
+  TRY(dalloc(c, &f.bkey2, F_ENBUFFSIZE));
+  TRY(dalloc(c, &f.sidx, F_ENBUFFSIZE));
+  TRY(dalloc(c, &f.rmeta, 2));
   TRY(dalloc(c, &f.q, F_ENBUFFSIZE));
   TRY(dalloc(c, &f.q_off, n));
   TRY(dalloc(c, &f.q_cnt, n));
@@ -205,11 +241,22 @@ static int create_faithful(gm_ctx *c) {
   TRY(dalloc(c, &f.fcols, (size_t)n * n));
   TRY(dalloc(c, &f.s1, 33));
   TRY(dalloc(c, &f.draws, f.draw_cap));
+  TRY(dalloc(c, &f.sbase, n));
+  TRY(dalloc(c, &f.smeta, 3));
+  TRY(dalloc(c, &f.spre, (size_t)f.draw_cap + 1));
+  TRY(dalloc(c, &f.qidx, F_ENBUFFSIZE));
+  TRY(dalloc(c, &f.s1mat, (size_t)64 * 31 * 32));
+  TRY(dalloc(c, &f.s1vb, (size_t)(f.draw_cap / 1984 + 2) * 32));
   TRY(dalloc(c, &f.sent, (size_t)(F_MAX_NODES + 1) * f.tmax));
   TRY(dalloc(c, &f.recv, (size_t)(F_MAX_NODES + 1) * f.tmax));
-  TRY(dalloc(c, &f.ev, f.ev_cap));
-  TRY(dalloc(c, &f.ev_count, 1));
-  TRY(dalloc(c, &f.err, 1));
+  // one block = the tick's mailbox: event count, error flags, then the events, so that one
+  // small copy per tick brings back all three (GM_F_MAILBOX events; more: a second copy)
+  uint8_t *mb = nullptr;
+  TRY(dalloc(c, &mb, 16 + sizeof(FEvent) * (size_t)f.ev_cap));
+  f.ev_count = (unsigned long long *)mb;
+  f.err = (uint32_t *)(mb + 8);
+  f.ev = (FEvent *)(mb + 16);
+  if (hipHostMalloc(&c->f_mail, 16 + sizeof(FEvent) * GM_F_MAILBOX, hipHostMallocDefault) != hipSuccess) return GM_ENOMEM;
   HIPCHECK(hipMemset(f.table, 0xFF, sizeof(uint32_t) * (size_t)n * f.np));
   std::vector<int32_t> start(n);
   for (int i = 0; i < n; i++) start[i] = (int)(0.25 * i);  // (int)(STEP_RATE*i), Application.cpp:143
@@ -225,6 +272,9 @@ static int create_faithful(gm_ctx *c) {
   int32_t st[33];
   s1_seed(c->cfg.time_seed, st);  // srand(time(NULL)) at Application.cpp:50 and :96
   HIPCHECK(hipMemcpy(f.s1, st, sizeof st, hipMemcpyHostToDevice));
+  const std::vector<uint32_t> pm = s1_round_powers();
+  HIPCHECK(hipMemcpy(f.s1mat, pm.data(), sizeof(uint32_t) * pm.size(), hipMemcpyHostToDevice));
+  HIPCHECK(hipFuncSetAttribute((const void *)gm_f_recv, hipFuncAttributeMaxDynamicSharedMemorySize, F_RECV_LDS));
   const int nw = f.np / 64;
   c->f_smem = (size_t)f.np * 8 + (size_t)nw * 8 * 3 + (size_t)nw * 4 + 624 * 4 + 48 * 4;
   return GM_OK;
@@ -463,6 +513,7 @@ extern "C" int gm_destroy(gm_ctx *c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm) (void)ncclCommDestroy(c->comm);
   for (void *p : c->allocs) (void)hipFree(p);
+  if (c->f_mail) (void)hipHostFree(c->f_mail);
   for (hipEvent_t e : {c->e0, c->e1, c->k0, c->k1})
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : c->tev) (void)hipEventDestroy(e);
@@ -501,30 +552,48 @@ static int tick_faithful(gm_ctx *c) {
       c->fail_t[i] = 0x7FFFFFFF;
     }
   FState st = c->f;
+  hipLaunchKernelGGL(gm_f_recv, dim3(1), dim3(1024), F_RECV_LDS, c->stream, st, c->t);
+  hipLaunchKernelGGL(gm_f_recvout, dim3(64), dim3(256), 0, c->stream, st, c->t);
+  std::swap(c->f.buf, c->f.buf2);  // gm_f_recvout compacted the survivors into buf2
+  std::swap(c->f.bkey, c->f.bkey2);
+  st = c->f;
   st.drop_pct_now = c->dropmsg ? (int)(c->cfg.drop_prob * 100) : -1;  // EmulNet.cpp:92
-  hipLaunchKernelGGL(gm_f_recv, dim3(1), dim3(1024), 0, c->stream, st, c->t);
   hipLaunchKernelGGL(gm_f_node, dim3(c->n), dim3(256), c->f_smem, c->stream, st, c->t);
-  hipLaunchKernelGGL(gm_f_send, dim3(1), dim3(1024), 0, c->stream, st, c->t);
+  hipLaunchKernelGGL(gm_f_sendprep, dim3(1), dim3(64), 0, c->stream, st);
+  const int rounds = st.draw_cap / 31 + 1;
+  hipLaunchKernelGGL(gm_f_s1expand, dim3(std::min(1024, (rounds + 7) / 8)), dim3(256), 0, c->stream, st);
+  hipLaunchKernelGGL(gm_f_sendscan, dim3(1), dim3(1024), 0, c->stream, st, c->t);
+  hipLaunchKernelGGL(gm_f_sendemit, dim3(std::min(1024, (st.draw_cap + 255) / 256)), dim3(256), 0, c->stream, st);
   HIPCHECK(hipGetLastError());
-  unsigned long long nev = 0;
-  HIPCHECK(hipMemcpyAsync(&nev, c->f.ev_count, sizeof nev, hipMemcpyDeviceToHost, c->stream));
+  // one copy of the mailbox (count, error flags, the first GM_F_MAILBOX events) and one
+  // wait per tick; gm_f_recv of the next tick zeroes the count
+  HIPCHECK(hipMemcpyAsync(c->f_mail, c->f.ev_count, 16 + sizeof(FEvent) * GM_F_MAILBOX, hipMemcpyDeviceToHost,
+                          c->stream));
   HIPCHECK(hipStreamSynchronize(c->stream));
+  const unsigned long long nev = *(const unsigned long long *)c->f_mail;
+  const uint32_t e = *(const uint32_t *)((const uint8_t *)c->f_mail + 8);
   if (nev > (unsigned long long)c->f.ev_cap) {
     c->latched = GM_ERANGE;
     return c->latched;
   }
   if (nev) {
     std::vector<FEvent> ev(nev);
-    HIPCHECK(hipMemcpyAsync(ev.data(), c->f.ev, sizeof(FEvent) * nev, hipMemcpyDeviceToHost, c->stream));
-    HIPCHECK(hipMemsetAsync(c->f.ev_count, 0, sizeof(unsigned long long), c->stream));
-    HIPCHECK(hipStreamSynchronize(c->stream));
+    memcpy(ev.data(), (const uint8_t *)c->f_mail + 16, sizeof(FEvent) * std::min<size_t>(nev, GM_F_MAILBOX));
+    if (nev > GM_F_MAILBOX) {
+      HIPCHECK(hipMemcpy(ev.data() + GM_F_MAILBOX, c->f.ev + GM_F_MAILBOX, sizeof(FEvent) * (nev - GM_F_MAILBOX),
+                         hipMemcpyDeviceToHost));
+    }
     std::sort(ev.begin(), ev.end(), ev_order);
     for (const FEvent &e : ev) {
       c->pending.push_back(gm_event{e.t, e.logger, e.kind, e.subject});
       if (e.kind > 0 && e.kind < 6) c->ev_tot[e.kind]++;
     }
   }
-  return check_err(c);
+  if (e) {
+    snprintf(g_errbuf, sizeof g_errbuf, "device error flags 0x%x", e);
+    c->latched = (e & (GM_ERR_SELF | GM_ERR_BUFFER)) ? GM_ESTATE : GM_ERANGE;
+  }
+  return c->latched;
 }
 
 static int tick_sharded(gm_ctx *c);

@@ -12,7 +12,8 @@
 #   prof_sc    rocprofv3 --kernel-trace --stats of S-C  -> $O/prof_sc/
 #   pmc_sa     FETCH_SIZE / WRITE_SIZE passes of S-A    -> $O/pmc_sa_{fetch,write}/ + traffic json
 #   pmc_sc     FETCH_SIZE / WRITE_SIZE passes of S-C    -> $O/pmc_sc_{fetch,write}/ + traffic json
-#   faithful   ./Application on the three testcases, timed -> $O/faithful_wall.txt
+#   faithful   ./Application on the three testcases + N = 70, timed -> $O/faithful_wall.txt
+#   prof_faithful rocprofv3 --kernel-trace --stats of ./Application at N = 70 -> $O/prof_n70/
 #
 # Every GPU step runs under its own timeout; steps are chained so the first
 # failure ends the call (no retries). Extra bench flags: BENCH_ARGS env.
@@ -49,9 +50,11 @@ run_step() {
               python3 bench.py --scenario S-C --no-cpu --steps 3 --warmup 1 > $O/pmc_sc_write.log 2>&1 &&
             python3 scripts/pmc_traffic.py --kernel gm_p_tick --fetch $O/pmc_sc_fetch --write $O/pmc_sc_write \
               --layout partial-v32 --n 16777216 --out $O/traffic_sc_n16777216.json > $O/pmc_sc.txt 2>&1 ;;
-    faithful) ( TIMEFORMAT="%R s"; for c in singlefailure multifailure msgdropsinglefailure; do
+    faithful) ( TIMEFORMAT="%R s"; for c in singlefailure multifailure msgdropsinglefailure n70; do
                   echo -n "$c "; { time timeout -k 10 60 ./Application testcases/$c.conf > /dev/null; } 2>&1 || exit 1
                 done ) > $O/faithful_wall.txt 2>&1 ;;
+    prof_faithful) timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_n70 -o n70 -- \
+               ./Application testcases/n70.conf > $O/prof_n70.log 2>&1 ;;
     *) echo "unknown step $1"; return 2 ;;
   esac
 }
