@@ -10,6 +10,7 @@
 // nondeterministic as the reference.
 #include "Application.h"
 
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <ctime>
@@ -32,7 +33,11 @@ Application::Application(const char *conf) {
   cfg_.shard_count = 1;
   log_.reset(new Log());
   for (int i = 0; i < cfg_.n; i++) log_->LOG(i + 1, 0, "APP");  // Application.cpp:66
+  const auto t0 = std::chrono::steady_clock::now();
   rc_ = gm_create(&cfg_, &ctx_);
+  if (getenv("GM_APP_TIMING"))
+    fprintf(stderr, "gm_create %.1f ms\n",
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
 }
 
 Application::~Application() {
@@ -68,9 +73,11 @@ void Application::drain() {
   }
 }
 
+// Ticks are enqueued without a host wait; the log is written from drained records
+// before every line the host itself logs (fail) and at the end, so dbg.log keeps the
+// reference's order (Application.cpp:121-164 logs inside the tick).
 void Application::mp1Run() {
   check(gm_tick(ctx_));
-  drain();
   // "i-th introduced node" lines, in node-phase order (Application.cpp:143-147)
   for (int i = cfg_.n - 1; i >= 0; i--)
     if (t_ == (int)(0.25 * i)) printf("%d-th introduced node is assigned with the address: %d:0\n", i, i + 1);
@@ -79,6 +86,7 @@ void Application::mp1Run() {
 void Application::fail() {
   char s[64];
   if (cfg_.drop_msg && t_ == 50) check(gm_set_dropmsg(ctx_, 1));
+  if (t_ == 100) drain();  // this tick's records precede the failure lines
   if (cfg_.single_failure && t_ == 100) {
     int32_t r = 0;
     check(gm_rand(ctx_, &r));
@@ -103,10 +111,15 @@ void Application::fail() {
 
 int Application::run() {
   if (rc_ != GM_OK) return rc_;
+  const auto t0 = std::chrono::steady_clock::now();
   for (t_ = 0; t_ < TOTAL_RUNNING_TIME && rc_ == GM_OK; ++t_) {
     mp1Run();
     fail();
   }
+  drain();
+  if (getenv("GM_APP_TIMING"))
+    fprintf(stderr, "%d ticks %.1f ms\n", t_,
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
   // ENcleanup: msgcount.log (EmulNet.cpp:184-220), node 67 special-cased
   const int n = cfg_.n, T = t_;
   std::vector<int32_t> sent((size_t)n * T), recv((size_t)n * T);

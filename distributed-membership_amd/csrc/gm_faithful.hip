@@ -102,7 +102,6 @@ __global__ __launch_bounds__(F_RECV_THREADS) void gm_f_recv(FState s, int t) {
   const int B00 = B;
   uint64_t c1 = 0;
 #endif
-  if (threadIdx.x == 0) *s.ev_count = 0;  // the host copied the last tick's records (mailbox)
   for (int j = threadIdx.x; j < (n + 1) * nsw; j += F_RECV_THREADS) cw[j] = 0;
   for (int i = threadIdx.x; i < n; i += F_RECV_THREADS)
     act[i] = t > s.start[i] && !s.failed[i];  // Application.cpp:130

@@ -41,7 +41,7 @@ hipError_t gm_launch_partial_chunk(const PState &s, int t, const uint32_t *mtraw
 size_t gm_partial_lds_bytes();
 
 #define GM_T_LIMIT 32766  // packed 16-bit hb/ts stay exact: hb <= 2t+1 < 0xFFFF
-#define GM_F_MAILBOX 512  // FAITHFUL events copied back with the tick's count and error flags  // packed 16-bit hb/ts stay exact: hb <= 2t+1 < 0xFFFF
+#define GM_F_MAILBOX 4096  // FAITHFUL events copied back with the count and error flags  // packed 16-bit hb/ts stay exact: hb <= 2t+1 < 0xFFFF
 #define GM_D_FIRST S_MT_RAW  // S2 outputs per row in the first round (steady state needs ~5-6)
 #define GM_D_MORE 64          // S2 outputs per row in later rounds (transients with many stale entries)
 #define GM_MAX_ROUNDS 4096    // draw rounds per sharded tick (16 + 64 * 4096 S2 outputs per row)
@@ -79,6 +79,7 @@ struct gm_ctx {
   FState f{};
   size_t f_smem = 0;
   void *f_mail = nullptr;            // pinned host copy of the FAITHFUL tick mailbox
+  int f_inflight = 0;                // FAITHFUL ticks enqueued since the last mailbox collection
   std::vector<gm_event> pending;
   // SCALED
   SState s{};
@@ -213,7 +214,7 @@ static int create_faithful(gm_ctx *c) {
   f.gstride = n + GM_FANOUT;
   f.draw_cap = 5 * n * n + 2 * n + 1024;
   f.rd_seed = c->cfg.rd_seed;
-  f.ev_cap = std::max(4096, 4 * n * n + 64 * n);
+  f.ev_cap = std::max(1 << 18, 4 * n * n + 64 * n);
   TRY(dalloc(c, &f.table, (size_t)n * f.np));
   TRY(dalloc(c, &f.start, n));
   TRY(dalloc(c, &f.failed, n));
@@ -543,35 +544,23 @@ static bool ev_order(const FEvent &a, const FEvent &b) {
   return a.seq < b.seq;
 }
 
-static int tick_faithful(gm_ctx *c) {
-  if (c->t >= F_MAX_TIME) return GM_ERANGE;  // EmulNet.cpp:109 assert(time < MAX_TIME)
-  // nodeStart of this tick's starters resets bFailed on the device (MP1Node.cpp:108-116); mirror it
-  for (int i = 0; i < c->n; i++)
-    if ((int)(0.25 * i) == c->t && c->failed_h[i]) {
-      c->failed_h[i] = 0;
-      c->fail_t[i] = 0x7FFFFFFF;
-    }
-  FState st = c->f;
-  hipLaunchKernelGGL(gm_f_recv, dim3(1), dim3(1024), F_RECV_LDS, c->stream, st, c->t);
-  hipLaunchKernelGGL(gm_f_recvout, dim3(64), dim3(256), 0, c->stream, st, c->t);
-  std::swap(c->f.buf, c->f.buf2);  // gm_f_recvout compacted the survivors into buf2
-  std::swap(c->f.bkey, c->f.bkey2);
-  st = c->f;
-  st.drop_pct_now = c->dropmsg ? (int)(c->cfg.drop_prob * 100) : -1;  // EmulNet.cpp:92
-  hipLaunchKernelGGL(gm_f_node, dim3(c->n), dim3(256), c->f_smem, c->stream, st, c->t);
-  hipLaunchKernelGGL(gm_f_sendprep, dim3(1), dim3(64), 0, c->stream, st);
-  const int rounds = st.draw_cap / 31 + 1;
-  hipLaunchKernelGGL(gm_f_s1expand, dim3(std::min(1024, (rounds + 7) / 8)), dim3(256), 0, c->stream, st);
-  hipLaunchKernelGGL(gm_f_sendscan, dim3(1), dim3(1024), 0, c->stream, st, c->t);
-  hipLaunchKernelGGL(gm_f_sendemit, dim3(std::min(1024, (st.draw_cap + 255) / 256)), dim3(256), 0, c->stream, st);
-  HIPCHECK(hipGetLastError());
-  // one copy of the mailbox (count, error flags, the first GM_F_MAILBOX events) and one
-  // wait per tick; gm_f_recv of the next tick zeroes the count
+// Records of a FAITHFUL tick can be at most n * (2n + 4): per node n joins, n removals and
+// the start / join / time-mark lines.
+static int64_t f_tick_event_bound(const gm_ctx *c) { return (int64_t)c->n * (2 * c->n + 4); }
+
+// Collect the mailbox of every tick enqueued since the last collection: one copy of the
+// count, the error flags and the first GM_F_MAILBOX records (more: a second copy), one
+// wait; the records are staged to `pending` in the reference's order, the count reset in
+// stream order.
+static int f_collect(gm_ctx *c) {
+  if (c->f_inflight == 0) return c->latched;
+  c->f_inflight = 0;
   HIPCHECK(hipMemcpyAsync(c->f_mail, c->f.ev_count, 16 + sizeof(FEvent) * GM_F_MAILBOX, hipMemcpyDeviceToHost,
                           c->stream));
   HIPCHECK(hipStreamSynchronize(c->stream));
   const unsigned long long nev = *(const unsigned long long *)c->f_mail;
   const uint32_t e = *(const uint32_t *)((const uint8_t *)c->f_mail + 8);
+  HIPCHECK(hipMemsetAsync(c->f.ev_count, 0, sizeof(unsigned long long), c->stream));
   if (nev > (unsigned long long)c->f.ev_cap) {
     c->latched = GM_ERANGE;
     return c->latched;
@@ -593,6 +582,39 @@ static int tick_faithful(gm_ctx *c) {
     snprintf(g_errbuf, sizeof g_errbuf, "device error flags 0x%x", e);
     c->latched = (e & (GM_ERR_SELF | GM_ERR_BUFFER)) ? GM_ESTATE : GM_ERANGE;
   }
+  return c->latched;
+}
+
+// Everything that reads FAITHFUL state (records, tables, counters, the S1 stream) first
+// completes the enqueued ticks.
+static int f_settle(gm_ctx *c) { return c->cfg.mode == GM_MODE_FAITHFUL ? f_collect(c) : GM_OK; }
+
+// FAITHFUL ticks are enqueued without a host wait: the records stay on the device until a
+// call needs them (f_settle) or the next tick could overflow the record buffer.
+static int tick_faithful(gm_ctx *c) {
+  if (c->t >= F_MAX_TIME) return GM_ERANGE;  // EmulNet.cpp:109 assert(time < MAX_TIME)
+  if ((c->f_inflight + 1) * f_tick_event_bound(c) > c->f.ev_cap) TRY(f_collect(c));
+  // nodeStart of this tick's starters resets bFailed on the device (MP1Node.cpp:108-116); mirror it
+  for (int i = 0; i < c->n; i++)
+    if ((int)(0.25 * i) == c->t && c->failed_h[i]) {
+      c->failed_h[i] = 0;
+      c->fail_t[i] = 0x7FFFFFFF;
+    }
+  FState st = c->f;
+  hipLaunchKernelGGL(gm_f_recv, dim3(1), dim3(1024), F_RECV_LDS, c->stream, st, c->t);
+  hipLaunchKernelGGL(gm_f_recvout, dim3(64), dim3(256), 0, c->stream, st, c->t);
+  std::swap(c->f.buf, c->f.buf2);  // gm_f_recvout compacted the survivors into buf2
+  std::swap(c->f.bkey, c->f.bkey2);
+  st = c->f;
+  st.drop_pct_now = c->dropmsg ? (int)(c->cfg.drop_prob * 100) : -1;  // EmulNet.cpp:92
+  hipLaunchKernelGGL(gm_f_node, dim3(c->n), dim3(256), c->f_smem, c->stream, st, c->t);
+  hipLaunchKernelGGL(gm_f_sendprep, dim3(1), dim3(64), 0, c->stream, st);
+  const int rounds = st.draw_cap / 31 + 1;
+  hipLaunchKernelGGL(gm_f_s1expand, dim3(std::min(1024, (rounds + 7) / 8)), dim3(256), 0, c->stream, st);
+  hipLaunchKernelGGL(gm_f_sendscan, dim3(1), dim3(1024), 0, c->stream, st, c->t);
+  hipLaunchKernelGGL(gm_f_sendemit, dim3(std::min(1024, (st.draw_cap + 255) / 256)), dim3(256), 0, c->stream, st);
+  HIPCHECK(hipGetLastError());
+  c->f_inflight++;
   return c->latched;
 }
 
@@ -701,6 +723,7 @@ extern "C" int gm_tick(gm_ctx *c) {
 
 extern "C" int gm_sync(gm_ctx *c) {
   if (!c) return GM_EINVAL;
+  TRY(f_settle(c));
   HIPCHECK(hipStreamSynchronize(c->stream));
   return check_err(c);
 }
@@ -714,6 +737,7 @@ extern "C" int gm_time(gm_ctx *c, int32_t *t) {
 extern "C" int gm_rand(gm_ctx *c, int32_t *out) {
   if (!c || !out) return GM_EINVAL;
   if (c->cfg.mode != GM_MODE_FAITHFUL) return GM_EUNSUPPORTED;
+  TRY(f_settle(c));
   int32_t st[33];
   HIPCHECK(hipMemcpyAsync(st, c->f.s1, sizeof st, hipMemcpyDeviceToHost, c->stream));
   HIPCHECK(hipStreamSynchronize(c->stream));
@@ -731,6 +755,7 @@ extern "C" int gm_set_failed(gm_ctx *c, const int32_t *idx, int32_t n) {
   if (!c || n < 0 || (n > 0 && !idx)) return GM_EINVAL;
   for (int k = 0; k < n; k++)  // validate everything before any state changes
     if (idx[k] < 0 || idx[k] >= c->n) return GM_EINVAL;
+  TRY(f_settle(c));
   for (int k = 0; k < n; k++) {
     c->nfailed += c->failed_h[idx[k]] == 0;
     if (!c->failed_h[idx[k]]) c->fail_t[idx[k]] = c->t - 1;
@@ -832,6 +857,7 @@ static int drain_partial(gm_ctx *c, std::vector<gm_event> &out) {
 // SCALED / PARTIAL: move the last tick's device records (one tick's worth is kept on the
 // device, overwritten by the next tick) to the host list, in canonical order.
 static int stage_events(gm_ctx *c) {
+  TRY(f_settle(c));
   if (!c->undrained) return GM_OK;
   c->undrained = false;
   const size_t first = c->pending.size();
@@ -867,6 +893,7 @@ extern "C" int gm_drain_events(gm_ctx *c, gm_event *out, size_t cap, size_t *n) 
 
 extern "C" int gm_event_counts(gm_ctx *c, uint64_t counts[6]) {
   if (!c || !counts) return GM_EINVAL;
+  TRY(f_settle(c));
   for (int k = 0; k < 6; k++) counts[k] = 0;
   if (c->cfg.mode == GM_MODE_SCALED) {
     std::vector<uint32_t> bc;
@@ -891,6 +918,7 @@ extern "C" int gm_event_counts(gm_ctx *c, uint64_t counts[6]) {
 
 extern "C" int gm_event_totals(gm_ctx *c, uint64_t totals[6]) {
   if (!c || !totals) return GM_EINVAL;
+  TRY(f_settle(c));
   for (int k = 0; k < 6; k++) totals[k] = c->ev_tot[k];
   if (c->cfg.mode == GM_MODE_PARTIAL) return GM_EUNSUPPORTED;
   if (c->cfg.mode == GM_MODE_SCALED) {
@@ -914,6 +942,7 @@ extern "C" int gm_msgcount(gm_ctx *c, int32_t t, int32_t *sent, int32_t *recv) {
   if (!c || !sent || !recv || t < 0) return GM_EINVAL;
   if (c->cfg.mode != GM_MODE_FAITHFUL) return GM_EUNSUPPORTED;
   if (t > c->f.tmax) return GM_EINVAL;
+  TRY(f_settle(c));
   HIPCHECK(hipStreamSynchronize(c->stream));
   std::vector<int32_t> hs((size_t)(F_MAX_NODES + 1) * c->f.tmax), hr(hs.size());
   HIPCHECK(hipMemcpy(hs.data(), c->f.sent, sizeof(int32_t) * hs.size(), hipMemcpyDeviceToHost));
@@ -929,6 +958,7 @@ extern "C" int gm_msgcount(gm_ctx *c, int32_t t, int32_t *sent, int32_t *recv) {
 // Row r of this context's table as absolute (hb, ts) per column, -1 = absent.
 static int read_table_row(gm_ctx *c, int r, std::vector<int32_t> &hb, std::vector<int32_t> &ts, int &w) {
   if (c->cfg.mode == GM_MODE_FAITHFUL) {
+    TRY(f_settle(c));
     w = c->n;
     std::vector<uint32_t> row(w);
     HIPCHECK(hipMemcpy(row.data(), c->f.table + (size_t)r * c->f.np, sizeof(uint32_t) * w, hipMemcpyDeviceToHost));
@@ -1004,6 +1034,7 @@ extern "C" int gm_read_views(gm_ctx *c, int32_t r0, int32_t count, uint64_t *out
 
 extern "C" int gm_read_nodes(gm_ctx *c, int32_t *st4) {
   if (!c || !st4) return GM_EINVAL;
+  TRY(f_settle(c));
   HIPCHECK(hipStreamSynchronize(c->stream));
   const int n = c->cfg.mode == GM_MODE_PARTIAL ? c->p.nloc : c->n;  // a row shard reports its own nodes
   std::vector<int32_t> a(n), b(n), f(n), h(n);

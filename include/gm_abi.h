@@ -124,7 +124,12 @@ int gm_create(const gm_config *cfg, gm_ctx **out);
 int gm_destroy(gm_ctx *ctx);
 
 /* Enqueue one Application::mp1Run tick at the context's current globaltime,
- * then advance globaltime. Returns a latched device error from an earlier tick. */
+ * then advance globaltime. Returns a latched device error from an earlier tick.
+ * FAITHFUL ticks do not wait on the host either: their records and error flags
+ * are collected by the next call that reads state (gm_drain_events, gm_sync,
+ * gm_rand, gm_set_failed, gm_msgcount, gm_read_*, gm_event_*), or by gm_tick
+ * itself once the device record buffer could fill; an error raised by tick t is
+ * reported by that call. */
 int gm_tick(gm_ctx *ctx);
 int gm_sync(gm_ctx *ctx);
 int gm_time(gm_ctx *ctx, int32_t *t);
