@@ -75,6 +75,8 @@ def parse():
     p.add_argument("--crash-frac", type=float, default=0.01)
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--drop-pct", type=int, default=0,
+                   help="diagnostics (S-A): keyed per-entry drops on every tick (the drop path of gm_s_band)")
     p.add_argument("--force-shard", action="store_true",
                    help="diagnostics: at N=1 run the column-shard protocol with RCCL over one rank")
     return p.parse_args()
@@ -109,6 +111,8 @@ def main():
     n = a.cluster
     ncrash = int(round(n * a.crash_frac))
     init = dict(init_mode=1 if a.t0 > 0 else 0, init_t0=a.t0, init_seed=11)
+    if a.drop_pct:
+        init.update(drop_pct=a.drop_pct, drop_from=0, drop_to=1 << 30, drop_seed=5)
     if world > 1:
         sim = distributed_shard(n, rank, world, local, rd_seed=7, **init)
     elif a.force_shard:
@@ -157,7 +161,8 @@ def main():
     # TREMOVE sweep of the crashed nodes (MP1Node.cpp:429-444) -- every live observer removed
     # every crashed node exactly once, nothing else was removed or joined (device counters)
     tot = sim.event_totals()
-    removed_ok = (a.prologue + a.warmup + a.steps >= a.crash_tick + 38 and a.t0 > 0)  # last removals ~tick 42
+    removed_ok = (a.prologue + a.warmup + a.steps >= a.crash_tick + 38 and a.t0 > 0  # last removals ~tick 42
+                  and not a.drop_pct)  # loss can remove live nodes too
     if removed_ok:
         c0, wl = sim.shard_layout() if world > 1 else (0, n)  # a column shard counts its own columns
         crash_here = int(((crash >= c0) & (crash < c0 + wl)).sum())
@@ -203,7 +208,8 @@ def main():
         "vs_baseline": None,
         "dtype": "u16 cells / 4-bit payload (integer)",
         "data": "synthetic (converged full-membership table, seeded crash set)",
-        "config": {"workload": "S-A: SCALED full membership, 1% crash at tick 10, fanout 5, TFAIL 5, TREMOVE 20",
+        "config": {"workload": "S-A: SCALED full membership, 1% crash at tick 10, fanout 5, TFAIL 5, TREMOVE 20"
+                   + (f", DIAGNOSTIC keyed {a.drop_pct}% per-entry drops" if a.drop_pct else ""),
                    "n": n, "start": f"warm t0={a.t0}" if a.t0 > 0 else "cold", "prologue_to_tick": a.prologue, "crashed": ncrash, "live": n_live,
                    "lists_per_tick": m_lists, "parallelism": f"column-shard x{world}" if world > 1 else
                    ("column-shard x1 (RCCL, forced)" if a.force_shard else "single GPU")},
