@@ -363,6 +363,7 @@ def main_partial(a):
                                          f"core ({secs:.1f} s, oracle/ref_cpu.c op_tick)"}
     if rank == 0:
         print(json.dumps(out), flush=True)
+    sim.close()
     if dist is not None:
         dist.destroy_process_group()
 

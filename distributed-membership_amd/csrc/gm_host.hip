@@ -36,9 +36,11 @@ hipError_t gm_launch_partial_tick(const PState &s, int t, uint32_t *mtraw, hipSt
                                   hipEvent_t k1);
 hipError_t gm_launch_partial_init(const PState &s, int t0, uint64_t init_seed, hipStream_t st);
 hipError_t gm_launch_partial_unpack(const PState &s, int t, int base, int nrecv, hipStream_t st);
-hipError_t gm_launch_partial_mtgen(const PState &s, int t, uint32_t *mtraw, hipStream_t st);
+hipError_t gm_launch_partial_mtgen(const PState &s, int t, uint32_t *mtraw, hipStream_t st, bool reset);
+hipError_t gm_launch_partial_reset(const PState &s, hipStream_t st);
 hipError_t gm_launch_partial_chunk(const PState &s, int t, const uint32_t *mtraw, int c, hipStream_t st);
 size_t gm_partial_lds_bytes();
+void gm_partial_profile_dump();
 
 #define GM_T_LIMIT 32766  // packed 16-bit hb/ts stay exact: hb <= 2t+1 < 0xFFFF
 #define GM_F_MAILBOX 4096  // FAITHFUL events copied back with the count and error flags  // packed 16-bit hb/ts stay exact: hb <= 2t+1 < 0xFFFF
@@ -85,7 +87,11 @@ struct gm_ctx {
   SState s{};
   // PARTIAL
   PState p{};
-  uint32_t *p_mtraw = nullptr;
+  uint32_t *p_mtraw = nullptr;        // [2][nloc][16] S2 outputs by tick parity
+  hipStream_t p_side = nullptr;        // S2 outputs of tick t+1, computed while tick t runs
+  hipEvent_t p_tickev[2] = {nullptr, nullptr};  // by parity: the tick that read that S2 buffer is done
+  hipEvent_t p_mtev[2] = {nullptr, nullptr};    // by parity: the prefetched S2 outputs are written
+  int p_mt_next = -1;                  // the tick whose S2 outputs were prefetched
   int64_t p_recv_last = 0;  // lists received from other row shards in the last tick
   bool p_sharded = false;   // row-shard exchange each tick (G > 1, or one rank forced by GM_FORCE_SHARD=1)
   hipStream_t p_comm = nullptr;        // row shards: RCCL exchange stream (overlaps the next chunk's kernels)
@@ -442,7 +448,12 @@ static int create_partial(gm_ctx *c) {
   TRY(dalloc(c, &p.targets, (size_t)nl * GM_FANOUT));
   TRY(dalloc(c, &p.big, nl));
   TRY(dalloc(c, &p.err, 1));
-  TRY(dalloc(c, &c->p_mtraw, (size_t)nl * 16));
+  TRY(dalloc(c, &c->p_mtraw, (size_t)nl * 16 * 2));
+  HIPCHECK(hipStreamCreateWithFlags(&c->p_side, hipStreamNonBlocking));
+  for (int q = 0; q < 2; q++) {
+    HIPCHECK(hipEventCreateWithFlags(&c->p_tickev[q], hipEventDisableTiming));
+    HIPCHECK(hipEventCreateWithFlags(&c->p_mtev[q], hipEventDisableTiming));
+  }
   c->p_sharded = G > 1 || (getenv("GM_FORCE_SHARD") && atoi(getenv("GM_FORCE_SHARD")) == 1);
   // row shards pipeline their exchange over K chunks of their nodes (GM_CHUNKS, default 4)
   p.nchunk = c->p_sharded ? (getenv("GM_CHUNKS") ? atoi(getenv("GM_CHUNKS")) : 4) : 1;
@@ -521,6 +532,15 @@ extern "C" int gm_destroy(gm_ctx *c) {
   for (hipEvent_t e : c->p_chev) (void)hipEventDestroy(e);
   if (c->p_done) (void)hipEventDestroy(c->p_done);
   if (c->p_comm) (void)hipStreamDestroy(c->p_comm);
+  if (c->cfg.mode == GM_MODE_PARTIAL) gm_partial_profile_dump();
+  if (c->p_side) {
+    (void)hipStreamSynchronize(c->p_side);
+    (void)hipStreamDestroy(c->p_side);
+  }
+  for (int q = 0; q < 2; q++) {
+    if (c->p_tickev[q]) (void)hipEventDestroy(c->p_tickev[q]);
+    if (c->p_mtev[q]) (void)hipEventDestroy(c->p_mtev[q]);
+  }
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return GM_OK;
@@ -680,15 +700,25 @@ static int tick_partial(gm_ctx *c) {
   st.drop_pct = drop ? c->cfg.drop_pct : -1;
   hipEvent_t k0 = nullptr, k1 = nullptr;
   if (c->timing) TRY(timing_slot(c, &k0, &k1));
+  // S2 outputs of this tick: prefetched on the side stream while the last tick ran
+  // (they depend only on (seed, t, id)), else computed here
+  const int t = c->t, par = t & 1;
+  uint32_t *mt = c->p_mtraw + (size_t)par * st.nloc * 16;
+  if (c->p_mt_next == t) {
+    HIPCHECK(hipStreamWaitEvent(c->stream, c->p_mtev[par], 0));
+    HIPCHECK(gm_launch_partial_reset(st, c->stream));
+  } else {
+    HIPCHECK(gm_launch_partial_mtgen(st, t, mt, c->stream, true));
+  }
+  if (k0) HIPCHECK(hipEventRecord(k0, c->stream));
   if (!c->p_sharded) {
-    HIPCHECK(gm_launch_partial_tick(st, c->t, c->p_mtraw, c->stream, k0, k1));
+    HIPCHECK(gm_launch_partial_chunk(st, t, mt, 0, c->stream));
+    if (k1) HIPCHECK(hipEventRecord(k1, c->stream));
   } else {
     // chunk pipeline: every chunk's node ticks queue on the compute stream; the exchange of
     // chunk q runs on the comm stream once q's kernels are done, while q+1.. still compute
-    HIPCHECK(gm_launch_partial_mtgen(st, c->t, c->p_mtraw, c->stream));
-    if (k0) HIPCHECK(hipEventRecord(k0, c->stream));
     for (int q = 0; q < st.nchunk; q++) {
-      HIPCHECK(gm_launch_partial_chunk(st, c->t, c->p_mtraw, q, c->stream));
+      HIPCHECK(gm_launch_partial_chunk(st, t, mt, q, c->stream));
       HIPCHECK(hipEventRecord(c->p_chev[q], c->stream));
     }
     if (k1) HIPCHECK(hipEventRecord(k1, c->stream));
@@ -701,6 +731,12 @@ static int tick_partial(gm_ctx *c) {
     HIPCHECK(hipEventRecord(c->p_done, c->p_comm));
     HIPCHECK(hipStreamWaitEvent(c->stream, c->p_done, 0));  // the next tick reads the unpacked inboxes
   }
+  // prefetch tick t+1's S2 outputs into the other parity buffer, last read by tick t-1
+  HIPCHECK(hipEventRecord(c->p_tickev[par], c->stream));
+  HIPCHECK(hipStreamWaitEvent(c->p_side, c->p_tickev[par ^ 1], 0));
+  HIPCHECK(gm_launch_partial_mtgen(st, t + 1, c->p_mtraw + (size_t)(par ^ 1) * st.nloc * 16, c->p_side, false));
+  HIPCHECK(hipEventRecord(c->p_mtev[par ^ 1], c->p_side));
+  c->p_mt_next = t + 1;
   if (c->timing) {
     HIPCHECK(hipEventRecord(c->e1, c->stream));
     c->timed_ticks++;

@@ -35,9 +35,24 @@
 // Lists are double-buffered by tick parity: a receiver reads its senders' lists
 // of tick t-1 directly, so no separate payload copy is written.
 #include <algorithm>
+#include <cstdio>
 
 #include "gm_device.h"
 #include "gm_partial.h"
+
+#ifdef GM_P_PROFILE  // measurement builds only: per-section shader clocks of every 64th node
+__device__ unsigned long long g_pprof[16];
+#define PPROF(k)                                      \
+  do {                                                \
+    const uint64_t pnow_ = __builtin_amdgcn_s_memtime(); \
+    pp_[k] += pnow_ - pt_;                            \
+    pt_ = pnow_;                                      \
+  } while (0)
+#else
+#define PPROF(k) \
+  do {           \
+  } while (0)
+#endif
 
 #define P_IDMASK 0x01FFFFFFu  // ids <= 2^25
 #define P_OWN 0x80000000u     // table id-word flag: the id was in the node's own list
@@ -157,6 +172,9 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
   constexpr int KK = BIG ? P_KP : P_KSMALL;           // lists merged at most
   constexpr int DS = ((1 + KK) * P_VMAX + 63) / 64;   // dense entries per lane
   constexpr int NSTEP = (KK + 1) / 2;                 // list-load steps (>= 2 lists per step)
+#ifdef GM_P_PROFILE
+  uint64_t pp_[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, pt_ = __builtin_amdgcn_s_memtime();
+#endif
   uint32_t *tid = (uint32_t *)base;
   uint32_t *thb = tid + H;
   uint32_t *hist = thb + H;
@@ -222,6 +240,7 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
   if (dropping)
     pairv = gm_mix64(s.drop_seed ^ ((uint64_t)(uint32_t)(t - 1) << 48) ^ ((uint64_t)(uint32_t)sg << 24) ^
                      (uint64_t)(uint32_t)i);
+  PPROF(0);
   p_wsync();
   // ---- 2. merge: own entries first (they carry P_OWN), then the delivered lists
   int hslot = -1;
@@ -230,6 +249,7 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
     const uint32_t id = (uint32_t)(own >> 32);
     hslot = p_insert<H>(tid, thb, id, id | P_OWN, (uint32_t)own);
   }
+  PPROF(1);
   p_wsync();
   {
     const uint32_t tfresh = (uint32_t)max(0, 2 * t - 11);  // hb >= 2t-11 <=> (t-1) - (hb+1)/2 < TFAIL
@@ -248,6 +268,7 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
       if (take) (void)p_insert<H>(tid, thb, id, id, (uint32_t)e);
     }
   }
+  PPROF(2);
   p_wsync();
   // ---- 3. self bump (heartbeat++; myPos->setheartbeat(heartbeat++)), then sweep + compaction
   {
@@ -269,6 +290,7 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
       s.hbctr[li] = hbnew + 1;
     }
   }
+  PPROF(3);
   p_wsync();
   uint32_t *evr = s.ev + (size_t)li * 2 * V;
   int m, removed, nrem;
@@ -316,6 +338,7 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
       pos += a;
     }
   }
+  PPROF(4);
   p_wsync();
   // ---- 4. dense entries e = s*64 + lane; eviction to V
   // only the first dm = ceil(m / 64) of the DS per-lane slots hold entries (m is wave-uniform):
@@ -423,6 +446,7 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
       }
     }
   }
+  PPROF(5);
   // ---- 5. compact the kept entries (<= V), rank them by id
   int cnt = 0;
   p_wsync();  // the eviction histogram is dead: it takes the stores of the entries not kept
@@ -470,6 +494,7 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
   const int nj = __builtin_popcountll(jb);
   if (lane < cnt && !(f & 2u)) evr[p_below(jb)] = (P_EV_ADD << 30) | (uint32_t)(x >> 32);
   const int numfailed = removed + __builtin_popcountll(__ballot(lane < cnt && p_aged(t, (uint32_t)x, GM_TFAIL)));
+  PPROF(6);
   // ---- 6. gossip draw over the final list (MP1Node.cpp:449-489)
   const int numpot = cnt - 1 - numfailed;
   const int target = min(GM_FANOUT, numpot);
@@ -555,6 +580,7 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
       if (lane < ng) gl[lane] = (uint32_t)(lane == 0 ? g0 : lane == 1 ? g1 : lane == 2 ? g2 : lane == 3 ? g3 : g4);
     }
   }
+  PPROF(7);
   p_wsync();
   // ---- sends: one parallel round of inbox appends, one lane per target; targets owned by
   // another row shard get one record per (sender, shard): header + this tick's list
@@ -606,6 +632,13 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
   if (s.G > 1 && lane == 0) s.recmask[li] = rmask;
   if (lane < 4) s.rowstat[(size_t)li * 4 + lane] = lane == 0 ? kk : lane == 1 ? cnt : lane == 2 ? numfailed : ng;
   if (lane == 0) s.ev_cnt[li] = nj | (nrem << 16);
+#ifdef GM_P_PROFILE
+  PPROF(8);
+  if (lane == 0 && (li & 63) == 0) {
+    for (int q = 0; q < 9; q++) atomicAdd(&g_pprof[q], (unsigned long long)pp_[q]);
+    atomicAdd(&g_pprof[15], 1ull);
+  }
+#endif
 }
 
 // crashed node: frozen (its list carried to this tick's buffer unchanged), inbox dropped
@@ -653,10 +686,10 @@ __global__ __launch_bounds__(256) void gm_p_tick_big(PState s, int t, const uint
 
 // first 16 S2 outputs of every node for tick t (see gm_mt_first16); resets the big
 // worklist and the outgoing record counts
-__global__ __launch_bounds__(256) void gm_p_mtgen(PState s, int t, uint32_t *mtraw) {
+__global__ __launch_bounds__(256) void gm_p_mtgen(PState s, int t, uint32_t *mtraw, int reset) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r < s.nchunk) s.big_cnt[r] = 0;
-  if (s.send_cnt && r < s.nchunk * s.G) s.send_cnt[r] = 0;
+  if (reset && r < s.nchunk) s.big_cnt[r] = 0;
+  if (reset && s.send_cnt && r < s.nchunk * s.G) s.send_cnt[r] = 0;
   if (r >= s.nloc) return;
   uint32_t out[16];
   gm_mt_first16(gm_rd_seed(s.rd_seed, t, s.n0 + r + 1), out);
@@ -773,9 +806,17 @@ __global__ __launch_bounds__(P_PACK) void gm_p_pack_copy(PState s, int c, int r0
 #define P_BIG_GRID 1024
 
 // S2 precompute for every row + reset of the per-chunk worklists and record counts
-hipError_t gm_launch_partial_mtgen(const PState &s, int t, uint32_t *mtraw, hipStream_t st) {
-  hipLaunchKernelGGL(gm_p_mtgen, dim3((std::max(s.nloc, s.nchunk * s.G) + 255) / 256), dim3(256), 0, st, s, t, mtraw);
+hipError_t gm_launch_partial_mtgen(const PState &s, int t, uint32_t *mtraw, hipStream_t st, bool reset) {
+  hipLaunchKernelGGL(gm_p_mtgen, dim3((std::max(s.nloc, s.nchunk * s.G) + 255) / 256), dim3(256), 0, st, s, t, mtraw,
+                     reset ? 1 : 0);
   return hipGetLastError();
+}
+
+// the per-tick resets gm_p_mtgen does when the S2 outputs were prefetched without them
+hipError_t gm_launch_partial_reset(const PState &s, hipStream_t st) {
+  hipError_t e = hipMemsetAsync(s.big_cnt, 0, sizeof(int32_t) * s.nchunk, st);
+  if (e == hipSuccess && s.send_cnt) e = hipMemsetAsync(s.send_cnt, 0, sizeof(int32_t) * s.nchunk * s.G, st);
+  return e;
 }
 
 // the node ticks of chunk c (rows [nloc*c/K, nloc*(c+1)/K))
@@ -798,7 +839,7 @@ hipError_t gm_launch_partial_chunk(const PState &s, int t, const uint32_t *mtraw
 
 hipError_t gm_launch_partial_tick(const PState &s, int t, uint32_t *mtraw, hipStream_t st, hipEvent_t k0,
                                   hipEvent_t k1) {
-  hipError_t e = gm_launch_partial_mtgen(s, t, mtraw, st);
+  hipError_t e = gm_launch_partial_mtgen(s, t, mtraw, st, true);
   if (e != hipSuccess) return e;
   if (k0) (void)hipEventRecord(k0, st);
   for (int c = 0; c < s.nchunk && e == hipSuccess; c++) e = gm_launch_partial_chunk(s, t, mtraw, c, st);
@@ -817,3 +858,17 @@ hipError_t gm_launch_partial_unpack(const PState &s, int t, int base, int nrecv,
 }
 
 size_t gm_partial_lds_bytes() { return 4 * (size_t)PLds<P_HB>::bytes; }
+
+// measurement builds: the per-section clocks (0 elsewhere)
+void gm_partial_profile_dump() {
+#ifdef GM_P_PROFILE
+  unsigned long long h[16];
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_pprof), sizeof h) == hipSuccess && h[15]) {
+    const char *nm[9] = {"loads", "own-insert", "merge", "self", "sweep", "evict", "rank+store", "draw", "sends"};
+    unsigned long long tot = 0;
+    for (int q = 0; q < 9; q++) tot += h[q];
+    for (int q = 0; q < 9; q++)
+      fprintf(stderr, "pprof %-10s %8.0f clk/node %5.1f%%\n", nm[q], (double)h[q] / h[15], 100.0 * h[q] / tot);
+  }
+#endif
+}
