@@ -358,15 +358,19 @@ static int create_scaled(gm_ctx *c) {
   // converged start (cold or warm, gm_config.init_mode); padding columns absent
   const bool warm = c->cfg.init_mode == 1;
   const int t0 = warm ? c->cfg.init_t0 : 0;
-  // join ramp (init_mode 2): one context; with keyed drops a joiner can miss its own entry
-  // and take updateMyPos's quirk path (MP1Node.cpp:316), handled in gm_s_band
+  // join ramp (init_mode 2); with keyed drops a joiner can miss its own entry and take
+  // updateMyPos's quirk path (MP1Node.cpp:316), handled in gm_s_band within the row's start
+  // group (ids 4g..4g+3): column shards must not split a group
   const bool ramp = c->cfg.init_mode == 2;
   if (c->cfg.init_mode < 0 || c->cfg.init_mode > 2 || (warm && (t0 < 5 || t0 > GM_T_LIMIT / 2))) return GM_EINVAL;
-  if (ramp && s.sharded) return GM_EUNSUPPORTED;
+  if (ramp)
+    for (int g = 1; g < G; g++)
+      if ((int64_t)n * g / G % 4 != 0) return GM_EUNSUPPORTED;
   s.ramp = ramp ? 1 : 0;
   s.intro_until = 0x7FFFFFFF;
   if (ramp) {
     TRY(dalloc(c, &s.mecol, n));
+    HIPCHECK(hipMemset(s.mecol, 0xFF, sizeof(int32_t) * n));  // -1: written by the rank owning the row's column
     TRY(dalloc(c, &s.selfadd, S_SELFADD_CAP));
     TRY(dalloc(c, &s.selfadd_cnt, 1));
     HIPCHECK(hipMemset(s.selfadd_cnt, 0, sizeof(uint32_t)));
@@ -390,7 +394,7 @@ static int create_scaled(gm_ctx *c) {
     TRY(dalloc(c, &s.status, (size_t)n * c->dmax));
     // bounded rounds (tick_sharded): round 0 takes every row's first 16 S2 outputs, round 1
     // the next 64 for up to plist_cap rows left pending -- no host round trip per tick
-    s.plist_cap[1] = std::min(S_PLIST_CAP, std::max(256, n / 16));  // round 1: 64 more outputs
+    s.plist_cap[1] = std::min(S_PLIST_CAP, std::max(std::min(n, 1024), n / 16));  // round 1: 64 more outputs
     s.plist_cap[2] = 256;                                             // round 2: 256 more outputs
     for (int l = 1; l <= 2; l++) {
       TRY(dalloc(c, &s.plist[l], s.plist_cap[l]));
@@ -664,19 +668,24 @@ static int timing_slot(gm_ctx *c, hipEvent_t *k0, hipEvent_t *k1) {
   return GM_OK;
 }
 
+// Join ramp: nodeStart of this tick's starters clears bFailed (MP1Node.cpp:108)
+static int ramp_starters(gm_ctx *c) {
+  if (!c->s.ramp) return GM_OK;
+  const int j0 = 4 * c->t, j1 = std::min(c->n, 4 * c->t + 4);
+  for (int j = j0; j < j1; j++)
+    if (c->failed_h[j]) {
+      c->failed_h[j] = 0;
+      c->fail_t[j] = 0x7FFFFFFF;
+      HIPCHECK(hipMemcpyAsync(c->s.failed + j, c->failed_h.data() + j, sizeof(int32_t), hipMemcpyHostToDevice,
+                              c->stream));
+    }
+  return GM_OK;
+}
+
 static int tick_scaled(gm_ctx *c) {
   if (c->t > GM_T_LIMIT) return GM_ERANGE;
   if (c->s.sharded) return tick_sharded(c);
-  if (c->s.ramp) {  // nodeStart of this tick's starters clears bFailed (MP1Node.cpp:108)
-    const int j0 = 4 * c->t, j1 = std::min(c->n, 4 * c->t + 4);
-    for (int j = j0; j < j1; j++)
-      if (c->failed_h[j]) {
-        c->failed_h[j] = 0;
-        c->fail_t[j] = 0x7FFFFFFF;
-        HIPCHECK(hipMemcpyAsync(c->s.failed + j, c->failed_h.data() + j, sizeof(int32_t), hipMemcpyHostToDevice,
-                                c->stream));
-      }
-  }
+  TRY(ramp_starters(c));
   const int t_send = c->t - 1;
   const bool drop = c->cfg.drop_pct > 0 && t_send >= c->cfg.drop_from && t_send < c->cfg.drop_to;
   hipEvent_t k0 = nullptr, k1 = nullptr;
@@ -1281,6 +1290,7 @@ static int shard_ready(gm_ctx *c) {
 extern "C" int gm_shard_merge(gm_ctx *c) {
   TRY(shard_ready(c));
   TRY(before_tick_events(c));
+  TRY(ramp_starters(c));
   const int t_send = c->t - 1;
   const bool drop = c->cfg.drop_pct > 0 && t_send >= c->cfg.drop_from && t_send < c->cfg.drop_to;
   HIPCHECK(hipMemsetAsync(c->s.xcnt + (size_t)c->s.shard_rank * c->n * 2, 0, sizeof(int32_t) * 2 * (size_t)c->n,

@@ -25,6 +25,9 @@ __host__ __device__ inline int s_hbase(int ramp, int j) { return (ramp && j > 0)
 __host__ __device__ inline bool s_ingroup(int ramp, int intro_until, int r, int t) {
   return !ramp || r == 0 || (t >= s_start(r) + 2 && s_start(r) + 1 <= intro_until);
 }
+// column shards: xcnt's per-(rank, row) present word carries a flag for a self append
+#define S_XC_SELFAPP 0x40000000
+#define S_XC_COUNT 0x3FFFFFFF
 #define S_H(c) ((c) >> 5)
 #define S_AGE(c) ((c) & 31u)
 // payload (sendMemberList's fresh entries, re-based to the receiving tick: h' = h - 2):

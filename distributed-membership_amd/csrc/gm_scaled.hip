@@ -296,8 +296,8 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
       // entry {hb 0, ts t} = stored heartbeat 2t (offset 2(t-1+1)) = h 255 (MP1Node.cpp:226-251)
 #pragma unroll
       for (int q = 0; q < Q; q++) {
-        const int c = s.c0 + colb + q;
-        if (c >= 1 && c < s.n && s_start(c) == t - 1) key5[q >> 1][q & 1] = (uint16_t)(255u << 5);
+        const int c = s.c0 + colb + q;  // a real column of this shard (not row padding)
+        if (c >= 1 && colb + q < s.w && s_start(c) == t - 1) key5[q >> 1][q & 1] = (uint16_t)(255u << 5);
       }
     }
     // merge: re-base the cell to tick t (h -= 2, age += 1; absent stays 0), then max
@@ -334,6 +334,8 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
             const uint32_t slot = atomicAdd(s.selfadd_cnt, 1u);
             if (slot < S_SELFADD_CAP) s.selfadd[slot] = r;
             else atomicOr(s.err, GM_ERR_SELF);
+            // column shards: the other ranks check their (higher) columns in gm_s_draw
+            if (s.sharded) atomicOr((uint32_t *)(s.xcnt + ((size_t)s.shard_rank * s.n + r) * 2), S_XC_SELFAPP);
           }
         }
       }
@@ -826,28 +828,54 @@ __global__ __launch_bounds__(256) void gm_s_draw(SState s, int t, int round, int
   const int G = s.shard_count;
   int32_t *acc = s.acc + (size_t)r * 8;
   if (round == 0) {
+    const bool live = !s.failed[r] && s_ingroup(s.ramp, s.intro_until, r, t);  // else untouched
     if (lane == 0) {  // lists delivered this tick; consumed by gm_s_band, the append target of tick t+2
       const int par = t & 1;
-      s.rowstat[(size_t)r * 4] = s.failed[r] ? 0 : s.inbox_cnt[par][r];
+      s.rowstat[(size_t)r * 4] = live ? s.inbox_cnt[par][r] : 0;
       s.inbox_cnt[par][r] = 0;
     }
     int size = 0, nf = 0;
+    bool selfapp = false;
     for (int g = 0; g < G; g++) {
-      size += s.xcnt[((size_t)g * s.n + r) * 2];
+      const int pr = s.xcnt[((size_t)g * s.n + r) * 2];
+      size += pr & S_XC_COUNT;
+      selfapp |= (pr & S_XC_SELFAPP) != 0;
       nf += s.xcnt[((size_t)g * s.n + r) * 2 + 1];
     }
+    if (selfapp && lane == 0) {
+      // join ramp: row r appended its own entry (updateMyPos found no larger id in its start
+      // group, gm_s_band); the reference appends only if no larger id is present at all --
+      // the shards above the group must hold nothing of the row (present, or removed this tick)
+      for (int g = 0; g < G; g++) {
+        const int c0g = (int)((int64_t)s.n * g / G);
+        if (c0g > (r | 3) && ((s.xcnt[((size_t)g * s.n + r) * 2] & S_XC_COUNT) || s.xcnt[((size_t)g * s.n + r) * 2 + 1]))
+          atomicOr(s.err, GM_ERR_SELF);
+      }
+    }
     const int numpot = size - 1 - nf;
-    const bool live = !s.failed[r];
-    const bool pend = live && numpot > 0;
+    int nj = 0, jn[4] = {0, 0, 0, 0};
+    if (s.ramp && r == 0 && live)  // gossipnodes = newNodes first (MP1Node.cpp:458): this tick's joiners, ascending id
+      for (int c = max(1, 4 * (t - 1)); c < min(s.n, 4 * t); c++) jn[nj++] = c;
+    const bool pend = live && numpot > 0 && nj < min(GM_FANOUT, numpot);
     if (lane == 0) {
-      acc[0] = 0;
+      acc[0] = nj;
+      for (int q = 0; q < 4; q++) acc[1 + q] = jn[q];
       acc[6] = numpot;
       acc[7] = size;
       s.pending[r] = pend;
       int32_t *stat = s.rowstat + (size_t)r * 4;
       stat[1] = live ? size : 0;
       stat[2] = live ? nf : 0;
-      stat[3] = 0;
+      stat[3] = live && !pend ? nj : 0;
+      if (live && !pend && nj) {  // the joiners alone (no draws): enqueue now, like gm_s_accept
+        int32_t *cnt_out = s.inbox_cnt[(t & 1) ^ 1];
+        for (int q = 0; q < nj; q++) {
+          s.targets[(size_t)r * GM_FANOUT + q] = jn[q];
+          const int slot = atomicAdd(&cnt_out[jn[q]], 1);
+          if (slot < S_KMAX) s.inbox[(t & 1) ^ 1][(size_t)jn[q] * S_KMAX + slot] = r;
+          else atomicOr(s.err, GM_ERR_INBOX);
+        }
+      }
     }
     if (!pend) return;
   } else if (!s.pending[r]) {
@@ -855,8 +883,13 @@ __global__ __launch_bounds__(256) void gm_s_draw(SState s, int t, int round, int
   }
   const uint32_t size = (uint32_t)acc[7];
   uint32_t own_lo = 0;
-  for (int g = 0; g < s.shard_rank; g++) own_lo += (uint32_t)s.xcnt[((size_t)g * s.n + r) * 2];
-  const uint32_t own_cnt = (uint32_t)s.xcnt[((size_t)s.shard_rank * s.n + r) * 2];
+  for (int g = 0; g < s.shard_rank; g++) own_lo += (uint32_t)s.xcnt[((size_t)g * s.n + r) * 2] & S_XC_COUNT;
+  const uint32_t own_cnt = (uint32_t)s.xcnt[((size_t)s.shard_rank * s.n + r) * 2] & S_XC_COUNT;
+  // "me" (myPos's id, MP1Node.cpp:459-460,470) is the row's own column, or in the join ramp
+  // the quirk's target column; only the rank owning it knows it (mecol is -1 elsewhere), and
+  // only that rank resolves a draw there: it reports "me" as not fresh, which the acceptance
+  // skips the same way
+  const int me = s.ramp ? s.mecol[r] : r;
   bool have_pre = false;  // this shard's chunk prefix of the row, built on first use
   const uint32_t thr = (0u - size) % size;
   GmLazyMT mt;
@@ -898,7 +931,7 @@ __global__ __launch_bounds__(256) void gm_s_draw(SState s, int t, int round, int
       gm_resolve8<B>(s, r, pre, grp < c8, myix, lane, col, fr);
 #pragma unroll
       for (int i = 0; i < 8; i++)
-        if (i < c8 && lane == d[i]) val = col[i] < 0 ? -1 : (((s.c0 + col[i]) << 1) | fr[i]);
+        if (i < c8 && lane == d[i]) val = col[i] < 0 ? -1 : (((s.c0 + col[i]) << 1) | (fr[i] && s.c0 + col[i] != me));
     }
     if (lane < cnt) st[d0 + lane] = val;
   }
@@ -924,7 +957,7 @@ __global__ __launch_bounds__(256) void gm_s_accept(SState s, int t, int D, int i
   int g[GM_FANOUT];
   for (int q = 0; q < n; q++) g[q] = acc[1 + q];
   const int32_t *st = in_list ? s.statusl[in_list] + (size_t)i * D : s.status + (size_t)r * D;
-  bool done = false;
+  bool done = n >= GM_FANOUT || n >= numpot;
   for (int d = 0; d < D && !done; d++) {
     const int32_t v = st[d];
     if (v == -2) continue;  // output rejected by Lemire: not a draw

@@ -85,3 +85,78 @@ def test_rccl_single_rank_matches_fused_kernel(n, drop, ncrash, rounds, monkeypa
         assert sorted(sh.drain_events()) == sorted(ref.drain_events()), f"events differ at tick {t}"
         assert sh.dump_tables() == ref.dump_tables(), f"tables differ at tick {t}"
     assert sh.tick_stats()["err"] == 0
+
+
+def _crash_seed_with(n, count, want):
+    for seed in range(1, 10000):
+        if want in set(crash_set(n, count, seed).tolist()):
+            return seed
+    raise AssertionError("no seed")
+
+
+@pytest.mark.parametrize("n,world,drop,intro", [(400, 2, 0, False), (600, 3, 30, False), (1024, 4, 10, False),
+                                                (256, 2, 0, True)])
+def test_ramp_shards_match_fused_kernel(n, world, drop, intro):
+    """The join ramp (init_mode 2: JOINREQ / JOINREP / newNodes-first gossip) on G column
+    shards equals the single context tick for tick: tables, node state, events. With keyed
+    drops a joiner that misses its own entry takes updateMyPos's quirk path (MP1Node.cpp:316)
+    on the shard owning its start group, which reports its "me" column to the draw; the
+    introducer's joiners-first targets (MP1Node.cpp:458) are enqueued on every rank."""
+    kw = dict(rd_seed=7, init_mode=2, drop_pct=drop, drop_from=0, drop_to=1 << 20, drop_seed=42)
+    ref = Simulator(n, GM_MODE_SCALED, **kw)
+    shards = [Simulator(n, GM_MODE_SCALED, shard_rank=g, shard_count=world, **kw) for g in range(world)]
+    owners = np.zeros(n, dtype=int)
+    for g, s in enumerate(shards):
+        c0, w = s.shard_layout()
+        owners[c0:c0 + w] = g
+    cnt = max(2, n // 32)
+    crash = crash_set(n, cnt, _crash_seed_with(n, cnt, 0) if intro else 42)
+    crash_tick = n // 8  # mid-ramp: crashed starters revive at their nodeStart
+    for _ in range(n // 4 + 30):
+        t = ref.time
+        ref.tick()
+        loopback_tick(shards)
+        if t == crash_tick:
+            ref.set_failed(crash)
+            for s in shards:
+                s.set_failed(crash)
+        ev = sorted(e for s in shards for e in s.drain_events())
+        assert ev == sorted(ref.drain_events()), f"events differ at tick {t}"
+        if t % 4 == 0:
+            got = merge_dumps([s.dump_tables() for s in shards], owners)
+            assert got == ref.dump_tables(), f"tables differ at tick {t}"
+    assert merge_dumps([s.dump_tables() for s in shards], owners) == ref.dump_tables()
+    for s in shards:
+        assert s.tick_stats()["err"] == 0
+    assert ref.tick_stats()["err"] == 0
+
+
+def test_ramp_shards_need_whole_start_groups():
+    """A column shard boundary inside a start group (ids 4g..4g+3) is refused."""
+    from membership.abi import GmError
+    with pytest.raises(GmError):
+        Simulator(602, GM_MODE_SCALED, rd_seed=7, init_mode=2, shard_rank=0, shard_count=3)
+
+
+def test_rccl_single_rank_ramp_matches_fused_kernel(monkeypatch):
+    """The join ramp through gm_tick's RCCL-driven sharded tick (one forced shard):
+    bounded draw rounds, joiners-first introducer targets, keyed drops."""
+    from membership.abi import comm_unique_id
+    n = 300
+    kw = dict(rd_seed=7, init_mode=2, drop_pct=20, drop_from=0, drop_to=1 << 20, drop_seed=42)
+    ref = Simulator(n, GM_MODE_SCALED, **kw)
+    monkeypatch.setenv("GM_FORCE_SHARD", "1")
+    sh = Simulator(n, GM_MODE_SCALED, shard_rank=0, shard_count=1, **kw)
+    monkeypatch.delenv("GM_FORCE_SHARD")
+    sh.comm_init(comm_unique_id(), 1, 0)
+    crash = crash_set(n, 9, 42)
+    for _ in range(n // 4 + 30):
+        t = ref.time
+        ref.tick()
+        sh.tick()
+        if t == 40:
+            ref.set_failed(crash)
+            sh.set_failed(crash)
+        assert sorted(sh.drain_events()) == sorted(ref.drain_events()), f"events differ at tick {t}"
+        assert sh.dump_tables() == ref.dump_tables(), f"tables differ at tick {t}"
+    assert sh.tick_stats()["err"] == 0
