@@ -28,7 +28,7 @@ PT="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
 
 run_step() {
   case "$1" in
-    tests) timeout -k 10 900 $PT ${TESTS:-tests} -m gpu --durations 15 > $O/gpu_tests.txt 2>&1 ;;
+    tests) timeout -k 10 1400 $PT ${TESTS:-tests} -m gpu --durations 15 > $O/gpu_tests.txt 2>&1 ;;
     smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 ;;
     sa) timeout -k 10 300 python -u bench.py ${BENCH_ARGS:-} > $O/bench_sa.json 2> $O/bench_sa.err ;;
     sc) timeout -k 10 400 python -u bench.py --scenario S-C ${BENCH_ARGS:-} > $O/bench_sc.json 2> $O/bench_sc.err ;;
