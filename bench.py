@@ -199,6 +199,7 @@ def main():
         "metric": "simulated node-ticks/sec + achieved HBM GB/s at N=65,536 full-membership",
         "value": value,
         "unit": "node-ticks/s",
+        "value_note": "all N simulated nodes per tick, the 1% crashed (frozen) ones included",
         "n_gpus": world,
         "steps": a.steps,
         "warmup": a.warmup,
@@ -321,6 +322,8 @@ def main_partial(a):
         "metric": "simulated node-ticks/sec (S-C partial view)",
         "value": n * a.steps / elapsed,
         "unit": "node-ticks/s",
+        "value_note": "all N simulated nodes per tick, the 1% crashed (frozen) ones included; "
+                      "live-only rate = value * live / n",
         "n_gpus": world,
         "steps": a.steps,
         "warmup": a.warmup,
