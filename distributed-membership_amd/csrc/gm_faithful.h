@@ -51,7 +51,7 @@ struct FState {
   int32_t *spre;               // [draw_cap + 1] exclusive prefix count of kept sends
   uint32_t *s1mat;             // [64][31][32] P_q = R^(q+1), R = one 31-draw round of the S1 register
   uint32_t *s1vb;              // [draw_cap / 1984 + 2][32] S1 register at every 64th round
-  int32_t *sent, *recv;        // [(F_MAX_NODES+1)][tmax]
+  int32_t *sent, *recv;        // [n + 1][tmax] (row = node id)
   FEvent *ev;
   unsigned long long *ev_count;
   int ev_cap;

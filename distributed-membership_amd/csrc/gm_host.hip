@@ -7,6 +7,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -187,28 +188,20 @@ static void s1_seed(uint32_t seed, int32_t st[33]) {
 // P_q = R^(q+1), q = 0..63, rows padded to 32 words: R is one 31-draw round of the S1
 // register in fptr-rotated order, x[j] += x[(j + 28) % 31] for j ascending (gm_f_s1expand)
 static std::vector<uint32_t> s1_round_powers() {
-  uint32_t R[31][31], cur[31][31], nxt[31][31];
-  for (int i = 0; i < 31; i++) {  // column i = the round applied to basis vector e_i
+  // column i of P_q = the round applied q+1 times to basis vector e_i (31 adds per round)
+  std::vector<uint32_t> P((size_t)64 * 31 * 32, 0u);
+  for (int i = 0; i < 31; i++) {
     uint32_t x[31] = {0};
     x[i] = 1;
-    for (int j = 0; j < 31; j++) x[j] += x[(j + 28) % 31];
-    for (int k = 0; k < 31; k++) R[k][i] = x[k];
-  }
-  std::vector<uint32_t> P((size_t)64 * 31 * 32, 0u);
-  memcpy(cur, R, sizeof R);
-  for (int q = 0; q < 64; q++) {
-    for (int k = 0; k < 31; k++)
-      for (int j = 0; j < 31; j++) P[((size_t)q * 31 + k) * 32 + j] = cur[k][j];
-    for (int k = 0; k < 31; k++)
-      for (int j = 0; j < 31; j++) {
-        uint32_t a = 0;
-        for (int l = 0; l < 31; l++) a += R[k][l] * cur[l][j];
-        nxt[k][j] = a;
-      }
-    memcpy(cur, nxt, sizeof cur);
+    for (int q = 0; q < 64; q++) {
+      for (int j = 0; j < 31; j++) x[j] += x[(j + 28) % 31];
+      for (int k = 0; k < 31; k++) P[((size_t)q * 31 + k) * 32 + i] = x[k];
+    }
   }
   return P;
 }
+
+static void lap(const char *what);
 
 static int create_faithful(gm_ctx *c) {
   const int n = c->n;
@@ -254,8 +247,8 @@ static int create_faithful(gm_ctx *c) {
   TRY(dalloc(c, &f.qidx, F_ENBUFFSIZE));
   TRY(dalloc(c, &f.s1mat, (size_t)64 * 31 * 32));
   TRY(dalloc(c, &f.s1vb, (size_t)(f.draw_cap / 1984 + 2) * 32));
-  TRY(dalloc(c, &f.sent, (size_t)(F_MAX_NODES + 1) * f.tmax));
-  TRY(dalloc(c, &f.recv, (size_t)(F_MAX_NODES + 1) * f.tmax));
+  TRY(dalloc(c, &f.sent, (size_t)(n + 1) * f.tmax));  // rows 1..n: sent_msgs[id][time]
+  TRY(dalloc(c, &f.recv, (size_t)(n + 1) * f.tmax));
   // one block = the tick's mailbox: event count, error flags, then the events, so that one
   // small copy per tick brings back all three (GM_F_MAILBOX events; more: a second copy)
   uint8_t *mb = nullptr;
@@ -263,7 +256,9 @@ static int create_faithful(gm_ctx *c) {
   f.ev_count = (unsigned long long *)mb;
   f.err = (uint32_t *)(mb + 8);
   f.ev = (FEvent *)(mb + 16);
+  lap("faithful allocations");
   if (hipHostMalloc(&c->f_mail, 16 + sizeof(FEvent) * GM_F_MAILBOX, hipHostMallocDefault) != hipSuccess) return GM_ENOMEM;
+  lap("pinned mailbox");
   HIPCHECK(hipMemset(f.table, 0xFF, sizeof(uint32_t) * (size_t)n * f.np));
   std::vector<int32_t> start(n);
   for (int i = 0; i < n; i++) start[i] = (int)(0.25 * i);  // (int)(STEP_RATE*i), Application.cpp:143
@@ -271,17 +266,20 @@ static int create_faithful(gm_ctx *c) {
   for (int32_t *p : {f.failed, f.inited, f.ingroup, f.hbctr, f.started_now, f.q_off, f.q_cnt,
                      f.scount, f.jcnt, f.gcnt, f.fcnt})
     HIPCHECK(hipMemset(p, 0, sizeof(int32_t) * (size_t)n));
-  HIPCHECK(hipMemset(f.sent, 0, sizeof(int32_t) * (size_t)(F_MAX_NODES + 1) * f.tmax));
-  HIPCHECK(hipMemset(f.recv, 0, sizeof(int32_t) * (size_t)(F_MAX_NODES + 1) * f.tmax));
+  HIPCHECK(hipMemset(f.sent, 0, sizeof(int32_t) * (size_t)(n + 1) * f.tmax));
+  HIPCHECK(hipMemset(f.recv, 0, sizeof(int32_t) * (size_t)(n + 1) * f.tmax));
   HIPCHECK(hipMemset(f.bufsize, 0, sizeof(int32_t)));
   HIPCHECK(hipMemset(f.ev_count, 0, sizeof(unsigned long long)));
   HIPCHECK(hipMemset(f.err, 0, sizeof(uint32_t)));
   int32_t st[33];
   s1_seed(c->cfg.time_seed, st);  // srand(time(NULL)) at Application.cpp:50 and :96
   HIPCHECK(hipMemcpy(f.s1, st, sizeof st, hipMemcpyHostToDevice));
+  lap("faithful memsets");
   const std::vector<uint32_t> pm = s1_round_powers();
   HIPCHECK(hipMemcpy(f.s1mat, pm.data(), sizeof(uint32_t) * pm.size(), hipMemcpyHostToDevice));
+  lap("S1 powers");
   HIPCHECK(hipFuncSetAttribute((const void *)gm_f_recv, hipFuncAttributeMaxDynamicSharedMemorySize, F_RECV_LDS));
+  lap("kernel attributes");
   const int nw = f.np / 64;
   c->f_smem = (size_t)f.np * 8 + (size_t)nw * 8 * 3 + (size_t)nw * 4 + 624 * 4 + 48 * 4;
   return GM_OK;
@@ -494,6 +492,15 @@ static int create_partial(gm_ctx *c) {
   return GM_OK;
 }
 
+// diagnostics (GM_CREATE_TIMING): where context creation time goes
+static std::chrono::steady_clock::time_point g_ctime;
+static void lap(const char *what) {
+  if (!getenv("GM_CREATE_TIMING")) return;
+  const auto t1 = std::chrono::steady_clock::now();
+  fprintf(stderr, "[gm] create: %-24s %7.2f ms\n", what, std::chrono::duration<double, std::milli>(t1 - g_ctime).count());
+  g_ctime = t1;
+}
+
 extern "C" int gm_create(const gm_config *cfg, gm_ctx **out) {
   if (!cfg || !out) return GM_EINVAL;
   *out = nullptr;
@@ -507,15 +514,22 @@ extern "C" int gm_create(const gm_config *cfg, gm_ctx **out) {
   c->failed_h.assign(cfg->n, 0);
   c->fail_t.assign(cfg->n, 0x7FFFFFFF);
   int rc = GM_OK;
-  if (hipSetDevice(cfg->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+  g_ctime = std::chrono::steady_clock::now();
+  if (hipSetDevice(cfg->device) != hipSuccess) rc = GM_EDEVICE;
+  lap("hipSetDevice");
+  if (rc == GM_OK && hipFree(nullptr) != hipSuccess) rc = GM_EDEVICE;  // runtime + device init
+  lap("runtime init");
+  if (rc != GM_OK || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&c->e0) != hipSuccess || hipEventCreate(&c->e1) != hipSuccess ||
       hipEventCreate(&c->k0) != hipSuccess || hipEventCreate(&c->k1) != hipSuccess) {
     snprintf(g_errbuf, sizeof g_errbuf, "HIP device %d unavailable", cfg->device);
     rc = GM_EDEVICE;
   }
+  lap("stream + events");
   if (rc == GM_OK)
     rc = cfg->mode == GM_MODE_FAITHFUL ? create_faithful(c) : cfg->mode == GM_MODE_SCALED ? create_scaled(c)
                                                                                         : create_partial(c);
+  lap("mode state");
   if (rc != GM_OK) {
     gm_destroy(c);
     return rc;
@@ -989,7 +1003,7 @@ extern "C" int gm_msgcount(gm_ctx *c, int32_t t, int32_t *sent, int32_t *recv) {
   if (t > c->f.tmax) return GM_EINVAL;
   TRY(f_settle(c));
   HIPCHECK(hipStreamSynchronize(c->stream));
-  std::vector<int32_t> hs((size_t)(F_MAX_NODES + 1) * c->f.tmax), hr(hs.size());
+  std::vector<int32_t> hs((size_t)(c->n + 1) * c->f.tmax), hr(hs.size());
   HIPCHECK(hipMemcpy(hs.data(), c->f.sent, sizeof(int32_t) * hs.size(), hipMemcpyDeviceToHost));
   HIPCHECK(hipMemcpy(hr.data(), c->f.recv, sizeof(int32_t) * hr.size(), hipMemcpyDeviceToHost));
   for (int i = 0; i < c->n; i++)

@@ -173,7 +173,7 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
   constexpr int DS = ((1 + KK) * P_VMAX + 63) / 64;   // dense entries per lane
   constexpr int NSTEP = (KK + 1) / 2;                 // list-load steps (>= 2 lists per step)
 #ifdef GM_P_PROFILE
-  uint64_t pp_[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, pt_ = __builtin_amdgcn_s_memtime();
+  uint64_t pp_[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, pt_ = __builtin_amdgcn_s_memtime();
 #endif
   uint32_t *tid = (uint32_t *)base;
   uint32_t *thb = tid + H;
@@ -388,6 +388,11 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
       keep |= (v & (uint32_t)(((dw[q] & P_SELF) != 0) | (d < dcut))) << q;
       bucket |= (v & (uint32_t)(!(dw[q] & P_SELF) && d == dcut)) << q;
     }
+#ifdef GM_P_PROFILE
+    pp_[10] += 1;  // evictions
+    pp_[11] += needb != bsz;  // key radix path
+    pp_[13] += bsz;
+#endif
     if (needb == bsz) {
       keep |= bucket;
     } else {
@@ -426,6 +431,9 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
       if (needc == bsz2) {
         keep |= cand;
       } else {
+#ifdef GM_P_PROFILE
+        pp_[12] += needc;  // min-selection rounds
+#endif
         for (; needc > 0; needc--) {  // take the smallest remaining candidate key (keys are distinct)
           uint64_t mn = ~0ull;
 #pragma unroll
@@ -635,7 +643,8 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
 #ifdef GM_P_PROFILE
   PPROF(8);
   if (lane == 0 && (li & 63) == 0) {
-    for (int q = 0; q < 9; q++) atomicAdd(&g_pprof[q], (unsigned long long)pp_[q]);
+    pp_[14] = (uint64_t)m;
+    for (int q = 0; q < 15; q++) atomicAdd(&g_pprof[q], (unsigned long long)pp_[q]);
     atomicAdd(&g_pprof[15], 1ull);
   }
 #endif
@@ -869,6 +878,8 @@ void gm_partial_profile_dump() {
     for (int q = 0; q < 9; q++) tot += h[q];
     for (int q = 0; q < 9; q++)
       fprintf(stderr, "pprof %-10s %8.0f clk/node %5.1f%%\n", nm[q], (double)h[q] / h[15], 100.0 * h[q] / tot);
+    fprintf(stderr, "pprof per node: evictions %.3f, key-radix path %.3f, min-selection rounds %.3f, cut bucket %.1f, union m %.1f\n",
+            (double)h[10] / h[15], (double)h[11] / h[15], (double)h[12] / h[15], (double)h[13] / h[15], (double)h[14] / h[15]);
   }
 #endif
 }
