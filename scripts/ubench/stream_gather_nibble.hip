@@ -17,13 +17,20 @@ __device__ __forceinline__ uint32_t mix(uint32_t x) {
 }
 
 // table [nb][n][B] u16; pay [nb][n][2][B/2] bytes; inbox [n][8] i32
-template <int B, int K, int DEP>
+// XCD = 1: workgroups are dispatched round-robin over the 8 XCDs, so workgroup w runs on
+// XCD w % 8; map it to band 8*(j / BPB) + w % 8 (j = w / 8, BPB workgroups per band): every
+// XCD sweeps its own bands, and a band's payload slab is gathered through one L2 only
+template <int B, int K, int DEP, int XCD = 0>
 __global__ __launch_bounds__(256) void kband(uint16_t *table, uint8_t *pay, const int *inbox, int n, int nb,
                                              uint32_t *sink) {
   constexpr int LPR = B / 16, RPW = 64 / LPR;
   const int lane = threadIdx.x & 63, sub = lane / LPR, li = lane % LPR;
   const int U = n / RPW;
-  const int u = blockIdx.x * 4 + (threadIdx.x >> 6);
+  int u = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (XCD) {
+    const int bpb = U / 4, w = blockIdx.x, j = w >> 3;
+    u = (8 * (j / bpb) + (w & 7)) * U + (j % bpb) * 4 + (threadIdx.x >> 6);
+  }
   if (u >= U * nb) return;
   const int band = u / U, r = (u - band * U) * RPW + sub;
   const size_t slab = (size_t)band * n;
@@ -55,16 +62,16 @@ __global__ __launch_bounds__(256) void kband(uint16_t *table, uint8_t *pay, cons
   if (acc.x == 0x7b && r == 3) sink[0] = 1;
 }
 
-template <int B, int K, int DEP>
+template <int B, int K, int DEP, int XCD = 0>
 float run(uint16_t *table, uint8_t *pay, const int *inbox, int n, int nb, uint32_t *sink, int reps) {
   constexpr int RPW = 64 / (B / 16);
   const int grid = ((n / RPW) * nb + 3) / 4;
   hipEvent_t e0, e1;
   hipEventCreate(&e0); hipEventCreate(&e1);
-  hipLaunchKernelGGL((kband<B, K, DEP>), dim3(grid), dim3(256), 0, 0, table, pay, inbox, n, nb, sink);
+  hipLaunchKernelGGL((kband<B, K, DEP, XCD>), dim3(grid), dim3(256), 0, 0, table, pay, inbox, n, nb, sink);
   hipEventRecord(e0);
   for (int i = 0; i < reps; i++)
-    hipLaunchKernelGGL((kband<B, K, DEP>), dim3(grid), dim3(256), 0, 0, table, pay, inbox, n, nb, sink);
+    hipLaunchKernelGGL((kband<B, K, DEP, XCD>), dim3(grid), dim3(256), 0, 0, table, pay, inbox, n, nb, sink);
   hipEventRecord(e1);
   hipEventSynchronize(e1);
   float ms; hipEventElapsedTime(&ms, e0, e1);
@@ -92,10 +99,9 @@ int main() {
     fflush(stdout);
   };
 #define RUN(B, K, D) rep(D ? "inbox" : "hash", B, K, run<B, K, D>(table, pay, inbox, n, wp / B, sink, 3))
-  RUN(512, 0, 0); RUN(256, 0, 0);
-  RUN(512, 5, 0); RUN(256, 5, 0); RUN(128, 5, 0);
-  RUN(512, 5, 1); RUN(256, 5, 1); RUN(128, 5, 1);
-  RUN(512, 8, 1);
-  RUN(1024, 0, 0); RUN(1024, 5, 0); RUN(1024, 5, 1);
+#define RUNX(B, K, D) rep(D ? "inbox-xcd" : "hash-xcd", B, K, run<B, K, D, 1>(table, pay, inbox, n, wp / B, sink, 3))
+  RUN(1024, 0, 0); RUN(1024, 5, 1); RUN(512, 5, 1); RUN(256, 5, 1); RUN(128, 5, 1); RUN(64, 5, 1);
+  RUNX(1024, 5, 1); RUNX(512, 5, 1); RUNX(256, 5, 1); RUNX(128, 5, 1); RUNX(64, 5, 1);
+  RUN(128, 0, 0); RUN(64, 0, 0);
   return 0;
 }
