@@ -33,7 +33,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "distributed-membership_amd"))
 
 PEAK_HBM_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
-LAYOUT_SA = "nibble-band"  # profiles/traffic_n65536.json must describe this payload layout
+LAYOUT_SA = "byte-band"  # profiles/traffic_n65536.json must describe this payload layout
 
 
 class Roctx:
@@ -171,18 +171,19 @@ def main():
     n_live, m_lists = st["live"], st["lists"]
     W = sim.shard_layout()[1] if world > 1 else n  # this rank's subject columns
     # algorithmic bytes of one tick in this layout: per live row and
-    # column 2 B cell read + 2 B cell write + 0.5 B payload write, plus 0.5 B per
+    # column 1 B cell read + 1 B cell write + 0.5 B payload write, plus 0.5 B per
     # delivered gossip list (payload read) -- the survey's formulation (SURVEY.md §8(d):
     # read and write the receiver's row once, read each delivered sender row once per
-    # delivery) in this build's 16-bit cell / 4-bit payload units
-    b_alg = (9 * n_live + m_lists) * W // 2
+    # delivery) in this build's byte cell / 4-bit payload units (escaped cells' wide
+    # plane traffic is not counted: it is the layout's overhead, seen by PMC traffic)
+    b_alg = (5 * n_live + m_lists) * W // 2
     # the survey's int32 (hb, ts) formulation of the same work
     b_survey = 16 * n_live * W + 8 * m_lists * W
     achieved = b_alg / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else None
     # DRAM bytes the layout cannot avoid: the cell read + write and the payload write per
     # live cell, plus ONE read of each sender's payload (its ~5 re-reads are served by the
     # Infinity Cache while the band is in flight; FETCH_SIZE counts those hits too)
-    dram_est = 5 * n_live * W
+    dram_est = 3 * n_live * W
     frac_dram = (dram_est / (kernel_ms * 1e-3) / 1e9 / PEAK_HBM_GBPS) if kernel_ms > 0 else None
     traffic, traffic_src = None, None
     tpath_ok = world == 1
@@ -207,7 +208,7 @@ def main():
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        "dtype": "u16 cells / 4-bit payload (integer)",
+        "dtype": "u8 cells (u16 escape plane) / 4-bit payload (integer)",
         "data": "synthetic (converged full-membership table, seeded crash set)",
         "config": {"workload": "S-A: SCALED full membership, 1% crash at tick 10, fanout 5, TFAIL 5, TREMOVE 20"
                    + (f", DIAGNOSTIC keyed {a.drop_pct}% per-entry drops" if a.drop_pct else ""),

@@ -331,7 +331,8 @@ static int create_scaled(gm_ctx *c) {
   s.rd_seed = c->cfg.rd_seed;
   s.drop_seed = c->cfg.drop_seed;
   const size_t cells = (size_t)n * s.wp;
-  TRY(dalloc(c, &s.table, cells));
+  TRY(dalloc(c, &s.table, cells));   // stored cell bytes
+  TRY(dalloc(c, &s.twide, cells));   // 16-bit cells of the escaped bytes
   c->nt = !(getenv("GM_NT") && !atoi(getenv("GM_NT")));  // non-temporal table streams, default on
   s.pipe_waves = getenv("GM_BAND_PIPE") ? std::max(0, atoi(getenv("GM_BAND_PIPE"))) : 0;
   c->shard_sync = getenv("GM_SHARD_SYNC") ? (atoi(getenv("GM_SHARD_SYNC")) ? 1 : 0) : -1;
@@ -1049,16 +1050,19 @@ static int read_table_row(gm_ctx *c, int r, std::vector<int32_t> &hb, std::vecto
   }
   const SState &s = c->s;  // band-tiled: one B-cell piece of the row per band slab
   w = s.w;  // this context's columns
-  std::vector<uint16_t> row(s.wp);
+  std::vector<uint8_t> row(s.wp);
+  std::vector<uint16_t> wrow(s.wp);
   int32_t wt = 0;
-  const size_t piece = sizeof(uint16_t) * s.band;
+  const size_t piece = s.band;  // bytes of one (band, row) piece of the stored cells
   HIPCHECK(hipMemcpy2D(row.data(), piece, s.table + (size_t)r * s.band, piece * s.n, piece, s.nb,
+                       hipMemcpyDeviceToHost));
+  HIPCHECK(hipMemcpy2D(wrow.data(), 2 * piece, s.twide + (size_t)r * s.band, 2 * piece * s.n, 2 * piece, s.nb,
                        hipMemcpyDeviceToHost));
   HIPCHECK(hipMemcpy(&wt, s.wtick + r, sizeof wt, hipMemcpyDeviceToHost));
   hb.resize(w);
   ts.resize(w);
   for (int j = 0; j < w; j++) {  // cells are relative to the row's last written tick
-    const uint32_t e = row[j];
+    const uint32_t e = row[j] == S_B_ESC ? (uint32_t)wrow[j] : s_widen(row[j]);
     hb[j] = e == 0 ? -1 : 2 * wt - 255 + (int32_t)S_H(e) - s_hbase(s.ramp, s.c0 + j);
     ts[j] = e == 0 ? -1 : wt - (int32_t)S_AGE(e);
   }

@@ -20,6 +20,24 @@
 // at tick t is 2t-1 (h = 254); h falls by 2 per tick of heartbeat lag, and a present
 // entry lagging more than ~126 ticks sets GM_ERR_LAG instead of wrapping.
 #define S_CELL(h, age) (((h) << 5) | (age))
+// Stored table cell (round 2): ONE BYTE per (observer, subject). The 16-bit cell above is
+// the working format in registers; in HBM a cell is
+//   0            absent
+//   S_B_ESC (1)  escaped: the 16-bit cell is in the wide table plane (same band layout)
+//   h4 << 4 | a  h = 224 + 2 h4 (h4 in [1, 15]: even h in [226, 254], heartbeat lag <= 14
+//                ticks), age a <= 15 -- every live entry of a warm, steady cluster.
+// Cells outside that range (odd h of cold-start / JOINREQ entries, lag > 14 or age > 15,
+// e.g. a crashed node's entries in the ticks before TREMOVE) escape to the wide plane,
+// which is read and written only where a byte says so.
+#define S_B_ESC 1u
+__host__ __device__ inline uint32_t s_widen(uint32_t b) {  // byte -> 16-bit cell (S_B_ESC: look in the wide plane)
+  return b == 0 ? 0u : (7168u + ((b & 0xF0u) << 2) + (b & 0x0Fu));
+}
+__host__ __device__ inline uint32_t s_narrow(uint32_t c) {  // 16-bit cell -> byte (S_B_ESC if not representable)
+  if (c == 0) return 0u;
+  const uint32_t h = c >> 5, a = c & 31u;
+  return (h >= 226 && !(h & 1) && a <= 15) ? (((h - 224) >> 1) << 4) | a : S_B_ESC;
+}
 __host__ __device__ inline int s_start(int j) { return j >> 2; }  // (int)(0.25 * j) for j >= 0
 __host__ __device__ inline int s_hbase(int ramp, int j) { return (ramp && j > 0) ? 2 * (s_start(j) + 1) : 0; }
 __host__ __device__ inline bool s_ingroup(int ramp, int intro_until, int r, int t) {
@@ -60,7 +78,8 @@ struct SState {
   uint64_t rd_seed, drop_seed;
   // Band-tiled layout: cell (r, c) of band b = c / band lives at ((b * n + r) * band + c % band),
   // so one band of all rows is one contiguous slab (the unit gm_s_band sweeps).
-  uint16_t *table;         // [nb][n][band] S_CELL
+  uint8_t *table;          // [nb][n][band] stored cell bytes (s_narrow of S_CELL)
+  uint16_t *twide;         // [nb][n][band] S_CELL of the escaped cells (valid only where the byte is S_B_ESC)
   uint8_t *msg;            // [nb][n][2][band/2] gossip payload nibbles, both tick parities of a (band, row) adjacent
   uint8_t *wide;           // [nb][n][2][band] escaped payload bytes (written / read only where the nibble is 15)
   int32_t *wtick;          // [n] tick each row's cells are relative to (last written)

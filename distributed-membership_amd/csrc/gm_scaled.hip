@@ -114,6 +114,16 @@ __device__ __forceinline__ u16x2 pmin1(u16x2 a) {
   return pk(r);
 }
 
+// stored cell bytes 0,1 (hi = 0) or 2,3 (hi = 1) of a dword, zero-extended into the two u16 halves
+__device__ __forceinline__ uint32_t byte_pair(uint32_t w, int hi) {
+  return __builtin_amdgcn_perm(0u, w, hi ? 0x0c030c02u : 0x0c010c00u);
+}
+// s_widen of two stored bytes (nz = min(x, 1)); an escape byte gives garbage, replaced by its wide cell
+__device__ __forceinline__ u16x2 widen2(u16x2 x, u16x2 nz) {
+  const uint32_t xv = unpk(x);
+  return nz * (u16x2)(7168) + pk((xv & 0x000F000Fu) | ((xv << 2) & 0x03C003C0u));
+}
+
 // Payload nibbles (gm_scaled.h S_NIB_*): dword w of a lane's 8-byte slice holds cells
 // 8w..8w+7; cell 8w+2k sits in nibble 3-k of the low u16, cell 8w+2k+1 in nibble 3-k
 // of the high u16. So v_pk_max_u16 of the dword shifted left by 4k leaves, in the top
@@ -148,27 +158,37 @@ template <int B>
 struct UnitIn {
   int band, r, k;  // k: lists delivered to this lane's row, -1 = not merged (crashed / absent / not in the group)
   int snd[S_SB];
-  u32x4 ta, tb;    // the row's 16 cells of this lane (as loaded)
+  u32x4 ta;        // the row's 16 cell bytes of this lane (as loaded)
+  bool pre;        // the wide cells below were prefetched (last tick this lane stored escapes)
+  u32x4 wa, wb;    // the lane's 16 wide cells (valid where its bytes are S_B_ESC)
 };
 
 template <int B>
-__device__ __forceinline__ void unit_load(const SState &s, int t, int u, UnitIn<B> &in) {
+__device__ __forceinline__ void unit_load(const SState &s, int t, int band, int ub, UnitIn<B> &in) {
   constexpr int LPR = B / S_COLS_PER_LANE, RPW = 64 / LPR, Q = S_COLS_PER_LANE;
   const int lane = threadIdx.x & 63;
   const int sub = lane / LPR, li = lane % LPR;
-  const int U = (s.n + RPW - 1) / RPW;  // units per band
-  in.band = u / U;
-  in.r = (u - in.band * U) * RPW + sub;
+  in.band = band;
+  in.r = ub * RPW + sub;
   const size_t slab = (size_t)in.band * s.n;
-  const __amdgpu_buffer_rsrc_t trs = gm_rsrc(s.table + slab * B, (uint32_t)(s.n * B * 2));
-  const uint32_t toff = (uint32_t)(in.r * B + li * Q) * 2;  // r >= n: out of range -> zeros, dropped
+  const __amdgpu_buffer_rsrc_t trs = gm_rsrc(s.table + slab * B, (uint32_t)(s.n * B));
+  const uint32_t toff = (uint32_t)(in.r * B + li * Q);  // r >= n: out of range -> zeros, dropped
   const RowMeta<B> meta = row_meta<B>(s, in.r, t & 1, t);
 #pragma unroll
   for (int j = 0; j < S_SB; j++) in.snd[j] = meta.snd[j];
   in.k = meta.k;
   // the table slice is independent of the metadata: both in flight together
   in.ta = __builtin_amdgcn_raw_buffer_load_b128(trs, toff, 0, GM_AUX_NT);
-  in.tb = __builtin_amdgcn_raw_buffer_load_b128(trs, toff + 16, 0, GM_AUX_NT);
+  // lanes that stored escaped cells last tick (the (band, row) record's escape mask, written by
+  // unit_finish) fetch their wide cells now, with the table slice, instead of one round trip later
+  const uint32_t hint = in.r < s.n ? s.brec[slab + in.r].w : 0u;
+  in.pre = (hint >> (LPR == 64 ? li >> 1 : li)) & 1u;
+  in.wa = in.wb = (u32x4){0u, 0u, 0u, 0u};
+  if (in.pre) {
+    const __amdgpu_buffer_rsrc_t wrs = gm_rsrc(s.twide + slab * B, (uint32_t)(s.n * B * 2));
+    in.wa = __builtin_amdgcn_raw_buffer_load_b128(wrs, 2 * toff, 0, 0);
+    in.wb = __builtin_amdgcn_raw_buffer_load_b128(wrs, 2 * toff + 16, 0, 0);
+  }
 }
 
 // every payload slice at once; slots j >= k read out of range (zeros = "not sent")
@@ -196,10 +216,12 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
   const int band = in.band, r = in.r;
   const int colb = band * B + li * Q;  // shard-local column of this lane's first cell
   const size_t slab = (size_t)band * s.n;
-  // this band's slabs: table [n][B] cells, payload nibbles [n][2][B/2] bytes (32-bit offsets)
-  const __amdgpu_buffer_rsrc_t trs = gm_rsrc(s.table + slab * B, (uint32_t)(s.n * B * 2));
+  // this band's slabs: table [n][B] cell bytes, wide table [n][B] 16-bit cells (escaped cells
+  // only), payload nibbles [n][2][B/2] bytes (32-bit offsets)
+  const __amdgpu_buffer_rsrc_t trs = gm_rsrc(s.table + slab * B, (uint32_t)(s.n * B));
+  const __amdgpu_buffer_rsrc_t wrs = gm_rsrc(s.twide + slab * B, (uint32_t)(s.n * B * 2));
   const __amdgpu_buffer_rsrc_t prs = gm_rsrc(s.msg + slab * B, (uint32_t)(s.n * B));
-  const uint32_t toff = (uint32_t)(r * B + li * Q) * 2;
+  const uint32_t toff = (uint32_t)(r * B + li * Q);  // bytes; the wide cells at 2 * toff
   const uint32_t poff = (uint32_t)((par ^ 1) * (B / 2) + li * 8);  // + sender * B
   // escape plane of this band: [n][2][B] bytes, cell (sender, parity, column)
   const uint8_t *wsrc = s.wide + slab * 2 * B + (size_t)(par ^ 1) * B + li * Q;
@@ -209,7 +231,7 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
     k = S_KMAX;
   }
   const bool live = k >= 0;
-  const u32x4 ta = in.ta, tb = in.tb;
+  const u32x4 ta = in.ta;
   struct {
     int snd[S_SB];
   } meta;
@@ -224,7 +246,7 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
   }
   int npres = 0, nfail = 0, nev = 0;
   uint32_t evk = 0;  // 2 bits per cell: event kind
-  bool esc_out = false;  // this lane sends a value only the wide plane can carry
+  bool esc_st = false;  // this lane stored escaped cells (announced in the (band, row) record)
   if (live) {
     // merge key per cell = the largest delivered payload h' (0 = nothing delivered), as
     // key5 = h' << 5 (the cell with age 0) in the u16 halves of each table word
@@ -300,13 +322,44 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
         if (c >= 1 && colb + q < s.w && s_start(c) == t - 1) key5[q >> 1][q & 1] = (uint16_t)(255u << 5);
       }
     }
+    // widen the stored bytes to 16-bit cells; a lane holding escaped cells (rare: a crashed
+    // node's entries before their removal, cold-start / JOINREQ entries) takes those from
+    // the wide plane. npb: cells present as loaded (join detection below).
+    const uint32_t tb4[4] = {ta.x, ta.y, ta.z, ta.w};
+    uint32_t esc_in = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {  // any byte == S_B_ESC: zero-byte test of w ^ 0x01010101
+      const uint32_t z = tb4[q] ^ 0x01010101u;
+      esc_in |= (z - 0x01010101u) & ~z & 0x80808080u;
+    }
+    u16x2 tw[8], npb = (u16x2)(0);
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const u16x2 x = pk(byte_pair(tb4[i >> 1], i & 1));
+      const u16x2 nz = pmin1(x);
+      npb = padd(npb, nz);
+      tw[i] = widen2(x, nz);
+    }
+    if (esc_in) {
+      u32x4 wa = in.wa, wb = in.wb;
+      if (!in.pre) {  // escapes the record did not announce (cold start, a row not swept last tick)
+        wa = __builtin_amdgcn_raw_buffer_load_b128(wrs, 2 * toff, 0, 0);
+        wb = __builtin_amdgcn_raw_buffer_load_b128(wrs, 2 * toff + 16, 0, 0);
+      }
+      const uint32_t wv[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        const u16x2 x = pk(byte_pair(tb4[i >> 1], i & 1));
+        const u16x2 keepn = pmin1(x ^ (u16x2)(S_B_ESC));  // 0 where escaped
+        tw[i] = pk(wv[i]) + keepn * (tw[i] - pk(wv[i]));
+      }
+    }
     // merge: re-base the cell to tick t (h -= 2, age += 1; absent stays 0), then max
     // with the delivered key (insert if absent; raise hb and stamp ts = t if newer)
-    const uint32_t tw[8] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y, tb.z, tb.w};
     u16x2 mm[8];
 #pragma unroll
     for (int i = 0; i < 8; i++)
-      mm[i] = __builtin_elementwise_max(__builtin_elementwise_sub_sat(pk(tw[i]), (u16x2)(63)), key5[i]);
+      mm[i] = __builtin_elementwise_max(__builtin_elementwise_sub_sat(tw[i], (u16x2)(63)), key5[i]);
     const int selfc = (r >= s.c0 && r < s.c0 + s.w) ? r - s.c0 - colb : -1;
     int selfapp = -1;  // lane cell of an appended self entry: no join record (push_back, not logNodeAdd)
     if (selfc >= 0 && selfc < Q) {  // updateMyPos + heartbeat++ + myPos->setheartbeat(heartbeat++)
@@ -352,9 +405,13 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
       }
     }
     // sweep (MP1Node.cpp:426-444), one packed pass: age >= TFAIL counts toward numfailed,
-    // age >= TREMOVE removes; fresh entries (age < TFAIL) form the payload sent at tick t
-    u16x2 np2 = (u16x2)(0), nf2 = (u16x2)(0), evany = (u16x2)(0), lagmin = (u16x2)(0xFFFF), bad = (u16x2)(0);
-    uint32_t cw[8], nw[2] = {0u, 0u};
+    // age >= TREMOVE removes; fresh entries (age < TFAIL) form the payload sent at tick t.
+    // The swept cell is narrowed to its stored byte (S_B_ESC where the byte cannot hold it).
+    // A fresh stored byte h4 << 4 | a sends h' = h - 2, i.e. the nibble h4 - 1; h4 = 1 and
+    // escaped cells send the escape nibble 15 (their byte h' goes to the payload's wide plane).
+    u16x2 np2 = (u16x2)(0), nf2 = (u16x2)(0), ng2 = (u16x2)(0), badv = (u16x2)(0), nmx = (u16x2)(0);
+    u16x2 nwv[2] = {(u16x2)(0), (u16x2)(0)};
+    uint32_t cw[8], bw[4], bprev = 0;
 #pragma unroll
     for (int i = 0; i < 8; i++) {
       const u16x2 v = mm[i];
@@ -362,46 +419,41 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
       const u16x2 stale = (a + (u16x2)(32 - GM_TFAIL)) >> (u16x2)(5);   // age >= TFAIL
       const u16x2 gone = (a + (u16x2)(32 - GM_TREMOVE)) >> (u16x2)(5);  // age >= TREMOVE
       const u16x2 v2 = v * ((u16x2)(1) - gone);
+      const u16x2 pres = pmin1(v2);
       nf2 = padd(nf2, stale);
-      np2 = padd(np2, pmin1(v2));
-      // h - 2 for fresh cells; stale ones subtract >= 257 and saturate to 0 (not sent)
-      const u16x2 p2 = __builtin_elementwise_sub_sat(v >> (u16x2)(5), stale * (u16x2)(255) + (u16x2)(2));
-      // nibble: n = (h' - 224) / 2, valid iff re-encoding gives h' back (even h' in [226, 252]);
-      // the re-encoding is forced to 0 for n = 0, so a sent value that maps to n = 0 escapes
-      // too, while "not sent" (h' = 0) stays 0; escapes carry 15 (the max)
-      const u16x2 n0 = __builtin_elementwise_sub_sat(p2, (u16x2)(S_NIB_BASE)) >> (u16x2)(1);
-      const u16x2 re = (n0 * (u16x2)(2) + (u16x2)(S_NIB_BASE)) * pmin1(n0);
-      const u16x2 b = pmin1(re ^ p2);
-      bad |= b;
-      const u16x2 nib = __builtin_elementwise_max(n0, b * (u16x2)(S_NIB_ESC));
-      nw[i >> 2] += unpk(nib * (u16x2)(1u << (4 * (3 - (i & 3)))));
-      // joins: absent before, present after the merge (t * 0xFFFF = -t saturates v away unless
-      // t = 0); removals: gone
-      evany |= __builtin_elementwise_sub_sat(v, pk(tw[i]) * (u16x2)(0xFFFF)) | gone;
-      lagmin = __builtin_elementwise_min(lagmin, v2 - (u16x2)(32));  // present with h <= 2
+      np2 = padd(np2, pres);
+      ng2 = padd(ng2, gone);
+      // stored byte: tt = v2 - S_CELL(226, 0) (wraps below h = 226) = (h - 226) << 5 | age;
+      // representable iff nothing above the h4 field (h <= 254, no wrap), h even (bit 5),
+      // age <= 15 (bit 4)
+      const u16x2 tt = v2 - (u16x2)(7232);
+      const u16x2 bad = pmin1(tt & (u16x2)(0xFC30)) & pres;
+      const uint32_t tu = unpk(tt);
+      const u16x2 enc = pk((tu & 0x000F000Fu) | ((tu >> 2) & 0x00F000F0u)) + (u16x2)(16);
+      const u16x2 b = enc * (pres - bad) + bad;  // absent 0, escaped S_B_ESC (= 1)
+      // payload nibble of the fresh present cells: h4 - 1, or 15 where that is 0 (h4 <= 1)
+      const u16x2 p = __builtin_elementwise_sub_sat(pres, stale);
+      const u16x2 qn = __builtin_elementwise_sub_sat(b >> (u16x2)(4), (u16x2)(1));
+      const u16x2 nib = p * (qn + (u16x2)(S_NIB_ESC) - (u16x2)(S_NIB_ESC) * pmin1(qn));
+      nwv[i >> 2] = nwv[i >> 2] + nib * (u16x2)(1u << (4 * (3 - (i & 3))));
+      badv |= bad;
+      nmx = __builtin_elementwise_max(nmx, nib);
       cw[i] = unpk(v2);
+      if (i & 1) bw[i >> 1] = __builtin_amdgcn_perm(unpk(b), bprev, 0x06040200u);
+      else bprev = unpk(b);
     }
-    esc_out = unpk(bad) != 0;
-    nfail = (int)nf2.x + (int)nf2.y;
-    npres = (int)np2.x + (int)np2.y;
-    if (__builtin_elementwise_min(lagmin.x, lagmin.y) < 64) atomicOr(s.err, GM_ERR_LAG);
-    if (unpk(evany)) {  // rare: this lane's joins / removals, as 2-bit kinds per cell
-      // the cells as loaded, re-read (still in memory: the stores come below) rather than
-      // kept live through the sweep for this rare path (21 VGPRs: occupancy 5 -> 8)
-      const u32x4 ra = __builtin_amdgcn_raw_buffer_load_b128(trs, toff, 0, 0);
-      const u32x4 rb = __builtin_amdgcn_raw_buffer_load_b128(trs, toff + 16, 0, 0);
-      const uint32_t tb0[8] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
+    esc_st = unpk(badv) != 0;
+    if (esc_st) {  // rare: cells the byte cannot hold, as 16-bit cells into the wide plane
+      u16x2 lagmin = (u16x2)(0xFFFF);
 #pragma unroll
-      for (int q = 0; q < Q; q++) {  // from the loaded and the swept cells only (the merge never deletes:
-        // present before and absent after = removed; a cell inserted this tick has age 0)
-        const uint32_t before = (tb0[q >> 1] >> (16 * (q & 1))) & 0xFFFFu;
-        const uint32_t after = (cw[q >> 1] >> (16 * (q & 1))) & 0xFFFFu;
-        const uint32_t ev = !before ? (after && q != selfapp ? S_EV_ADD : 0u) : (!after ? S_EV_REMOVE : 0u);
-        evk |= ev << (2 * q);
-      }
-      nev = __builtin_popcount((evk | (evk >> 1)) & 0x55555555u);
+      for (int i = 0; i < 8; i++) lagmin = __builtin_elementwise_min(lagmin, pk(cw[i]) - (u16x2)(32));
+      if (__builtin_elementwise_min(lagmin.x, lagmin.y) < 64) atomicOr(s.err, GM_ERR_LAG);  // present with h <= 2
+      const u32x4 wa = {cw[0], cw[1], cw[2], cw[3]}, wb = {cw[4], cw[5], cw[6], cw[7]};
+      __builtin_amdgcn_raw_buffer_store_b128(wa, wrs, 2 * toff, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(wb, wrs, 2 * toff + 16, 0, 0);
     }
-    if (esc_out) {  // rare: the lane's 16 payload bytes h' into the escape plane (read where the nibble is 15)
+    if (__builtin_elementwise_max(nmx.x, nmx.y) == S_NIB_ESC) {
+      // rare: the lane's 16 payload bytes h' into the escape plane (read where the nibble is 15)
       uint32_t pw[8];
 #pragma unroll
       for (int i = 0; i < 8; i++) {  // removed cells send nothing: the swept cells suffice
@@ -413,27 +465,62 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
                         __builtin_amdgcn_perm(pw[5], pw[4], 0x06040200u), __builtin_amdgcn_perm(pw[7], pw[6], 0x06040200u)};
       *(u32x4 *)(s.wide + slab * 2 * B + (size_t)r * 2 * B + (size_t)par * B + li * Q) = wv;
     }
-    const u32x4 na = {cw[0], cw[1], cw[2], cw[3]}, nb4 = {cw[4], cw[5], cw[6], cw[7]};
-    __builtin_amdgcn_raw_buffer_store_b128(na, trs, toff, 0, GM_AUX_NT);
-    __builtin_amdgcn_raw_buffer_store_b128(nb4, trs, toff + 16, 0, GM_AUX_NT);
-    const u32x2 ov = {nw[0], nw[1]};
+    nfail = (int)nf2.x + (int)nf2.y;
+    npres = (int)np2.x + (int)np2.y;
+    const int ngone = (int)ng2.x + (int)ng2.y;
+    // joins: present after the merge (npres + ngone) but not as loaded (npb) -- the merge never
+    // deletes; removals: ngone. Rare: this lane's events, as 2-bit kinds per cell
+    if (npres + ngone != (int)npb.x + (int)npb.y || ngone) {
+      // the bytes as loaded, re-read (still in memory: the stores come below) rather than
+      // kept live through the sweep for this rare path
+      const u32x4 ra = __builtin_amdgcn_raw_buffer_load_b128(trs, toff, 0, 0);
+      const uint32_t tb0[4] = {ra.x, ra.y, ra.z, ra.w};
+#pragma unroll
+      for (int q = 0; q < Q; q++) {  // from the loaded and the swept cells only (the merge never deletes:
+        // present before and absent after = removed; a cell inserted this tick has age 0)
+        const uint32_t before = (tb0[q >> 2] >> (8 * (q & 3))) & 0xFFu;
+        const uint32_t after = (bw[q >> 2] >> (8 * (q & 3))) & 0xFFu;  // stored byte: 0 = absent
+        const uint32_t ev = !before ? (after && q != selfapp ? S_EV_ADD : 0u) : (!after ? S_EV_REMOVE : 0u);
+        evk |= ev << (2 * q);
+      }
+      nev = __builtin_popcount((evk | (evk >> 1)) & 0x55555555u);
+    }
+    const u32x4 nb4 = {bw[0], bw[1], bw[2], bw[3]};
+    __builtin_amdgcn_raw_buffer_store_b128(nb4, trs, toff, 0, GM_AUX_NT);
+    const u32x2 ov = {unpk(nwv[0]), unpk(nwv[1])};
     __builtin_amdgcn_raw_buffer_store_b64(ov, prs, (uint32_t)(r * B + par * (B / 2) + li * 8), 0, GM_AUX_NT);
     if (band == 0 && li == 0) s.wtick[r] = t;
   }
   // present cells per 64-column chunk (4 lanes) for the draw's rank-select, gathered
   // into the row's first lane: bytes 0..B/64-1 of the (band, row) record
   constexpr int CH = S_CHUNK(B), LPC = CH / Q;  // columns / lanes per rank-select chunk
-  int cc = npres;
-#pragma unroll
-  for (int o = 1; o < LPC; o <<= 1) cc += __shfl_xor(cc, o, 64);
-  uint64_t piece = 0;
-#pragma unroll
-  for (int c = 0; c < B / CH; c++) piece |= (uint64_t)(__shfl(cc, sub * LPR + LPC * c, 64) & 0xFF) << (8 * c);
   // per-row reductions over the row's LPR lanes (aligned lane segments): counts packed
   // as present | numfailed << 16 (each <= B)
   int pf = npres | (nfail << 16);
+  uint64_t piece = 0;
+  if (LPR == 64 && LPC == 8) {
+    // one row per wave: 8-lane chunk sums on DPP (xor 1, xor 2 by quad_perm, then + the
+    // mirrored lane of the other quad), then the 8 chunk words by readlane on the scalar side
+    pf += __builtin_amdgcn_update_dpp(0, pf, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    pf += __builtin_amdgcn_update_dpp(0, pf, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+    pf += __builtin_amdgcn_update_dpp(0, pf, 0x141, 0xF, 0xF, false);  // row_half_mirror
+    int tsum = 0;
 #pragma unroll
-  for (int o = LPR / 2; o >= 1; o >>= 1) pf += __shfl_xor(pf, o, 64);
+    for (int c = 0; c < 8; c++) {
+      const int v = __builtin_amdgcn_readlane(pf, 8 * c);
+      piece |= (uint64_t)(v & 0xFF) << (8 * c);
+      tsum += v;
+    }
+    pf = tsum;
+  } else {
+    int cc = npres;
+#pragma unroll
+    for (int o = 1; o < LPC; o <<= 1) cc += __shfl_xor(cc, o, 64);
+#pragma unroll
+    for (int c = 0; c < B / CH; c++) piece |= (uint64_t)(__shfl(cc, sub * LPR + LPC * c, 64) & 0xFF) << (8 * c);
+#pragma unroll
+    for (int o = LPR / 2; o >= 1; o >>= 1) pf += __shfl_xor(pf, o, 64);
+  }
   int x = 0, tot = 0;
   if (__builtin_amdgcn_ballot_w64(nev != 0)) {  // wave-uniform: events anywhere in this wave
     x = nev;
@@ -452,7 +539,7 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
   const int E = s.evs;
   uint32_t sbase = 0;  // one spill-ring reservation per (row, band) that overflows its slots
   if (live && li == 0 && tot > E) sbase = atomicAdd(s.ev_spill_cnt, (uint32_t)(tot - E));
-  sbase = __shfl(sbase, sub * LPR, 64);
+  sbase = LPR == 64 ? __builtin_amdgcn_readfirstlane(sbase) : __shfl(sbase, sub * LPR, 64);
   if (live && nev) {
     int slot = x - nev;
     uint32_t *slots = s.ev_band + ((size_t)r * s.nb + band) * E;
@@ -471,10 +558,26 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
       slot++;
     }
   }
+  // the row's lanes that stored escapes (bit li, or li / 2 for 64 lanes per row): the next
+  // tick's unit_load prefetches their wide cells
+  uint32_t emask;
+  {
+    const uint64_t eb = __builtin_amdgcn_ballot_w64(esc_st);
+    if (LPR == 64) {
+      uint64_t x = (eb | (eb >> 1)) & 0x5555555555555555ull;  // pairs -> even bits, then compress
+      x = (x | (x >> 1)) & 0x3333333333333333ull;
+      x = (x | (x >> 2)) & 0x0F0F0F0F0F0F0F0Full;
+      x = (x | (x >> 4)) & 0x00FF00FF00FF00FFull;
+      x = (x | (x >> 8)) & 0x0000FFFF0000FFFFull;
+      emask = (uint32_t)(x | (x >> 16));
+    } else {
+      emask = (uint32_t)(eb >> (sub * LPR)) & (uint32_t)((1ull << LPR) - 1);
+    }
+  }
   if (li == 0 && r < s.n) {
     // one 16-byte record per (band, row), consecutive rows adjacent: whole-line writes
     const uint32_t bc = (uint32_t)(pf & 0xFFFF) | ((uint32_t)(pf >> 16) << 11) | ((uint32_t)min(tot, 1023) << 22);
-    s.brec[slab + r] = live ? make_uint4((uint32_t)piece, (uint32_t)(piece >> 32), bc, 0u) : make_uint4(0u, 0u, 0u, 0u);
+    s.brec[slab + r] = live ? make_uint4((uint32_t)piece, (uint32_t)(piece >> 32), bc, emask) : make_uint4(0u, 0u, 0u, 0u);
     // column shard: this shard's row totals (present, numfailed) for the all-gather,
     // accumulated as one packed 64-bit add per (row, band) into the zeroed slot
     if (s.sharded && live)
@@ -487,11 +590,12 @@ template <int B, bool DROP>
 __global__ __launch_bounds__(256) void gm_s_band(SState s, int t, int drop_pct) {
   constexpr int RPW = 64 / (B / S_COLS_PER_LANE);
   const int U = (s.n + RPW - 1) / RPW;
-  // wave-uniform unit index (scalar registers: the band / row split stays on the SALU)
-  const int u = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
-  if (u >= U * s.nb) return;  // whole wave
+  // grid (units of a band / 4, bands): blockIdx.y is the band, so workgroups still dispatch
+  // band-major, and the wave-uniform unit index needs no division
+  const int ub = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  if (ub >= U) return;  // whole wave
   UnitIn<B> in;
-  unit_load<B>(s, t, u, in);
+  unit_load<B>(s, t, (int)blockIdx.y, ub, in);
   u32x2 m[S_SB];
   unit_gather<B, DROP>(s, t, in, m);
   unit_finish<B, DROP>(s, t, drop_pct, in, m);
@@ -509,12 +613,13 @@ __global__ __launch_bounds__(256) void gm_s_band_pipe(SState s, int t, int nwave
   if (u >= total) return;
   UnitIn<B> cur, nxt;
   u32x2 m[S_SB];
-  unit_load<B>(s, t, u, cur);
+  const int U = (s.n + RPW - 1) / RPW;
+  unit_load<B>(s, t, u / U, u % U, cur);
   unit_gather<B, false>(s, t, cur, m);
   for (;;) {
     const int un = u + nwaves;
     const bool more = un < total;  // wave-uniform
-    if (more) unit_load<B>(s, t, un, nxt);
+    if (more) unit_load<B>(s, t, un / U, un % U, nxt);
     unit_finish<B, false>(s, t, -1, cur, m);
     if (!more) break;
     unit_gather<B, false>(s, t, nxt, m);
@@ -543,7 +648,7 @@ __global__ __launch_bounds__(256) void gm_s_selfcheck(SState s) {
       bad |= S_BC_PRES(v) != 0 || S_BC_NEV(v) != 0;
     }
     if (b0 < s.nb) {
-      const uint16_t *cells = s.table + ((size_t)b0 * s.n + r) * s.band;
+      const uint8_t *cells = s.table + ((size_t)b0 * s.n + r) * s.band;
       for (int j = lane; j < s.band; j += 64)
         bad |= b0 * s.band + j > gend && cells[j] != 0;
       const uint32_t v = s.brec[(size_t)b0 * s.n + r].z;
@@ -611,8 +716,8 @@ __device__ __forceinline__ void gm_row_totals(const SState &s, int r, int lane, 
 
 // Resolve up to 8 draws at once, one per 8-lane group: group g holds shard-local rank
 // ix_g (valid iff act) of a present entry of row r. The chunk-word prefix finds the
-// 64-column chunk; its 64 cells (128 B, 8 per lane) give the column. Returns, to every
-// lane, the shard-local column of each draw (-1 if none) and whether it is fresh.
+// 64- or 128-column chunk; its cell bytes (8 or 16 per lane) give the column. Returns, to
+// every lane, the shard-local column of each draw (-1 if none) and whether it is fresh.
 template <int B>
 __device__ __forceinline__ void gm_resolve8(const SState &s, int r, const uint32_t *pre, bool act, uint32_t ix, int lane,
                                             int col[8], int fresh[8]) {
@@ -633,13 +738,12 @@ __device__ __forceinline__ void gm_resolve8(const SState &s, int r, const uint32
     q = ix - pre[lo];
     const int col0 = lo * CH + gl * CPL;  // this lane's cells
     base = col0;
-    const uint16_t *cp = s.table + ((size_t)(col0 / B) * s.n + r) * B + (col0 % B);
+    const uint8_t *cp = s.table + ((size_t)(col0 / B) * s.n + r) * B + (col0 % B);
 #pragma unroll
     for (int h = 0; h < CPL / 8; h++) {
-      const uint4 t4 = *(const uint4 *)(cp + 8 * h);
-      const uint32_t w[4] = {t4.x, t4.y, t4.z, t4.w};
+      const uint2 t2 = *(const uint2 *)(cp + 8 * h);
 #pragma unroll
-      for (int v = 0; v < 8; v++) en[8 * h + v] = (w[v >> 1] >> (16 * (v & 1))) & 0xFFFFu;
+      for (int v = 0; v < 8; v++) en[8 * h + v] = ((v < 4 ? t2.x : t2.y) >> (8 * (v & 3))) & 0xFFu;
     }
 #pragma unroll
     for (int v = 0; v < CPL; v++) cnt += en[v] != 0;
@@ -661,7 +765,10 @@ __device__ __forceinline__ void gm_resolve8(const SState &s, int r, const uint32
       if (en[v] != 0) {
         if (need == 0) {
           mycol = base + v;
-          myfresh = S_AGE(en[v]) < GM_TFAIL;  // the table is as of tick t
+          // the table is as of tick t; an escaped cell's age is in the wide plane
+          const uint32_t c16 = en[v] == S_B_ESC ? (uint32_t)s.twide[((size_t)(mycol / B) * s.n + r) * B + mycol % B]
+                                                 : s_widen(en[v]);
+          myfresh = S_AGE(c16) < GM_TFAIL;
         }
         need--;
       }
@@ -1023,7 +1130,10 @@ __global__ void gm_s_init(SState s, int warm, int t0, uint64_t seed) {
         e = S_CELL((uint32_t)(252 - 2 * a), (uint32_t)a);
       }
     }
-    s.table[((size_t)(j / s.band) * s.n + r) * s.band + j % s.band] = (uint16_t)e;
+    const size_t at = ((size_t)(j / s.band) * s.n + r) * s.band + j % s.band;
+    const uint32_t b = s_narrow(e);
+    s.table[at] = (uint8_t)b;
+    if (b == S_B_ESC) s.twide[at] = (uint16_t)e;
   }
   if (threadIdx.x == 0) {
     s.hbctr[r] = warm == 1 ? 2 * t0 : 0;
@@ -1036,7 +1146,8 @@ __global__ void gm_s_init(SState s, int warm, int t0, uint64_t seed) {
 template <int B>
 static hipError_t launch_tick_b(const SState &s, int t, int drop_pct, bool nt, hipStream_t st, hipEvent_t k0,
                                 hipEvent_t k1, bool pick) {
-  const int nblk = (int)(((int64_t)s.nb * ((s.n + 64 / (B / S_COLS_PER_LANE) - 1) / (64 / (B / S_COLS_PER_LANE))) + 3) / 4);
+  constexpr int RPW = 64 / (B / S_COLS_PER_LANE);
+  const dim3 nblk((((s.n + RPW - 1) / RPW) + 3) / 4, s.nb);  // (units of a band / 4, bands)
   // the event records of a tick (per-(row, band) slots + spill ring) stay readable until the next tick
   (void)hipMemsetAsync(s.ev_spill_cnt, 0, sizeof(uint32_t), st);
   hipLaunchKernelGGL(gm_s_mtgen, dim3((s.n + 255) / 256), dim3(256), 0, st, s, t);
