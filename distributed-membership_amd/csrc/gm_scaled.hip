@@ -63,21 +63,35 @@ template <int B>
 struct RowMeta {
   int k;           // lists delivered to the row (-1: no such row, or a crashed node)
   int snd[S_SB];   // first S_SB senders
+  uint32_t hint;   // the (band, row) record's escape mask of the last tick (see unit_finish)
 };
 
-template <int B>
-__device__ __forceinline__ RowMeta<B> row_meta(const SState &s, int r, int par, int t) {
+// Every load of the row's metadata issues at once, none behind a branch on another (one
+// memory round trip before the payload gathers can issue, not a chain of three).
+template <int B, bool UNI>
+__device__ __forceinline__ RowMeta<B> row_meta(const SState &s, int r, int par, int t, size_t slab) {
   RowMeta<B> m;
-  m.k = -1;
-  if (r < s.n) {
-    const int32_t *ib = s.inbox[par] + (size_t)r * S_KMAX;
-    const int4 a = *(const int4 *)ib;
-    const int4 b = *(const int4 *)(ib + 4);
-    m.snd[0] = a.x; m.snd[1] = a.y; m.snd[2] = a.z; m.snd[3] = a.w;
-    m.snd[4] = b.x; m.snd[5] = b.y; m.snd[6] = b.z; m.snd[7] = b.w;
-    const int k = s.inbox_cnt[par][r];
-    m.k = (s.failed[r] || !s_ingroup(s.ramp, s.intro_until, r, t)) ? -1 : k;  // not in the group: untouched
+  const int rc = min(r, s.n - 1);  // r >= n (a partial unit): loads stay in bounds, k = -1
+  const int32_t *ib = s.inbox[par] + (size_t)rc * S_KMAX;
+  int4 a = *(const int4 *)ib;
+  int4 b = *(const int4 *)(ib + 4);
+  int k = s.inbox_cnt[par][rc];
+  int failed = s.failed[rc];
+  m.hint = s.brec[slab + rc].w;
+  // empty asm statements that read the values here: without them the compiler sinks the
+  // inbox-count load into a branch on `failed` and the sender ids behind that, two more
+  // round trips before the gathers (one row per wave: scalar registers)
+  if (UNI) {
+    asm volatile("" : "+s"(k), "+s"(failed), "+s"(a.x), "+s"(a.y), "+s"(a.z), "+s"(a.w));
+    asm volatile("" : "+s"(b.x), "+s"(b.y), "+s"(b.z), "+s"(b.w));
+  } else {
+    asm volatile("" : "+v"(k), "+v"(failed));
   }
+  m.snd[0] = a.x; m.snd[1] = a.y; m.snd[2] = a.z; m.snd[3] = a.w;
+  m.snd[4] = b.x; m.snd[5] = b.y; m.snd[6] = b.z; m.snd[7] = b.w;
+  // not in the group (join ramp) or crashed: untouched
+  m.k = (r >= s.n || failed || !s_ingroup(s.ramp, s.intro_until, r, t)) ? -1 : k;
+  if (r >= s.n) m.hint = 0;
   return m;
 }
 
@@ -119,9 +133,20 @@ __device__ __forceinline__ uint32_t byte_pair(uint32_t w, int hi) {
   return __builtin_amdgcn_perm(0u, w, hi ? 0x0c030c02u : 0x0c010c00u);
 }
 // s_widen of two stored bytes (nz = min(x, 1)); an escape byte gives garbage, replaced by its wide cell
+// (h4 << 4 | a -> 7168 + (h4 << 6) + a = x + 3 (x & 0xF0) + 7168: two multiply-adds)
 __device__ __forceinline__ u16x2 widen2(u16x2 x, u16x2 nz) {
-  const uint32_t xv = unpk(x);
-  return nz * (u16x2)(7168) + pk((xv & 0x000F000Fu) | ((xv << 2) & 0x03C003C0u));
+  return nz * (u16x2)(7168) + ((x & (u16x2)(0xF0)) * (u16x2)(3) + x);
+}
+
+// Stored bytes of two swept cells (pres = min(v2, 1)): tt = v2 - S_CELL(226, 0) (wraps below
+// h = 226) = (h - 226) << 5 | age; representable iff nothing above the h4 field (h <= 254, no
+// wrap), h even (bit 5) and age <= 15 (bit 4) -> h4 << 4 | age, else S_B_ESC (bad = 1); absent 0
+__device__ __forceinline__ u16x2 narrow2(u16x2 v2, u16x2 pres, u16x2 &bad) {
+  const u16x2 tt = v2 - (u16x2)(7232);
+  bad = pmin1(tt & (u16x2)(0xFC30)) & pres;
+  const uint32_t tu = unpk(tt);
+  const u16x2 enc = pk((tu & 0x000F000Fu) | ((tu >> 2) & 0x00F000F0u)) + (u16x2)(16);
+  return enc * (pres - bad) + bad;
 }
 
 // Payload nibbles (gm_scaled.h S_NIB_*): dword w of a lane's 8-byte slice holds cells
@@ -163,7 +188,8 @@ struct UnitIn {
   u32x4 wa, wb;    // the lane's 16 wide cells (valid where its bytes are S_B_ESC)
 };
 
-template <int B>
+// UNI: the row is wave-uniform and known to be (one row per wave, a grid-derived unit)
+template <int B, bool UNI = false>
 __device__ __forceinline__ void unit_load(const SState &s, int t, int band, int ub, UnitIn<B> &in) {
   constexpr int LPR = B / S_COLS_PER_LANE, RPW = 64 / LPR, Q = S_COLS_PER_LANE;
   const int lane = threadIdx.x & 63;
@@ -173,16 +199,15 @@ __device__ __forceinline__ void unit_load(const SState &s, int t, int band, int 
   const size_t slab = (size_t)in.band * s.n;
   const __amdgpu_buffer_rsrc_t trs = gm_rsrc(s.table + slab * B, (uint32_t)(s.n * B));
   const uint32_t toff = (uint32_t)(in.r * B + li * Q);  // r >= n: out of range -> zeros, dropped
-  const RowMeta<B> meta = row_meta<B>(s, in.r, t & 1, t);
+  // the table slice first: it is independent of the metadata, both in flight together
+  in.ta = __builtin_amdgcn_raw_buffer_load_b128(trs, toff, 0, GM_AUX_NT);
+  const RowMeta<B> meta = row_meta<B, UNI>(s, in.r, t & 1, t, slab);
 #pragma unroll
   for (int j = 0; j < S_SB; j++) in.snd[j] = meta.snd[j];
   in.k = meta.k;
-  // the table slice is independent of the metadata: both in flight together
-  in.ta = __builtin_amdgcn_raw_buffer_load_b128(trs, toff, 0, GM_AUX_NT);
   // lanes that stored escaped cells last tick (the (band, row) record's escape mask, written by
   // unit_finish) fetch their wide cells now, with the table slice, instead of one round trip later
-  const uint32_t hint = in.r < s.n ? s.brec[slab + in.r].w : 0u;
-  in.pre = (hint >> (LPR == 64 ? li >> 1 : li)) & 1u;
+  in.pre = (meta.hint >> (LPR == 64 ? li >> 1 : li)) & 1u;
   in.wa = in.wb = (u32x4){0u, 0u, 0u, 0u};
   if (in.pre) {
     const __amdgpu_buffer_rsrc_t wrs = gm_rsrc(s.twide + slab * B, (uint32_t)(s.n * B * 2));
@@ -269,7 +294,7 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
         const u16x2 nb = acc[i] >> (u16x2)(12);
         nmax = __builtin_elementwise_max(nmax, nb);
         // h' = 224 + 2n for n >= 1: key5 = 7168 + 64 n, 0 for n = 0
-        key5[i] = pmin1(nb) * (u16x2)(S_NIB_BASE << 5) + (nb << (u16x2)(6));
+        key5[i] = pmin1(nb) * (u16x2)(S_NIB_BASE << 5) + nb * (u16x2)(64);
       }
       if (__builtin_elementwise_max(nmax.x, nmax.y) == S_NIB_ESC) {
         // rare (cold start, JOINREQ entries, lag > 13 ticks): some list escaped a cell of
@@ -409,38 +434,53 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
     // The swept cell is narrowed to its stored byte (S_B_ESC where the byte cannot hold it).
     // A fresh stored byte h4 << 4 | a sends h' = h - 2, i.e. the nibble h4 - 1; h4 = 1 and
     // escaped cells send the escape nibble 15 (their byte h' goes to the payload's wide plane).
-    u16x2 np2 = (u16x2)(0), nf2 = (u16x2)(0), ng2 = (u16x2)(0), badv = (u16x2)(0), nmx = (u16x2)(0);
+    u16x2 np2 = (u16x2)(0), nf2 = (u16x2)(0), badv = (u16x2)(0), nmx = (u16x2)(0), amax = (u16x2)(0);
     u16x2 nwv[2] = {(u16x2)(0), (u16x2)(0)};
     uint32_t cw[8], bw[4], bprev = 0;
 #pragma unroll
     for (int i = 0; i < 8; i++) {
       const u16x2 v = mm[i];
       const u16x2 a = v & (u16x2)(31);
-      const u16x2 stale = (a + (u16x2)(32 - GM_TFAIL)) >> (u16x2)(5);   // age >= TFAIL
-      const u16x2 gone = (a + (u16x2)(32 - GM_TREMOVE)) >> (u16x2)(5);  // age >= TREMOVE
-      const u16x2 v2 = v * ((u16x2)(1) - gone);
-      const u16x2 pres = pmin1(v2);
+      const u16x2 stale = (a + (u16x2)(32 - GM_TFAIL)) >> (u16x2)(5);  // age >= TFAIL
+      amax = __builtin_elementwise_max(amax, a);  // TREMOVE removals (rare) are applied below
+      const u16x2 pres = pmin1(v);
       nf2 = padd(nf2, stale);
       np2 = padd(np2, pres);
-      ng2 = padd(ng2, gone);
-      // stored byte: tt = v2 - S_CELL(226, 0) (wraps below h = 226) = (h - 226) << 5 | age;
-      // representable iff nothing above the h4 field (h <= 254, no wrap), h even (bit 5),
-      // age <= 15 (bit 4)
-      const u16x2 tt = v2 - (u16x2)(7232);
-      const u16x2 bad = pmin1(tt & (u16x2)(0xFC30)) & pres;
-      const uint32_t tu = unpk(tt);
-      const u16x2 enc = pk((tu & 0x000F000Fu) | ((tu >> 2) & 0x00F000F0u)) + (u16x2)(16);
-      const u16x2 b = enc * (pres - bad) + bad;  // absent 0, escaped S_B_ESC (= 1)
+      u16x2 bad;
+      const u16x2 b = narrow2(v, pres, bad);
       // payload nibble of the fresh present cells: h4 - 1, or 15 where that is 0 (h4 <= 1)
       const u16x2 p = __builtin_elementwise_sub_sat(pres, stale);
       const u16x2 qn = __builtin_elementwise_sub_sat(b >> (u16x2)(4), (u16x2)(1));
-      const u16x2 nib = p * (qn + (u16x2)(S_NIB_ESC) - (u16x2)(S_NIB_ESC) * pmin1(qn));
+      const u16x2 nib = p * (__builtin_elementwise_sub_sat((u16x2)(1), qn) * (u16x2)(S_NIB_ESC) + qn);
       nwv[i >> 2] = nwv[i >> 2] + nib * (u16x2)(1u << (4 * (3 - (i & 3))));
       badv |= bad;
       nmx = __builtin_elementwise_max(nmx, nib);
-      cw[i] = unpk(v2);
+      cw[i] = unpk(v);
       if (i & 1) bw[i >> 1] = __builtin_amdgcn_perm(unpk(b), bprev, 0x06040200u);
       else bprev = unpk(b);
+    }
+    int ngone = 0;
+    if (__builtin_elementwise_max(amax.x, amax.y) >= GM_TREMOVE) {
+      // rare: age >= TREMOVE removes (MP1Node.cpp:429-444) -- the lane's cells again, with the
+      // removed ones absent (they sent nothing: stale, so the nibbles stand)
+      u16x2 ng2 = (u16x2)(0);
+      np2 = badv = (u16x2)(0);
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        const u16x2 v = pk(cw[i]);
+        const u16x2 gone = ((v & (u16x2)(31)) + (u16x2)(32 - GM_TREMOVE)) >> (u16x2)(5);
+        const u16x2 v2 = v * ((u16x2)(1) - gone);
+        const u16x2 pres = pmin1(v2);
+        np2 = padd(np2, pres);
+        ng2 = padd(ng2, gone);
+        u16x2 bad;
+        const u16x2 b = narrow2(v2, pres, bad);
+        badv |= bad;
+        cw[i] = unpk(v2);
+        if (i & 1) bw[i >> 1] = __builtin_amdgcn_perm(unpk(b), bprev, 0x06040200u);
+        else bprev = unpk(b);
+      }
+      ngone = (int)ng2.x + (int)ng2.y;
     }
     esc_st = unpk(badv) != 0;
     if (esc_st) {  // rare: cells the byte cannot hold, as 16-bit cells into the wide plane
@@ -467,7 +507,6 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
     }
     nfail = (int)nf2.x + (int)nf2.y;
     npres = (int)np2.x + (int)np2.y;
-    const int ngone = (int)ng2.x + (int)ng2.y;
     // joins: present after the merge (npres + ngone) but not as loaded (npb) -- the merge never
     // deletes; removals: ngone. Rare: this lane's events, as 2-bit kinds per cell
     if (npres + ngone != (int)npb.x + (int)npb.y || ngone) {
@@ -595,7 +634,7 @@ __global__ __launch_bounds__(256) void gm_s_band(SState s, int t, int drop_pct) 
   const int ub = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
   if (ub >= U) return;  // whole wave
   UnitIn<B> in;
-  unit_load<B>(s, t, (int)blockIdx.y, ub, in);
+  unit_load<B, RPW == 1>(s, t, (int)blockIdx.y, ub, in);
   u32x2 m[S_SB];
   unit_gather<B, DROP>(s, t, in, m);
   unit_finish<B, DROP>(s, t, drop_pct, in, m);
