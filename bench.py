@@ -342,9 +342,9 @@ def main_partial(a):
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                      "frac": (achieved / PEAK_HBM_GBPS) if achieved else None, "traffic": traffic,
                      "kernel": "gm_p_tick", "kernel_ms": kernel_ms, "alg_bytes_per_launch": b_alg,
-                     "note": "instruction-issue bound, not HBM bound: ~900 VALU + ~940 SALU instructions per "
-                             "node, both issue ports ~70% busy (PMC, profiles/r01/partial_v2/variants/pmc_base.txt; "
-                             "DESIGN.md PARTIAL)"},
+                     "note": "instruction-issue bound, not HBM bound: ~960 VALU + ~570 SALU instructions per "
+                             "node (PMC, profiles/r01/partial_v3/pmc_instr_mix_n4m.txt; DESIGN.md PARTIAL); the "
+                             "contract's bound field only offers hbm|mfma"},
     }
     if world > 1:
         out["roofline"]["note"] = "rank 0's local kernels (its n/G nodes)"
