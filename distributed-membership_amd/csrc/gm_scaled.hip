@@ -138,6 +138,18 @@ __device__ __forceinline__ u16x2 widen2(u16x2 x, u16x2 nz) {
   return nz * (u16x2)(7168) + ((x & (u16x2)(0xF0)) * (u16x2)(3) + x);
 }
 
+// wave-wide inclusive scan on DPP: row_shr 1/2/4/8 within each 16-lane row, row_bcast15 /
+// row_bcast31 carry the row totals upward (lanes a DPP source does not reach add 0)
+__device__ __forceinline__ int dpp_scan(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);  // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);  // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);  // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);  // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+  return v;
+}
+
 // Stored bytes of two swept cells (pres = min(v2, 1)): tt = v2 - S_CELL(226, 0) (wraps below
 // h = 226) = (h - 226) << 5 | age; representable iff nothing above the h4 field (h <= 254, no
 // wrap), h even (bit 5) and age <= 15 (bit 4) -> h4 << 4 | age, else S_B_ESC (bad = 1); absent 0
@@ -460,6 +472,7 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
       else bprev = unpk(b);
     }
     int ngone = 0;
+    uint32_t gmask = 0;  // lane cells removed this tick (bit q = cell q)
     if (__builtin_elementwise_max(amax.x, amax.y) >= GM_TREMOVE) {
       // rare: age >= TREMOVE removes (MP1Node.cpp:429-444) -- the lane's cells again, with the
       // removed ones absent (they sent nothing: stale, so the nibbles stand)
@@ -469,6 +482,7 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
       for (int i = 0; i < 8; i++) {
         const u16x2 v = pk(cw[i]);
         const u16x2 gone = ((v & (u16x2)(31)) + (u16x2)(32 - GM_TREMOVE)) >> (u16x2)(5);
+        gmask |= ((unpk(gone) & 1u) | ((unpk(gone) >> 15) & 2u)) << (2 * i);
         const u16x2 v2 = v * ((u16x2)(1) - gone);
         const u16x2 pres = pmin1(v2);
         np2 = padd(np2, pres);
@@ -509,9 +523,18 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
     npres = (int)np2.x + (int)np2.y;
     // joins: present after the merge (npres + ngone) but not as loaded (npb) -- the merge never
     // deletes; removals: ngone. Rare: this lane's events, as 2-bit kinds per cell
-    if (npres + ngone != (int)npb.x + (int)npb.y || ngone) {
-      // the bytes as loaded, re-read (still in memory: the stores come below) rather than
-      // kept live through the sweep for this rare path
+    if (npres + ngone == (int)npb.x + (int)npb.y && ngone) {
+      // removals only (the crash case): REMOVE kinds (10) at the removed cells
+      uint32_t x = gmask;
+      x = (x | (x << 8)) & 0x00FF00FFu;
+      x = (x | (x << 4)) & 0x0F0F0F0Fu;
+      x = (x | (x << 2)) & 0x33333333u;
+      x = (x | (x << 1)) & 0x55555555u;
+      evk = x << 1;
+      nev = __builtin_popcount(gmask);
+    } else if (npres + ngone != (int)npb.x + (int)npb.y) {
+      // joins (and possibly removals): the bytes as loaded, re-read (still in memory: the
+      // stores come below) rather than kept live through the sweep for this rare path
       const u32x4 ra = __builtin_amdgcn_raw_buffer_load_b128(trs, toff, 0, 0);
       const uint32_t tb0[4] = {ra.x, ra.y, ra.z, ra.w};
 #pragma unroll
@@ -562,18 +585,28 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
   }
   int x = 0, tot = 0;
   if (__builtin_amdgcn_ballot_w64(nev != 0)) {  // wave-uniform: events anywhere in this wave
-    x = nev;
-#pragma unroll
-    for (int o = 1; o < LPR; o <<= 1) {
-      const int y = __shfl_up(x, o, 64);
-      if (li >= o) x += y;
-    }
-    tot = __shfl(x, sub * LPR + LPR - 1, 64);
     // cumulative (joins, removals) of this (row, band): ADD kinds are 01, REMOVE kinds 10
     int jr = __builtin_popcount(evk & 0x55555555u) | (__builtin_popcount(evk & 0xAAAAAAAAu) << 16);
+    x = nev;
+    if (LPR == 64) {  // one row per wave: inclusive scans on DPP, totals from lane 63
+      x = dpp_scan(x);
+      jr = dpp_scan(jr);
+      tot = __builtin_amdgcn_readlane(x, 63);
+      jr = __builtin_amdgcn_readlane(jr, 63);
+    } else {
 #pragma unroll
-    for (int o = LPR / 2; o >= 1; o >>= 1) jr += __shfl_xor(jr, o, 64);
-    if (live && li == 0 && jr) s.evcum[(size_t)r * s.nb + band] += (uint64_t)(jr & 0xFFFF) | ((uint64_t)(jr >> 16) << 32);
+      for (int o = 1; o < LPR; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (li >= o) x += y;
+      }
+      tot = __shfl(x, sub * LPR + LPR - 1, 64);
+#pragma unroll
+      for (int o = LPR / 2; o >= 1; o >>= 1) jr += __shfl_xor(jr, o, 64);
+    }
+    // single writer per (row, band); a no-return atomic keeps the wave from waiting on a load
+    if (live && li == 0 && jr)
+      atomicAdd((unsigned long long *)&s.evcum[(size_t)r * s.nb + band],
+                (unsigned long long)(jr & 0xFFFF) | ((unsigned long long)(jr >> 16) << 32));
   }
   const int E = s.evs;
   uint32_t sbase = 0;  // one spill-ring reservation per (row, band) that overflows its slots
