@@ -54,13 +54,6 @@ __device__ unsigned long long g_pprof[16];
   } while (0)
 #endif
 
-// measurement builds only (scripts/sc_variants.sh): GM_P_ABL bits switch sections off to
-// price them -- 1 no eviction (first V-1 entries + self), 2 non-returning inbox appends
-// (fixed slots), 4 no id rank, 8 no drop hashes. Results are NOT the specification's.
-#ifndef GM_P_ABL
-#define GM_P_ABL 0
-#endif
-
 #define P_IDMASK 0x01FFFFFFu  // ids <= 2^25
 #define P_OWN 0x80000000u     // table id-word flag: the id was in the node's own list
 #define P_SELF 0x40000000u    // table id-word flag: the node's own entry
@@ -242,7 +235,7 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
     dv[st] = e;
   }
   // drop keys: one (t_send, src, dst) hash per delivered list, lane j for list j
-  const bool dropping = s.drop_pct >= 0 && !(GM_P_ABL & 8);
+  const bool dropping = s.drop_pct >= 0;
   uint64_t pairv = 0;
   if (dropping)
     pairv = gm_mix64(s.drop_seed ^ ((uint64_t)(uint32_t)(t - 1) << 48) ^ ((uint64_t)(uint32_t)sg << 24) ^
@@ -363,12 +356,7 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
     }
   }
   uint32_t keep = 0;
-  if (m <= V || (GM_P_ABL & 1)) {
-    if (GM_P_ABL & 1) {
-#pragma unroll
-      for (int q = 0; q < DS; q++)
-        if (q < dm && dw[q] && (q * 64 + lane < V - 1 || (dw[q] & P_SELF))) keep |= 1u << q;
-    } else
+  if (m <= V) {
 #pragma unroll
     for (int q = 0; q < DS; q++)
       if (q < dm && dw[q]) keep |= 1u << q;
@@ -499,7 +487,6 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
       rank += (v.x < mw) + (v.y < mw) + (v.z < mw) + (v.w < mw);
     }
     rank += __shfl_xor(rank, 32, 64);
-    if (GM_P_ABL & 4) rank = e;
     p_wsync();
     if (lane < cnt) {
       fin[rank] = ((uint64_t)myid << 32) | mh;
@@ -610,13 +597,7 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
   if (lane < ng) {
     s.targets[(size_t)li * GM_FANOUT + lane] = dst;
     if (owner == s.rank) {
-      int slot;
-      if (GM_P_ABL & 2) {
-        atomicAdd(&s.inbox_cnt[par ^ 1][dst - s.n0], 1);
-        slot = (li + lane) & 15;
-      } else {
-        slot = atomicAdd(&s.inbox_cnt[par ^ 1][dst - s.n0], 1);
-      }
+      const int slot = atomicAdd(&s.inbox_cnt[par ^ 1][dst - s.n0], 1);
       if (slot < P_KMAX) s.inbox[par ^ 1][(size_t)(dst - s.n0) * P_KMAX + slot] = li;
       else atomicOr(s.err, GM_ERR_INBOX);
     }

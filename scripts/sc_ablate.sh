@@ -1,6 +1,11 @@
+#!/bin/bash
+# GPU-box step: S-C bench per measurement build of scripts/sc_variants.sh (build_var/<name>/libgm.so)
+# VARIANTS="name ..." (default: the in-tree library only, as "main"); results in gpurun_out/abl/
 set -o pipefail
 mkdir -p gpurun_out/abl
-for v in base noevict noret norank nodrop all; do
+for v in ${VARIANTS:-main}; do
   echo "[$(date +%T)] $v" >> gpurun_out/abl/steps.txt
-  GM_LIBRARY=build_var/$v/libgm.so timeout -k 10 150 python -u bench.py --scenario S-C --no-cpu --steps 10 --warmup 2 > gpurun_out/abl/$v.json 2> gpurun_out/abl/$v.err || exit 1
+  lib=build_var/$v/libgm.so; [ "$v" = main ] && lib=distributed-membership_amd/lib/libgm.so
+  GM_LIBRARY=$lib timeout -k 10 150 python -u bench.py --scenario S-C --no-cpu --steps 10 --warmup 2 \
+    > gpurun_out/abl/$v.json 2> gpurun_out/abl/$v.err || exit 1
 done

@@ -1,8 +1,8 @@
 #!/bin/bash
-# Measurement builds of libgm with parts of the PARTIAL tick switched off (GM_P_ABL bits,
-# see gm_partial.hip) or the per-section clock build (GM_P_PROFILE), into
+# Measurement builds of libgm (e.g. the per-section clock build -DGM_P_PROFILE, or a candidate
+# kernel change kept beside the in-tree library for an A/B timing) into
 # build_var/<name>/libgm.so; run with GM_LIBRARY=build_var/<name>/libgm.so python bench.py ...
-# Usage: scripts/sc_variants.sh name:FLAGS ...   e.g. noevict:-DGM_P_ABL=1
+# Usage: scripts/sc_variants.sh name:FLAGS ...   e.g. prof:-DGM_P_PROFILE
 set -e
 cd "$(dirname "$0")/.."
 HIPFLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Iinclude -Idistributed-membership_amd/csrc -Wno-unused-result"
