@@ -40,6 +40,7 @@ hipError_t gm_launch_partial_unpack(const PState &s, int t, int base, int nrecv,
 hipError_t gm_launch_partial_mtgen(const PState &s, int t, uint32_t *mtraw, hipStream_t st, bool reset);
 hipError_t gm_launch_partial_reset(const PState &s, hipStream_t st);
 hipError_t gm_launch_partial_chunk(const PState &s, int t, const uint32_t *mtraw, int c, hipStream_t st);
+hipError_t gm_launch_msgcount(const SState &s, int t, bool dropped, hipStream_t st);
 size_t gm_partial_lds_bytes();
 void gm_partial_profile_dump();
 
@@ -67,6 +68,7 @@ struct gm_ctx {
   int dropmsg = 0;
   int latched = GM_OK;
   bool timing = false;
+  int64_t ticks_done = 0;  // gm_tick calls that enqueued a tick
   int timed_ticks = 0;  // ticks in the current timing window
   int ktimed = 0;       // band-kernel event pairs recorded in the window (ring slots in use: min(ktimed, GM_TEV_RING))
   hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -706,6 +708,7 @@ static int tick_scaled(gm_ctx *c) {
   hipEvent_t k0 = nullptr, k1 = nullptr;
   if (c->timing) TRY(timing_slot(c, &k0, &k1));
   HIPCHECK(gm_launch_tick(c->s, c->t, drop ? c->cfg.drop_pct : -1, c->nt, c->stream, k0, k1, true));
+  if (c->s.mc_sent && c->t < c->s.mc_tmax) HIPCHECK(gm_launch_msgcount(c->s, c->t, drop, c->stream));
   if (c->timing) {
     HIPCHECK(hipEventRecord(c->e1, c->stream));
     c->timed_ticks++;
@@ -776,6 +779,7 @@ extern "C" int gm_tick(gm_ctx *c) {
                                                                                              : tick_partial(c);
   if (rc == GM_OK) {
     c->t++;
+    c->ticks_done++;
     c->undrained = c->cfg.mode != GM_MODE_FAITHFUL;
   }
   return rc;
@@ -998,9 +1002,58 @@ extern "C" int gm_event_totals(gm_ctx *c, uint64_t totals[6]) {
   return GM_OK;
 }
 
+// SCALED / PARTIAL: per-tick, per-node entry counts from the next tick on, for ticks < tmax
+// (FAITHFUL always counts, as EmulNet does)
+extern "C" int gm_msgcount_record(gm_ctx *c, int32_t tmax) {
+  if (!c || tmax <= 0 || tmax > GM_T_LIMIT + 1) return GM_EINVAL;
+  if (c->cfg.mode == GM_MODE_FAITHFUL) return GM_OK;
+  if (c->ticks_done) return GM_ESTATE;  // the received counts need the senders' counts of the tick before
+  if (c->cfg.mode == GM_MODE_SCALED && c->s.sharded) return GM_EUNSUPPORTED;
+  if (c->cfg.mode == GM_MODE_SCALED ? c->s.mc_sent != nullptr : c->p.mc_sent != nullptr) return GM_ESTATE;
+  const size_t rows = c->cfg.mode == GM_MODE_SCALED ? (size_t)c->n : (size_t)c->p.nloc;
+  uint32_t *ms = nullptr, *mr = nullptr;
+  TRY(dalloc(c, &ms, (size_t)tmax * rows));
+  TRY(dalloc(c, &mr, (size_t)tmax * rows));
+  HIPCHECK(hipMemsetAsync(ms, 0, sizeof(uint32_t) * tmax * rows, c->stream));
+  HIPCHECK(hipMemsetAsync(mr, 0, sizeof(uint32_t) * tmax * rows, c->stream));
+  if (c->cfg.mode == GM_MODE_SCALED) {
+    TRY(dalloc(c, &c->s.mc_fresh, 2 * rows));
+    TRY(dalloc(c, &c->s.mc_rdrop, rows));
+    HIPCHECK(hipMemsetAsync(c->s.mc_fresh, 0, sizeof(uint32_t) * 2 * rows, c->stream));
+    HIPCHECK(hipMemsetAsync(c->s.mc_rdrop, 0, sizeof(uint32_t) * rows, c->stream));
+    c->s.mc_sent = ms;
+    c->s.mc_recv = mr;
+    c->s.mc_tmax = tmax;
+  } else {
+    c->p.mc_sent = ms;
+    c->p.mc_recv = mr;
+    c->p.mc_tmax = tmax;
+  }
+  return GM_OK;
+}
+
 extern "C" int gm_msgcount(gm_ctx *c, int32_t t, int32_t *sent, int32_t *recv) {
   if (!c || !sent || !recv || t < 0) return GM_EINVAL;
-  if (c->cfg.mode != GM_MODE_FAITHFUL) return GM_EUNSUPPORTED;
+  if (c->cfg.mode != GM_MODE_FAITHFUL) {  // [nodes][t] of this context's nodes, from the recorded history
+    const bool sc = c->cfg.mode == GM_MODE_SCALED;
+    const uint32_t *ms = sc ? c->s.mc_sent : c->p.mc_sent, *mr = sc ? c->s.mc_recv : c->p.mc_recv;
+    const int tmax = sc ? c->s.mc_tmax : c->p.mc_tmax;
+    if (!ms) return GM_ESTATE;  // gm_msgcount_record was not called
+    if (t > tmax) return GM_EINVAL;
+    const size_t rows = sc ? (size_t)c->n : (size_t)c->p.nloc;
+    HIPCHECK(hipStreamSynchronize(c->stream));
+    std::vector<uint32_t> hs((size_t)t * rows), hr(hs.size());
+    if (t > 0) {
+      HIPCHECK(hipMemcpy(hs.data(), ms, sizeof(uint32_t) * hs.size(), hipMemcpyDeviceToHost));
+      HIPCHECK(hipMemcpy(hr.data(), mr, sizeof(uint32_t) * hr.size(), hipMemcpyDeviceToHost));
+    }
+    for (size_t i = 0; i < rows; i++)
+      for (int j = 0; j < t; j++) {
+        sent[i * t + j] = (int32_t)hs[(size_t)j * rows + i];
+        recv[i * t + j] = (int32_t)hr[(size_t)j * rows + i];
+      }
+    return GM_OK;
+  }
   if (t > c->f.tmax) return GM_EINVAL;
   TRY(f_settle(c));
   HIPCHECK(hipStreamSynchronize(c->stream));

@@ -54,4 +54,8 @@ struct PState {
   int32_t *recv_cnt;     // [K][G] records received from each shard, per chunk
   int32_t *shard_n0;     // [G+1] first node of every row shard (shard_n0[G] = n)
   uint32_t *err;
+  // msgcount analogue (gm_msgcount_record; nullptr = off): per tick and local node, view
+  // entries sent (fresh entries x targets, before loss) / received (after loss, lists merged)
+  uint32_t *mc_sent, *mc_recv;  // [mc_tmax][nloc]
+  int mc_tmax;
 };

@@ -163,7 +163,8 @@ __device__ __forceinline__ PPre p_preload(const PState &s, int t, const uint32_t
 
 // One node's tick on one wave. li: the node's local row (global index n0 + li);
 // pre.k: lists queued for it this tick.
-template <int H, bool BIG>
+// MC: the msgcount-recording instantiation (gm_msgcount_record); the others carry no trace of it
+template <int H, bool BIG, bool MC>
 __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, int li, int lane, unsigned char *base,
                                        int chunk, int r0) {
   int k = pre.k;
@@ -236,6 +237,8 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
   }
   // drop keys: one (t_send, src, dst) hash per delivered list, lane j for list j
   const bool dropping = s.drop_pct >= 0;
+  const bool mc = MC && t < s.mc_tmax;  // msgcount recording (wave-uniform)
+  int nrecv = 0;                                           // delivered entries kept (msgcount)
   uint64_t pairv = 0;
   if (dropping)
     pairv = gm_mix64(s.drop_seed ^ ((uint64_t)(uint32_t)(t - 1) << 48) ^ ((uint64_t)(uint32_t)sg << 24) ^
@@ -266,6 +269,7 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
         take = take && (int)(h % 100u) >= s.drop_pct;
       }
       if (take) (void)p_insert<H>(tid, thb, id, id, (uint32_t)e);
+      if (mc) nrecv += __builtin_popcountll(__ballot(take));
     }
   }
   PPROF(2);
@@ -640,6 +644,10 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
   if (s.G > 1 && lane == 0) s.recmask[li] = rmask;
   if (lane < 4) s.rowstat[(size_t)li * 4 + lane] = lane == 0 ? kk : lane == 1 ? cnt : lane == 2 ? numfailed : ng;
   if (lane == 0) s.ev_cnt[li] = nj | (nrem << 16);
+  if (mc && lane == 0) {  // entries sent = fresh entries of the final list x targets (MP1Node.cpp:372-375)
+    s.mc_sent[(size_t)t * s.nloc + li] = (uint32_t)(ng * (cnt - (numfailed - removed)));
+    s.mc_recv[(size_t)t * s.nloc + li] = (uint32_t)nrecv;
+  }
 #ifdef GM_P_PROFILE
   PPROF(8);
   if (lane == 0 && (li & 63) == 0) {
@@ -663,6 +671,7 @@ __device__ __forceinline__ void p_frozen(const PState &s, int t, int li, int lan
 }
 
 // rows [r0, r1) = chunk `chunk` of this shard's nodes
+template <bool MC>
 __global__ __launch_bounds__(256) void gm_p_tick_small(PState s, int t, const uint32_t *mtraw, int chunk, int r0,
                                                        int r1) {
   extern __shared__ __align__(16) unsigned char p_smem[];
@@ -678,10 +687,11 @@ __global__ __launch_bounds__(256) void gm_p_tick_small(PState s, int t, const ui
     if (lane == 0) s.big[r0 + atomicAdd(&s.big_cnt[chunk], 1)] = li;
     return;
   }
-  p_node<P_HS, false>(s, t, pre, li, lane, p_smem + (size_t)wave * PLds<P_HS>::bytes, chunk, r0);
+  p_node<P_HS, false, MC>(s, t, pre, li, lane, p_smem + (size_t)wave * PLds<P_HS>::bytes, chunk, r0);
 }
 
 // drains the worklist gm_p_tick_small filled (a fixed grid; every wave exits when the list is done)
+template <bool MC>
 __global__ __launch_bounds__(256) void gm_p_tick_big(PState s, int t, const uint32_t *mtraw, int chunk, int r0) {
   extern __shared__ __align__(16) unsigned char p_smem[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -689,7 +699,7 @@ __global__ __launch_bounds__(256) void gm_p_tick_big(PState s, int t, const uint
   for (int w = blockIdx.x * 4 + wave; w < nbig; w += gridDim.x * 4) {
     const int li = s.big[r0 + w];
     const PPre pre = p_preload(s, t, mtraw, li, lane, P_KMAX);
-    p_node<P_HB, true>(s, t, pre, li, lane, p_smem + (size_t)wave * PLds<P_HB>::bytes, chunk, r0);
+    p_node<P_HB, true, MC>(s, t, pre, li, lane, p_smem + (size_t)wave * PLds<P_HB>::bytes, chunk, r0);
   }
 }
 
@@ -831,10 +841,12 @@ hipError_t gm_launch_partial_reset(const PState &s, hipStream_t st) {
 // the node ticks of chunk c (rows [nloc*c/K, nloc*(c+1)/K))
 hipError_t gm_launch_partial_chunk(const PState &s, int t, const uint32_t *mtraw, int c, hipStream_t st) {
   const int r0 = (int)((int64_t)s.nloc * c / s.nchunk), r1 = (int)((int64_t)s.nloc * (c + 1) / s.nchunk);
+  const bool mc = s.mc_sent != nullptr && t < s.mc_tmax;
   if (r1 > r0)
-    hipLaunchKernelGGL(gm_p_tick_small, dim3((r1 - r0 + 3) / 4), dim3(256), 4 * PLds<P_HS>::bytes, st, s, t, mtraw, c,
-                       r0, r1);
-  hipLaunchKernelGGL(gm_p_tick_big, dim3(P_BIG_GRID), dim3(256), 4 * PLds<P_HB>::bytes, st, s, t, mtraw, c, r0);
+    hipLaunchKernelGGL(mc ? gm_p_tick_small<true> : gm_p_tick_small<false>, dim3((r1 - r0 + 3) / 4), dim3(256),
+                       4 * PLds<P_HS>::bytes, st, s, t, mtraw, c, r0, r1);
+  hipLaunchKernelGGL(mc ? gm_p_tick_big<true> : gm_p_tick_big<false>, dim3(P_BIG_GRID), dim3(256),
+                     4 * PLds<P_HB>::bytes, st, s, t, mtraw, c, r0);
   if (s.G > 1 && r1 > r0) {  // pack the chunk's records for the exchange
     const int nbq = (r1 - r0 + P_PACK - 1) / P_PACK;
     hipLaunchKernelGGL(gm_p_pack_count, dim3(s.G * nbq), dim3(P_PACK), 0, st, s, c, r0, r1, nbq);

@@ -126,4 +126,11 @@ struct SState {
   int32_t *plist[3];
   uint32_t *plist_cnt[3];
   int32_t *statusl[3];
+  // ---- msgcount analogue (gm_msgcount_record, single context; nullptr = off): per tick and
+  // row, gossip entries sent (fresh entries x targets, before loss) and received (after loss),
+  // EmulNet's sent_msgs / recv_msgs per entry message (EmulNet.cpp:111,172)
+  uint32_t *mc_sent, *mc_recv;  // [mc_tmax][n]
+  uint32_t *mc_fresh;           // [2][n] fresh entries of each row's payload, by tick parity
+  uint32_t *mc_rdrop;           // [n] entries a row received after keyed loss (DROP band kernel)
+  int mc_tmax;
 };

@@ -282,6 +282,7 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
     for (int w = 0; w < RPW; w++) kw = max(kw, __builtin_amdgcn_readlane(kl, w * LPR));
   }
   int npres = 0, nfail = 0, nev = 0;
+  int nkept = 0;     // DROP: delivered entries this lane kept after the keyed loss (msgcount)
   uint32_t evk = 0;  // 2 bits per cell: event kind
   bool esc_st = false;  // this lane stored escaped cells (announced in the (band, row) record)
   if (live) {
@@ -345,6 +346,7 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
           if (!nb) continue;
           const uint32_t h = (uint32_t)(gm_mix64(pair + (uint64_t)(s.c0 + colb + q)) >> 32);
           if ((int)(h % 100u) < drop_pct) continue;
+          nkept++;
           kk[q] = max(kk[q], nib_value(nb, wsrc + (size_t)sn * 2 * B + q));
         }
       }
@@ -552,6 +554,12 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
     const u32x2 ov = {unpk(nwv[0]), unpk(nwv[1])};
     __builtin_amdgcn_raw_buffer_store_b64(ov, prs, (uint32_t)(r * B + par * (B / 2) + li * 8), 0, GM_AUX_NT);
     if (band == 0 && li == 0) s.wtick[r] = t;
+  }
+  if (DROP && s.mc_rdrop) {  // msgcount: the row's kept entries (wave-uniform test)
+    int v = nkept;
+#pragma unroll
+    for (int o = 1; o < LPR; o <<= 1) v += __shfl_xor(v, o, 64);
+    if (live && li == 0 && v) atomicAdd(&s.mc_rdrop[r], (uint32_t)v);
   }
   // present cells per 64-column chunk (4 lanes) for the draw's rank-select, gathered
   // into the row's first lane: bytes 0..B/64-1 of the (band, row) record
@@ -981,6 +989,57 @@ __global__ __launch_bounds__(256) void gm_s_pick(SState s, int t) {
     stat[2] = (int)numfailed;
     stat[3] = n;
   }
+}
+
+// ------------------------------------------------------------ gm_s_msgcount
+// msgcount analogue of tick t (gm_msgcount_record), after gm_s_pick, one wave per row:
+// fresh = the row's non-zero payload nibbles of this tick (the entries it sends, MP1Node.cpp:
+// 372-375), sent = fresh x targets; received = the entries of its delivered lists -- the
+// senders' fresh counts of tick t-1, or the DROP band kernel's count of kept entries.
+__device__ __forceinline__ uint32_t nz_nibbles(uint32_t x) {
+  return (uint32_t)__builtin_popcount((x | (x >> 1) | (x >> 2) | (x >> 3)) & 0x11111111u);
+}
+template <int B>
+__global__ __launch_bounds__(256) void gm_s_msgcount(SState s, int t, int dropped) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= s.n) return;  // whole wave
+  const int par = t & 1, half = B / 2, tot = s.nb * half;
+  uint32_t f = 0;
+  for (int off = lane * 16; off < tot; off += 64 * 16) {  // 16-byte pieces never straddle a band
+    const int b = off / half, o = off % half;
+    const uint4 v = *(const uint4 *)(s.msg + ((size_t)b * s.n + r) * B + par * half + o);
+    f += nz_nibbles(v.x) + nz_nibbles(v.y) + nz_nibbles(v.z) + nz_nibbles(v.w);
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) f += __shfl_xor(f, o, 64);
+  if (lane == 0) {
+    const int32_t *stat = s.rowstat + (size_t)r * 4;
+    uint32_t recv = 0;
+    if (dropped) {
+      recv = s.mc_rdrop[r];
+      s.mc_rdrop[r] = 0;
+    } else {
+      const int k = min(stat[0], S_KMAX);  // 0 for rows not merged this tick
+      for (int q = 0; q < k; q++) recv += s.mc_fresh[(size_t)(par ^ 1) * s.n + s.inbox[par][(size_t)r * S_KMAX + q]];
+    }
+    s.mc_sent[(size_t)t * s.n + r] = (uint32_t)stat[3] * f;
+    s.mc_recv[(size_t)t * s.n + r] = recv;
+    s.mc_fresh[(size_t)par * s.n + r] = f;
+  }
+}
+
+hipError_t gm_launch_msgcount(const SState &s, int t, bool dropped, hipStream_t st) {
+  const dim3 g((s.n + 3) / 4), b(256);
+  switch (s.band) {
+    case 64: hipLaunchKernelGGL(gm_s_msgcount<64>, g, b, 0, st, s, t, dropped ? 1 : 0); break;
+    case 128: hipLaunchKernelGGL(gm_s_msgcount<128>, g, b, 0, st, s, t, dropped ? 1 : 0); break;
+    case 256: hipLaunchKernelGGL(gm_s_msgcount<256>, g, b, 0, st, s, t, dropped ? 1 : 0); break;
+    case 512: hipLaunchKernelGGL(gm_s_msgcount<512>, g, b, 0, st, s, t, dropped ? 1 : 0); break;
+    case 1024: hipLaunchKernelGGL(gm_s_msgcount<1024>, g, b, 0, st, s, t, dropped ? 1 : 0); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------- column-sharded mode

@@ -38,7 +38,8 @@ EXPORTS = ["gm_parse_conf", "gm_create", "gm_destroy", "gm_tick", "gm_sync", "gm
            "gm_dump_tables", "gm_tick_stats", "gm_set_timing", "gm_last_kernel_ms", "gm_crash_set", "gm_strerror",
            "gm_comm_unique_id", "gm_comm_init", "gm_shard_layout", "gm_shard_merge", "gm_shard_draw",
            "gm_shard_accept", "gm_shard_end_tick", "gm_shard_loopback", "gm_partial_loopback_tick",
-           "gm_shard_exchange_bytes", "gm_keep_events", "gm_event_totals", "gm_read_views", "gm_shard_stub"]
+           "gm_shard_exchange_bytes", "gm_keep_events", "gm_event_totals", "gm_read_views", "gm_shard_stub",
+           "gm_msgcount_record"]
 
 _lib = None
 
@@ -70,6 +71,7 @@ def load_library():
         "gm_event_counts": [ctypes.c_void_p, P(u64)], "gm_event_totals": [ctypes.c_void_p, P(u64)],
         "gm_keep_events": [ctypes.c_void_p, i32], "gm_shard_stub": [ctypes.c_void_p, i32], "gm_read_views": [ctypes.c_void_p, i32, i32, P(u64)],
         "gm_msgcount": [ctypes.c_void_p, i32, P(i32), P(i32)],
+        "gm_msgcount_record": [ctypes.c_void_p, i32],
         "gm_read_row": [ctypes.c_void_p, i32, i32, i32, P(i32), P(i32)],
         "gm_read_nodes": [ctypes.c_void_p, P(i32)],
         "gm_dump_tables": [ctypes.c_void_p, ctypes.c_char_p, sz, P(sz)],
@@ -223,9 +225,15 @@ class Simulator:
         self._call("gm_read_views", self.h, r0, count, _ptr(out, ctypes.c_uint64))
         return out
 
-    def msgcount(self, t):
-        sent = np.zeros((self.n, t), dtype=np.int32)
-        recv = np.zeros((self.n, t), dtype=np.int32)
+    def msgcount_record(self, tmax):
+        """SCALED / PARTIAL: record per-node entry counts for ticks < tmax (before the first tick)"""
+        self._call("gm_msgcount_record", self.h, tmax)
+
+    def msgcount(self, t, rows=None):
+        """[rows][t] sent / recv entry messages per node and tick (rows: this context's nodes)"""
+        rows = self.n if rows is None else rows
+        sent = np.zeros((rows, t), dtype=np.int32)
+        recv = np.zeros((rows, t), dtype=np.int32)
         self._call("gm_msgcount", self.h, t, _ptr(sent), _ptr(recv))
         return sent, recv
 

@@ -159,8 +159,19 @@ int gm_event_counts(gm_ctx *ctx, uint64_t counts[6]);
  * band) cell). PARTIAL: GM_EUNSUPPORTED (views churn ~V joins per node and tick). */
 int gm_event_totals(gm_ctx *ctx, uint64_t totals[6]);
 
-/* sent/recv message counts per node id 1..n for ticks [0, t): out arrays [n][t] */
+/* sent/recv message counts per node id 1..n for ticks [0, t): out arrays [n][t].
+ * FAITHFUL: EmulNet's sent_msgs / recv_msgs (EmulNet.cpp:111,172), always recorded.
+ * SCALED / PARTIAL: the same per-entry-message counts in the list-gossip regime, recorded
+ * once gm_msgcount_record was called (GM_ESTATE otherwise): sent = entries a node put on
+ * the wire (its fresh entries x its targets, before loss: the loss is decided in flight),
+ * recv = entries of the lists delivered to it that survived the loss (PARTIAL: of the <= 16
+ * lists it merges). Gossip LIST entries only (the ramp's JOINREQ / JOINREP are not counted).
+ * A PARTIAL row shard reports its own nodes ([nloc][t]). */
 int gm_msgcount(gm_ctx *ctx, int32_t t, int32_t *sent, int32_t *recv);
+/* SCALED / PARTIAL: start recording the per-node counts of gm_msgcount for ticks < tmax
+ * (device history of 8 * tmax bytes per node). Only before the first tick (GM_ESTATE
+ * after); single-context SCALED only (GM_EUNSUPPORTED for column shards); FAITHFUL: no-op. */
+int gm_msgcount_record(gm_ctx *ctx, int32_t tmax);
 
 /* Dense readback of observer row r: hb/ts per subject column (absent -> -1),
  * columns [c0, c0+len) of this context's shard (c0 relative to the shard start). */

@@ -208,6 +208,9 @@ struct oc_ctx {
   int intro_last;
   /* test telemetry: updateMyPos quirk firings and the largest start-tick gap self -> target */
   int64_t quirk_n, quirk_maxgap;
+  /* SCALED msgcount analogue of the last tick (EmulNet.cpp:111,172 per entry message):
+   * gossip entries node i put on the wire (fresh entries x targets) / received after loss */
+  int32_t *mc_sent, *mc_recv;
 };
 
 static int is_scaled(const oc_ctx *c) { return c->cfg.mode == OC_SCALED; }
@@ -409,6 +412,7 @@ static void node_loop_ops(oc_ctx *c, int idx, const entry *new_nodes, int n_new)
   }
   c->ntgt_next[idx] = n;
   for (int k = 0; k < n; k++) c->tgt_next[(size_t)idx * FANOUT + k] = gossip[k].id - 1;
+  c->mc_sent[idx] = s->n * n;
   free(gossip);
 }
 
@@ -475,6 +479,7 @@ static void scaled_recv(oc_ctx *c, int idx) {
           uint32_t h = (uint32_t)(mix64(pair + (uint64_t)(p->ids[e] - 1)) >> 32);
           if ((int)(h % 100u) < c->cfg.drop_pct) continue;
         }
+        c->mc_recv[idx]++;
         update_list(c, idx, p->ids[e], 0, p->hbs[e]);
       }
     }
@@ -511,6 +516,8 @@ static void mp1_run(oc_ctx *c) {
     return;
   }
   c->nev = 0;
+  memset(c->mc_sent, 0, sizeof(int32_t) * (size_t)c->n);
+  memset(c->mc_recv, 0, sizeof(int32_t) * (size_t)c->n);
   const int ramp = c->cfg.init_mode == 2;
   for (int i = c->n - 1; i >= 0; i--) {
     const int start = (int)(0.25 * i); /* Application.cpp:130,143 (STEP_RATE 0.25) */
@@ -649,6 +656,8 @@ oc_ctx *oc_create(const oc_config *cfg) {
     c->tgt_next = (int32_t *)calloc((size_t)c->n * FANOUT, sizeof(int32_t));
     c->ntgt = (int32_t *)calloc((size_t)c->n, sizeof(int32_t));
     c->ntgt_next = (int32_t *)calloc((size_t)c->n, sizeof(int32_t));
+    c->mc_sent = (int32_t *)calloc((size_t)c->n, sizeof(int32_t));
+    c->mc_recv = (int32_t *)calloc((size_t)c->n, sizeof(int32_t));
     c->crash = (int32_t *)calloc((size_t)(cfg->crash_count > 0 ? cfg->crash_count : 1), sizeof(int32_t));
     if (cfg->crash_count > 0 && oc_crash_set(c->n, cfg->crash_count, cfg->crash_seed, c->crash)) {
       oc_destroy(c);
@@ -669,6 +678,7 @@ void oc_destroy(oc_ctx *c) {
   }
   free(c->snaps); free(c->snaps_next);
   free(c->tgt); free(c->tgt_next); free(c->ntgt); free(c->ntgt_next);
+  free(c->mc_sent); free(c->mc_recv);
   free(c->crash); free(c->ev);
   free(c->nodes);
   free(c->buff.v);
@@ -721,6 +731,15 @@ const char *oc_msgcount(oc_ctx *c, size_t *len) {
   }
   *len = c->tmp.n;
   return c->tmp.p;
+}
+
+/* SCALED: per-node gossip entries sent (fresh entries x targets, before loss) and received
+ * (after loss) in the last tick; JOINREQ/JOINREP of the ramp are not counted */
+int oc_last_msgcount(const oc_ctx *c, int32_t *sent, int32_t *recv) {
+  if (!is_scaled(c)) return -1;
+  memcpy(sent, c->mc_sent, sizeof(int32_t) * (size_t)c->n);
+  memcpy(recv, c->mc_recv, sizeof(int32_t) * (size_t)c->n);
+  return 0;
 }
 
 /* state of the tick just finished, in oracle/shim/dump_main.cpp's line format */
@@ -889,6 +908,8 @@ struct op_ctx {
   /* scratch */
   int32_t *cid, *chb, *cown;
   int ccap;
+  /* msgcount analogue of the last tick: entries put on the wire / received after loss */
+  int32_t *mc_sent, *mc_recv;
 };
 
 static void op_emit(op_ctx *c, int logger, int kind, int32_t subject) {
@@ -954,6 +975,8 @@ op_ctx *op_create(const op_config *cfg) {
   if (cfg->crash_count > 0) oc_crash_set(n, cfg->crash_count, cfg->crash_seed, c->crash);
   c->rcv_off = (int32_t *)calloc((size_t)n + 1, sizeof(int32_t));
   c->rcv_src = (int32_t *)calloc((size_t)n * FANOUT + 1, sizeof(int32_t));
+  c->mc_sent = (int32_t *)calloc((size_t)n, sizeof(int32_t));
+  c->mc_recv = (int32_t *)calloc((size_t)n, sizeof(int32_t));
   return c;
 }
 
@@ -969,6 +992,7 @@ void op_destroy(op_ctx *c) {
   free(c->crash); free(c->ev); free(c->dump.p);
   free(c->cid); free(c->chb); free(c->cown);
   free(c->rcv_off); free(c->rcv_src);
+  free(c->mc_sent); free(c->mc_recv);
   free(c);
 }
 
@@ -1010,6 +1034,7 @@ static void op_node(op_ctx *c, int i, pcand *m) {
         if ((int)(h % 100u) < c->cfg.drop_pct) continue;
       }
       m[cnt].id = sp->ids[e]; m[cnt].hb = sp->hbs[e]; m[cnt].own = 0; cnt++;
+      c->mc_recv[i]++;
     }
   }
   /* merge per id (updatelistCallBack): the largest hb; "own" if the id was in i's list */
@@ -1076,12 +1101,15 @@ static void op_node(op_ctx *c, int i, pcand *m) {
   sn->n = 0;
   for (int k = 0; k < cnt; k++)
     if (t - (m[k].hb + 1) / 2 < TFAIL) { sn->ids[sn->n] = m[k].id; sn->hbs[sn->n] = m[k].hb; sn->n++; }
+  c->mc_sent[i] = sn->n * ng;
 }
 
 int op_tick(op_ctx *c) {
   const int n = c->n;
   pcand *m = (pcand *)malloc(sizeof(pcand) * (size_t)c->V * (OP_KP + 2));
   c->nev = 0;
+  memset(c->mc_sent, 0, sizeof(int32_t) * (size_t)n);
+  memset(c->mc_recv, 0, sizeof(int32_t) * (size_t)n);
   /* counting sort of last tick's (sender, target) pairs by target, senders ascending */
   memset(c->rcv_off, 0, sizeof(int32_t) * (size_t)(n + 1));
   for (int s = 0; s < n; s++)
@@ -1112,6 +1140,13 @@ int op_tick(op_ctx *c) {
 }
 
 int op_time(const op_ctx *c) { return c->t; }
+
+/* per-node entries sent (fresh entries of the final list x targets, before loss) and
+ * received (entries of the merged lists that survived the loss) in the last tick */
+void op_last_msgcount(const op_ctx *c, int32_t *sent, int32_t *recv) {
+  memcpy(sent, c->mc_sent, sizeof(int32_t) * (size_t)c->n);
+  memcpy(recv, c->mc_recv, sizeof(int32_t) * (size_t)c->n);
+}
 
 size_t op_events(op_ctx *c, const oc_event **ev) {
   *ev = c->ev;

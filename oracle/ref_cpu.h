@@ -75,6 +75,8 @@ const char *oc_dump(oc_ctx *c, size_t *len);
 size_t oc_events(oc_ctx *c, const oc_event **ev);
 /* dense readback: hb/ts of row r (absent -> -1), len n */
 int oc_row(oc_ctx *c, int r, int32_t *hb, int32_t *ts);
+/* SCALED: per-node gossip entries sent (before loss) / received (after loss) in the last tick */
+int oc_last_msgcount(const oc_ctx *c, int32_t *sent, int32_t *recv);
 /* node state: inited, inGroup, bFailed, heartbeat counter */
 int oc_node(oc_ctx *c, int r, int32_t *state4);
 /* test telemetry: [0] = updateMyPos quirk firings, [1] = largest start-tick gap self -> target */
@@ -102,6 +104,8 @@ int op_time(const op_ctx *c);
 size_t op_events(op_ctx *c, const oc_event **ev);
 /* "t i 1 1 failed hbctr cnt id:hb:ts ..." per node, ts = (hb+1)/2 */
 const char *op_dump(op_ctx *c, size_t *len);
+/* per-node entries sent (before loss) / received (after loss) in the last tick */
+void op_last_msgcount(const op_ctx *c, int32_t *sent, int32_t *recv);
 uint64_t op_evict_key(uint64_t view_seed, int32_t t, int32_t obs, int32_t id);
 
 /* CPU-baseline sample: time node-ticks of the SCALED workload at size n (see ref_cpu.c) */

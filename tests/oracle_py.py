@@ -61,6 +61,9 @@ def lib():
         L.oc_row.argtypes = [ctypes.c_void_p, ctypes.c_int, P(ctypes.c_int32), P(ctypes.c_int32)]
         L.oc_node.argtypes = [ctypes.c_void_p, ctypes.c_int, P(ctypes.c_int32)]
         L.oc_quirks.argtypes = [ctypes.c_void_p, P(ctypes.c_int64)]
+        L.oc_last_msgcount.argtypes = [ctypes.c_void_p, P(ctypes.c_int32), P(ctypes.c_int32)]
+        L.op_last_msgcount.argtypes = [ctypes.c_void_p, P(ctypes.c_int32), P(ctypes.c_int32)]
+        L.op_last_msgcount.restype = None
         L.oc_quirks.restype = None
         L.oc_crash_set.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint64, P(ctypes.c_int32)]
         L.oc_srand.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
@@ -149,6 +152,14 @@ class Oracle:
         self.L.oc_node(self.h, r, _i32p(st))
         return st
 
+    def last_msgcount(self):
+        """SCALED: per-node gossip entries sent (before loss) / received (after loss) last tick"""
+        sent = np.zeros(self.n, dtype=np.int32)
+        recv = np.zeros(self.n, dtype=np.int32)
+        if self.L.oc_last_msgcount(self.h, _i32p(sent), _i32p(recv)):
+            raise RuntimeError("oc_last_msgcount: SCALED only")
+        return sent, recv
+
 
 class PartialOracle:
     """PARTIAL mode (V-entry views, scenario S-C): the oracle IS the specification."""
@@ -187,6 +198,13 @@ class PartialOracle:
         p = ctypes.POINTER(OcEvent)()
         n = self.L.op_events(self.h, ctypes.byref(p))
         return [(p[k].t, p[k].logger, p[k].kind, p[k].subject) for k in range(n)]
+
+    def last_msgcount(self):
+        """per-node entries sent (before loss) / received (after loss) in the last tick"""
+        sent = np.zeros(self.n, dtype=np.int32)
+        recv = np.zeros(self.n, dtype=np.int32)
+        self.L.op_last_msgcount(self.h, _i32p(sent), _i32p(recv))
+        return sent, recv
 
 
 def crash_set(n, count, seed):
