@@ -79,7 +79,32 @@ def parse():
                    help="diagnostics (S-A): keyed per-entry drops on every tick (the drop path of gm_s_band)")
     p.add_argument("--force-shard", action="store_true",
                    help="diagnostics: at N=1 run the column-shard protocol with RCCL over one rank")
+    p.add_argument("--pmc", action="store_true",
+                   help="N=1: after the timed run, measure roofline.traffic live (two rocprofv3 --pmc passes "
+                        "of this workload, FETCH_SIZE and WRITE_SIZE, as scripts/gpu.sh pmc_sa / pmc_sc)")
     return p.parse_args()
+
+
+def live_traffic(kernel, layout, n, extra):
+    """HBM bytes per launch of `kernel` measured now: this bench (5 ticks) under two rocprofv3
+    PMC passes (each counter in a run of its own, --kernel-trace only), reduced by
+    scripts/pmc_traffic.py (gfx950 FETCH_SIZE x2 correction). Child processes, so the
+    measured run and this one never share a profiler."""
+    import subprocess
+    import tempfile
+    d = tempfile.mkdtemp(prefix="gm_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
+    child = [sys.executable, os.path.abspath(__file__), "--no-cpu", "--steps", "5", "--warmup", "1"] + extra
+    for ctr, sub in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
+        cmd = ["rocprofv3", "--pmc", ctr, "--kernel-trace", "--output-format", "csv", "-d", os.path.join(d, sub),
+               "-o", "p", "--"] + child
+        subprocess.run(cmd, timeout=300, check=True, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    out = os.path.join(d, "traffic.json")
+    subprocess.run([sys.executable, os.path.join(REPO, "scripts", "pmc_traffic.py"), "--kernel", kernel, "--fetch",
+                    os.path.join(d, "fetch"), "--write", os.path.join(d, "write"), "--layout", layout, "--n", str(n),
+                    "--out", out], timeout=120, check=True, stdout=subprocess.DEVNULL)
+    with open(out) as f:
+        tj = json.load(f)
+    return tj["hbm_bytes_per_launch"], f"live: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this workload ({d})"
 
 
 def main():
@@ -225,6 +250,10 @@ def main():
         "check": {"removed_rank0": tot["removed"], "joined_rank0": tot["joined"], "removed_all_expected":
                   (n - ncrash) * ncrash if removed_ok else None},
     }
+    if a.pmc and world == 1:
+        sim.close()  # the PMC passes are child processes with their own context
+        out["roofline"]["traffic"], out["roofline"]["traffic_source"] = live_traffic(
+            "gm_s_band", LAYOUT_SA, n, ["--cluster", str(n)] + (["--drop-pct", str(a.drop_pct)] if a.drop_pct else []))
     if rank == 0 and world == 1 and not a.no_cpu:
         sys.path.insert(0, os.path.join(REPO, "tests"))
         import oracle_py  # the oracle is the CPU baseline here, never the measured path
@@ -348,6 +377,10 @@ def main_partial(a):
     }
     if world > 1:
         out["roofline"]["note"] = "rank 0's local kernels (its n/G nodes)"
+    if a.pmc and world == 1:
+        sim.close()  # the PMC passes are child processes with their own context
+        out["roofline"]["traffic"], out["roofline"]["traffic_source"] = live_traffic(
+            "gm_p_tick", "partial-v32", n, ["--scenario", "S-C", "--cluster", str(n), "--view", str(V)])
     if rank == 0 and world == 1 and not a.no_cpu:
         sys.path.insert(0, os.path.join(REPO, "tests"))
         import oracle_py  # the oracle is the CPU baseline here, never the measured path
