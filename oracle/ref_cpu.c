@@ -412,7 +412,7 @@ static void node_loop_ops(oc_ctx *c, int idx, const entry *new_nodes, int n_new)
   }
   c->ntgt_next[idx] = n;
   for (int k = 0; k < n; k++) c->tgt_next[(size_t)idx * FANOUT + k] = gossip[k].id - 1;
-  c->mc_sent[idx] = s->n * n;
+  if (c->mc_sent) c->mc_sent[idx] = s->n * n;  /* (oc_bench_sample's context counts nothing) */
   free(gossip);
 }
 
@@ -479,7 +479,7 @@ static void scaled_recv(oc_ctx *c, int idx) {
           uint32_t h = (uint32_t)(mix64(pair + (uint64_t)(p->ids[e] - 1)) >> 32);
           if ((int)(h % 100u) < c->cfg.drop_pct) continue;
         }
-        c->mc_recv[idx]++;
+        if (c->mc_recv) c->mc_recv[idx]++;
         update_list(c, idx, p->ids[e], 0, p->hbs[e]);
       }
     }
