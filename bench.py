@@ -107,8 +107,31 @@ def live_traffic(kernel, layout, n, extra):
     return tj["hbm_bytes_per_launch"], f"live: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this workload ({d})"
 
 
+_JSON_FD = None
+
+
+def quiet_stdout():
+    """The bench's stdout carries exactly ONE JSON line: native libraries' own stdout
+    (RCCL's version banner at communicator init, ...) goes to stderr instead."""
+    global _JSON_FD
+    if _JSON_FD is None:
+        sys.stdout.flush()
+        _JSON_FD = os.dup(1)
+        os.dup2(2, 1)
+
+
+def emit(out):
+    line = (json.dumps(out) + "\n").encode()
+    if _JSON_FD is None:
+        sys.stdout.write(line.decode())
+        sys.stdout.flush()
+    else:
+        os.write(_JSON_FD, line)
+
+
 def main():
     a = parse()
+    quiet_stdout()
     if a.scenario == "S-C":
         return main_partial(a)
     a.cluster = a.cluster or 65536
@@ -263,7 +286,7 @@ def main():
                                          f"({secs:.1f} s): per node-tick 5 gossip lists x {n} entries merged via "
                                          "updatelistCallBack + nodeLoopOps sweep/sort/draw (oracle/ref_cpu.c)"}
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        emit(out)
     if dist is not None:
         dist.destroy_process_group()
 
@@ -399,7 +422,7 @@ def main_partial(a):
                                "sample": f"{ticks} steady ticks of an N={ns} S-C cluster (V={V}, 5% drop) on one host "
                                          f"core ({secs:.1f} s, oracle/ref_cpu.c op_tick)"}
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        emit(out)
     sim.close()
     if dist is not None:
         dist.destroy_process_group()

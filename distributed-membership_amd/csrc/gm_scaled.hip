@@ -974,16 +974,15 @@ __global__ __launch_bounds__(256) void gm_s_pick(SState s, int t) {
       }
     }
   }
+  if (lane < n) {  // delivery: one target per lane, the n appends in flight together (the targets
+                   // are wave-uniform; an inbox's order is free: the merge is a max)
+    const int dst = lane == 0 ? g0 : lane == 1 ? g1 : lane == 2 ? g2 : lane == 3 ? g3 : g4;
+    s.targets[(size_t)r * GM_FANOUT + lane] = dst;
+    const int slot = atomicAdd(&s.inbox_cnt[par ^ 1][dst], 1);
+    if (slot < S_KMAX) s.inbox[par ^ 1][(size_t)dst * S_KMAX + slot] = r;
+    else atomicOr(s.err, GM_ERR_INBOX);
+  }
   if (lane == 0) {
-    int32_t *cnt_out = s.inbox_cnt[par ^ 1];
-    const int g[GM_FANOUT] = {g0, g1, g2, g3, g4};
-    for (int q = 0; q < n; q++) {
-      const int dst = g[q];
-      s.targets[(size_t)r * GM_FANOUT + q] = dst;
-      const int slot = atomicAdd(&cnt_out[dst], 1);
-      if (slot < S_KMAX) s.inbox[par ^ 1][(size_t)dst * S_KMAX + slot] = r;
-      else atomicOr(s.err, GM_ERR_INBOX);
-    }
     stat[0] = k;
     stat[1] = (int)size;
     stat[2] = (int)numfailed;
@@ -1229,11 +1228,15 @@ __global__ __launch_bounds__(256) void gm_s_accept(SState s, int t, int D, int i
   s.pending[r] = 0;
   const int par = t & 1;
   int32_t *cnt_out = s.inbox_cnt[par ^ 1];
-  for (int q = 0; q < n; q++) {
-    const int dst = g[q];
-    s.targets[(size_t)r * GM_FANOUT + q] = dst;
-    const int slot = atomicAdd(&cnt_out[dst], 1);
-    if (slot < S_KMAX) s.inbox[par ^ 1][(size_t)dst * S_KMAX + slot] = r;
+  int slot[GM_FANOUT];
+#pragma unroll
+  for (int q = 0; q < GM_FANOUT; q++)  // the row's appends in flight together, then their stores
+    if (q < n) slot[q] = atomicAdd(&cnt_out[g[q]], 1);
+#pragma unroll
+  for (int q = 0; q < GM_FANOUT; q++) {
+    if (q >= n) continue;
+    s.targets[(size_t)r * GM_FANOUT + q] = g[q];
+    if (slot[q] < S_KMAX) s.inbox[par ^ 1][(size_t)g[q] * S_KMAX + slot[q]] = r;
     else atomicOr(s.err, GM_ERR_INBOX);
   }
   s.rowstat[(size_t)r * 4 + 3] = n;
