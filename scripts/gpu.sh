@@ -14,6 +14,7 @@
 #   pmc_sa     FETCH_SIZE / WRITE_SIZE passes of S-A    -> $O/pmc_sa_{fetch,write}/ + traffic json
 #   mix_sa     SQ instruction mix of S-A (one --pmc pass)  -> $O/mix_sa/
 #   pmc_sc     FETCH_SIZE / WRITE_SIZE passes of S-C    -> $O/pmc_sc_{fetch,write}/ + traffic json
+#   mix_sc     SQ instruction mix / wave-cycle split of S-C (one --pmc pass) -> $O/mix_sc/
 #   faithful   ./Application on the three testcases + N = 70, timed -> $O/faithful_wall.txt
 #   prof_faithful rocprofv3 --kernel-trace --stats of ./Application at N = 70 -> $O/prof_n70/
 #
@@ -49,6 +50,8 @@ run_step() {
               --layout byte-band --out $O/traffic_n65536.json > $O/pmc_sa.txt 2>&1 ;;
     mix_sa) timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY \
               --kernel-trace --output-format csv -d $O/mix_sa -o p -- python3 bench.py --no-cpu --steps 5 --warmup 1 > $O/mix_sa.log 2>&1 ;;
+    mix_sc) timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+              --kernel-trace --output-format csv -d $O/mix_sc -o p -- python3 bench.py --scenario S-C --no-cpu --steps 3 --warmup 1 > $O/mix_sc.log 2>&1 ;;
     pmc_sc) timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/pmc_sc_fetch -o p -- \
               python3 bench.py --scenario S-C --no-cpu --steps 3 --warmup 1 > $O/pmc_sc_fetch.log 2>&1 &&
             timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/pmc_sc_write -o p -- \
