@@ -113,6 +113,13 @@ static thread_local char g_errbuf[256];
     }                                                                                 \
   } while (0)
 
+// inbox slots per receiver: the compiled capacity; GM_INBOX_CAP (diagnostics, tests) lowers it
+// to show that an overflow fails loudly (GM_ERR_INBOX -> GM_ERANGE), never silently
+static int inbox_cap(int cap) {
+  const char *e = getenv("GM_INBOX_CAP");
+  return e ? std::max(1, std::min(cap, atoi(e))) : cap;
+}
+
 template <class T>
 static int dalloc(gm_ctx *c, T **p, size_t count) {
   void *q = nullptr;
@@ -337,6 +344,7 @@ static int create_scaled(gm_ctx *c) {
   TRY(dalloc(c, &s.twide, cells));   // 16-bit cells of the escaped bytes
   c->nt = !(getenv("GM_NT") && !atoi(getenv("GM_NT")));  // non-temporal table streams, default on
   s.pipe_waves = getenv("GM_BAND_PIPE") ? std::max(0, atoi(getenv("GM_BAND_PIPE"))) : 0;
+  s.kcap = inbox_cap(S_KMAX);
   c->shard_sync = getenv("GM_SHARD_SYNC") ? (atoi(getenv("GM_SHARD_SYNC")) ? 1 : 0) : -1;
   TRY(dalloc(c, &s.msg, cells));        // nibbles: 2 parities x band/2 bytes per (band, row)
   TRY(dalloc(c, &s.wide, 2 * cells));   // escape bytes: 2 parities x band
@@ -462,6 +470,7 @@ static int create_partial(gm_ctx *c) {
   c->p_sharded = G > 1 || (getenv("GM_FORCE_SHARD") && atoi(getenv("GM_FORCE_SHARD")) == 1);
   // row shards pipeline their exchange over K chunks of their nodes (GM_CHUNKS, default 4)
   p.nchunk = c->p_sharded ? (getenv("GM_CHUNKS") ? atoi(getenv("GM_CHUNKS")) : 4) : 1;
+  p.kcap = inbox_cap(P_KMAX);
   if (p.nchunk < 1 || p.nchunk > 64) return GM_EINVAL;
   TRY(dalloc(c, &p.big_cnt, p.nchunk));
   if (c->p_sharded) {

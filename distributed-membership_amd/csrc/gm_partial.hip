@@ -602,7 +602,7 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
     s.targets[(size_t)li * GM_FANOUT + lane] = dst;
     if (owner == s.rank) {
       const int slot = atomicAdd(&s.inbox_cnt[par ^ 1][dst - s.n0], 1);
-      if (slot < P_KMAX) s.inbox[par ^ 1][(size_t)(dst - s.n0) * P_KMAX + slot] = li;
+      if (slot < s.kcap) s.inbox[par ^ 1][(size_t)(dst - s.n0) * P_KMAX + slot] = li;
       else atomicOr(s.err, GM_ERR_INBOX);
     }
   }
@@ -764,7 +764,7 @@ __global__ __launch_bounds__(256) void gm_p_unpack(PState s, int t, int base, in
       continue;
     }
     const int slot = atomicAdd(&s.inbox_cnt[par ^ 1][d], 1);
-    if (slot < P_KMAX) s.inbox[par ^ 1][(size_t)d * P_KMAX + slot] = s.nloc + j;
+    if (slot < s.kcap) s.inbox[par ^ 1][(size_t)d * P_KMAX + slot] = s.nloc + j;
     else atomicOr(s.err, GM_ERR_INBOX);
   }
 }

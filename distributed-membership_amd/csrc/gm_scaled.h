@@ -133,4 +133,5 @@ struct SState {
   uint32_t *mc_fresh;           // [2][n] fresh entries of each row's payload, by tick parity
   uint32_t *mc_rdrop;           // [n] entries a row received after keyed loss (DROP band kernel)
   int mc_tmax;
+  int kcap;                     // inbox slots used (S_KMAX; lowered only by the diagnostics env GM_INBOX_CAP)
 };

@@ -979,7 +979,7 @@ __global__ __launch_bounds__(256) void gm_s_pick(SState s, int t) {
     const int dst = lane == 0 ? g0 : lane == 1 ? g1 : lane == 2 ? g2 : lane == 3 ? g3 : g4;
     s.targets[(size_t)r * GM_FANOUT + lane] = dst;
     const int slot = atomicAdd(&s.inbox_cnt[par ^ 1][dst], 1);
-    if (slot < S_KMAX) s.inbox[par ^ 1][(size_t)dst * S_KMAX + slot] = r;
+    if (slot < s.kcap) s.inbox[par ^ 1][(size_t)dst * S_KMAX + slot] = r;
     else atomicOr(s.err, GM_ERR_INBOX);
   }
   if (lane == 0) {
@@ -1109,7 +1109,7 @@ __global__ __launch_bounds__(256) void gm_s_draw(SState s, int t, int round, int
         for (int q = 0; q < nj; q++) {
           s.targets[(size_t)r * GM_FANOUT + q] = jn[q];
           const int slot = atomicAdd(&cnt_out[jn[q]], 1);
-          if (slot < S_KMAX) s.inbox[(t & 1) ^ 1][(size_t)jn[q] * S_KMAX + slot] = r;
+          if (slot < s.kcap) s.inbox[(t & 1) ^ 1][(size_t)jn[q] * S_KMAX + slot] = r;
           else atomicOr(s.err, GM_ERR_INBOX);
         }
       }
@@ -1236,7 +1236,7 @@ __global__ __launch_bounds__(256) void gm_s_accept(SState s, int t, int D, int i
   for (int q = 0; q < GM_FANOUT; q++) {
     if (q >= n) continue;
     s.targets[(size_t)r * GM_FANOUT + q] = g[q];
-    if (slot[q] < S_KMAX) s.inbox[par ^ 1][(size_t)g[q] * S_KMAX + slot[q]] = r;
+    if (slot[q] < s.kcap) s.inbox[par ^ 1][(size_t)g[q] * S_KMAX + slot[q]] = r;
     else atomicOr(s.err, GM_ERR_INBOX);
   }
   s.rowstat[(size_t)r * 4 + 3] = n;
