@@ -110,6 +110,20 @@ def live_traffic(kernel, layout, n, extra):
 _JSON_FD = None
 
 
+def host_cpu():
+    """model name and logical CPU count of the host the CPU baseline ran on"""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return f"{model}, {os.cpu_count()} logical CPUs visible"
+
+
 def quiet_stdout():
     """The bench's stdout carries exactly ONE JSON line: native libraries' own stdout
     (RCCL's version banner at communicator init, ...) goes to stderr instead."""
@@ -282,6 +296,7 @@ def main():
         import oracle_py  # the oracle is the CPU baseline here, never the measured path
         nodes, secs = oracle_py.bench_sample(n, lists=5, min_seconds=a.cpu_seconds)
         out["cpu_baseline"] = {"value": nodes / secs, "unit": "node-ticks/s", "cores": 1, "kind": "port",
+                               "host": host_cpu(),
                                "sample": f"{nodes} node-ticks of the N={n} SCALED workload on one host core "
                                          f"({secs:.1f} s): per node-tick 5 gossip lists x {n} entries merged via "
                                          "updatelistCallBack + nodeLoopOps sweep/sort/draw (oracle/ref_cpu.c)"}
@@ -419,6 +434,7 @@ def main_partial(a):
             secs += time.perf_counter() - c0
             ticks += 1
         out["cpu_baseline"] = {"value": ns * ticks / secs, "unit": "node-ticks/s", "cores": 1, "kind": "port",
+                               "host": host_cpu(),
                                "sample": f"{ticks} steady ticks of an N={ns} S-C cluster (V={V}, 5% drop) on one host "
                                          f"core ({secs:.1f} s, oracle/ref_cpu.c op_tick)"}
     if rank == 0:
