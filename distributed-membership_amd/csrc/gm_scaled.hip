@@ -761,25 +761,21 @@ __device__ __forceinline__ void gm_row_totals(const SState &s, int r, int lane, 
   const int nb = s.nb, perb = (nb + 63) >> 6;
   const int b0 = min(nb, lane * perb), b1 = min(nb, b0 + perb);
   uint32_t fs = 0, ps = 0;
+  uint4 rec0 = make_uint4(0u, 0u, 0u, 0u);  // the lane's first (band, row) record (all of them when nb <= 64)
   for (int b = b0; b < b1; b++) {
-    const uint32_t v = s.brec[(size_t)b * s.n + r].z;
-    fs += S_BC_FAIL(v);
-    ps += S_BC_PRES(v);
+    const uint4 rc = s.brec[(size_t)b * s.n + r];
+    if (b == b0) rec0 = rc;
+    fs += S_BC_FAIL(rc.z);
+    ps += S_BC_PRES(rc.z);
   }
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) fs += __shfl_xor(fs, o, 64);
-  nfail = fs;
-  uint32_t x = ps;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
-  }
-  size = __shfl(x, 63, 64);
+  // wave sums / prefix on DPP (no LDS round trips): inclusive scans, totals from lane 63
+  nfail = (uint32_t)__builtin_amdgcn_readlane(dpp_scan((int)fs), 63);
+  const uint32_t x = (uint32_t)dpp_scan((int)ps);
+  size = (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
   if (pre) {
     uint32_t a = x - ps;
     for (int b = b0; b < b1; b++) {
-      const uint2 pc = *(const uint2 *)&s.brec[(size_t)b * s.n + r];
+      const uint2 pc = b == b0 ? make_uint2(rec0.x, rec0.y) : *(const uint2 *)&s.brec[(size_t)b * s.n + r];
       const uint64_t v = (uint64_t)pc.x | ((uint64_t)pc.y << 32);
 #pragma unroll
       for (int c = 0; c < CPB; c++) {
