@@ -776,6 +776,17 @@ int oc_row(oc_ctx *c, int r, int32_t *hb, int32_t *ts) {
   return 0;
 }
 
+/* SCALED: fail these nodes now, i.e. at the end of the tick just run (the host side of
+ * Application::fail, Application.cpp:184-196, with the victims chosen by the caller) */
+int oc_set_failed(oc_ctx *c, const int32_t *idx, int k) {
+  if (!is_scaled(c)) return -1;
+  for (int j = 0; j < k; j++) {
+    if (idx[j] < 0 || idx[j] >= c->n) return -1;
+    c->nodes[idx[j]].failed = 1;
+  }
+  return 0;
+}
+
 int oc_node(oc_ctx *c, int r, int32_t *st) {
   if (r < 0 || r >= c->n) return -1;
   node *nd = &c->nodes[r];

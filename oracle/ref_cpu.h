@@ -79,6 +79,8 @@ int oc_row(oc_ctx *c, int r, int32_t *hb, int32_t *ts);
 int oc_last_msgcount(const oc_ctx *c, int32_t *sent, int32_t *recv);
 /* node state: inited, inGroup, bFailed, heartbeat counter */
 int oc_node(oc_ctx *c, int r, int32_t *state4);
+/* SCALED: fail nodes idx[0..k) at the end of the tick just run (host fail() with caller-chosen victims) */
+int oc_set_failed(oc_ctx *c, const int32_t *idx, int k);
 /* test telemetry: [0] = updateMyPos quirk firings, [1] = largest start-tick gap self -> target */
 void oc_quirks(const oc_ctx *c, int64_t out[2]);
 /* the crash set the SCALED driver uses (host fault injection) */

@@ -61,6 +61,7 @@ def lib():
         L.oc_row.argtypes = [ctypes.c_void_p, ctypes.c_int, P(ctypes.c_int32), P(ctypes.c_int32)]
         L.oc_node.argtypes = [ctypes.c_void_p, ctypes.c_int, P(ctypes.c_int32)]
         L.oc_quirks.argtypes = [ctypes.c_void_p, P(ctypes.c_int64)]
+        L.oc_set_failed.argtypes = [ctypes.c_void_p, P(ctypes.c_int32), ctypes.c_int]
         L.oc_last_msgcount.argtypes = [ctypes.c_void_p, P(ctypes.c_int32), P(ctypes.c_int32)]
         L.op_last_msgcount.argtypes = [ctypes.c_void_p, P(ctypes.c_int32), P(ctypes.c_int32)]
         L.op_last_msgcount.restype = None
@@ -151,6 +152,12 @@ class Oracle:
         st = np.zeros(4, dtype=np.int32)
         self.L.oc_node(self.h, r, _i32p(st))
         return st
+
+    def set_failed(self, idx):
+        """SCALED: fail these nodes at the end of the tick just run"""
+        a = np.ascontiguousarray(idx, dtype=np.int32)
+        if self.L.oc_set_failed(self.h, _i32p(a), len(a)):
+            raise ValueError("oc_set_failed")
 
     def last_msgcount(self):
         """SCALED: per-node gossip entries sent (before loss) / received (after loss) last tick"""

@@ -127,3 +127,28 @@ def test_ramp_with_drops_at_scale():
     for r in (0, 1, n // 2, n - 1):  # spot rows: everyone present
         hb, ts = sim.read_row(r)
         assert (hb >= 0).all(), r
+
+
+@pytest.mark.parametrize("case", ["singlefailure_T1_R1", "multifailure_T42_R7", "n20_single", "n70_single"])
+def test_ramp_equals_reference_fixtures(case):
+    """HIP SCALED join ramp vs the seeded reference itself (no oracle in between): with no drops and
+    N < 78 (EmulNet's buffer never fills) every tick's tables equal the golden FAITHFUL digests and
+    the events the golden dbg.log's join/remove lines (tests/test_oracle_scaled_pin.py)."""
+    from golden_util import load_case, parse_conf
+    from test_oracle_scaled_pin import _canon, _parse_dbg
+
+    m = load_case(case)
+    n, _single, drop, _p = parse_conf(m["conf"])
+    assert not drop
+    ev, fails = _parse_dbg(m["dbg"])
+    sim = Simulator(n, GM_MODE_SCALED, rd_seed=m["rd_seed"], init_mode=2)
+    assert sim.time == 1  # the context starts as of tick 0
+    assert digest64(sim.dump_tables()) == int(m["tick_digests"][0])
+    for t in range(1, m["ticks"]):
+        sim.tick()
+        if fails.get(t):
+            sim.set_failed(fails[t])
+        got = [(e[1], e[2], e[3]) for e in sim.drain_events()]
+        assert got == _canon(ev.get(t, [])), f"{case}: events differ at t={t}"
+        assert digest64(sim.dump_tables()) == int(m["tick_digests"][t]), f"{case}: tables differ at t={t}"
+    assert sim.tick_stats()["err"] == 0
