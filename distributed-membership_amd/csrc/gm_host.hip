@@ -341,13 +341,29 @@ static int create_scaled(gm_ctx *c) {
   s.drop_seed = c->cfg.drop_seed;
   const size_t cells = (size_t)n * s.wp;
   TRY(dalloc(c, &s.table, cells));   // stored cell bytes
-  TRY(dalloc(c, &s.twide, cells));   // 16-bit cells of the escaped bytes
   c->nt = !(getenv("GM_NT") && !atoi(getenv("GM_NT")));  // non-temporal table streams, default on
   s.pipe_waves = getenv("GM_BAND_PIPE") ? std::max(0, atoi(getenv("GM_BAND_PIPE"))) : 0;
   s.kcap = inbox_cap(S_KMAX);
   c->shard_sync = getenv("GM_SHARD_SYNC") ? (atoi(getenv("GM_SHARD_SYNC")) ? 1 : 0) : -1;
   TRY(dalloc(c, &s.msg, cells));        // nibbles: 2 parities x band/2 bytes per (band, row)
-  TRY(dalloc(c, &s.wide, 2 * cells));   // escape bytes: 2 parities x band
+  // Escape pools (gm_scaled.h), one per tick parity. Up to 2^31 cells they hold every cell (the
+  // dense equivalent: no run can overflow them); beyond, 1/16 of the cells and 1/16 of the
+  // payload lanes -- a warm cluster escapes only a crashed node's entries in the ticks before
+  // their removal (~1 % of the cells at a 1 % crash) -- and an overflow fails loudly
+  // (GM_ERR_ESC -> GM_ERANGE). GM_ESC_CAP (cells; diagnostics, tests) lowers the table pool.
+  const bool dense = cells <= (1ull << 31);
+  s.tesc_cap = (uint32_t)std::min<size_t>(dense ? cells : std::max<size_t>(cells / 16, 1ull << 26), 0xFFFFFFF0ull);
+  s.pesc_cap = (uint32_t)std::min<size_t>(dense ? cells / 16 : std::max<size_t>(cells / 256, 1ull << 22), 0xFFFFFFF0ull);
+  if (getenv("GM_ESC_CAP")) s.tesc_cap = (uint32_t)std::max(1L, std::min<long>(atol(getenv("GM_ESC_CAP")), s.tesc_cap));
+  for (int p = 0; p < 2; p++) {
+    TRY(dalloc(c, &s.tesc[p], s.tesc_cap));
+    TRY(dalloc(c, &s.pesc[p], (size_t)s.pesc_cap * 16));
+    TRY(dalloc(c, &s.pesc_rec[p], (size_t)n * s.nb));
+  }
+  TRY(dalloc(c, &s.tesc_cnt, 2));
+  TRY(dalloc(c, &s.pesc_cnt, 2));
+  HIPCHECK(hipMemset(s.tesc_cnt, 0, 2 * sizeof(unsigned long long)));
+  HIPCHECK(hipMemset(s.pesc_cnt, 0, 2 * sizeof(unsigned long long)));
   for (int p = 0; p < 2; p++) {
     TRY(dalloc(c, &s.inbox_cnt[p], n));
     TRY(dalloc(c, &s.inbox[p], (size_t)n * S_KMAX));
@@ -387,13 +403,19 @@ static int create_scaled(gm_ctx *c) {
   HIPCHECK(hipMemset(s.msg, 0, sizeof(uint8_t) * cells));
   for (int p = 0; p < 2; p++) HIPCHECK(hipMemset(s.inbox_cnt[p], 0, sizeof(int32_t) * n));
   HIPCHECK(hipMemset(s.failed, 0, sizeof(int32_t) * n));
-  HIPCHECK(gm_launch_init(s, ramp ? 2 : warm ? 1 : 0, t0, c->cfg.init_seed, c->stream));
+  HIPCHECK(hipMemset(s.err, 0, sizeof(uint32_t)));
+  HIPCHECK(hipDeviceSynchronize());  // the memsets above are done before the init kernel runs on c->stream
+  HIPCHECK(gm_launch_init(s, ramp ? 2 : warm ? 1 : 0, t0, c->cfg.init_seed, c->stream));  // table, records, pool
   HIPCHECK(hipStreamSynchronize(c->stream));
-  HIPCHECK(hipMemset(s.brec, 0, sizeof(uint4) * (size_t)n * s.nb));
+  uint32_t ierr = 0;
+  HIPCHECK(hipMemcpy(&ierr, s.err, sizeof ierr, hipMemcpyDeviceToHost));
+  if (ierr) {  // a cold start escapes every cell: beyond the dense-pool size it does not fit
+    snprintf(g_errbuf, sizeof g_errbuf, "initial state overflows the escape pool (%u cells)", s.tesc_cap);
+    return GM_ERANGE;
+  }
   HIPCHECK(hipMemset(s.ev_spill_cnt, 0, sizeof(uint32_t)));
   HIPCHECK(hipMemset(s.evcum, 0, sizeof(uint64_t) * (size_t)n * s.nb));
   HIPCHECK(hipMemset(s.rowstat, 0, sizeof(int32_t) * n * 4));
-  HIPCHECK(hipMemset(s.err, 0, sizeof(uint32_t)));
   if (s.sharded) {
     TRY(dalloc(c, &s.acc, (size_t)n * 8));
     TRY(dalloc(c, &s.pending, n));
@@ -1077,6 +1099,22 @@ extern "C" int gm_msgcount(gm_ctx *c, int32_t t, int32_t *sent, int32_t *recv) {
   return GM_OK;
 }
 
+// One row of stored bytes (column order) -> absolute (hb, ts), -1 = absent; escaped cells take
+// the next value of `esc` (the row's pool lists, concatenated in column order). Cells are
+// relative to the row's last written tick wt.
+static void decode_scaled_row(const gm_ctx *c, const uint8_t *row, const uint16_t *esc, int wt,
+                              std::vector<int32_t> &hb, std::vector<int32_t> &ts) {
+  const SState &s = c->s;
+  hb.resize(s.w);
+  ts.resize(s.w);
+  size_t k = 0;
+  for (int j = 0; j < s.w; j++) {
+    const uint32_t e = s_is_esc(row[j]) ? (uint32_t)esc[k++] : s_widen(row[j]);
+    hb[j] = e == 0 ? -1 : 2 * wt - 255 + (int32_t)S_H(e) - s_hbase(s.ramp, s.c0 + j);
+    ts[j] = e == 0 ? -1 : wt - (int32_t)S_AGE(e);
+  }
+}
+
 // Row r of this context's table as absolute (hb, ts) per column, -1 = absent.
 static int read_table_row(gm_ctx *c, int r, std::vector<int32_t> &hb, std::vector<int32_t> &ts, int &w) {
   if (c->cfg.mode == GM_MODE_FAITHFUL) {
@@ -1113,21 +1151,26 @@ static int read_table_row(gm_ctx *c, int r, std::vector<int32_t> &hb, std::vecto
   const SState &s = c->s;  // band-tiled: one B-cell piece of the row per band slab
   w = s.w;  // this context's columns
   std::vector<uint8_t> row(s.wp);
-  std::vector<uint16_t> wrow(s.wp);
+  std::vector<uint32_t> eb(s.nb);
   int32_t wt = 0;
   const size_t piece = s.band;  // bytes of one (band, row) piece of the stored cells
   HIPCHECK(hipMemcpy2D(row.data(), piece, s.table + (size_t)r * s.band, piece * s.n, piece, s.nb,
                        hipMemcpyDeviceToHost));
-  HIPCHECK(hipMemcpy2D(wrow.data(), 2 * piece, s.twide + (size_t)r * s.band, 2 * piece * s.n, 2 * piece, s.nb,
-                       hipMemcpyDeviceToHost));
+  HIPCHECK(hipMemcpy2D(eb.data(), sizeof(uint32_t), (const uint8_t *)(s.brec + r) + 12, sizeof(uint4) * s.n,
+                       sizeof(uint32_t), s.nb, hipMemcpyDeviceToHost));
   HIPCHECK(hipMemcpy(&wt, s.wtick + r, sizeof wt, hipMemcpyDeviceToHost));
-  hb.resize(w);
-  ts.resize(w);
-  for (int j = 0; j < w; j++) {  // cells are relative to the row's last written tick
-    const uint32_t e = row[j] == S_B_ESC ? (uint32_t)wrow[j] : s_widen(row[j]);
-    hb[j] = e == 0 ? -1 : 2 * wt - 255 + (int32_t)S_H(e) - s_hbase(s.ramp, s.c0 + j);
-    ts[j] = e == 0 ? -1 : wt - (int32_t)S_AGE(e);
+  std::vector<uint16_t> esc(s.wp);  // the escaped cells in column order (pool lists of the row's bands)
+  const uint16_t *pool = s.tesc[(c->t - 1) & 1];
+  size_t ne = 0;
+  for (int b = 0; b < s.nb; b++) {
+    size_t k = 0;
+    for (int j = 0; j < s.band; j++) k += s_is_esc(row[(size_t)b * s.band + j]);
+    if (!k) continue;
+    if (eb[b] == S_ESC_NONE || (size_t)eb[b] + k > s.tesc_cap) return GM_ESTATE;
+    HIPCHECK(hipMemcpy(esc.data() + ne, pool + eb[b], sizeof(uint16_t) * k, hipMemcpyDeviceToHost));
+    ne += k;
   }
+  decode_scaled_row(c, row.data(), esc.data(), wt, hb, ts);
   return GM_OK;
 }
 
@@ -1225,9 +1268,49 @@ extern "C" int gm_dump_tables(gm_ctx *c, char *buf, size_t cap, size_t *len) {
     return GM_OK;
   }
   std::vector<int32_t> rh, rt;
+  // SCALED: one copy of the table, the records and the last tick's pool, decoded row by row
+  std::vector<uint8_t> tab;
+  std::vector<uint4> rec;
+  std::vector<uint16_t> pool, esc;
+  std::vector<int32_t> wts;
+  std::vector<uint8_t> row;
+  if (c->cfg.mode == GM_MODE_SCALED) {
+    const SState &s = c->s;
+    tab.resize((size_t)s.n * s.wp);
+    rec.resize((size_t)s.n * s.nb);
+    wts.resize(s.n);
+    unsigned long long cnt = 0;
+    HIPCHECK(hipMemcpy(tab.data(), s.table, tab.size(), hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(rec.data(), s.brec, sizeof(uint4) * rec.size(), hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(wts.data(), s.wtick, sizeof(int32_t) * s.n, hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(&cnt, s.tesc_cnt + ((c->t - 1) & 1), sizeof cnt, hipMemcpyDeviceToHost));
+    pool.resize(std::min<unsigned long long>(cnt, s.tesc_cap));
+    if (!pool.empty())
+      HIPCHECK(hipMemcpy(pool.data(), s.tesc[(c->t - 1) & 1], sizeof(uint16_t) * pool.size(), hipMemcpyDeviceToHost));
+    row.resize(s.wp);
+    esc.resize(s.wp);
+  }
   for (int i = 0; i < c->n; i++) {
     int w;
-    TRY(read_table_row(c, i, rh, rt, w));
+    if (c->cfg.mode == GM_MODE_SCALED) {
+      const SState &s = c->s;
+      size_t ne = 0;
+      for (int b = 0; b < s.nb; b++) {
+        const uint8_t *pc = tab.data() + ((size_t)b * s.n + i) * s.band;
+        memcpy(row.data() + (size_t)b * s.band, pc, s.band);
+        size_t k = 0;
+        for (int j = 0; j < s.band; j++) k += s_is_esc(pc[j]);
+        if (!k) continue;
+        const uint32_t base = rec[(size_t)b * s.n + i].w;
+        if (base == S_ESC_NONE || (size_t)base + k > pool.size()) return GM_ESTATE;
+        memcpy(esc.data() + ne, pool.data() + base, sizeof(uint16_t) * k);
+        ne += k;
+      }
+      decode_scaled_row(c, row.data(), esc.data(), wts[i], rh, rt);
+      w = s.w;
+    } else {
+      TRY(read_table_row(c, i, rh, rt, w));
+    }
     int cnt = 0;
     const int c0 = c->cfg.mode == GM_MODE_SCALED ? c->s.c0 : 0;
     for (int j = 0; j < w; j++) cnt += rh[j] >= 0;

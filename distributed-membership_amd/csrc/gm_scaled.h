@@ -2,6 +2,8 @@
 #pragma once
 #include <stdint.h>
 
+#include "gm_device.h"
+
 #define S_KMAX 64                // inbox capacity (gossip lists per receiver per tick)
 #define S_COLS_PER_LANE 16       // 32 B of table + 16 B per sender payload per lane and row
 #define S_ROW_ALIGN 512          // padded row width granule (a multiple of every band width up to 512)
@@ -20,23 +22,33 @@
 // at tick t is 2t-1 (h = 254); h falls by 2 per tick of heartbeat lag, and a present
 // entry lagging more than ~126 ticks sets GM_ERR_LAG instead of wrapping.
 #define S_CELL(h, age) (((h) << 5) | (age))
-// Stored table cell (round 2): ONE BYTE per (observer, subject). The 16-bit cell above is
-// the working format in registers; in HBM a cell is
-//   0            absent
-//   S_B_ESC (1)  escaped: the 16-bit cell is in the wide table plane (same band layout)
-//   h4 << 4 | a  h = 224 + 2 h4 (h4 in [1, 15]: even h in [226, 254], heartbeat lag <= 14
-//                ticks), age a <= 15 -- every live entry of a warm, steady cluster.
-// Cells outside that range (odd h of cold-start / JOINREQ entries, lag > 14 or age > 15,
-// e.g. a crashed node's entries in the ticks before TREMOVE) escape to the wide plane,
-// which is read and written only where a byte says so.
+// Stored table cell: ONE BYTE per (observer, subject). The 16-bit cell above is the
+// working format in registers; in HBM a cell is
+//   0             absent
+//   h4 << 4 | a   h = 224 + 2 h4 (h4 in [1, 15]: even h in [226, 254], heartbeat lag <= 14
+//                 ticks), age a <= 15 -- every live entry of a warm, steady cluster
+//   1..15         escaped (h4 = 0): the exact 16-bit cell is in the tick's escape pool.
+//                 S_B_ESC (1) = escaped and fresh (age < TFAIL), S_B_ESCS (2) = escaped and
+//                 stale, so the gossip draw's freshness test never needs the pool.
+// Cells outside the byte's range (odd h of cold-start / JOINREQ entries, lag > 14 or age > 15,
+// e.g. a crashed node's entries in the ticks before TREMOVE) escape. The pool is COMPACT: per
+// (band, row) the escaped cells of the row's band slice, in column order, as consecutive u16
+// cells of the pool of the tick that wrote them (tick parity: written at t, read at t+1); the
+// (band, row) record's .w holds the list's first index (S_ESC_NONE: no escapes). Capacity is
+// bounded (gm_host.hip: dense-equivalent for small clusters, a fraction of the cells beyond);
+// an overflow sets GM_ERR_ESC (-> GM_ERANGE) -- never a silent divergence.
 #define S_B_ESC 1u
-__host__ __device__ inline uint32_t s_widen(uint32_t b) {  // byte -> 16-bit cell (S_B_ESC: look in the wide plane)
+#define S_B_ESCS 2u
+#define S_ESC_NONE 0xFFFFFFFFu
+__host__ __device__ inline bool s_is_esc(uint32_t b) { return b != 0 && b < 16; }
+__host__ __device__ inline uint32_t s_widen(uint32_t b) {  // byte -> 16-bit cell (escape codes: look in the pool)
   return b == 0 ? 0u : (7168u + ((b & 0xF0u) << 2) + (b & 0x0Fu));
 }
-__host__ __device__ inline uint32_t s_narrow(uint32_t c) {  // 16-bit cell -> byte (S_B_ESC if not representable)
+__host__ __device__ inline uint32_t s_narrow(uint32_t c) {  // 16-bit cell -> byte (an escape code if not representable)
   if (c == 0) return 0u;
   const uint32_t h = c >> 5, a = c & 31u;
-  return (h >= 226 && !(h & 1) && a <= 15) ? (((h - 224) >> 1) << 4) | a : S_B_ESC;
+  if (h >= 226 && !(h & 1) && a <= 15) return (((h - 224) >> 1) << 4) | a;
+  return a < GM_TFAIL ? S_B_ESC : S_B_ESCS;
 }
 __host__ __device__ inline int s_start(int j) { return j >> 2; }  // (int)(0.25 * j) for j >= 0
 __host__ __device__ inline int s_hbase(int ramp, int j) { return (ramp && j > 0) ? 2 * (s_start(j) + 1) : 0; }
@@ -79,16 +91,27 @@ struct SState {
   // Band-tiled layout: cell (r, c) of band b = c / band lives at ((b * n + r) * band + c % band),
   // so one band of all rows is one contiguous slab (the unit gm_s_band sweeps).
   uint8_t *table;          // [nb][n][band] stored cell bytes (s_narrow of S_CELL)
-  uint16_t *twide;         // [nb][n][band] S_CELL of the escaped cells (valid only where the byte is S_B_ESC)
+  uint16_t *tesc[2];       // escape pools by tick parity: S_CELL of escaped cells, per (band, row) a
+                           // contiguous list in column order starting at brec.w (S_ESC_NONE: none)
+  unsigned long long *tesc_cnt;  // [2] cells allocated in each pool this tick (zeroed a tick ahead)
+  uint32_t tesc_cap;       // cells per pool
   uint8_t *msg;            // [nb][n][2][band/2] gossip payload nibbles, both tick parities of a (band, row) adjacent
-  uint8_t *wide;           // [nb][n][2][band] escaped payload bytes (written / read only where the nibble is 15)
+  // escaped payload bytes (nibble 15): per (band, sender) of tick parity p the lanes holding escapes
+  // write their 16 payload bytes h' into consecutive 16-byte slots of pesc[p] from the record's base,
+  // in lane order (pesc_rec[p][band * n + sender] = {base, lane mask lo, lane mask hi, 0}, written
+  // only by senders with escapes and read only where a receiver meets nibble 15)
+  uint8_t *pesc[2];
+  uint4 *pesc_rec[2];
+  unsigned long long *pesc_cnt;  // [2] slots allocated this tick
+  uint32_t pesc_cap;       // 16-byte slots per pool
   int32_t *wtick;          // [n] tick each row's cells are relative to (last written)
   int32_t *inbox_cnt[2];   // [n] lists queued for each receiver, by delivery-tick parity
   int32_t *inbox[2];       // [n][S_KMAX] sender rows
   int32_t *hbctr;          // [n] MP1Node heartbeat counter (Member::heartbeat)
   int32_t *failed;         // [n] Member::bFailed
   uint4 *brec;             // [nb][n] per-(band, row) record after the sweep: .x/.y = present cells per 64-column
-                           // chunk (band/64 bytes, rank-select), .z = bcnt word (S_BC_*); rows adjacent = whole-line writes
+                           // chunk (band/64 bytes, rank-select), .z = bcnt word (S_BC_*), .w = first index of the
+                           // slice's escaped cells in tesc[t & 1] (S_ESC_NONE: none); rows adjacent = whole-line writes
   uint32_t *ev_band;       // [n][nb][evs] kind<<30 | subject id
   uint64_t *ev_spill;      // overflow: (logger<<32) | kind<<30 | subject id
   uint32_t *ev_spill_cnt;

@@ -63,7 +63,7 @@ template <int B>
 struct RowMeta {
   int k;           // lists delivered to the row (-1: no such row, or a crashed node)
   int snd[S_SB];   // first S_SB senders
-  uint32_t hint;   // the (band, row) record's escape mask of the last tick (see unit_finish)
+  uint32_t ebase;  // the (band, row) record's escape list of the last tick (S_ESC_NONE: no escaped cells)
 };
 
 // Every load of the row's metadata issues at once, none behind a branch on another (one
@@ -77,7 +77,7 @@ __device__ __forceinline__ RowMeta<B> row_meta(const SState &s, int r, int par, 
   int4 b = *(const int4 *)(ib + 4);
   int k = s.inbox_cnt[par][rc];
   int failed = s.failed[rc];
-  m.hint = s.brec[slab + rc].w;
+  m.ebase = s.brec[slab + rc].w;
   // empty asm statements that read the values here: without them the compiler sinks the
   // inbox-count load into a branch on `failed` and the sender ids behind that, two more
   // round trips before the gathers (one row per wave: scalar registers)
@@ -91,7 +91,7 @@ __device__ __forceinline__ RowMeta<B> row_meta(const SState &s, int r, int par, 
   m.snd[4] = b.x; m.snd[5] = b.y; m.snd[6] = b.z; m.snd[7] = b.w;
   // not in the group (join ramp) or crashed: untouched
   m.k = (r >= s.n || failed || !s_ingroup(s.ramp, s.intro_until, r, t)) ? -1 : k;
-  if (r >= s.n) m.hint = 0;
+  if (r >= s.n) m.ebase = S_ESC_NONE;
   return m;
 }
 
@@ -161,6 +161,80 @@ __device__ __forceinline__ u16x2 narrow2(u16x2 v2, u16x2 pres, u16x2 &bad) {
   return enc * (pres - bad) + bad;
 }
 
+// bit q (0..15) set where byte q of a lane's 16 stored bytes is an escape code (1..15: low
+// nibble non-zero, high nibble zero), SWAR per dword (no carries cross a byte)
+__device__ __forceinline__ uint32_t esc_mask16(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
+  const uint32_t w[4] = {w0, w1, w2, w3};
+  uint32_t m = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint32_t lo = ((w[i] & 0x0F0F0F0Fu) + 0x7F7F7F7Fu) & 0x80808080u;
+    const uint32_t hi = (((w[i] >> 1) & 0x78787878u) + 0x78787878u) & 0x80808080u;
+    const uint32_t e = (lo & ~hi) >> 7;                    // bits 0, 8, 16, 24
+    m |= (((e * 0x00204081u) >> 21) & 0xFu) << (4 * i);  // gathered to bits 21..24 (no two terms collide)
+  }
+  return m;
+}
+
+// exclusive prefix of v over the LPR aligned lanes of this lane's row, and the row total;
+// every lane of the row is active (the callers branch on row-uniform conditions only)
+template <int LPR>
+__device__ __forceinline__ int row_scan(int v, int li, int lane, int &total) {
+  int x = v;
+  if (LPR == 64) {
+    x = dpp_scan(v);
+    total = __builtin_amdgcn_readlane(x, 63);
+  } else {
+#pragma unroll
+    for (int o = 1; o < LPR; o <<= 1) {
+      const int y = __shfl_up(x, o, 64);
+      if (li >= o) x += y;
+    }
+    total = __shfl(x, lane - li + LPR - 1, 64);
+  }
+  return x - v;
+}
+
+// any lane of this lane's row
+template <int LPR>
+__device__ __forceinline__ bool row_any(bool p, int sub) {
+  const uint64_t b = __builtin_amdgcn_ballot_w64(p);
+  return LPR == 64 ? b != 0 : ((b >> (sub * LPR)) & ((1ull << LPR) - 1)) != 0;
+}
+
+// one reservation of `total` pool entries per row (its first lane), broadcast to the row;
+// S_ESC_NONE if the row has none or the pool overflowed (GM_ERR_ESC: the run is void)
+template <int LPR>
+__device__ __forceinline__ uint32_t row_alloc(unsigned long long *cnt, uint32_t cap, int total, int li, int lane,
+                                              uint32_t *err) {
+  uint32_t base = S_ESC_NONE;
+  if (li == 0 && total > 0) {
+    const unsigned long long b = atomicAdd(cnt, (unsigned long long)total);
+    if (b + (unsigned long long)total <= (unsigned long long)cap) base = (uint32_t)b;
+    else atomicOr(err, GM_ERR_ESC);
+  }
+  return LPR == 64 ? __builtin_amdgcn_readfirstlane(base) : (uint32_t)__shfl((int)base, lane - li, 64);
+}
+
+// the lane's escaped cells (mask em) into their u16 halves of tw, from its part of the row's list
+__device__ __forceinline__ void esc_load(const uint16_t *src, uint32_t em, u16x2 tw[8]) {
+  int idx = 0;
+#pragma unroll
+  for (int q = 0; q < 16; q++) {
+    if ((em >> q) & 1u) {
+      const uint32_t v = src[idx++];
+      const int sh = 16 * (q & 1);
+      tw[q >> 1] = pk((unpk(tw[q >> 1]) & ~(0xFFFFu << sh)) | (v << sh));
+    }
+  }
+}
+__device__ __forceinline__ void esc_store(uint16_t *dst, uint32_t em, const uint32_t cw[8]) {
+  int idx = 0;
+#pragma unroll
+  for (int q = 0; q < 16; q++)
+    if ((em >> q) & 1u) dst[idx++] = (uint16_t)(cw[q >> 1] >> (16 * (q & 1)));
+}
+
 // Payload nibbles (gm_scaled.h S_NIB_*): dword w of a lane's 8-byte slice holds cells
 // 8w..8w+7; cell 8w+2k sits in nibble 3-k of the low u16, cell 8w+2k+1 in nibble 3-k
 // of the high u16. So v_pk_max_u16 of the dword shifted left by 4k leaves, in the top
@@ -183,9 +257,17 @@ __device__ __forceinline__ uint32_t nib_of(uint32_t x0, uint32_t x1, int q) {
   const int c = q & 7;
   return (x >> (16 * (c & 1) + 4 * (3 - (c >> 1)))) & 15u;
 }
-// payload value of a delivered cell: h' from its nibble, or from the wide plane on escape
-__device__ __forceinline__ uint32_t nib_value(uint32_t nb, const uint8_t *wide_cell) {
-  return nb == S_NIB_ESC ? (uint32_t)*wide_cell : nb ? S_NIB_H(nb) : 0u;
+// escaped payload byte h' of lane li's cell q in sender sn's slice of tick parity pp: the
+// sender's escaping lanes hold consecutive 16-byte slots from its record's base, in lane order
+__device__ __forceinline__ uint32_t pesc_value(const SState &s, int pp, int band, int sn, int li, int q) {
+  const uint4 rc = s.pesc_rec[pp][(size_t)band * s.n + sn];
+  const uint64_t m = (uint64_t)rc.y | ((uint64_t)rc.z << 32);
+  const uint32_t slot = rc.x + (uint32_t)__builtin_popcountll(m & ((1ull << li) - 1));
+  return rc.x == S_ESC_NONE || slot >= s.pesc_cap ? 0u : (uint32_t)s.pesc[pp][(size_t)slot * 16 + q];
+}
+// payload value of a delivered cell: h' from its nibble, or from the sender's escape slots
+__device__ __forceinline__ uint32_t nib_value(uint32_t nb, const SState &s, int pp, int band, int sn, int li, int q) {
+  return nb == S_NIB_ESC ? pesc_value(s, pp, band, sn, li, q) : nb ? S_NIB_H(nb) : 0u;
 }
 
 // One work unit of the band sweep: unit u = (band u / U, rows [(u % U) * RPW, +RPW)).
@@ -196,8 +278,7 @@ struct UnitIn {
   int band, r, k;  // k: lists delivered to this lane's row, -1 = not merged (crashed / absent / not in the group)
   int snd[S_SB];
   u32x4 ta;        // the row's 16 cell bytes of this lane (as loaded)
-  bool pre;        // the wide cells below were prefetched (last tick this lane stored escapes)
-  u32x4 wa, wb;    // the lane's 16 wide cells (valid where its bytes are S_B_ESC)
+  uint32_t ebase;  // the row slice's escape list in the pool of tick t-1 (S_ESC_NONE: none)
 };
 
 // UNI: the row is wave-uniform and known to be (one row per wave, a grid-derived unit)
@@ -217,15 +298,7 @@ __device__ __forceinline__ void unit_load(const SState &s, int t, int band, int 
 #pragma unroll
   for (int j = 0; j < S_SB; j++) in.snd[j] = meta.snd[j];
   in.k = meta.k;
-  // lanes that stored escaped cells last tick (the (band, row) record's escape mask, written by
-  // unit_finish) fetch their wide cells now, with the table slice, instead of one round trip later
-  in.pre = (meta.hint >> (LPR == 64 ? li >> 1 : li)) & 1u;
-  in.wa = in.wb = (u32x4){0u, 0u, 0u, 0u};
-  if (in.pre) {
-    const __amdgpu_buffer_rsrc_t wrs = gm_rsrc(s.twide + slab * B, (uint32_t)(s.n * B * 2));
-    in.wa = __builtin_amdgcn_raw_buffer_load_b128(wrs, 2 * toff, 0, 0);
-    in.wb = __builtin_amdgcn_raw_buffer_load_b128(wrs, 2 * toff + 16, 0, 0);
-  }
+  in.ebase = meta.ebase;
 }
 
 // every payload slice at once; slots j >= k read out of range (zeros = "not sent")
@@ -253,15 +326,11 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
   const int band = in.band, r = in.r;
   const int colb = band * B + li * Q;  // shard-local column of this lane's first cell
   const size_t slab = (size_t)band * s.n;
-  // this band's slabs: table [n][B] cell bytes, wide table [n][B] 16-bit cells (escaped cells
-  // only), payload nibbles [n][2][B/2] bytes (32-bit offsets)
+  // this band's slabs: table [n][B] cell bytes, payload nibbles [n][2][B/2] bytes (32-bit offsets)
   const __amdgpu_buffer_rsrc_t trs = gm_rsrc(s.table + slab * B, (uint32_t)(s.n * B));
-  const __amdgpu_buffer_rsrc_t wrs = gm_rsrc(s.twide + slab * B, (uint32_t)(s.n * B * 2));
   const __amdgpu_buffer_rsrc_t prs = gm_rsrc(s.msg + slab * B, (uint32_t)(s.n * B));
-  const uint32_t toff = (uint32_t)(r * B + li * Q);  // bytes; the wide cells at 2 * toff
+  const uint32_t toff = (uint32_t)(r * B + li * Q);  // bytes
   const uint32_t poff = (uint32_t)((par ^ 1) * (B / 2) + li * 8);  // + sender * B
-  // escape plane of this band: [n][2][B] bytes, cell (sender, parity, column)
-  const uint8_t *wsrc = s.wide + slab * 2 * B + (size_t)(par ^ 1) * B + li * Q;
   int k = in.k;
   if (k > S_KMAX) {
     if (li == 0) atomicOr(s.err, GM_ERR_INBOX);
@@ -284,7 +353,21 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
   int npres = 0, nfail = 0, nev = 0;
   int nkept = 0;     // DROP: delivered entries this lane kept after the keyed loss (msgcount)
   uint32_t evk = 0;  // 2 bits per cell: event kind
-  bool esc_st = false;  // this lane stored escaped cells (announced in the (band, row) record)
+  bool esc_st = false;  // this lane stored escaped cells
+  uint32_t eb_out = S_ESC_NONE;  // the row slice's escape list in this tick's pool (the record's .w)
+  if (!live && in.ebase != S_ESC_NONE) {
+    // a row not swept this tick (crashed, not yet in the group) keeps its cells as they are: its
+    // escaped cells move to this tick's pool (row-uniform branch)
+    const uint32_t em = esc_mask16(in.ta.x, in.ta.y, in.ta.z, in.ta.w);
+    int etot;
+    const int eoff = row_scan<LPR>(__builtin_popcount(em), li, lane, etot);
+    eb_out = row_alloc<LPR>(&s.tesc_cnt[par], s.tesc_cap, etot, li, lane, s.err);
+    if (eb_out != S_ESC_NONE) {
+      const uint16_t *src = s.tesc[par ^ 1] + in.ebase + eoff;
+      uint16_t *dst = s.tesc[par] + eb_out + eoff;
+      for (int i = 0; i < __builtin_popcount(em); i++) dst[i] = src[i];
+    }
+  }
   if (live) {
     // merge key per cell = the largest delivered payload h' (0 = nothing delivered), as
     // key5 = h' << 5 (the cell with age 0) in the u16 halves of each table word
@@ -323,7 +406,7 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
             for (int j = 0; j < k; j++) {  // reloads (no dynamic register indexing: no scratch)
               const int sn = ib[j];
               const u32x2 mm = __builtin_amdgcn_raw_buffer_load_b64(prs, poff + (uint32_t)sn * B, 0, 0);
-              kv = max(kv, nib_value(nib_of(mm.x, mm.y, q), wsrc + (size_t)sn * 2 * B + q));
+              kv = max(kv, nib_value(nib_of(mm.x, mm.y, q), s, par ^ 1, band, sn, li, q));
             }
             key5[i][h] = (uint16_t)(kv << 5);
           }
@@ -347,7 +430,7 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
           const uint32_t h = (uint32_t)(gm_mix64(pair + (uint64_t)(s.c0 + colb + q)) >> 32);
           if ((int)(h % 100u) < drop_pct) continue;
           nkept++;
-          kk[q] = max(kk[q], nib_value(nb, wsrc + (size_t)sn * 2 * B + q));
+          kk[q] = max(kk[q], nib_value(nb, s, par ^ 1, band, sn, li, q));
         }
       }
 #pragma unroll
@@ -361,16 +444,10 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
         if (c >= 1 && colb + q < s.w && s_start(c) == t - 1) key5[q >> 1][q & 1] = (uint16_t)(255u << 5);
       }
     }
-    // widen the stored bytes to 16-bit cells; a lane holding escaped cells (rare: a crashed
-    // node's entries before their removal, cold-start / JOINREQ entries) takes those from
-    // the wide plane. npb: cells present as loaded (join detection below).
+    // widen the stored bytes to 16-bit cells; a row slice holding escaped cells (rare: a crashed
+    // node's entries before their removal, cold-start / JOINREQ entries) takes those from its
+    // list in the last tick's pool. npb: cells present as loaded (join detection below).
     const uint32_t tb4[4] = {ta.x, ta.y, ta.z, ta.w};
-    uint32_t esc_in = 0;
-#pragma unroll
-    for (int q = 0; q < 4; q++) {  // any byte == S_B_ESC: zero-byte test of w ^ 0x01010101
-      const uint32_t z = tb4[q] ^ 0x01010101u;
-      esc_in |= (z - 0x01010101u) & ~z & 0x80808080u;
-    }
     u16x2 tw[8], npb = (u16x2)(0);
 #pragma unroll
     for (int i = 0; i < 8; i++) {
@@ -379,19 +456,11 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
       npb = padd(npb, nz);
       tw[i] = widen2(x, nz);
     }
-    if (esc_in) {
-      u32x4 wa = in.wa, wb = in.wb;
-      if (!in.pre) {  // escapes the record did not announce (cold start, a row not swept last tick)
-        wa = __builtin_amdgcn_raw_buffer_load_b128(wrs, 2 * toff, 0, 0);
-        wb = __builtin_amdgcn_raw_buffer_load_b128(wrs, 2 * toff + 16, 0, 0);
-      }
-      const uint32_t wv[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
-#pragma unroll
-      for (int i = 0; i < 8; i++) {
-        const u16x2 x = pk(byte_pair(tb4[i >> 1], i & 1));
-        const u16x2 keepn = pmin1(x ^ (u16x2)(S_B_ESC));  // 0 where escaped
-        tw[i] = pk(wv[i]) + keepn * (tw[i] - pk(wv[i]));
-      }
+    if (in.ebase != S_ESC_NONE) {  // row-uniform: the lane's part of the list follows its row predecessors'
+      const uint32_t em = esc_mask16(ta.x, ta.y, ta.z, ta.w);
+      int etot;
+      const int eoff = row_scan<LPR>(__builtin_popcount(em), li, lane, etot);
+      esc_load(s.tesc[par ^ 1] + in.ebase + eoff, em, tw);
     }
     // merge: re-base the cell to tick t (h -= 2, age += 1; absent stays 0), then max
     // with the delivered key (insert if absent; raise hb and stamp ts = t if newer)
@@ -499,17 +568,38 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
       ngone = (int)ng2.x + (int)ng2.y;
     }
     esc_st = unpk(badv) != 0;
-    if (esc_st) {  // rare: cells the byte cannot hold, as 16-bit cells into the wide plane
-      u16x2 lagmin = (u16x2)(0xFFFF);
+    if (row_any<LPR>(esc_st, sub)) {  // rare: cells the byte cannot hold, as 16-bit cells into this tick's pool
+      uint32_t em = 0;
+      if (esc_st) {
+        u16x2 lagmin = (u16x2)(0xFFFF);
 #pragma unroll
-      for (int i = 0; i < 8; i++) lagmin = __builtin_elementwise_min(lagmin, pk(cw[i]) - (u16x2)(32));
-      if (__builtin_elementwise_min(lagmin.x, lagmin.y) < 64) atomicOr(s.err, GM_ERR_LAG);  // present with h <= 2
-      const u32x4 wa = {cw[0], cw[1], cw[2], cw[3]}, wb = {cw[4], cw[5], cw[6], cw[7]};
-      __builtin_amdgcn_raw_buffer_store_b128(wa, wrs, 2 * toff, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b128(wb, wrs, 2 * toff + 16, 0, 0);
+        for (int i = 0; i < 8; i++) lagmin = __builtin_elementwise_min(lagmin, pk(cw[i]) - (u16x2)(32));
+        if (__builtin_elementwise_min(lagmin.x, lagmin.y) < 64) atomicOr(s.err, GM_ERR_LAG);  // present with h <= 2
+        em = esc_mask16(bw[0], bw[1], bw[2], bw[3]);
+        // a stale escaped cell stores S_B_ESCS (the gossip draw reads freshness from the byte)
+#pragma unroll
+        for (int q = 0; q < Q; q++)
+          if (((em >> q) & 1u) && ((cw[q >> 1] >> (16 * (q & 1))) & 31u) >= GM_TFAIL) bw[q >> 2] += 1u << (8 * (q & 3));
+      }
+      int etot;
+      const int eoff = row_scan<LPR>(__builtin_popcount(em), li, lane, etot);
+      eb_out = row_alloc<LPR>(&s.tesc_cnt[par], s.tesc_cap, etot, li, lane, s.err);
+      if (em && eb_out != S_ESC_NONE) esc_store(s.tesc[par] + eb_out + eoff, em, cw);
     }
-    if (__builtin_elementwise_max(nmx.x, nmx.y) == S_NIB_ESC) {
-      // rare: the lane's 16 payload bytes h' into the escape plane (read where the nibble is 15)
+    const bool pesc = __builtin_elementwise_max(nmx.x, nmx.y) == S_NIB_ESC;
+    if (row_any<LPR>(pesc, sub)) {
+      // rare: the escaping lanes' 16 payload bytes h' into consecutive slots of this tick's payload
+      // pool (read where a receiver meets nibble 15), one reservation per row
+      const uint64_t bal = __builtin_amdgcn_ballot_w64(pesc);
+      const uint64_t rm = LPR == 64 ? bal : (bal >> (sub * LPR)) & ((1ull << LPR) - 1);
+      uint32_t pbase = S_ESC_NONE;
+      if (li == 0) {
+        const unsigned long long b = atomicAdd(&s.pesc_cnt[par], (unsigned long long)__builtin_popcountll(rm));
+        if (b + (unsigned long long)__builtin_popcountll(rm) <= (unsigned long long)s.pesc_cap) pbase = (uint32_t)b;
+        else atomicOr(s.err, GM_ERR_ESC);
+        s.pesc_rec[par][slab + r] = make_uint4(pbase, (uint32_t)rm, (uint32_t)(rm >> 32), 0u);
+      }
+      pbase = LPR == 64 ? __builtin_amdgcn_readfirstlane(pbase) : (uint32_t)__shfl((int)pbase, lane - li, 64);
       uint32_t pw[8];
 #pragma unroll
       for (int i = 0; i < 8; i++) {  // removed cells send nothing: the swept cells suffice
@@ -519,7 +609,8 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
       }
       const u32x4 wv = {__builtin_amdgcn_perm(pw[1], pw[0], 0x06040200u), __builtin_amdgcn_perm(pw[3], pw[2], 0x06040200u),
                         __builtin_amdgcn_perm(pw[5], pw[4], 0x06040200u), __builtin_amdgcn_perm(pw[7], pw[6], 0x06040200u)};
-      *(u32x4 *)(s.wide + slab * 2 * B + (size_t)r * 2 * B + (size_t)par * B + li * Q) = wv;
+      if (pesc && pbase != S_ESC_NONE)
+        *(u32x4 *)(s.pesc[par] + ((size_t)pbase + __builtin_popcountll(rm & ((1ull << li) - 1))) * 16) = wv;
     }
     nfail = (int)nf2.x + (int)nf2.y;
     npres = (int)np2.x + (int)np2.y;
@@ -638,26 +729,11 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
       slot++;
     }
   }
-  // the row's lanes that stored escapes (bit li, or li / 2 for 64 lanes per row): the next
-  // tick's unit_load prefetches their wide cells
-  uint32_t emask;
-  {
-    const uint64_t eb = __builtin_amdgcn_ballot_w64(esc_st);
-    if (LPR == 64) {
-      uint64_t x = (eb | (eb >> 1)) & 0x5555555555555555ull;  // pairs -> even bits, then compress
-      x = (x | (x >> 1)) & 0x3333333333333333ull;
-      x = (x | (x >> 2)) & 0x0F0F0F0F0F0F0F0Full;
-      x = (x | (x >> 4)) & 0x00FF00FF00FF00FFull;
-      x = (x | (x >> 8)) & 0x0000FFFF0000FFFFull;
-      emask = (uint32_t)(x | (x >> 16));
-    } else {
-      emask = (uint32_t)(eb >> (sub * LPR)) & (uint32_t)((1ull << LPR) - 1);
-    }
-  }
   if (li == 0 && r < s.n) {
     // one 16-byte record per (band, row), consecutive rows adjacent: whole-line writes
     const uint32_t bc = (uint32_t)(pf & 0xFFFF) | ((uint32_t)(pf >> 16) << 11) | ((uint32_t)min(tot, 1023) << 22);
-    s.brec[slab + r] = live ? make_uint4((uint32_t)piece, (uint32_t)(piece >> 32), bc, emask) : make_uint4(0u, 0u, 0u, 0u);
+    s.brec[slab + r] = live ? make_uint4((uint32_t)piece, (uint32_t)(piece >> 32), bc, eb_out)
+                            : make_uint4(0u, 0u, 0u, eb_out);
     // column shard: this shard's row totals (present, numfailed) for the all-gather,
     // accumulated as one packed 64-bit add per (row, band) into the zeroed slot
     if (s.sharded && live)
@@ -679,6 +755,10 @@ __global__ __launch_bounds__(256) void gm_s_band(SState s, int t, int drop_pct) 
   u32x2 m[S_SB];
   unit_gather<B, DROP>(s, t, in, m);
   unit_finish<B, DROP>(s, t, drop_pct, in, m);
+  if (ub == 0 && blockIdx.y == 0 && threadIdx.x == 0) {  // the pools of tick t+1 start empty (the tick t-1
+    s.tesc_cnt[(t & 1) ^ 1] = 0;                          // lists in them are read through their bases,
+    s.pesc_cnt[(t & 1) ^ 1] = 0;                          // never through the counter)
+  }
 }
 
 // Software-pipelined variant (GM_BAND_PIPE=<waves>): a fixed grid of waves strides over the
@@ -691,6 +771,10 @@ __global__ __launch_bounds__(256) void gm_s_band_pipe(SState s, int t, int nwave
   const int total = ((s.n + RPW - 1) / RPW) * s.nb;
   int u = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
   if (u >= total) return;
+  if (u == 0 && threadIdx.x == 0) {
+    s.tesc_cnt[(t & 1) ^ 1] = 0;
+    s.pesc_cnt[(t & 1) ^ 1] = 0;
+  }
   UnitIn<B> cur, nxt;
   u32x2 m[S_SB];
   const int U = (s.n + RPW - 1) / RPW;
@@ -841,10 +925,8 @@ __device__ __forceinline__ void gm_resolve8(const SState &s, int r, const uint32
       if (en[v] != 0) {
         if (need == 0) {
           mycol = base + v;
-          // the table is as of tick t; an escaped cell's age is in the wide plane
-          const uint32_t c16 = en[v] == S_B_ESC ? (uint32_t)s.twide[((size_t)(mycol / B) * s.n + r) * B + mycol % B]
-                                                 : s_widen(en[v]);
-          myfresh = S_AGE(c16) < GM_TFAIL;
+          // the table is as of tick t; an escaped cell's byte says whether it is fresh
+          myfresh = s_is_esc(en[v]) ? en[v] == S_B_ESC : S_AGE(s_widen(en[v])) < GM_TFAIL;
         }
         need--;
       }
@@ -1245,29 +1327,54 @@ __global__ __launch_bounds__(256) void gm_s_accept(SState s, int t, int D, int i
 // Cells are encoded relative to tick t0 (S_CELL: h = 255 - (2*t0 - hb), age = t0 - ts).
 // Join ramp (warm = 2): nobody in any list but the introducer's own entry {hb 0, ts 0}
 // (nodeStart of node 0 at tick 0, MP1Node.cpp:126-140); state as of tick 0.
-__global__ void gm_s_init(SState s, int warm, int t0, uint64_t seed) {
-  const int r = blockIdx.x;
-  for (int j = threadIdx.x; j < s.wp; j += blockDim.x) {
-    uint32_t e = 0;  // absent
-    if (j < s.w && warm == 2) {
-      if (r == 0 && s.c0 + j == 0) e = S_CELL(255u, 0u);
-    } else if (j < s.w) {
-      const int c = s.c0 + j;
-      if (!warm) e = S_CELL(255u, 0u);  // hb 0 = 2*t0 at t0 = 0
-      else if (c == r) e = S_CELL(254u, 0u);
-      else {
-        const int a = (int)((gm_mix64(seed ^ ((uint64_t)(uint32_t)r << 32) ^ (uint64_t)(uint32_t)c) >> 40) % 4);
-        e = S_CELL((uint32_t)(252 - 2 * a), (uint32_t)a);
+// The band kernel's lane mapping (one wave per (band, rows) unit, 16 cells per lane), so the
+// escaped cells (a cold start escapes them all: odd h) form the same per-(band, row) lists
+// in the pool of tick t0 that gm_s_band writes, and every record's .w names its list.
+template <int B>
+__global__ __launch_bounds__(256) void gm_s_init(SState s, int warm, int t0, uint64_t seed) {
+  constexpr int LPR = B / S_COLS_PER_LANE, RPW = 64 / LPR, Q = S_COLS_PER_LANE;
+  const int U = (s.n + RPW - 1) / RPW;
+  const int ub = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  if (ub >= U) return;  // whole wave
+  const int lane = threadIdx.x & 63, li = lane % LPR;
+  const int band = blockIdx.y, r = ub * RPW + lane / LPR;
+  const bool row = r < s.n;
+  uint32_t cw[8] = {0, 0, 0, 0, 0, 0, 0, 0}, bw[4] = {0, 0, 0, 0};
+  if (row) {
+#pragma unroll
+    for (int q = 0; q < Q; q++) {
+      const int j = band * B + li * Q + q;  // shard-local column
+      uint32_t e = 0;                       // absent
+      if (j < s.w && warm == 2) {
+        if (r == 0 && s.c0 + j == 0) e = S_CELL(255u, 0u);
+      } else if (j < s.w) {
+        const int c = s.c0 + j;
+        if (!warm) e = S_CELL(255u, 0u);  // hb 0 = 2*t0 at t0 = 0
+        else if (c == r) e = S_CELL(254u, 0u);
+        else {
+          const int a = (int)((gm_mix64(seed ^ ((uint64_t)(uint32_t)r << 32) ^ (uint64_t)(uint32_t)c) >> 40) % 4);
+          e = S_CELL((uint32_t)(252 - 2 * a), (uint32_t)a);
+        }
       }
+      cw[q >> 1] |= e << (16 * (q & 1));
+      bw[q >> 2] |= s_narrow(e) << (8 * (q & 3));
     }
-    const size_t at = ((size_t)(j / s.band) * s.n + r) * s.band + j % s.band;
-    const uint32_t b = s_narrow(e);
-    s.table[at] = (uint8_t)b;
-    if (b == S_B_ESC) s.twide[at] = (uint16_t)e;
   }
-  if (threadIdx.x == 0) {
-    s.hbctr[r] = warm == 1 ? 2 * t0 : 0;
-    s.wtick[r] = t0;
+  const uint32_t em = esc_mask16(bw[0], bw[1], bw[2], bw[3]);
+  int etot;
+  const int eoff = row_scan<LPR>(__builtin_popcount(em), li, lane, etot);
+  const int par = t0 & 1;  // the state is "as of tick t0": tick t0 + 1 reads this pool
+  const uint32_t base = row_alloc<LPR>(&s.tesc_cnt[par], s.tesc_cap, etot, li, lane, s.err);
+  if (em && base != S_ESC_NONE) esc_store(s.tesc[par] + base + eoff, em, cw);
+  if (!row) return;
+  const size_t slab = (size_t)band * s.n;
+  *(u32x4 *)(s.table + (slab + r) * B + li * Q) = (u32x4){bw[0], bw[1], bw[2], bw[3]};
+  if (li == 0) {
+    s.brec[slab + r] = make_uint4(0u, 0u, 0u, base);
+    if (band == 0) {
+      s.hbctr[r] = warm == 1 ? 2 * t0 : 0;
+      s.wtick[r] = t0;
+    }
   }
 }
 
@@ -1362,7 +1469,21 @@ hipError_t gm_launch_plist_sort(const SState &s, int l, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t gm_launch_init(const SState &s, int warm, int t0, uint64_t seed, hipStream_t st) {
-  hipLaunchKernelGGL(gm_s_init, dim3(s.n), dim3(256), 0, st, s, warm, t0, seed);
+template <int B>
+static hipError_t launch_init_b(const SState &s, int warm, int t0, uint64_t seed, hipStream_t st) {
+  constexpr int RPW = 64 / (B / S_COLS_PER_LANE);
+  const dim3 nblk((((s.n + RPW - 1) / RPW) + 3) / 4, s.nb);
+  hipLaunchKernelGGL(gm_s_init<B>, nblk, dim3(256), 0, st, s, warm, t0, seed);
   return hipGetLastError();
+}
+
+hipError_t gm_launch_init(const SState &s, int warm, int t0, uint64_t seed, hipStream_t st) {
+  switch (s.band) {
+    case 64: return launch_init_b<64>(s, warm, t0, seed, st);
+    case 128: return launch_init_b<128>(s, warm, t0, seed, st);
+    case 256: return launch_init_b<256>(s, warm, t0, seed, st);
+    case 512: return launch_init_b<512>(s, warm, t0, seed, st);
+    case 1024: return launch_init_b<1024>(s, warm, t0, seed, st);
+    default: return hipErrorInvalidValue;
+  }
 }

@@ -4,6 +4,9 @@ size-independent properties (the oracle cannot finish these sizes in seconds):
 * S-A (configs[2]): N = 65,536 full membership, warm start, 1 % crash at tick 10 --
   exactly bench.py's schedule. Every live observer removes every crashed node exactly
   once (the TREMOVE sweep, /root/reference/MP1Node.cpp:429-444) and nothing else.
+* S-B (configs[3]) on ONE GPU: N = 262,144, the same schedule (2,621 crashed nodes) -- the
+  1-GPU point of the strong-scaling curve. 1 B of table + 1 B of payload nibbles per cell
+  (137 GB) plus the bounded escape pools (gm_scaled.h) fit one 288 GB MI355X.
 * S-C (configs[4], one GPU): N = 16,777,216, V = 32 partial views, 5 % keyed drops on
   every tick, 1 % crash at tick 10 -- bench.py --scenario S-C's schedule. Views stay
   full, id-sorted, self-present and fresh; crashed nodes leave every live view.
@@ -19,6 +22,36 @@ from membership import GM_EV_JOINED, GM_EV_REMOVED, GM_MODE_PARTIAL, GM_MODE_SCA
 pytestmark = pytest.mark.gpu
 
 TFAIL, TREMOVE = 5, 20
+
+
+def test_sb_config_on_one_gpu_removes_exactly_the_crashed_nodes():
+    n, crash_tick = 262144, 10
+    ncrash = int(round(n * 0.01))
+    sim = Simulator(n, GM_MODE_SCALED, rd_seed=7, init_mode=1, init_t0=8, init_seed=11)
+    sim.keep_events(0)  # 687 M removal records: counted on the device (event totals), not staged
+    crash = crash_set(n, ncrash, 42)
+    while sim.time <= 48:
+        t = sim.time
+        sim.tick()
+        if t == crash_tick:
+            sim.set_failed(crash)
+    sim.sync()
+    st = sim.tick_stats()
+    assert st["err"] == 0 and st["live"] == n - ncrash
+    assert st["lists"] == 5 * (n - ncrash)
+    tot = sim.event_totals()
+    assert tot["removed"] == (n - ncrash) * ncrash and tot["joined"] == 0, tot
+    crashed = np.zeros(n, bool)
+    crashed[crash] = True
+    t = sim.time - 1
+    for r in (0, n // 2 + 1, n - 1):
+        if crashed[r]:
+            continue
+        hb, ts = sim.read_row(r)
+        assert np.all(hb[crashed] == -1) and np.all(hb[~crashed] >= 0)
+        assert np.all(t - ts[~crashed] < TREMOVE)
+        assert hb[r] == 2 * t - 1 and ts[r] == t
+    sim.close()
 
 
 def test_sa_bench_config_removes_exactly_the_crashed_nodes():
