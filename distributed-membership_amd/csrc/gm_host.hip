@@ -45,11 +45,11 @@ size_t gm_partial_lds_bytes();
 void gm_partial_profile_dump();
 
 #define GM_T_LIMIT 32766  // packed 16-bit hb/ts stay exact: hb <= 2t+1 < 0xFFFF
-#define GM_F_MAILBOX 4096  // FAITHFUL events copied back with the count and error flags  // packed 16-bit hb/ts stay exact: hb <= 2t+1 < 0xFFFF
+#define GM_F_MAILBOX 4096  // FAITHFUL events copied back with the count and error flags
 #define GM_D_FIRST S_MT_RAW  // S2 outputs per row in the first round (steady state needs ~5-6)
-#define GM_D_MORE 64          // S2 outputs per row in later rounds (transients with many stale entries)
+#define GM_D_MORE GM_D_MORE_ROUND  // S2 outputs per row in later rounds (transients with many stale entries)
 #define GM_MAX_ROUNDS 4096    // draw rounds per sharded tick (16 + 64 * 4096 S2 outputs per row)
-#define GM_D_LAST 256         // bounded rounds: S2 outputs of round 2 (outputs [80, 336))
+#define GM_D_LAST GM_D_LAST_ROUND  // bounded rounds: S2 outputs of round 2 (outputs [80, 336))
 
 struct gm_ctx {
   gm_config cfg;
@@ -62,7 +62,12 @@ struct gm_ctx {
   bool nt = true;                    // non-temporal table streams (env GM_NT=0 to disable)
   int shard_sync = -1;               // sharded tick draw rounds: 1 host-driven unbounded loop, 0 bounded
                                      // stream-ordered, -1 auto (env GM_SHARD_SYNC)
-  int64_t nfailed = 0;               // nodes with failed_h set (gm_set_failed)
+  int64_t nfailed = 0;               // nodes with failed_h set (gm_set_failed; nodeStart clears it)
+  // sharded bounded draw rounds: rows they could not finish (npending) copied back without a
+  // wait; the next call that needs the tick finishes them with host-driven rounds (draw_settle)
+  int32_t *draw_left_h = nullptr;    // pinned
+  hipEvent_t draw_ev = nullptr;
+  bool draw_check = false;
   int t = 0;
   int n = 0;
   int dropmsg = 0;
@@ -374,7 +379,7 @@ static int create_scaled(gm_ctx *c) {
   TRY(dalloc(c, &s.brec, (size_t)n * s.nb));
   TRY(dalloc(c, &s.ev_band, (size_t)n * s.nb * s.evs));
   TRY(dalloc(c, &s.ev_spill, s.ev_spill_cap));
-  TRY(dalloc(c, &s.ev_spill_cnt, 1));
+  TRY(dalloc(c, &s.ev_spill_cnt, 2));
   TRY(dalloc(c, &s.evcum, (size_t)n * s.nb));
   TRY(dalloc(c, &s.mtraw, (size_t)n * S_MT_RAW));
   TRY(dalloc(c, &s.rowstat, (size_t)n * 4));
@@ -413,7 +418,7 @@ static int create_scaled(gm_ctx *c) {
     snprintf(g_errbuf, sizeof g_errbuf, "initial state overflows the escape pool (%u cells)", s.tesc_cap);
     return GM_ERANGE;
   }
-  HIPCHECK(hipMemset(s.ev_spill_cnt, 0, sizeof(uint32_t)));
+  HIPCHECK(hipMemset(s.ev_spill_cnt, 0, 2 * sizeof(uint32_t)));
   HIPCHECK(hipMemset(s.evcum, 0, sizeof(uint64_t) * (size_t)n * s.nb));
   HIPCHECK(hipMemset(s.rowstat, 0, sizeof(int32_t) * n * 4));
   if (s.sharded) {
@@ -427,6 +432,11 @@ static int create_scaled(gm_ctx *c) {
     // the next 64 for up to plist_cap rows left pending -- no host round trip per tick
     s.plist_cap[1] = std::min(S_PLIST_CAP, std::max(std::min(n, 1024), n / 16));  // round 1: 64 more outputs
     s.plist_cap[2] = 256;                                             // round 2: 256 more outputs
+    if (getenv("GM_PLIST_CAP"))  // diagnostics (tests): smaller lists, so rows overflow to the host-driven rounds
+      for (int l = 1; l <= 2; l++) s.plist_cap[l] = std::max(1, std::min(s.plist_cap[l], atoi(getenv("GM_PLIST_CAP"))));
+    if (hipHostMalloc(&c->draw_left_h, sizeof(int32_t), hipHostMallocDefault) != hipSuccess) return GM_ENOMEM;
+    *c->draw_left_h = 0;
+    HIPCHECK(hipEventCreateWithFlags(&c->draw_ev, hipEventDisableTiming));
     for (int l = 1; l <= 2; l++) {
       TRY(dalloc(c, &s.plist[l], s.plist_cap[l]));
       TRY(dalloc(c, &s.plist_cnt[l], 1));
@@ -575,8 +585,12 @@ extern "C" int gm_create(const gm_config *cfg, gm_ctx **out) {
 extern "C" int gm_destroy(gm_ctx *c) {
   if (!c) return GM_EINVAL;
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->p_side) (void)hipStreamSynchronize(c->p_side);  // the S2 prefetch of tick t+1 may still be writing
+  if (c->p_comm) (void)hipStreamSynchronize(c->p_comm);
   if (c->comm) (void)ncclCommDestroy(c->comm);
   for (void *p : c->allocs) (void)hipFree(p);
+  if (c->draw_left_h) (void)hipHostFree(c->draw_left_h);
+  if (c->draw_ev) (void)hipEventDestroy(c->draw_ev);
   if (c->f_mail) (void)hipHostFree(c->f_mail);
   for (hipEvent_t e : {c->e0, c->e1, c->k0, c->k1})
     if (e) (void)hipEventDestroy(e);
@@ -657,9 +671,14 @@ static int f_collect(gm_ctx *c) {
   return c->latched;
 }
 
-// Everything that reads FAITHFUL state (records, tables, counters, the S1 stream) first
-// completes the enqueued ticks.
-static int f_settle(gm_ctx *c) { return c->cfg.mode == GM_MODE_FAITHFUL ? f_collect(c) : GM_OK; }
+static int draw_settle(gm_ctx *c);
+
+// Everything that reads the state (records, tables, counters, the S1 stream) or starts the
+// next tick first completes the enqueued ticks: FAITHFUL collects its mailboxes; a column
+// shard finishes the draws its bounded rounds left (rare).
+static int f_settle(gm_ctx *c) {
+  return c->cfg.mode == GM_MODE_FAITHFUL ? f_collect(c) : c->cfg.mode == GM_MODE_SCALED ? draw_settle(c) : GM_OK;
+}
 
 // FAITHFUL ticks are enqueued without a host wait: the records stay on the device until a
 // call needs them (f_settle) or the next tick could overflow the record buffer.
@@ -671,6 +690,7 @@ static int tick_faithful(gm_ctx *c) {
     if ((int)(0.25 * i) == c->t && c->failed_h[i]) {
       c->failed_h[i] = 0;
       c->fail_t[i] = 0x7FFFFFFF;
+      c->nfailed--;
     }
   FState st = c->f;
   hipLaunchKernelGGL(gm_f_recv, dim3(1), dim3(1024), F_RECV_LDS, c->stream, st, c->t);
@@ -724,6 +744,7 @@ static int ramp_starters(gm_ctx *c) {
     if (c->failed_h[j]) {
       c->failed_h[j] = 0;
       c->fail_t[j] = 0x7FFFFFFF;
+      c->nfailed--;
       HIPCHECK(hipMemcpyAsync(c->s.failed + j, c->failed_h.data() + j, sizeof(int32_t), hipMemcpyHostToDevice,
                               c->stream));
     }
@@ -805,6 +826,7 @@ static int tick_partial(gm_ctx *c) {
 extern "C" int gm_tick(gm_ctx *c) {
   if (!c) return GM_EINVAL;
   if (c->latched != GM_OK) return c->latched;
+  if (c->cfg.mode == GM_MODE_SCALED) TRY(draw_settle(c));
   TRY(before_tick_events(c));
   int rc = c->cfg.mode == GM_MODE_FAITHFUL ? tick_faithful(c) : c->cfg.mode == GM_MODE_SCALED ? tick_scaled(c)
                                                                                              : tick_partial(c);
@@ -885,12 +907,20 @@ static int read_bcnt(gm_ctx *c, std::vector<uint32_t> &bc) {
   return GM_OK;
 }
 
+// Host-side staging bound: records kept for gm_drain_events (a caller that never drains gets
+// GM_ERANGE instead of unbounded host memory)
+#define GM_PENDING_CAP (1ull << 27)
+
 static int drain_scaled(gm_ctx *c, std::vector<gm_event> &out) {
   const SState &s = c->s;
   const size_t nrb = (size_t)c->n * s.nb;
   std::vector<uint32_t> bc;
-  uint32_t nsp = 0;
-  HIPCHECK(hipMemcpyAsync(&nsp, s.ev_spill_cnt, sizeof nsp, hipMemcpyDeviceToHost, c->stream));
+  uint32_t cnt[2] = {0, 0};  // spilled records, the tick's total
+  HIPCHECK(hipMemcpyAsync(cnt, s.ev_spill_cnt, sizeof cnt, hipMemcpyDeviceToHost, c->stream));
+  HIPCHECK(hipStreamSynchronize(c->stream));
+  if (cnt[1] == 0) return GM_OK;  // the common tick: nothing to stage, one 8-byte copy
+  if (out.size() + cnt[1] > GM_PENDING_CAP) return GM_ERANGE;
+  uint32_t nsp = cnt[0];
   TRY(read_bcnt(c, bc));
   const int t = c->t - 1;
   auto push = [&](int r, uint32_t rec) {
@@ -991,11 +1021,10 @@ extern "C" int gm_event_counts(gm_ctx *c, uint64_t counts[6]) {
   TRY(f_settle(c));
   for (int k = 0; k < 6; k++) counts[k] = 0;
   if (c->cfg.mode == GM_MODE_SCALED) {
-    std::vector<uint32_t> bc;
-    TRY(read_bcnt(c, bc));
-    uint64_t tot = 0;
-    for (uint32_t v : bc) tot += S_BC_NEV(v);  // slots + spilled, per (row, band)
-    counts[0] = tot;  // join+remove records of the last tick (per-kind split needs a drain)
+    uint32_t cnt[2] = {0, 0};
+    HIPCHECK(hipMemcpyAsync(cnt, c->s.ev_spill_cnt, sizeof cnt, hipMemcpyDeviceToHost, c->stream));
+    HIPCHECK(hipStreamSynchronize(c->stream));
+    counts[0] = cnt[1];  // join+remove records of the last tick (per-kind split needs a drain)
   } else if (c->cfg.mode == GM_MODE_PARTIAL) {
     std::vector<int32_t> cnt(c->p.nloc);
     HIPCHECK(hipMemcpyAsync(cnt.data(), c->p.ev_cnt, sizeof(int32_t) * c->p.nloc, hipMemcpyDeviceToHost, c->stream));
@@ -1176,6 +1205,7 @@ static int read_table_row(gm_ctx *c, int r, std::vector<int32_t> &hb, std::vecto
 
 extern "C" int gm_read_row(gm_ctx *c, int32_t r, int32_t c0, int32_t len, int32_t *hb, int32_t *ts) {
   if (!c || !hb || !ts || r < 0 || r >= c->n || c0 < 0 || len < 0) return GM_EINVAL;
+  TRY(f_settle(c));
   HIPCHECK(hipStreamSynchronize(c->stream));
   std::vector<int32_t> rh, rt;
   int w;
@@ -1489,6 +1519,7 @@ extern "C" int gm_shard_end_tick(gm_ctx *c) {
     c->timed_ticks++;
   }
   c->t++;
+  c->ticks_done++;
   c->undrained = true;
   return GM_OK;
 }
@@ -1561,6 +1592,7 @@ static int tick_sharded(gm_ctx *c) {
     // round 1 serves with the next 64; a row still short after that sets GM_ERR_DRAWS
     SState &s = c->s;
     for (int l = 1; l <= 2; l++) HIPCHECK(hipMemsetAsync(s.plist_cnt[l], 0, sizeof(uint32_t), c->stream));
+    HIPCHECK(hipMemsetAsync(s.npending, 0, sizeof(int32_t), c->stream));
     HIPCHECK(gm_launch_draw(s, c->t, 0, GM_D_FIRST, 0, c->stream));
     if (!s.stub)
       NCCLCHECK(ncclAllReduce(s.status, s.status, n * GM_D_FIRST, ncclInt32, ncclMax, c->comm, c->stream));
@@ -1583,8 +1615,13 @@ static int tick_sharded(gm_ctx *c) {
       fprintf(stderr, "[gm] t=%d rows pending after round 0: %u (cap %d), after round 1: %u (cap %d), err 0x%x\n", c->t,
               pc1, s.plist_cap[1], pc2, s.plist_cap[2], e);
     }
+    // rows the bounded rounds could not take: counted on the device, read back without a wait
+    HIPCHECK(hipMemcpyAsync(c->draw_left_h, s.npending, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHECK(hipEventRecord(c->draw_ev, c->stream));
+    c->draw_check = true;
     c->t--;  // gm_tick advances globaltime
     TRY(gm_shard_end_tick(c));
+    c->ticks_done--;  // gm_tick counts it
     return GM_OK;
   }
   int round = 0, D = GM_D_FIRST;
@@ -1606,7 +1643,38 @@ static int tick_sharded(gm_ctx *c) {
   }
   c->t--;  // gm_tick advances globaltime
   TRY(gm_shard_end_tick(c));
+  c->ticks_done--;  // gm_tick counts it
   return GM_OK;
+}
+
+// The rows the last sharded tick's bounded rounds left (a full pending list, or still short of
+// targets after 336 S2 outputs): host-driven rounds, each row continuing from its own next round
+// (gm_s_draw with round >= 1 reads it from pending[r]), until every row has its targets --
+// tick t = c->t - 1 completes before anything reads it or the next tick starts.
+static int draw_settle(gm_ctx *c) {
+  if (!c->draw_check) return c->latched;
+  c->draw_check = false;
+  HIPCHECK(hipEventSynchronize(c->draw_ev));
+  int32_t pend = *c->draw_left_h;
+  const int t = c->t - 1;
+  const size_t n = (size_t)c->n;
+  for (int round = 0; pend > 0; round++) {
+    if (getenv("GM_DEBUG_ROUNDS")) fprintf(stderr, "[gm] t=%d settle round %d: %d rows still drawing\n", t, round, pend);
+    if (round >= GM_MAX_ROUNDS) {
+      uint32_t e = GM_ERR_DRAWS;
+      HIPCHECK(hipMemcpy(c->s.err, &e, sizeof e, hipMemcpyHostToDevice));
+      c->latched = GM_ERANGE;
+      return c->latched;
+    }
+    HIPCHECK(gm_launch_draw(c->s, t, 1, GM_D_MORE, 0, c->stream));
+    if (!c->s.stub)
+      NCCLCHECK(ncclAllReduce(c->s.status, c->s.status, n * GM_D_MORE, ncclInt32, ncclMax, c->comm, c->stream));
+    HIPCHECK(hipMemsetAsync(c->s.npending, 0, sizeof(int32_t), c->stream));
+    HIPCHECK(gm_launch_accept(c->s, t, GM_D_MORE, 0, 0, c->stream));
+    HIPCHECK(hipMemcpyAsync(&pend, c->s.npending, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHECK(hipStreamSynchronize(c->stream));
+  }
+  return c->latched;
 }
 
 // ------------------------------------------------------------ PARTIAL row shards
@@ -1705,6 +1773,7 @@ extern "C" int gm_partial_loopback_tick(gm_ctx **ctxs, int32_t G) {
     HIPCHECK(hipStreamSynchronize(ctxs[g]->stream));
     TRY(check_err(ctxs[g]));
     ctxs[g]->t++;
+    ctxs[g]->ticks_done++;
     ctxs[g]->undrained = true;
   }
   return GM_OK;

@@ -12,6 +12,8 @@
 #define S_MT_RAW 16              // mt19937 outputs precomputed per row and tick (gm_s_mtgen)
 #define S_SELFADD_CAP 65536      // join ramp: self appends verified per tick (gm_s_selfcheck)
 #define S_PLIST_CAP 4096         // sharded tick: rows a second (bounded) draw round takes
+#define GM_D_MORE_ROUND 64       // S2 outputs of bounded round 1 (= one host-driven round)
+#define GM_D_LAST_ROUND 256      // S2 outputs of bounded round 2 (= host-driven rounds 2..5)
 
 // SCALED cell (16 bits), relative to the tick w the row was last written at:
 //   h = 255 - (2w - hb) (8 bits, the heartbeat; larger = newer), age = w - ts (5 bits);
@@ -114,7 +116,7 @@ struct SState {
                            // slice's escaped cells in tesc[t & 1] (S_ESC_NONE: none); rows adjacent = whole-line writes
   uint32_t *ev_band;       // [n][nb][evs] kind<<30 | subject id
   uint64_t *ev_spill;      // overflow: (logger<<32) | kind<<30 | subject id
-  uint32_t *ev_spill_cnt;
+  uint32_t *ev_spill_cnt;  // [2]: spill records, then the tick's total records (all rows and bands)
   uint64_t *evcum;         // [n][nb] cumulative events since create: joins | removals << 32 (single writer per cell)
   uint32_t *mtraw;        // [n][S_MT_RAW] first mt19937 outputs of each row's S2 stream this tick
   int32_t *rowstat;        // [n][4]: lists delivered, present, numfailed, targets chosen

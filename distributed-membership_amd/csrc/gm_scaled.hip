@@ -710,6 +710,7 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
   const int E = s.evs;
   uint32_t sbase = 0;  // one spill-ring reservation per (row, band) that overflows its slots
   if (live && li == 0 && tot > E) sbase = atomicAdd(s.ev_spill_cnt, (uint32_t)(tot - E));
+  if (live && li == 0 && tot) atomicAdd(s.ev_spill_cnt + 1, (uint32_t)tot);  // the tick's total (host staging)
   sbase = LPR == 64 ? __builtin_amdgcn_readfirstlane(sbase) : __shfl(sbase, sub * LPR, 64);
   if (live && nev) {
     int slot = x - nev;
@@ -1196,6 +1197,10 @@ __global__ __launch_bounds__(256) void gm_s_draw(SState s, int t, int round, int
   } else if (!s.pending[r]) {
     return;
   }
+  // the round of this row's draws: the launch's for a bounded round over a pending list;
+  // the row's own (pending[r] = its next round) in the host-driven loop, where rows that a
+  // bounded round could not take continue from where they stopped
+  const int rr = (round == 0 || listed) ? round : s.pending[r];
   const uint32_t size = (uint32_t)acc[7];
   uint32_t own_lo = 0;
   for (int g = 0; g < s.shard_rank; g++) own_lo += (uint32_t)s.xcnt[((size_t)g * s.n + r) * 2] & S_XC_COUNT;
@@ -1215,7 +1220,7 @@ __global__ __launch_bounds__(256) void gm_s_draw(SState s, int t, int round, int
     if (round == 0) {
       if (lane < cnt) raw = s.mtraw[(size_t)r * S_MT_RAW + d0 + lane];
     } else {  // round q >= 1 continues after 16 + 64 (q - 1) outputs (round 2 of the bounded tick: after 80)
-      raw = gm_mt_batch(mt, mts, gm_rd_seed(s.rd_seed, t, r + 1), d0 == 0, S_MT_RAW + 64 * (round - 1) + d0, cnt,
+      raw = gm_mt_batch(mt, mts, gm_rd_seed(s.rd_seed, t, r + 1), d0 == 0, S_MT_RAW + 64 * (rr - 1) + d0, cnt,
                         lane);
     }
     const uint64_t prod = (uint64_t)raw * size;
@@ -1250,6 +1255,7 @@ __global__ __launch_bounds__(256) void gm_s_draw(SState s, int t, int round, int
     }
     if (lane < cnt) st[d0 + lane] = val;
   }
+  if (rr > 0 && !listed && lane == 0) s.pending[r] = rr + 1;
 }
 
 // Phase C: with every draw resolved (MAX-allreduced status), run the acceptance loop
@@ -1292,14 +1298,21 @@ __global__ __launch_bounds__(256) void gm_s_accept(SState s, int t, int D, int i
   for (int q = 0; q < n; q++) acc[1 + q] = g[q];
   acc[0] = n;
   if (!done) {
+    // pending[r] = the row's next round: host-driven rounds q >= 1 draw S2 outputs
+    // [16 + 64(q-1), 16 + 64q), so bounded round 1 = host round 1 and bounded round 2 (outputs
+    // [80, 336)) = host rounds 2..5. A row no bounded round takes (its list is full, or it is
+    // still short after round 2) is counted in npending; the host finishes it with the
+    // host-driven rounds before anything reads the tick (draw_settle, gm_host.hip)
     if (out == 0) {
-      atomicAdd(s.npending, 1);
+      atomicAdd(s.npending, 1);  // gm_s_draw advanced pending[r]
     } else if (out > 0) {
+      s.pending[r] = out;
       const uint32_t slot = atomicAdd(s.plist_cnt[out], 1u);
       if (slot < (uint32_t)s.plist_cap[out]) s.plist[out][slot] = r;
-      else atomicOr(s.err, GM_ERR_DRAWS);  // more rows than the bounded round takes
+      else atomicAdd(s.npending, 1);
     } else {
-      atomicOr(s.err, GM_ERR_DRAWS);  // the bounded rounds' draws did not fill the row's targets
+      s.pending[r] = 1 + (GM_D_MORE_ROUND + GM_D_LAST_ROUND) / 64;
+      atomicAdd(s.npending, 1);
     }
     return;
   }
@@ -1386,7 +1399,7 @@ static hipError_t launch_tick_b(const SState &s, int t, int drop_pct, bool nt, h
   constexpr int RPW = 64 / (B / S_COLS_PER_LANE);
   const dim3 nblk((((s.n + RPW - 1) / RPW) + 3) / 4, s.nb);  // (units of a band / 4, bands)
   // the event records of a tick (per-(row, band) slots + spill ring) stay readable until the next tick
-  (void)hipMemsetAsync(s.ev_spill_cnt, 0, sizeof(uint32_t), st);
+  (void)hipMemsetAsync(s.ev_spill_cnt, 0, 2 * sizeof(uint32_t), st);
   hipLaunchKernelGGL(gm_s_mtgen, dim3((s.n + 255) / 256), dim3(256), 0, st, s, t);
   if (k0) (void)hipEventRecord(k0, st);
   if (drop_pct >= 0) hipLaunchKernelGGL((gm_s_band<B, true>), dim3(nblk), dim3(256), 0, st, s, t, drop_pct);

@@ -56,23 +56,28 @@ def test_shards_match_fused_kernel(n, world, drop, warm):
 
 
 @pytest.mark.parametrize("n,drop,ncrash,rounds", [(777, 0, 12, "auto"), (2048, 20, 32, "auto"), (777, 0, 12, "sync"),
-                                                  (777, 0, 388, "bounded")])
+                                                  (777, 0, 388, "bounded"), (777, 0, 388, "overflow")])
 def test_rccl_single_rank_matches_fused_kernel(n, drop, ncrash, rounds, monkeypatch):
     """The RCCL-driven sharded tick (gm_tick -> ncclAllGather / ncclAllReduce on the
     context stream) with one forced shard on the one GPU this box has: the exact
     collective calls the multi-GPU run makes, degenerate only in the rank count.
     "auto" takes the bounded, stream-ordered draw rounds here; "sync" the host-driven
     loop; "bounded" with half the cluster crashed forces the bounded path with many rows
-    left pending after round 0, so round 1 (the sorted pending list) does real work."""
+    left pending after round 0, so round 1 (the sorted pending list) does real work;
+    "overflow" shrinks both pending lists to 4 rows (GM_PLIST_CAP), so most pending rows
+    overflow them and finish in the host-driven rounds, each from its own next round."""
     from membership.abi import comm_unique_id
     kw = dict(rd_seed=7, drop_pct=drop, drop_from=3, drop_to=25, drop_seed=42, init_mode=1, init_t0=6, init_seed=5)
     ref = Simulator(n, GM_MODE_SCALED, **kw)
     monkeypatch.setenv("GM_FORCE_SHARD", "1")
     if rounds != "auto":
         monkeypatch.setenv("GM_SHARD_SYNC", "1" if rounds == "sync" else "0")
+    if rounds == "overflow":
+        monkeypatch.setenv("GM_PLIST_CAP", "4")
     sh = Simulator(n, GM_MODE_SCALED, shard_rank=0, shard_count=1, **kw)
     monkeypatch.delenv("GM_FORCE_SHARD")
     monkeypatch.delenv("GM_SHARD_SYNC", raising=False)
+    monkeypatch.delenv("GM_PLIST_CAP", raising=False)
     sh.comm_init(comm_unique_id(), 1, 0)
     crash = crash_set(n, ncrash, 42)
     for _ in range(32):
