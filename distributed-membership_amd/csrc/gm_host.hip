@@ -40,7 +40,7 @@ hipError_t gm_launch_partial_unpack(const PState &s, int t, int base, int nrecv,
 hipError_t gm_launch_partial_mtgen(const PState &s, int t, uint32_t *mtraw, hipStream_t st, bool reset);
 hipError_t gm_launch_partial_reset(const PState &s, hipStream_t st);
 hipError_t gm_launch_partial_chunk(const PState &s, int t, const uint32_t *mtraw, int c, hipStream_t st);
-hipError_t gm_launch_msgcount(const SState &s, int t, bool dropped, hipStream_t st);
+hipError_t gm_launch_msgcount(const SState &s, int t, bool dropped, int phase, hipStream_t st);
 size_t gm_partial_lds_bytes();
 void gm_partial_profile_dump();
 
@@ -340,7 +340,8 @@ static int create_scaled(gm_ctx *c) {
   s.nb = s.wp / s.band;
   if ((size_t)n * s.band * 2 >= (1ull << 31)) return GM_EUNSUPPORTED;  // 32-bit buffer offsets per band slab
   s.evs = s.band / 32;
-  if (sizeof(uint32_t) * 4 * ((size_t)(s.wp >> 6) + 1 + 624) > 65536) return GM_EUNSUPPORTED;  // draw kernels' LDS
+  // draw kernels' LDS: 4 waves x (chunk prefix + lazy MT state); N = 262,144 on one GPU: 42 KB
+  if (sizeof(uint32_t) * 4 * ((size_t)(s.wp / S_CHUNK(s.band)) + 1 + 624) > 65536) return GM_EUNSUPPORTED;
   s.ev_spill_cap = 1u << 24;
   s.rd_seed = c->cfg.rd_seed;
   s.drop_seed = c->cfg.drop_seed;
@@ -760,7 +761,10 @@ static int tick_scaled(gm_ctx *c) {
   hipEvent_t k0 = nullptr, k1 = nullptr;
   if (c->timing) TRY(timing_slot(c, &k0, &k1));
   HIPCHECK(gm_launch_tick(c->s, c->t, drop ? c->cfg.drop_pct : -1, c->nt, c->stream, k0, k1, true));
-  if (c->s.mc_sent && c->t < c->s.mc_tmax) HIPCHECK(gm_launch_msgcount(c->s, c->t, drop, c->stream));
+  if (c->s.mc_sent && c->t < c->s.mc_tmax) {
+    HIPCHECK(gm_launch_msgcount(c->s, c->t, drop, 0, c->stream));
+    HIPCHECK(gm_launch_msgcount(c->s, c->t, drop, 1, c->stream));
+  }
   if (c->timing) {
     HIPCHECK(hipEventRecord(c->e1, c->stream));
     c->timed_ticks++;
@@ -1068,7 +1072,6 @@ extern "C" int gm_msgcount_record(gm_ctx *c, int32_t tmax) {
   if (!c || tmax <= 0 || tmax > GM_T_LIMIT + 1) return GM_EINVAL;
   if (c->cfg.mode == GM_MODE_FAITHFUL) return GM_OK;
   if (c->ticks_done) return GM_ESTATE;  // the received counts need the senders' counts of the tick before
-  if (c->cfg.mode == GM_MODE_SCALED && c->s.sharded) return GM_EUNSUPPORTED;
   if (c->cfg.mode == GM_MODE_SCALED ? c->s.mc_sent != nullptr : c->p.mc_sent != nullptr) return GM_ESTATE;
   const size_t rows = c->cfg.mode == GM_MODE_SCALED ? (size_t)c->n : (size_t)c->p.nloc;
   uint32_t *ms = nullptr, *mr = nullptr;
@@ -1473,6 +1476,11 @@ extern "C" int gm_shard_layout(gm_ctx *c, int32_t *c0, int32_t *w) {
   return GM_OK;
 }
 
+static bool drop_tick(const gm_ctx *c, int t) {  // keyed loss applies to the lists sent at t - 1
+  return c->cfg.drop_pct > 0 && t - 1 >= c->cfg.drop_from && t - 1 < c->cfg.drop_to;
+}
+static bool mc_on(const gm_ctx *c, int t) { return c->s.mc_sent && t < c->s.mc_tmax; }
+
 static int shard_ready(gm_ctx *c) {
   if (!c || c->cfg.mode != GM_MODE_SCALED || !c->s.sharded) return GM_EINVAL;
   if (c->latched != GM_OK) return c->latched;
@@ -1491,6 +1499,8 @@ extern "C" int gm_shard_merge(gm_ctx *c) {
   hipEvent_t k0 = nullptr, k1 = nullptr;
   if (c->timing) TRY(timing_slot(c, &k0, &k1));
   HIPCHECK(gm_launch_tick(c->s, c->t, drop ? c->cfg.drop_pct : -1, c->nt, c->stream, k0, k1, false));
+  // msgcount: this shard's fresh counts (its columns), SUM-allreduced before the draws
+  if (mc_on(c, c->t)) HIPCHECK(gm_launch_msgcount(c->s, c->t, drop, 0, c->stream));
   return GM_OK;
 }
 
@@ -1514,6 +1524,9 @@ extern "C" int gm_shard_accept(gm_ctx *c, int32_t D, int32_t *npending) {
 
 extern "C" int gm_shard_end_tick(gm_ctx *c) {
   TRY(shard_ready(c));
+  // msgcount: sent / received once the targets are final (after draw_settle when bounded
+  // rounds left rows to the host-driven loop)
+  if (!c->draw_check && mc_on(c, c->t)) HIPCHECK(gm_launch_msgcount(c->s, c->t, drop_tick(c, c->t), 1, c->stream));
   if (c->timing) {  // band-kernel events are in the timing ring (no host wait here)
     HIPCHECK(hipEventRecord(c->e1, c->stream));
     c->timed_ticks++;
@@ -1528,9 +1541,14 @@ __global__ void gm_max_into(int32_t *dst, const int32_t *src, size_t n) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
     dst[i] = max(dst[i], src[i]);
 }
+__global__ void gm_add_into(uint32_t *dst, const uint32_t *src, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    dst[i] += src[i];
+}
 
 // In-process collectives between the G shard contexts of one device:
-// what = 0 all-gathers xcnt, what = 1 MAX-allreduces status[0, n*D).
+// what = 0 all-gathers xcnt, what = 1 MAX-allreduces status[0, n*D), what = 2 SUM-allreduces
+// the msgcount fresh counts of this tick (and the kept entries on a loss tick).
 extern "C" int gm_shard_loopback(gm_ctx **ctxs, int32_t G, int32_t what, int32_t D) {
   if (!ctxs || G < 2) return GM_EINVAL;
   for (int g = 0; g < G; g++) {
@@ -1546,6 +1564,15 @@ extern "C" int gm_shard_loopback(gm_ctx **ctxs, int32_t G, int32_t what, int32_t
         if (src != dst)
           HIPCHECK(hipMemcpyAsync(ctxs[dst]->s.xcnt + (size_t)src * n * 2, ctxs[src]->s.xcnt + (size_t)src * n * 2,
                                   sizeof(int32_t) * n * 2, hipMemcpyDeviceToDevice, st));
+  } else if (what == 2) {  // msgcount: SUM of the shards' fresh counts (and kept entries on loss ticks)
+    const int t = ctxs[0]->t;
+    if (!mc_on(ctxs[0], t)) return GM_ESTATE;
+    const bool dropped = drop_tick(ctxs[0], t);
+    for (int k = 0; k < (dropped ? 2 : 1); k++) {
+      auto buf = [&](int g) { return k == 0 ? ctxs[g]->s.mc_fresh + (size_t)(t & 1) * n : ctxs[g]->s.mc_rdrop; };
+      for (int g = 1; g < G; g++) hipLaunchKernelGGL(gm_add_into, dim3(64), dim3(256), 0, st, buf(0), buf(g), n);
+      for (int g = 1; g < G; g++) HIPCHECK(hipMemcpyAsync(buf(g), buf(0), sizeof(uint32_t) * n, hipMemcpyDeviceToDevice, st));
+    }
   } else {
     if (D <= 0 || D > ctxs[0]->dmax) return GM_EINVAL;
     const size_t cnt = n * (size_t)D;
@@ -1581,6 +1608,12 @@ static int tick_sharded(gm_ctx *c) {
   } else {
     NCCLCHECK(ncclAllGather(c->s.xcnt + (size_t)c->s.shard_rank * n * 2, c->s.xcnt, n * 2, ncclInt32, c->comm,
                             c->stream));
+    if (mc_on(c, c->t)) {  // msgcount: whole-row fresh counts (and kept entries on loss ticks)
+      NCCLCHECK(ncclAllReduce(c->s.mc_fresh + (size_t)(c->t & 1) * n, c->s.mc_fresh + (size_t)(c->t & 1) * n, n,
+                              ncclUint32, ncclSum, c->comm, c->stream));
+      if (drop_tick(c, c->t))
+        NCCLCHECK(ncclAllReduce(c->s.mc_rdrop, c->s.mc_rdrop, n, ncclUint32, ncclSum, c->comm, c->stream));
+    }
   }
   const int64_t nfailed = c->nfailed;
   // mass failure or heavy loss leaves many entries stale, so rows need many draws: the
@@ -1618,8 +1651,8 @@ static int tick_sharded(gm_ctx *c) {
     // rows the bounded rounds could not take: counted on the device, read back without a wait
     HIPCHECK(hipMemcpyAsync(c->draw_left_h, s.npending, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
     HIPCHECK(hipEventRecord(c->draw_ev, c->stream));
-    c->draw_check = true;
     c->t--;  // gm_tick advances globaltime
+    c->draw_check = true;  // before end_tick: the msgcount phase waits for draw_settle
     TRY(gm_shard_end_tick(c));
     c->ticks_done--;  // gm_tick counts it
     return GM_OK;
@@ -1674,6 +1707,7 @@ static int draw_settle(gm_ctx *c) {
     HIPCHECK(hipMemcpyAsync(&pend, c->s.npending, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
     HIPCHECK(hipStreamSynchronize(c->stream));
   }
+  if (mc_on(c, t)) HIPCHECK(gm_launch_msgcount(c->s, t, drop_tick(c, t), 1, c->stream));
   return c->latched;
 }
 

@@ -833,9 +833,12 @@ __global__ __launch_bounds__(256) void gm_s_selfcheck(SState s) {
 }
 
 // ------------------------------------------------------- wave-per-row helpers
-// LDS per wave of the draw kernels: chunk prefix [wp/64 + 1] u32, the fallback
-// generator's state [624] u32.
-__host__ __device__ __forceinline__ size_t gm_draw_lds_words(int wp) { return (size_t)(wp >> 6) + 1 + 624; }  // >= chunks + 1
+// LDS per wave of the draw kernels: chunk prefix [chunks + 1] u32 (S_CHUNK(B) columns per
+// chunk), the fallback generator's state [624] u32.
+__host__ __device__ __forceinline__ int gm_draw_chunks(int wp, int band) { return wp / S_CHUNK(band); }  // rank-select chunks per row
+__host__ __device__ __forceinline__ size_t gm_draw_lds_words(int wp, int band) {
+  return (size_t)gm_draw_chunks(wp, band) + 1 + 624;
+}
 
 // Row r of this shard: numfailed (band counts), size and the chunk prefix
 // pre[c] = present cells in chunks [0, c) (pre[nc] = size), from the chunk counts.
@@ -969,8 +972,8 @@ __global__ __launch_bounds__(256) void gm_s_pick(SState s, int t) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = blockIdx.x * 4 + wave;
   if (r >= s.n) return;  // whole wave; no workgroup barrier follows
-  uint32_t *pre = p_smem + wave * gm_draw_lds_words(s.wp);
-  uint32_t *mts = pre + (s.wp >> 6) + 1;
+  uint32_t *pre = p_smem + wave * gm_draw_lds_words(s.wp, B);
+  uint32_t *mts = pre + gm_draw_chunks(s.wp, B) + 1;
   const int par = t & 1;
   int32_t *stat = s.rowstat + (size_t)r * 4;
   const int k = s.inbox_cnt[par][r];
@@ -1070,15 +1073,19 @@ __global__ __launch_bounds__(256) void gm_s_pick(SState s, int t) {
 }
 
 // ------------------------------------------------------------ gm_s_msgcount
-// msgcount analogue of tick t (gm_msgcount_record), after gm_s_pick, one wave per row:
-// fresh = the row's non-zero payload nibbles of this tick (the entries it sends, MP1Node.cpp:
-// 372-375), sent = fresh x targets; received = the entries of its delivered lists -- the
-// senders' fresh counts of tick t-1, or the DROP band kernel's count of kept entries.
+// msgcount analogue of tick t (gm_msgcount_record), in two phases:
+//   gm_s_mcfresh (after gm_s_band, wave per row): fresh = the row's non-zero payload nibbles of
+//     this tick in this context's columns (the entries it sends, MP1Node.cpp:372-375);
+//     column shards SUM-allreduce it (and the DROP band kernel's per-row kept counts), so
+//     every rank holds the whole row's counts;
+//   gm_s_mcount (after the targets are final, thread per row): sent = fresh x targets;
+//     received = the entries of the delivered lists -- the senders' fresh counts of tick t-1,
+//     or on loss ticks the kept entries counted by the DROP band kernel.
 __device__ __forceinline__ uint32_t nz_nibbles(uint32_t x) {
   return (uint32_t)__builtin_popcount((x | (x >> 1) | (x >> 2) | (x >> 3)) & 0x11111111u);
 }
 template <int B>
-__global__ __launch_bounds__(256) void gm_s_msgcount(SState s, int t, int dropped) {
+__global__ __launch_bounds__(256) void gm_s_mcfresh(SState s, int t) {
   const int lane = threadIdx.x & 63;
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= s.n) return;  // whole wave
@@ -1091,30 +1098,39 @@ __global__ __launch_bounds__(256) void gm_s_msgcount(SState s, int t, int droppe
   }
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) f += __shfl_xor(f, o, 64);
-  if (lane == 0) {
-    const int32_t *stat = s.rowstat + (size_t)r * 4;
-    uint32_t recv = 0;
-    if (dropped) {
-      recv = s.mc_rdrop[r];
-      s.mc_rdrop[r] = 0;
-    } else {
-      const int k = min(stat[0], S_KMAX);  // 0 for rows not merged this tick
-      for (int q = 0; q < k; q++) recv += s.mc_fresh[(size_t)(par ^ 1) * s.n + s.inbox[par][(size_t)r * S_KMAX + q]];
-    }
-    s.mc_sent[(size_t)t * s.n + r] = (uint32_t)stat[3] * f;
-    s.mc_recv[(size_t)t * s.n + r] = recv;
-    s.mc_fresh[(size_t)par * s.n + r] = f;
-  }
+  if (lane == 0) s.mc_fresh[(size_t)par * s.n + r] = f;
 }
 
-hipError_t gm_launch_msgcount(const SState &s, int t, bool dropped, hipStream_t st) {
+__global__ __launch_bounds__(256) void gm_s_mcount(SState s, int t, int dropped) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= s.n) return;
+  const int par = t & 1;
+  const int32_t *stat = s.rowstat + (size_t)r * 4;
+  uint32_t recv = 0;
+  if (dropped) {
+    recv = s.mc_rdrop[r];
+    s.mc_rdrop[r] = 0;
+  } else {
+    const int k = min(stat[0], S_KMAX);  // 0 for rows not merged this tick
+    for (int q = 0; q < k; q++) recv += s.mc_fresh[(size_t)(par ^ 1) * s.n + s.inbox[par][(size_t)r * S_KMAX + q]];
+  }
+  s.mc_sent[(size_t)t * s.n + r] = (uint32_t)stat[3] * s.mc_fresh[(size_t)par * s.n + r];
+  s.mc_recv[(size_t)t * s.n + r] = recv;
+}
+
+// phase 0: fresh counts (gm_s_mcfresh); phase 1: sent / received (gm_s_mcount)
+hipError_t gm_launch_msgcount(const SState &s, int t, bool dropped, int phase, hipStream_t st) {
+  if (phase == 1) {
+    hipLaunchKernelGGL(gm_s_mcount, dim3((s.n + 255) / 256), dim3(256), 0, st, s, t, dropped ? 1 : 0);
+    return hipGetLastError();
+  }
   const dim3 g((s.n + 3) / 4), b(256);
   switch (s.band) {
-    case 64: hipLaunchKernelGGL(gm_s_msgcount<64>, g, b, 0, st, s, t, dropped ? 1 : 0); break;
-    case 128: hipLaunchKernelGGL(gm_s_msgcount<128>, g, b, 0, st, s, t, dropped ? 1 : 0); break;
-    case 256: hipLaunchKernelGGL(gm_s_msgcount<256>, g, b, 0, st, s, t, dropped ? 1 : 0); break;
-    case 512: hipLaunchKernelGGL(gm_s_msgcount<512>, g, b, 0, st, s, t, dropped ? 1 : 0); break;
-    case 1024: hipLaunchKernelGGL(gm_s_msgcount<1024>, g, b, 0, st, s, t, dropped ? 1 : 0); break;
+    case 64: hipLaunchKernelGGL(gm_s_mcfresh<64>, g, b, 0, st, s, t); break;
+    case 128: hipLaunchKernelGGL(gm_s_mcfresh<128>, g, b, 0, st, s, t); break;
+    case 256: hipLaunchKernelGGL(gm_s_mcfresh<256>, g, b, 0, st, s, t); break;
+    case 512: hipLaunchKernelGGL(gm_s_mcfresh<512>, g, b, 0, st, s, t); break;
+    case 1024: hipLaunchKernelGGL(gm_s_mcfresh<1024>, g, b, 0, st, s, t); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -1139,8 +1155,8 @@ __global__ __launch_bounds__(256) void gm_s_draw(SState s, int t, int round, int
   if (listed && i >= (int)min(*s.plist_cnt[listed], (uint32_t)s.plist_cap[listed])) return;
   const int r = listed ? s.plist[listed][i] : i;
   if (r >= s.n) return;
-  uint32_t *pre = p_smem + wave * gm_draw_lds_words(s.wp);
-  uint32_t *mts = pre + (s.wp >> 6) + 1;
+  uint32_t *pre = p_smem + wave * gm_draw_lds_words(s.wp, B);
+  uint32_t *mts = pre + gm_draw_chunks(s.wp, B) + 1;
   const int G = s.shard_count;
   int32_t *acc = s.acc + (size_t)r * 8;
   if (round == 0) {
@@ -1411,7 +1427,7 @@ static hipError_t launch_tick_b(const SState &s, int t, int drop_pct, bool nt, h
     hipLaunchKernelGGL(gm_s_selfcheck, dim3(16), dim3(256), 0, st, s);
     (void)hipMemsetAsync(s.selfadd_cnt, 0, sizeof(uint32_t), st);
   }
-  const size_t smem = sizeof(uint32_t) * 4 * gm_draw_lds_words(s.wp);
+  const size_t smem = sizeof(uint32_t) * 4 * gm_draw_lds_words(s.wp, s.band);
   if (pick) hipLaunchKernelGGL((gm_s_pick<B>), dim3((s.n + 3) / 4), dim3(256), smem, st, s, t);
   return hipGetLastError();
 }
@@ -1429,7 +1445,7 @@ hipError_t gm_launch_tick(const SState &s, int t, int drop_pct, bool nt, hipStre
 }
 
 hipError_t gm_launch_draw(const SState &s, int t, int round, int D, int listed, hipStream_t st) {
-  const size_t smem = sizeof(uint32_t) * 4 * gm_draw_lds_words(s.wp);
+  const size_t smem = sizeof(uint32_t) * 4 * gm_draw_lds_words(s.wp, s.band);
   const dim3 grid(((listed ? s.plist_cap[listed] : s.n) + 3) / 4), blk(256);
   switch (s.band) {
     case 64: hipLaunchKernelGGL(gm_s_draw<64>, grid, blk, smem, st, s, t, round, D, listed); break;

@@ -228,6 +228,10 @@ class Simulator:
     def msgcount_record(self, tmax):
         """SCALED / PARTIAL: record per-node entry counts for ticks < tmax (before the first tick)"""
         self._call("gm_msgcount_record", self.h, tmax)
+        self._mc_tmax = tmax
+
+    def msgcount_recording(self, t):
+        return t < getattr(self, "_mc_tmax", 0)
 
     def msgcount(self, t, rows=None):
         """[rows][t] sent / recv entry messages per node and tick (rows: this context's nodes)"""

@@ -32,6 +32,8 @@ def loopback_tick(sims):
     for s in sims:
         s.shard_merge()
     shard_loopback(sims, 0)
+    if sims[0].msgcount_recording(sims[0].time):
+        shard_loopback(sims, 2)  # msgcount: whole-row fresh counts on every shard
     rnd, d = 0, D_FIRST
     while True:
         for s in sims:

@@ -170,7 +170,9 @@ int gm_event_totals(gm_ctx *ctx, uint64_t totals[6]);
 int gm_msgcount(gm_ctx *ctx, int32_t t, int32_t *sent, int32_t *recv);
 /* SCALED / PARTIAL: start recording the per-node counts of gm_msgcount for ticks < tmax
  * (device history of 8 * tmax bytes per node). Only before the first tick (GM_ESTATE
- * after); single-context SCALED only (GM_EUNSUPPORTED for column shards); FAITHFUL: no-op. */
+ * after); FAITHFUL: no-op. SCALED column shards count their own columns' fresh entries and
+ * SUM-allreduce them (N x 4 B per tick, only while recording), so every rank returns the
+ * whole cluster's counts, equal to the single-context ones. */
 int gm_msgcount_record(gm_ctx *ctx, int32_t tmax);
 
 /* Dense readback of observer row r: hb/ts per subject column (absent -> -1),
@@ -201,7 +203,8 @@ int gm_last_kernel_ms(gm_ctx *ctx, float *ms);
  * runs the sharded tick: merge/sweep own columns -> ncclAllGather of per-row
  * (present, numfailed) -> rounds of {draw + resolve own-column draws ->
  * ncclAllReduce(MAX) of resolved draws -> acceptance} until every row has its
- * gossip targets. No gossip payload crosses GPUs. The phase functions expose
+ * gossip targets (stream-ordered bounded rounds; rows they cannot take finish in host-driven
+ * rounds before the tick is read or the next one starts). No gossip payload crosses GPUs. The phase functions expose
  * the same steps for G contexts on one device (gm_shard_loopback collectives). */
 int gm_comm_unique_id(uint8_t *out128);   /* ncclGetUniqueId, on one rank */
 int gm_comm_init(gm_ctx *ctx, const uint8_t *id128, int32_t nranks, int32_t rank);
@@ -210,7 +213,8 @@ int gm_shard_merge(gm_ctx *ctx);
 int gm_shard_draw(gm_ctx *ctx, int32_t round, int32_t D);
 int gm_shard_accept(gm_ctx *ctx, int32_t D, int32_t *npending);
 int gm_shard_end_tick(gm_ctx *ctx);
-/* what = 0: all-gather the per-row counts; what = 1: MAX-allreduce the first n*D draws */
+/* what = 0: all-gather the per-row counts; what = 1: MAX-allreduce the first n*D draws;
+ * what = 2 (msgcount recording, after what = 0): SUM-allreduce this tick's fresh counts */
 int gm_shard_loopback(gm_ctx **ctxs, int32_t G, int32_t what, int32_t D);
 /* Diagnostics: tick ONE column shard alone on a device (no RCCL): peers' per-row counts
  * mirror this shard's and draws landing in peer columns resolve to fresh column ix --

@@ -93,3 +93,45 @@ def test_msgcount_record_contract():
     sent, recv = sim.msgcount(12)
     assert sent.shape == (64, 12) and not sent[:, :9].any() and sent[:, 9:12].any()
     sim.close()
+
+
+@pytest.mark.parametrize("world,drop,rccl", [(2, 0, False), (3, 30, False), (1, 20, True)])
+def test_column_shard_msgcount_matches_fused_kernel(world, drop, rccl, monkeypatch):
+    """Column shards count their own columns' fresh entries (and kept entries on loss ticks);
+    the SUM-allreduce gives every rank the whole rows' counts -- equal, tick by tick, to the
+    single context's. rccl: one forced shard through ncclAllReduce, with the pending lists
+    shrunk so rows finish in the host-driven rounds (msgcount waits for them)."""
+    from membership.abi import comm_unique_id
+    from membership.sharded import loopback_tick
+    n, ticks, crash_tick = 611, 28, 9
+    kw = dict(rd_seed=7, drop_pct=drop, drop_from=4, drop_to=20, drop_seed=42, init_mode=1, init_t0=6, init_seed=5)
+    ref = Simulator(n, GM_MODE_SCALED, **kw)
+    if rccl:
+        monkeypatch.setenv("GM_FORCE_SHARD", "1")
+        monkeypatch.setenv("GM_SHARD_SYNC", "0")
+        monkeypatch.setenv("GM_PLIST_CAP", "4")
+    shards = [Simulator(n, GM_MODE_SCALED, shard_rank=g, shard_count=world, **kw) for g in range(world)]
+    for v in ("GM_FORCE_SHARD", "GM_SHARD_SYNC", "GM_PLIST_CAP"):
+        monkeypatch.delenv(v, raising=False)
+    if rccl:
+        shards[0].comm_init(comm_unique_id(), 1, 0)
+    tmax = ref.time + ticks
+    for s in [ref] + shards:
+        s.msgcount_record(tmax)
+    crash = crash_set(n, 40, 42)
+    for _ in range(ticks):
+        t = ref.time
+        ref.tick()
+        if rccl:
+            shards[0].tick()
+        else:
+            loopback_tick(shards)
+        if t == crash_tick:
+            for s in [ref] + shards:
+                s.set_failed(crash)
+    want = ref.msgcount(tmax)
+    assert want[0].sum() > 0 and want[1].sum() > 0
+    for s in shards:
+        got = s.msgcount(tmax)
+        assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1])
+        assert s.tick_stats()["err"] == 0
