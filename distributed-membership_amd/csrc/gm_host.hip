@@ -352,24 +352,40 @@ static int create_scaled(gm_ctx *c) {
   s.kcap = inbox_cap(S_KMAX);
   c->shard_sync = getenv("GM_SHARD_SYNC") ? (atoi(getenv("GM_SHARD_SYNC")) ? 1 : 0) : -1;
   TRY(dalloc(c, &s.msg, cells));        // nibbles: 2 parities x band/2 bytes per (band, row)
-  // Escape pools (gm_scaled.h), one per tick parity. Up to 2^31 cells they hold every cell (the
-  // dense equivalent: no run can overflow them); beyond, 1/16 of the cells and 1/16 of the
+  // Escape storage (gm_scaled.h), one set per tick parity: a 16-cell inline slot per (band, row)
+  // list (1/32 B per cell at B = 1024) and the pools. Up to 2^31 cells the pools hold every cell
+  // (the dense equivalent: no run can overflow them); beyond, 1/64 of the cells and 1/16 of the
   // payload lanes -- a warm cluster escapes only a crashed node's entries in the ticks before
-  // their removal (~1 % of the cells at a 1 % crash) -- and an overflow fails loudly
+  // their removal (~10 per list at a 1 % crash: inline) -- and an overflow fails loudly
   // (GM_ERR_ESC -> GM_ERANGE). GM_ESC_CAP (cells; diagnostics, tests) lowers the table pool.
+  // Striped: up to 1024 stripes, >= 64 (band, row) lists each; dense = every list's whole slice
+  // fits its stripe's region (ceil(lists / S) lists of `band` cells).
   const bool dense = cells <= (1ull << 31);
-  s.tesc_cap = (uint32_t)std::min<size_t>(dense ? cells : std::max<size_t>(cells / 16, 1ull << 26), 0xFFFFFFF0ull);
-  s.pesc_cap = (uint32_t)std::min<size_t>(dense ? cells / 16 : std::max<size_t>(cells / 256, 1ull << 22), 0xFFFFFFF0ull);
-  if (getenv("GM_ESC_CAP")) s.tesc_cap = (uint32_t)std::max(1L, std::min<long>(atol(getenv("GM_ESC_CAP")), s.tesc_cap));
+  const size_t lists = (size_t)n * s.nb;
+  int S = 1024;
+  while (S > 1 && lists / S < 64) S >>= 1;
+  while (dense && ((lists + S - 1) / S) * s.band > S_EW_REGION_MAX) S <<= 1;  // the list word's offset field
+  s.esc_stripes = S;
+  const size_t per = (lists + S - 1) / S;  // lists per stripe (at most)
+  size_t treg = dense ? per * s.band : std::max<size_t>(cells / 64 / S, 4 * (size_t)s.band);
+  size_t preg = dense ? per * (s.band / 16) : std::max<size_t>(cells / 256 / S, 4 * (size_t)(s.band / 16));
+  treg = std::min<size_t>(treg, S_EW_REGION_MAX);
+  preg = std::min<size_t>(preg, 0xFFFFFFF0ull / S);
+  if (getenv("GM_ESC_CAP")) treg = std::max<size_t>(1, std::min<size_t>(atol(getenv("GM_ESC_CAP")) / S, treg));
+  s.tesc_region = (uint32_t)treg;
+  s.pesc_region = (uint32_t)preg;
+  s.tesc_cap = (uint32_t)(treg * S);
+  s.pesc_cap = (uint32_t)(preg * S);
   for (int p = 0; p < 2; p++) {
+    TRY(dalloc(c, &s.tesc_in[p], lists * S_ESC_IN));
     TRY(dalloc(c, &s.tesc[p], s.tesc_cap));
     TRY(dalloc(c, &s.pesc[p], (size_t)s.pesc_cap * 16));
     TRY(dalloc(c, &s.pesc_rec[p], (size_t)n * s.nb));
   }
-  TRY(dalloc(c, &s.tesc_cnt, 2));
-  TRY(dalloc(c, &s.pesc_cnt, 2));
-  HIPCHECK(hipMemset(s.tesc_cnt, 0, 2 * sizeof(unsigned long long)));
-  HIPCHECK(hipMemset(s.pesc_cnt, 0, 2 * sizeof(unsigned long long)));
+  TRY(dalloc(c, &s.tesc_cnt, 2 * (size_t)S));
+  TRY(dalloc(c, &s.pesc_cnt, 2 * (size_t)S));
+  HIPCHECK(hipMemset(s.tesc_cnt, 0, 2 * S * sizeof(unsigned long long)));
+  HIPCHECK(hipMemset(s.pesc_cnt, 0, 2 * S * sizeof(unsigned long long)));
   for (int p = 0; p < 2; p++) {
     TRY(dalloc(c, &s.inbox_cnt[p], n));
     TRY(dalloc(c, &s.inbox[p], (size_t)n * S_KMAX));
@@ -380,7 +396,7 @@ static int create_scaled(gm_ctx *c) {
   TRY(dalloc(c, &s.brec, (size_t)n * s.nb));
   TRY(dalloc(c, &s.ev_band, (size_t)n * s.nb * s.evs));
   TRY(dalloc(c, &s.ev_spill, s.ev_spill_cap));
-  TRY(dalloc(c, &s.ev_spill_cnt, 2));
+  TRY(dalloc(c, &s.ev_spill_cnt, 1 + S_EV_STRIPES));
   TRY(dalloc(c, &s.evcum, (size_t)n * s.nb));
   TRY(dalloc(c, &s.mtraw, (size_t)n * S_MT_RAW));
   TRY(dalloc(c, &s.rowstat, (size_t)n * 4));
@@ -419,7 +435,7 @@ static int create_scaled(gm_ctx *c) {
     snprintf(g_errbuf, sizeof g_errbuf, "initial state overflows the escape pool (%u cells)", s.tesc_cap);
     return GM_ERANGE;
   }
-  HIPCHECK(hipMemset(s.ev_spill_cnt, 0, 2 * sizeof(uint32_t)));
+  HIPCHECK(hipMemset(s.ev_spill_cnt, 0, (1 + S_EV_STRIPES) * sizeof(uint32_t)));
   HIPCHECK(hipMemset(s.evcum, 0, sizeof(uint64_t) * (size_t)n * s.nb));
   HIPCHECK(hipMemset(s.rowstat, 0, sizeof(int32_t) * n * 4));
   if (s.sharded) {
@@ -915,16 +931,40 @@ static int read_bcnt(gm_ctx *c, std::vector<uint32_t> &bc) {
 // GM_ERANGE instead of unbounded host memory)
 #define GM_PENDING_CAP (1ull << 27)
 
+// The escape entries of one (band, row) list (k of them: inline slot, then pool) -> values by
+// column of the row; GM_ESTATE if the record cannot hold them or an entry's column is no escape
+static int place_entries(const SState &s, int b, const uint8_t *piece, const uint32_t *inl, const uint32_t *pool,
+                         size_t k, uint16_t *esc_row) {
+  for (size_t i = 0; i < k; i++) {
+    const uint32_t e = i < S_ESC_IN ? inl[i] : pool[i - S_ESC_IN];
+    const uint32_t col = e & 0xFFFFu;
+    if (col >= (uint32_t)s.band || !s_is_esc(piece[col])) return GM_ESTATE;
+    esc_row[(size_t)b * s.band + col] = (uint16_t)(e >> 16);
+  }
+  return GM_OK;
+}
+
+// SCALED: the last tick's join + remove records (the band kernel's striped partial sums) and
+// how many of them spilled to the ring
+static int tick_event_total(gm_ctx *c, uint64_t *total, uint32_t *spilled) {
+  uint32_t cnt[1 + S_EV_STRIPES];
+  HIPCHECK(hipMemcpyAsync(cnt, c->s.ev_spill_cnt, sizeof cnt, hipMemcpyDeviceToHost, c->stream));
+  HIPCHECK(hipStreamSynchronize(c->stream));
+  *spilled = cnt[0];
+  *total = 0;
+  for (int k = 1; k <= S_EV_STRIPES; k++) *total += cnt[k];
+  return GM_OK;
+}
+
 static int drain_scaled(gm_ctx *c, std::vector<gm_event> &out) {
   const SState &s = c->s;
   const size_t nrb = (size_t)c->n * s.nb;
   std::vector<uint32_t> bc;
-  uint32_t cnt[2] = {0, 0};  // spilled records, the tick's total
-  HIPCHECK(hipMemcpyAsync(cnt, s.ev_spill_cnt, sizeof cnt, hipMemcpyDeviceToHost, c->stream));
-  HIPCHECK(hipStreamSynchronize(c->stream));
-  if (cnt[1] == 0) return GM_OK;  // the common tick: nothing to stage, one 8-byte copy
-  if (out.size() + cnt[1] > GM_PENDING_CAP) return GM_ERANGE;
-  uint32_t nsp = cnt[0];
+  uint64_t total = 0;
+  uint32_t nsp = 0;
+  TRY(tick_event_total(c, &total, &nsp));
+  if (total == 0) return GM_OK;  // the common tick: nothing to stage, one 1 KB copy
+  if (out.size() + total > GM_PENDING_CAP) return GM_ERANGE;
   TRY(read_bcnt(c, bc));
   const int t = c->t - 1;
   auto push = [&](int r, uint32_t rec) {
@@ -1025,10 +1065,8 @@ extern "C" int gm_event_counts(gm_ctx *c, uint64_t counts[6]) {
   TRY(f_settle(c));
   for (int k = 0; k < 6; k++) counts[k] = 0;
   if (c->cfg.mode == GM_MODE_SCALED) {
-    uint32_t cnt[2] = {0, 0};
-    HIPCHECK(hipMemcpyAsync(cnt, c->s.ev_spill_cnt, sizeof cnt, hipMemcpyDeviceToHost, c->stream));
-    HIPCHECK(hipStreamSynchronize(c->stream));
-    counts[0] = cnt[1];  // join+remove records of the last tick (per-kind split needs a drain)
+    uint32_t nsp = 0;
+    TRY(tick_event_total(c, &counts[0], &nsp));  // join+remove records of the last tick (per-kind split needs a drain)
   } else if (c->cfg.mode == GM_MODE_PARTIAL) {
     std::vector<int32_t> cnt(c->p.nloc);
     HIPCHECK(hipMemcpyAsync(cnt.data(), c->p.ev_cnt, sizeof(int32_t) * c->p.nloc, hipMemcpyDeviceToHost, c->stream));
@@ -1097,6 +1135,7 @@ extern "C" int gm_msgcount_record(gm_ctx *c, int32_t tmax) {
 
 extern "C" int gm_msgcount(gm_ctx *c, int32_t t, int32_t *sent, int32_t *recv) {
   if (!c || !sent || !recv || t < 0) return GM_EINVAL;
+  TRY(f_settle(c));  // a column shard's last tick may still owe its host-driven draw rounds
   if (c->cfg.mode != GM_MODE_FAITHFUL) {  // [nodes][t] of this context's nodes, from the recorded history
     const bool sc = c->cfg.mode == GM_MODE_SCALED;
     const uint32_t *ms = sc ? c->s.mc_sent : c->p.mc_sent, *mr = sc ? c->s.mc_recv : c->p.mc_recv;
@@ -1132,16 +1171,15 @@ extern "C" int gm_msgcount(gm_ctx *c, int32_t t, int32_t *sent, int32_t *recv) {
 }
 
 // One row of stored bytes (column order) -> absolute (hb, ts), -1 = absent; escaped cells take
-// the next value of `esc` (the row's pool lists, concatenated in column order). Cells are
-// relative to the row's last written tick wt.
+// their value from `esc` (per column, from the row's escape entries). Cells are relative to the
+// row's last written tick wt.
 static void decode_scaled_row(const gm_ctx *c, const uint8_t *row, const uint16_t *esc, int wt,
                               std::vector<int32_t> &hb, std::vector<int32_t> &ts) {
   const SState &s = c->s;
   hb.resize(s.w);
   ts.resize(s.w);
-  size_t k = 0;
   for (int j = 0; j < s.w; j++) {
-    const uint32_t e = s_is_esc(row[j]) ? (uint32_t)esc[k++] : s_widen(row[j]);
+    const uint32_t e = s_is_esc(row[j]) ? (uint32_t)esc[j] : s_widen(row[j]);
     hb[j] = e == 0 ? -1 : 2 * wt - 255 + (int32_t)S_H(e) - s_hbase(s.ramp, s.c0 + j);
     ts[j] = e == 0 ? -1 : wt - (int32_t)S_AGE(e);
   }
@@ -1191,16 +1229,24 @@ static int read_table_row(gm_ctx *c, int r, std::vector<int32_t> &hb, std::vecto
   HIPCHECK(hipMemcpy2D(eb.data(), sizeof(uint32_t), (const uint8_t *)(s.brec + r) + 12, sizeof(uint4) * s.n,
                        sizeof(uint32_t), s.nb, hipMemcpyDeviceToHost));
   HIPCHECK(hipMemcpy(&wt, s.wtick + r, sizeof wt, hipMemcpyDeviceToHost));
-  std::vector<uint16_t> esc(s.wp);  // the escaped cells in column order (pool lists of the row's bands)
-  const uint16_t *pool = s.tesc[(c->t - 1) & 1];
-  size_t ne = 0;
+  std::vector<uint16_t> esc(s.wp);  // escaped cells by column (the entries of the row's band lists)
+  const int par = (c->t - 1) & 1;
+  std::vector<uint32_t> ent;
   for (int b = 0; b < s.nb; b++) {
+    const uint8_t *piece = row.data() + (size_t)b * s.band;
     size_t k = 0;
-    for (int j = 0; j < s.band; j++) k += s_is_esc(row[(size_t)b * s.band + j]);
+    for (int j = 0; j < s.band; j++) k += s_is_esc(piece[j]);
     if (!k) continue;
-    if (eb[b] == S_ESC_NONE || (size_t)eb[b] + k > s.tesc_cap) return GM_ESTATE;
-    HIPCHECK(hipMemcpy(esc.data() + ne, pool + eb[b], sizeof(uint16_t) * k, hipMemcpyDeviceToHost));
-    ne += k;
+    const size_t in = std::min<size_t>(k, S_ESC_IN);
+    if (S_EW_TOT(eb[b]) != k || S_EW_OFF(eb[b]) + (k - in) > s.tesc_region) return GM_ESTATE;
+    ent.resize(k);
+    HIPCHECK(hipMemcpy(ent.data(), s.tesc_in[par] + ((size_t)b * s.n + r) * S_ESC_IN, sizeof(uint32_t) * in,
+                       hipMemcpyDeviceToHost));
+    const size_t stripe = ((size_t)b * s.n + r) & (size_t)(s.esc_stripes - 1);
+    if (k > in)
+      HIPCHECK(hipMemcpy(ent.data() + in, s.tesc[par] + stripe * s.tesc_region + S_EW_OFF(eb[b]),
+                         sizeof(uint32_t) * (k - in), hipMemcpyDeviceToHost));
+    TRY(place_entries(s, b, piece, ent.data(), ent.data() + S_ESC_IN, k, esc.data()));
   }
   decode_scaled_row(c, row.data(), esc.data(), wt, hb, ts);
   return GM_OK;
@@ -1304,7 +1350,8 @@ extern "C" int gm_dump_tables(gm_ctx *c, char *buf, size_t cap, size_t *len) {
   // SCALED: one copy of the table, the records and the last tick's pool, decoded row by row
   std::vector<uint8_t> tab;
   std::vector<uint4> rec;
-  std::vector<uint16_t> pool, esc;
+  std::vector<uint32_t> pool, inl;
+  std::vector<uint16_t> esc;
   std::vector<int32_t> wts;
   std::vector<uint8_t> row;
   if (c->cfg.mode == GM_MODE_SCALED) {
@@ -1312,14 +1359,22 @@ extern "C" int gm_dump_tables(gm_ctx *c, char *buf, size_t cap, size_t *len) {
     tab.resize((size_t)s.n * s.wp);
     rec.resize((size_t)s.n * s.nb);
     wts.resize(s.n);
-    unsigned long long cnt = 0;
+    std::vector<unsigned long long> cnt(s.esc_stripes);
     HIPCHECK(hipMemcpy(tab.data(), s.table, tab.size(), hipMemcpyDeviceToHost));
     HIPCHECK(hipMemcpy(rec.data(), s.brec, sizeof(uint4) * rec.size(), hipMemcpyDeviceToHost));
     HIPCHECK(hipMemcpy(wts.data(), s.wtick, sizeof(int32_t) * s.n, hipMemcpyDeviceToHost));
-    HIPCHECK(hipMemcpy(&cnt, s.tesc_cnt + ((c->t - 1) & 1), sizeof cnt, hipMemcpyDeviceToHost));
-    pool.resize(std::min<unsigned long long>(cnt, s.tesc_cap));
-    if (!pool.empty())
-      HIPCHECK(hipMemcpy(pool.data(), s.tesc[(c->t - 1) & 1], sizeof(uint16_t) * pool.size(), hipMemcpyDeviceToHost));
+    const int par = (c->t - 1) & 1;
+    HIPCHECK(hipMemcpy(cnt.data(), s.tesc_cnt + (size_t)par * s.esc_stripes, sizeof(unsigned long long) * cnt.size(),
+                       hipMemcpyDeviceToHost));
+    inl.resize((size_t)s.n * s.nb * S_ESC_IN);
+    HIPCHECK(hipMemcpy(inl.data(), s.tesc_in[par], sizeof(uint32_t) * inl.size(), hipMemcpyDeviceToHost));
+    pool.resize(s.tesc_cap);  // each stripe's used part, at its absolute offsets
+    for (int k = 0; k < s.esc_stripes; k++) {
+      const size_t used = std::min<unsigned long long>(cnt[k], s.tesc_region);
+      if (used)
+        HIPCHECK(hipMemcpy(pool.data() + (size_t)k * s.tesc_region, s.tesc[par] + (size_t)k * s.tesc_region,
+                           sizeof(uint32_t) * used, hipMemcpyDeviceToHost));
+    }
     row.resize(s.wp);
     esc.resize(s.wp);
   }
@@ -1327,17 +1382,18 @@ extern "C" int gm_dump_tables(gm_ctx *c, char *buf, size_t cap, size_t *len) {
     int w;
     if (c->cfg.mode == GM_MODE_SCALED) {
       const SState &s = c->s;
-      size_t ne = 0;
       for (int b = 0; b < s.nb; b++) {
         const uint8_t *pc = tab.data() + ((size_t)b * s.n + i) * s.band;
         memcpy(row.data() + (size_t)b * s.band, pc, s.band);
         size_t k = 0;
         for (int j = 0; j < s.band; j++) k += s_is_esc(pc[j]);
         if (!k) continue;
-        const uint32_t base = rec[(size_t)b * s.n + i].w;
-        if (base == S_ESC_NONE || (size_t)base + k > pool.size()) return GM_ESTATE;
-        memcpy(esc.data() + ne, pool.data() + base, sizeof(uint16_t) * k);
-        ne += k;
+        const uint32_t w = rec[(size_t)b * s.n + i].w;
+        const size_t in = std::min<size_t>(k, S_ESC_IN);
+        if (S_EW_TOT(w) != k || S_EW_OFF(w) + (k - in) > s.tesc_region) return GM_ESTATE;
+        const size_t stripe = ((size_t)b * s.n + i) & (size_t)(s.esc_stripes - 1);
+        TRY(place_entries(s, b, pc, inl.data() + ((size_t)b * s.n + i) * S_ESC_IN,
+                          pool.data() + stripe * s.tesc_region + S_EW_OFF(w), k, esc.data()));
       }
       decode_scaled_row(c, row.data(), esc.data(), wts[i], rh, rt);
       w = s.w;

@@ -29,19 +29,26 @@
 //   0             absent
 //   h4 << 4 | a   h = 224 + 2 h4 (h4 in [1, 15]: even h in [226, 254], heartbeat lag <= 14
 //                 ticks), age a <= 15 -- every live entry of a warm, steady cluster
-//   1..15         escaped (h4 = 0): the exact 16-bit cell is in the tick's escape pool.
-//                 S_B_ESC (1) = escaped and fresh (age < TFAIL), S_B_ESCS (2) = escaped and
-//                 stale, so the gossip draw's freshness test never needs the pool.
+//   1 (S_B_ESC)   escaped: the exact 16-bit cell is an entry of the (band, row)'s escape list
+//                 (codes 2..15, h4 = 0, are unused)
 // Cells outside the byte's range (odd h of cold-start / JOINREQ entries, lag > 14 or age > 15,
 // e.g. a crashed node's entries in the ticks before TREMOVE) escape. The pool is COMPACT: per
 // (band, row) the escaped cells of the row's band slice, in column order, as consecutive u16
-// cells of the pool of the tick that wrote them (tick parity: written at t, read at t+1); the
-// (band, row) record's .w holds the list's first index (S_ESC_NONE: no escapes). Capacity is
+// ENTRIES of the tick that wrote them (tick parity: written at t, read at t+1), one u32 per
+// escaped cell: its column in the band (low 16 bits) | its 16-bit cell << 16. The first S_ESC_IN
+// entries sit in the list's fixed inline slot (no allocation: a crash window escapes ~1 % of a
+// row's cells, ~10 per 1024-column band), the rest in the pool region of the list's stripe.
+// The (band, row) record's .w is the list's word: entry count | offset in the stripe's region
+// << 11 (0: no escapes), so a reader knows the list's extent with the row's metadata and
+// prefetches the inline entries with the payload gathers; it scatters the entries into its
+// row's cells through LDS (entries carry their columns: no per-cell search). Capacity is
 // bounded (gm_host.hip: dense-equivalent for small clusters, a fraction of the cells beyond);
 // an overflow sets GM_ERR_ESC (-> GM_ERANGE) -- never a silent divergence.
 #define S_B_ESC 1u
-#define S_B_ESCS 2u
-#define S_ESC_NONE 0xFFFFFFFFu
+#define S_ESC_IN 16                 // entries of a (band, row) list held inline (64 B per list)
+#define S_EW_TOT(w) ((w) & 0x7FFu)  // escape-list word: entry count (<= band width)
+#define S_EW_OFF(w) ((w) >> 11)     // offset of entries S_ESC_IN.. in the stripe's pool region
+#define S_EW_REGION_MAX (1u << 21)  // pool entries per stripe the word can address
 __host__ __device__ inline bool s_is_esc(uint32_t b) { return b != 0 && b < 16; }
 __host__ __device__ inline uint32_t s_widen(uint32_t b) {  // byte -> 16-bit cell (escape codes: look in the pool)
   return b == 0 ? 0u : (7168u + ((b & 0xF0u) << 2) + (b & 0x0Fu));
@@ -50,7 +57,7 @@ __host__ __device__ inline uint32_t s_narrow(uint32_t c) {  // 16-bit cell -> by
   if (c == 0) return 0u;
   const uint32_t h = c >> 5, a = c & 31u;
   if (h >= 226 && !(h & 1) && a <= 15) return (((h - 224) >> 1) << 4) | a;
-  return a < GM_TFAIL ? S_B_ESC : S_B_ESCS;
+  return S_B_ESC;
 }
 __host__ __device__ inline int s_start(int j) { return j >> 2; }  // (int)(0.25 * j) for j >= 0
 __host__ __device__ inline int s_hbase(int ramp, int j) { return (ramp && j > 0) ? 2 * (s_start(j) + 1) : 0; }
@@ -71,6 +78,7 @@ __host__ __device__ inline bool s_ingroup(int ramp, int intro_until, int r, int 
 #define S_NIB_ESC 15u
 #define S_NIB_H(n) (S_NIB_BASE + 2u * (n))
 
+#define S_EV_STRIPES 256
 #define S_EV_ADD 1u
 #define S_EV_REMOVE 2u
 
@@ -93,10 +101,15 @@ struct SState {
   // Band-tiled layout: cell (r, c) of band b = c / band lives at ((b * n + r) * band + c % band),
   // so one band of all rows is one contiguous slab (the unit gm_s_band sweeps).
   uint8_t *table;          // [nb][n][band] stored cell bytes (s_narrow of S_CELL)
-  uint16_t *tesc[2];       // escape pools by tick parity: S_CELL of escaped cells, per (band, row) a
-                           // contiguous list in column order starting at brec.w (S_ESC_NONE: none)
-  unsigned long long *tesc_cnt;  // [2] cells allocated in each pool this tick (zeroed a tick ahead)
-  uint32_t tesc_cap;       // cells per pool
+  uint32_t *tesc_in[2];    // [nb * n][S_ESC_IN] by tick parity: the first entries of each (band, row) list
+  uint32_t *tesc[2];       // escape pools by tick parity: a list's entries beyond S_ESC_IN, from brec.w
+  // Allocation is STRIPED: (band, row) list u allocates in stripe (band * n + row) & (stripes - 1),
+  // a region of `region` entries with its own counter -- one global counter would serialise
+  // every (band, row) of a crash-window tick on one address (4 M atomics at S-A: 25 ms)
+  int esc_stripes;         // power of two
+  unsigned long long *tesc_cnt;  // [2][esc_stripes] cells allocated per stripe this tick (zeroed a tick ahead)
+  uint32_t tesc_region;    // entries per stripe
+  uint32_t tesc_cap;       // entries per pool = esc_stripes * tesc_region
   uint8_t *msg;            // [nb][n][2][band/2] gossip payload nibbles, both tick parities of a (band, row) adjacent
   // escaped payload bytes (nibble 15): per (band, sender) of tick parity p the lanes holding escapes
   // write their 16 payload bytes h' into consecutive 16-byte slots of pesc[p] from the record's base,
@@ -104,7 +117,8 @@ struct SState {
   // only by senders with escapes and read only where a receiver meets nibble 15)
   uint8_t *pesc[2];
   uint4 *pesc_rec[2];
-  unsigned long long *pesc_cnt;  // [2] slots allocated this tick
+  unsigned long long *pesc_cnt;  // [2][esc_stripes] slots allocated per stripe this tick
+  uint32_t pesc_region;    // 16-byte slots per stripe
   uint32_t pesc_cap;       // 16-byte slots per pool
   int32_t *wtick;          // [n] tick each row's cells are relative to (last written)
   int32_t *inbox_cnt[2];   // [n] lists queued for each receiver, by delivery-tick parity
@@ -112,11 +126,12 @@ struct SState {
   int32_t *hbctr;          // [n] MP1Node heartbeat counter (Member::heartbeat)
   int32_t *failed;         // [n] Member::bFailed
   uint4 *brec;             // [nb][n] per-(band, row) record after the sweep: .x/.y = present cells per 64-column
-                           // chunk (band/64 bytes, rank-select), .z = bcnt word (S_BC_*), .w = first index of the
-                           // slice's escaped cells in tesc[t & 1] (S_ESC_NONE: none); rows adjacent = whole-line writes
+                           // chunk (band/64 bytes, rank-select), .z = bcnt word (S_BC_*), .w = the slice's escape-list
+                           // word (S_EW_*, 0: none); rows adjacent = whole-line writes
   uint32_t *ev_band;       // [n][nb][evs] kind<<30 | subject id
   uint64_t *ev_spill;      // overflow: (logger<<32) | kind<<30 | subject id
-  uint32_t *ev_spill_cnt;  // [2]: spill records, then the tick's total records (all rows and bands)
+  uint32_t *ev_spill_cnt;  // [1 + S_EV_STRIPES]: spill records, then the tick's total records in
+                           // S_EV_STRIPES striped partial sums (one hot address would serialise)
   uint64_t *evcum;         // [n][nb] cumulative events since create: joins | removals << 32 (single writer per cell)
   uint32_t *mtraw;        // [n][S_MT_RAW] first mt19937 outputs of each row's S2 stream this tick
   int32_t *rowstat;        // [n][4]: lists delivered, present, numfailed, targets chosen

@@ -63,7 +63,7 @@ template <int B>
 struct RowMeta {
   int k;           // lists delivered to the row (-1: no such row, or a crashed node)
   int snd[S_SB];   // first S_SB senders
-  uint32_t ebase;  // the (band, row) record's escape list of the last tick (S_ESC_NONE: no escaped cells)
+  uint32_t ebase;  // the (band, row) record's escape-list word of the last tick (S_EW_*, 0: no escaped cells)
 };
 
 // Every load of the row's metadata issues at once, none behind a branch on another (one
@@ -91,7 +91,7 @@ __device__ __forceinline__ RowMeta<B> row_meta(const SState &s, int r, int par, 
   m.snd[4] = b.x; m.snd[5] = b.y; m.snd[6] = b.z; m.snd[7] = b.w;
   // not in the group (join ramp) or crashed: untouched
   m.k = (r >= s.n || failed || !s_ingroup(s.ramp, s.intro_until, r, t)) ? -1 : k;
-  if (r >= s.n) m.ebase = S_ESC_NONE;
+  if (r >= s.n) m.ebase = 0;
   return m;
 }
 
@@ -202,37 +202,90 @@ __device__ __forceinline__ bool row_any(bool p, int sub) {
   return LPR == 64 ? b != 0 : ((b >> (sub * LPR)) & ((1ull << LPR) - 1)) != 0;
 }
 
-// one reservation of `total` pool entries per row (its first lane), broadcast to the row;
-// S_ESC_NONE if the row has none or the pool overflowed (GM_ERR_ESC: the run is void)
+// stripe of the (band, row) list at slab + r (gm_scaled.h: striped pool allocation)
+__device__ __forceinline__ int esc_stripe(const SState &s, size_t slab, int r) {
+  return (int)((slab + (size_t)r) & (size_t)(s.esc_stripes - 1));
+}
+// The escape-list word of a (band, row) list of `total` escaped cells written at tick parity
+// par: up to S_ESC_IN entries need no allocation; beyond, one reservation (the row's first lane)
+// in its stripe's pool region, broadcast to the row -- 0 with GM_ERR_ESC if the region overflowed
+// (the run is void). total is row-uniform.
 template <int LPR>
-__device__ __forceinline__ uint32_t row_alloc(unsigned long long *cnt, uint32_t cap, int total, int li, int lane,
-                                              uint32_t *err) {
-  uint32_t base = S_ESC_NONE;
-  if (li == 0 && total > 0) {
-    const unsigned long long b = atomicAdd(cnt, (unsigned long long)total);
-    if (b + (unsigned long long)total <= (unsigned long long)cap) base = (uint32_t)b;
-    else atomicOr(err, GM_ERR_ESC);
+__device__ __forceinline__ uint32_t row_alloc(const SState &s, int par, size_t slab, int r, int total, int li,
+                                              int lane) {
+  if (total <= S_ESC_IN) return (uint32_t)total;
+  uint32_t w = 0;
+  if (li == 0) {
+    const int stripe = esc_stripe(s, slab, r);
+    const unsigned long long need = (unsigned long long)(total - S_ESC_IN);
+    const unsigned long long b = atomicAdd(s.tesc_cnt + par * s.esc_stripes + stripe, need);
+    if (b + need <= (unsigned long long)s.tesc_region) w = (uint32_t)total | ((uint32_t)b << 11);
+    else atomicOr(s.err, GM_ERR_ESC);
   }
-  return LPR == 64 ? __builtin_amdgcn_readfirstlane(base) : (uint32_t)__shfl((int)base, lane - li, 64);
+  return LPR == 64 ? __builtin_amdgcn_readfirstlane(w) : (uint32_t)__shfl((int)w, lane - li, 64);
+}
+// a list's storage: entry i < S_ESC_IN in the inline slot, the rest in its stripe's pool region
+struct EscList {
+  uint32_t *inl, *pool;
+  __device__ __forceinline__ uint32_t *at(int i) const { return i < S_ESC_IN ? inl + i : pool + (i - S_ESC_IN); }
+};
+__device__ __forceinline__ EscList esc_list(const SState &s, int par, size_t slab, int r, uint32_t word) {
+  EscList l;
+  l.inl = s.tesc_in[par] + (slab + (size_t)r) * S_ESC_IN;
+  l.pool = s.tesc[par] + (size_t)esc_stripe(s, slab, r) * s.tesc_region + S_EW_OFF(word);
+  return l;
 }
 
-// the lane's escaped cells (mask em) into their u16 halves of tw, from its part of the row's list
-__device__ __forceinline__ void esc_load(const uint16_t *src, uint32_t em, u16x2 tw[8]) {
-  int idx = 0;
-#pragma unroll
-  for (int q = 0; q < 16; q++) {
-    if ((em >> q) & 1u) {
-      const uint32_t v = src[idx++];
-      const int sh = 16 * (q & 1);
-      tw[q >> 1] = pk((unpk(tw[q >> 1]) & ~(0xFFFFu << sh)) | (v << sh));
-    }
-  }
+// LDS of the band kernel: 32 B per lane (its 16 working cells), i.e. one wave's rows' cells in
+// column order -- the meeting point of escape entries and the lanes holding their columns
+#define S_LDS_WAVE_WORDS (64 * 8)
+__device__ __forceinline__ void lds_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
-__device__ __forceinline__ void esc_store(uint16_t *dst, uint32_t em, const uint32_t cw[8]) {
-  int idx = 0;
-#pragma unroll
-  for (int q = 0; q < 16; q++)
-    if ((em >> q) & 1u) dst[idx++] = (uint16_t)(cw[q >> 1] >> (16 * (q & 1)));
+
+// Reader: the row's list (tot entries, row-uniform) into the lanes' cells: every lane of the
+// row parks its 16 cells in LDS, the row's lanes scatter the entries by column (lane li < 16
+// has entry li prefetched in `ent`; entries beyond S_ESC_IN load here), then every lane takes
+// its cells back. lds = this wave's area.
+template <int LPR>
+__device__ __forceinline__ void esc_apply(uint32_t *lds, int lane, int li, const EscList &l, int tot, uint32_t ent,
+                                          u16x2 tw[8]) {
+  u32x4 *mine = (u32x4 *)(lds + lane * 8);
+  mine[0] = (u32x4){unpk(tw[0]), unpk(tw[1]), unpk(tw[2]), unpk(tw[3])};
+  mine[1] = (u32x4){unpk(tw[4]), unpk(tw[5]), unpk(tw[6]), unpk(tw[7])};
+  lds_wave_sync();
+  uint16_t *row = (uint16_t *)(lds + (lane - li) * 8);  // the row's B cells in column order
+  constexpr int P = LPR < S_ESC_IN ? LPR : S_ESC_IN;  // entries prefetched (one per lane)
+  if (li < min(tot, P)) row[ent & 0xFFFFu] = (uint16_t)(ent >> 16);
+  for (int i = P + li; i < tot; i += LPR) {  // rare: lists longer than the prefetch
+    const uint32_t e = *l.at(i);
+    row[e & 0xFFFFu] = (uint16_t)(e >> 16);
+  }
+  lds_wave_sync();
+  const u32x4 a = mine[0], b = mine[1];
+  tw[0] = pk(a.x); tw[1] = pk(a.y); tw[2] = pk(a.z); tw[3] = pk(a.w);
+  tw[4] = pk(b.x); tw[5] = pk(b.y); tw[6] = pk(b.z); tw[7] = pk(b.w);
+}
+
+// Writer: the lane's 16 swept cells wait in its LDS slot (esc_park, right after the sweep, so
+// they need no registers through the stores); its escaped cells (mask em) become entries eoff,
+// eoff + 1, ... of the list, a set bit's cell one dynamic LDS read (no register indexing).
+// colb = the lane's first column in the band.
+__device__ __forceinline__ void esc_park(uint32_t *lds, int lane, const uint32_t cw[8]) {
+  u32x4 *mine = (u32x4 *)(lds + lane * 8);
+  mine[0] = (u32x4){cw[0], cw[1], cw[2], cw[3]};
+  mine[1] = (u32x4){cw[4], cw[5], cw[6], cw[7]};
+}
+__device__ __forceinline__ void esc_emit(uint32_t *lds, int lane, const EscList &l, int eoff, uint32_t em, int colb) {
+  if (!em) return;
+  const uint16_t *cells = (const uint16_t *)(lds + lane * 8);
+  int j = eoff;
+  for (uint32_t m = em; m; m &= m - 1) {
+    const int q = __builtin_ctz(m);
+    *l.at(j++) = (uint32_t)(colb + q) | ((uint32_t)cells[q] << 16);
+  }
 }
 
 // Payload nibbles (gm_scaled.h S_NIB_*): dword w of a lane's 8-byte slice holds cells
@@ -257,13 +310,14 @@ __device__ __forceinline__ uint32_t nib_of(uint32_t x0, uint32_t x1, int q) {
   const int c = q & 7;
   return (x >> (16 * (c & 1) + 4 * (3 - (c >> 1)))) & 15u;
 }
+#define S_PESC_NONE 0xFFFFFFFFu  // payload escape record: no slots (overflow)
 // escaped payload byte h' of lane li's cell q in sender sn's slice of tick parity pp: the
 // sender's escaping lanes hold consecutive 16-byte slots from its record's base, in lane order
 __device__ __forceinline__ uint32_t pesc_value(const SState &s, int pp, int band, int sn, int li, int q) {
   const uint4 rc = s.pesc_rec[pp][(size_t)band * s.n + sn];
   const uint64_t m = (uint64_t)rc.y | ((uint64_t)rc.z << 32);
   const uint32_t slot = rc.x + (uint32_t)__builtin_popcountll(m & ((1ull << li) - 1));
-  return rc.x == S_ESC_NONE || slot >= s.pesc_cap ? 0u : (uint32_t)s.pesc[pp][(size_t)slot * 16 + q];
+  return rc.x == S_PESC_NONE || slot >= s.pesc_cap ? 0u : (uint32_t)s.pesc[pp][(size_t)slot * 16 + q];
 }
 // payload value of a delivered cell: h' from its nibble, or from the sender's escape slots
 __device__ __forceinline__ uint32_t nib_value(uint32_t nb, const SState &s, int pp, int band, int sn, int li, int q) {
@@ -278,7 +332,7 @@ struct UnitIn {
   int band, r, k;  // k: lists delivered to this lane's row, -1 = not merged (crashed / absent / not in the group)
   int snd[S_SB];
   u32x4 ta;        // the row's 16 cell bytes of this lane (as loaded)
-  uint32_t ebase;  // the row slice's escape list in the pool of tick t-1 (S_ESC_NONE: none)
+  uint32_t ebase;  // the row slice's escape list in the pool of tick t-1 (S_PESC_NONE: none)
 };
 
 // UNI: the row is wave-uniform and known to be (one row per wave, a grid-derived unit)
@@ -301,11 +355,15 @@ __device__ __forceinline__ void unit_load(const SState &s, int t, int band, int 
   in.ebase = meta.ebase;
 }
 
-// every payload slice at once; slots j >= k read out of range (zeros = "not sent")
+// every payload slice at once; slots j >= k read out of range (zeros = "not sent"); with them,
+// lane li < 16 of a row whose slice held escaped cells fetches entry li of its list (ent)
 template <int B, bool DROP>
-__device__ __forceinline__ void unit_gather(const SState &s, int t, const UnitIn<B> &in, u32x2 m[S_SB]) {
+__device__ __forceinline__ void unit_gather(const SState &s, int t, const UnitIn<B> &in, u32x2 m[S_SB], uint32_t &ent) {
   constexpr int LPR = B / S_COLS_PER_LANE;
   const int li = (threadIdx.x & 63) % LPR;
+  ent = 0;
+  if (li < (int)min(S_EW_TOT(in.ebase), (uint32_t)S_ESC_IN))
+    ent = s.tesc_in[(t & 1) ^ 1][((size_t)in.band * s.n + in.r) * S_ESC_IN + li];
   const __amdgpu_buffer_rsrc_t prs = gm_rsrc(s.msg + (size_t)in.band * s.n * B, (uint32_t)(s.n * B));
   const uint32_t poff = (uint32_t)(((t & 1) ^ 1) * (B / 2) + li * 8);  // + sender * B
   const int k = min(in.k, S_KMAX);
@@ -316,7 +374,7 @@ __device__ __forceinline__ void unit_gather(const SState &s, int t, const UnitIn
 
 template <int B, bool DROP>
 __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct, const UnitIn<B> &in,
-                                            const u32x2 m[S_SB]) {
+                                            const u32x2 m[S_SB], uint32_t ent, uint32_t *lds) {
   constexpr int LPR = B / S_COLS_PER_LANE;  // lanes per row
   constexpr int RPW = 64 / LPR;             // rows per wave
   constexpr int Q = S_COLS_PER_LANE;        // cells per lane (8 packed pairs)
@@ -354,18 +412,17 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
   int nkept = 0;     // DROP: delivered entries this lane kept after the keyed loss (msgcount)
   uint32_t evk = 0;  // 2 bits per cell: event kind
   bool esc_st = false;  // this lane stored escaped cells
-  uint32_t eb_out = S_ESC_NONE;  // the row slice's escape list in this tick's pool (the record's .w)
-  if (!live && in.ebase != S_ESC_NONE) {
+  uint32_t eb_out = 0;  // the row slice's escape-list word of this tick (the record's .w)
+  if (!live && in.ebase != 0) {
     // a row not swept this tick (crashed, not yet in the group) keeps its cells as they are: its
-    // escaped cells move to this tick's pool (row-uniform branch)
-    const uint32_t em = esc_mask16(in.ta.x, in.ta.y, in.ta.z, in.ta.w);
-    int etot;
-    const int eoff = row_scan<LPR>(__builtin_popcount(em), li, lane, etot);
-    eb_out = row_alloc<LPR>(&s.tesc_cnt[par], s.tesc_cap, etot, li, lane, s.err);
-    if (eb_out != S_ESC_NONE) {
-      const uint16_t *src = s.tesc[par ^ 1] + in.ebase + eoff;
-      uint16_t *dst = s.tesc[par] + eb_out + eoff;
-      for (int i = 0; i < __builtin_popcount(em); i++) dst[i] = src[i];
+    // escape list moves to this tick's storage (row-uniform branch; entries carry their columns)
+    const int etot = (int)S_EW_TOT(in.ebase);
+    eb_out = row_alloc<LPR>(s, par, slab, r, etot, li, lane);
+    if (eb_out != 0) {
+      const EscList src = esc_list(s, par ^ 1, slab, r, in.ebase), dst = esc_list(s, par, slab, r, eb_out);
+      constexpr int P = LPR < S_ESC_IN ? LPR : S_ESC_IN;  // entries prefetched (one per lane)
+      if (li < min(etot, P)) *dst.at(li) = ent;
+      for (int i = P + li; i < etot; i += LPR) *dst.at(i) = *src.at(i);
     }
   }
   if (live) {
@@ -456,12 +513,8 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
       npb = padd(npb, nz);
       tw[i] = widen2(x, nz);
     }
-    if (in.ebase != S_ESC_NONE) {  // row-uniform: the lane's part of the list follows its row predecessors'
-      const uint32_t em = esc_mask16(ta.x, ta.y, ta.z, ta.w);
-      int etot;
-      const int eoff = row_scan<LPR>(__builtin_popcount(em), li, lane, etot);
-      esc_load(s.tesc[par ^ 1] + in.ebase + eoff, em, tw);
-    }
+    if (in.ebase != 0)  // row-uniform: the row slice held escaped cells after the last tick
+      esc_apply<LPR>(lds, lane, li, esc_list(s, par ^ 1, slab, r, in.ebase), (int)S_EW_TOT(in.ebase), ent, tw);
     // merge: re-base the cell to tick t (h -= 2, age += 1; absent stays 0), then max
     // with the delivered key (insert if absent; raise hb and stamp ts = t if newer)
     u16x2 mm[8];
@@ -568,23 +621,17 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
       ngone = (int)ng2.x + (int)ng2.y;
     }
     esc_st = unpk(badv) != 0;
-    if (row_any<LPR>(esc_st, sub)) {  // rare: cells the byte cannot hold, as 16-bit cells into this tick's pool
-      uint32_t em = 0;
+    const bool esc_row = row_any<LPR>(esc_st, sub);
+    uint32_t em = 0;  // the lane's escaped cells (entries of this tick's list, emitted after the stores)
+    if (esc_row) {  // rare: cells the byte cannot hold; the lane's cells wait in its LDS slot
       if (esc_st) {
         u16x2 lagmin = (u16x2)(0xFFFF);
 #pragma unroll
         for (int i = 0; i < 8; i++) lagmin = __builtin_elementwise_min(lagmin, pk(cw[i]) - (u16x2)(32));
         if (__builtin_elementwise_min(lagmin.x, lagmin.y) < 64) atomicOr(s.err, GM_ERR_LAG);  // present with h <= 2
         em = esc_mask16(bw[0], bw[1], bw[2], bw[3]);
-        // a stale escaped cell stores S_B_ESCS (the gossip draw reads freshness from the byte)
-#pragma unroll
-        for (int q = 0; q < Q; q++)
-          if (((em >> q) & 1u) && ((cw[q >> 1] >> (16 * (q & 1))) & 31u) >= GM_TFAIL) bw[q >> 2] += 1u << (8 * (q & 3));
+        esc_park(lds, lane, cw);
       }
-      int etot;
-      const int eoff = row_scan<LPR>(__builtin_popcount(em), li, lane, etot);
-      eb_out = row_alloc<LPR>(&s.tesc_cnt[par], s.tesc_cap, etot, li, lane, s.err);
-      if (em && eb_out != S_ESC_NONE) esc_store(s.tesc[par] + eb_out + eoff, em, cw);
     }
     const bool pesc = __builtin_elementwise_max(nmx.x, nmx.y) == S_NIB_ESC;
     if (row_any<LPR>(pesc, sub)) {
@@ -592,10 +639,12 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
       // pool (read where a receiver meets nibble 15), one reservation per row
       const uint64_t bal = __builtin_amdgcn_ballot_w64(pesc);
       const uint64_t rm = LPR == 64 ? bal : (bal >> (sub * LPR)) & ((1ull << LPR) - 1);
-      uint32_t pbase = S_ESC_NONE;
+      uint32_t pbase = S_PESC_NONE;
       if (li == 0) {
-        const unsigned long long b = atomicAdd(&s.pesc_cnt[par], (unsigned long long)__builtin_popcountll(rm));
-        if (b + (unsigned long long)__builtin_popcountll(rm) <= (unsigned long long)s.pesc_cap) pbase = (uint32_t)b;
+        const int ps = esc_stripe(s, slab, r);
+        const unsigned long long b = atomicAdd(s.pesc_cnt + par * s.esc_stripes + ps, (unsigned long long)__builtin_popcountll(rm));
+        if (b + (unsigned long long)__builtin_popcountll(rm) <= (unsigned long long)s.pesc_region)
+          pbase = (uint32_t)ps * s.pesc_region + (uint32_t)b;
         else atomicOr(s.err, GM_ERR_ESC);
         s.pesc_rec[par][slab + r] = make_uint4(pbase, (uint32_t)rm, (uint32_t)(rm >> 32), 0u);
       }
@@ -609,7 +658,7 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
       }
       const u32x4 wv = {__builtin_amdgcn_perm(pw[1], pw[0], 0x06040200u), __builtin_amdgcn_perm(pw[3], pw[2], 0x06040200u),
                         __builtin_amdgcn_perm(pw[5], pw[4], 0x06040200u), __builtin_amdgcn_perm(pw[7], pw[6], 0x06040200u)};
-      if (pesc && pbase != S_ESC_NONE)
+      if (pesc && pbase != S_PESC_NONE)
         *(u32x4 *)(s.pesc[par] + ((size_t)pbase + __builtin_popcountll(rm & ((1ull << li) - 1))) * 16) = wv;
     }
     nfail = (int)nf2.x + (int)nf2.y;
@@ -645,6 +694,12 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
     const u32x2 ov = {unpk(nwv[0]), unpk(nwv[1])};
     __builtin_amdgcn_raw_buffer_store_b64(ov, prs, (uint32_t)(r * B + par * (B / 2) + li * 8), 0, GM_AUX_NT);
     if (band == 0 && li == 0) s.wtick[r] = t;
+    if (esc_row) {  // the escaped cells as entries of this tick's list (the record's .w)
+      int etot;
+      const int eoff = row_scan<LPR>(__builtin_popcount(em), li, lane, etot);
+      eb_out = row_alloc<LPR>(s, par, slab, r, etot, li, lane);
+      if (eb_out != 0) esc_emit(lds, lane, esc_list(s, par, slab, r, eb_out), eoff, em, li * Q);
+    }
   }
   if (DROP && s.mc_rdrop) {  // msgcount: the row's kept entries (wave-uniform test)
     int v = nkept;
@@ -710,7 +765,8 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
   const int E = s.evs;
   uint32_t sbase = 0;  // one spill-ring reservation per (row, band) that overflows its slots
   if (live && li == 0 && tot > E) sbase = atomicAdd(s.ev_spill_cnt, (uint32_t)(tot - E));
-  if (live && li == 0 && tot) atomicAdd(s.ev_spill_cnt + 1, (uint32_t)tot);  // the tick's total (host staging)
+  if (live && li == 0 && tot)  // the tick's total (host staging), striped partial sums
+    atomicAdd(s.ev_spill_cnt + 1 + ((slab + (size_t)r) & (S_EV_STRIPES - 1)), (uint32_t)tot);
   sbase = LPR == 64 ? __builtin_amdgcn_readfirstlane(sbase) : __shfl(sbase, sub * LPR, 64);
   if (live && nev) {
     int slot = x - nev;
@@ -754,11 +810,16 @@ __global__ __launch_bounds__(256) void gm_s_band(SState s, int t, int drop_pct) 
   UnitIn<B> in;
   unit_load<B, RPW == 1>(s, t, (int)blockIdx.y, ub, in);
   u32x2 m[S_SB];
-  unit_gather<B, DROP>(s, t, in, m);
-  unit_finish<B, DROP>(s, t, drop_pct, in, m);
-  if (ub == 0 && blockIdx.y == 0 && threadIdx.x == 0) {  // the pools of tick t+1 start empty (the tick t-1
-    s.tesc_cnt[(t & 1) ^ 1] = 0;                          // lists in them are read through their bases,
-    s.pesc_cnt[(t & 1) ^ 1] = 0;                          // never through the counter)
+  uint32_t ent;
+  unit_gather<B, DROP>(s, t, in, m, ent);
+  __shared__ uint32_t lds_all[4 * S_LDS_WAVE_WORDS];  // escaped rows only (esc_apply / esc_emit)
+  unit_finish<B, DROP>(s, t, drop_pct, in, m, ent, lds_all + (threadIdx.x >> 6) * S_LDS_WAVE_WORDS);
+  if (ub == 0 && blockIdx.y == 0) {  // the pools of tick t+1 start empty (the tick t-1 lists in them are
+    const int S = s.esc_stripes;       // read through their bases, never through the counters)
+    for (int i = threadIdx.x; i < S; i += 64) {
+      s.tesc_cnt[((t & 1) ^ 1) * S + i] = 0;
+      s.pesc_cnt[((t & 1) ^ 1) * S + i] = 0;
+    }
   }
 }
 
@@ -772,22 +833,25 @@ __global__ __launch_bounds__(256) void gm_s_band_pipe(SState s, int t, int nwave
   const int total = ((s.n + RPW - 1) / RPW) * s.nb;
   int u = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
   if (u >= total) return;
-  if (u == 0 && threadIdx.x == 0) {
-    s.tesc_cnt[(t & 1) ^ 1] = 0;
-    s.pesc_cnt[(t & 1) ^ 1] = 0;
-  }
+  if (u == 0)
+    for (int i = threadIdx.x; i < s.esc_stripes; i += 64) {
+      s.tesc_cnt[((t & 1) ^ 1) * s.esc_stripes + i] = 0;
+      s.pesc_cnt[((t & 1) ^ 1) * s.esc_stripes + i] = 0;
+    }
   UnitIn<B> cur, nxt;
   u32x2 m[S_SB];
+  __shared__ uint32_t lds_all[4 * S_LDS_WAVE_WORDS];
   const int U = (s.n + RPW - 1) / RPW;
   unit_load<B>(s, t, u / U, u % U, cur);
-  unit_gather<B, false>(s, t, cur, m);
+  uint32_t ent;
+  unit_gather<B, false>(s, t, cur, m, ent);
   for (;;) {
     const int un = u + nwaves;
     const bool more = un < total;  // wave-uniform
     if (more) unit_load<B>(s, t, un / U, un % U, nxt);
-    unit_finish<B, false>(s, t, -1, cur, m);
+    unit_finish<B, false>(s, t, -1, cur, m, ent, lds_all + (threadIdx.x >> 6) * S_LDS_WAVE_WORDS);
     if (!more) break;
-    unit_gather<B, false>(s, t, nxt, m);
+    unit_gather<B, false>(s, t, nxt, m, ent);
     cur = nxt;
     u = un;
   }
@@ -878,6 +942,21 @@ __device__ __forceinline__ void gm_row_totals(const SState &s, int r, int lane, 
   }
 }
 
+// Freshness (age < TFAIL) of the escaped cell (r, col) of tick t, from its (band, row) list of
+// tick t (rare: a draw landing on an escaped cell)
+__device__ __forceinline__ bool esc_fresh(const SState &s, int r, int col) {
+  const int b = col / s.band, c = col % s.band;
+  const size_t slab = (size_t)b * s.n;
+  const uint32_t w = s.brec[slab + r].w;
+  // the pools of the tick just swept: its parity is that of the row's last written tick
+  const EscList l = esc_list(s, s.wtick[r] & 1, slab, r, w);
+  for (int i = 0; i < (int)S_EW_TOT(w); i++) {
+    const uint32_t e = *l.at(i);
+    if ((e & 0xFFFFu) == (uint32_t)c) return S_AGE(e >> 16) < GM_TFAIL;
+  }
+  return false;
+}
+
 // Resolve up to 8 draws at once, one per 8-lane group: group g holds shard-local rank
 // ix_g (valid iff act) of a present entry of row r. The chunk-word prefix finds the
 // 64- or 128-column chunk; its cell bytes (8 or 16 per lane) give the column. Returns, to
@@ -929,8 +1008,8 @@ __device__ __forceinline__ void gm_resolve8(const SState &s, int r, const uint32
       if (en[v] != 0) {
         if (need == 0) {
           mycol = base + v;
-          // the table is as of tick t; an escaped cell's byte says whether it is fresh
-          myfresh = s_is_esc(en[v]) ? en[v] == S_B_ESC : S_AGE(s_widen(en[v])) < GM_TFAIL;
+          // the table is as of tick t; an escaped cell's age is in its (band, row) escape list
+          myfresh = s_is_esc(en[v]) ? esc_fresh(s, r, mycol) : S_AGE(s_widen(en[v])) < GM_TFAIL;
         }
         need--;
       }
@@ -1393,10 +1472,13 @@ __global__ __launch_bounds__(256) void gm_s_init(SState s, int warm, int t0, uin
   int etot;
   const int eoff = row_scan<LPR>(__builtin_popcount(em), li, lane, etot);
   const int par = t0 & 1;  // the state is "as of tick t0": tick t0 + 1 reads this pool
-  const uint32_t base = row_alloc<LPR>(&s.tesc_cnt[par], s.tesc_cap, etot, li, lane, s.err);
-  if (em && base != S_ESC_NONE) esc_store(s.tesc[par] + base + eoff, em, cw);
-  if (!row) return;
   const size_t slab = (size_t)band * s.n;
+  const uint32_t base = row_alloc<LPR>(s, par, slab, min(r, s.n - 1), etot, li, lane);
+  __shared__ uint32_t lds_all[4 * S_LDS_WAVE_WORDS];
+  uint32_t *lds = lds_all + (threadIdx.x >> 6) * S_LDS_WAVE_WORDS;
+  if (em) esc_park(lds, lane, cw);
+  if (base != 0) esc_emit(lds, lane, esc_list(s, par, slab, r, base), eoff, em, li * Q);
+  if (!row) return;
   *(u32x4 *)(s.table + (slab + r) * B + li * Q) = (u32x4){bw[0], bw[1], bw[2], bw[3]};
   if (li == 0) {
     s.brec[slab + r] = make_uint4(0u, 0u, 0u, base);
@@ -1415,7 +1497,7 @@ static hipError_t launch_tick_b(const SState &s, int t, int drop_pct, bool nt, h
   constexpr int RPW = 64 / (B / S_COLS_PER_LANE);
   const dim3 nblk((((s.n + RPW - 1) / RPW) + 3) / 4, s.nb);  // (units of a band / 4, bands)
   // the event records of a tick (per-(row, band) slots + spill ring) stay readable until the next tick
-  (void)hipMemsetAsync(s.ev_spill_cnt, 0, 2 * sizeof(uint32_t), st);
+  (void)hipMemsetAsync(s.ev_spill_cnt, 0, (1 + S_EV_STRIPES) * sizeof(uint32_t), st);
   hipLaunchKernelGGL(gm_s_mtgen, dim3((s.n + 255) / 256), dim3(256), 0, st, s, t);
   if (k0) (void)hipEventRecord(k0, st);
   if (drop_pct >= 0) hipLaunchKernelGGL((gm_s_band<B, true>), dim3(nblk), dim3(256), 0, st, s, t, drop_pct);

@@ -6,6 +6,7 @@
 #   smoke      __graft_entry__.smoke()                  -> $O/smoke.txt
 #   sa         bench.py (S-A, with cpu_baseline)        -> $O/bench_sa.json
 #   sc         bench.py --scenario S-C                  -> $O/bench_sc.json
+#   ticks      scripts/tick_times.py: per-tick gm_s_band time of the S-A schedule -> $O/tick_times.txt
 #   sb         bench.py --cluster 262144 (S-B on one GPU) -> $O/bench_sb.json
 #   sa_pmc     bench.py --pmc (S-A, traffic measured live by two child PMC passes) -> $O/bench_sa_pmc.json
 #   shard      bench.py --force-shard (RCCL, 1 rank)    -> $O/bench_force_shard.json
@@ -36,6 +37,7 @@ run_step() {
     smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 ;;
     sa) timeout -k 10 300 python -u bench.py ${BENCH_ARGS:-} > $O/bench_sa.json 2> $O/bench_sa.err ;;
     sc) timeout -k 10 400 python -u bench.py --scenario S-C ${BENCH_ARGS:-} > $O/bench_sc.json 2> $O/bench_sc.err ;;
+    ticks) timeout -k 10 300 python -u scripts/tick_times.py ${TICKS_N:-65536} > $O/tick_times.txt 2>&1 ;;
     sb) timeout -k 10 400 python -u bench.py --cluster 262144 ${BENCH_ARGS:-} > $O/bench_sb.json 2> $O/bench_sb.err ;;
     sa_pmc) timeout -k 10 700 python -u bench.py --pmc --no-cpu ${BENCH_ARGS:-} > $O/bench_sa_pmc.json 2> $O/bench_sa_pmc.err ;;
     shard) timeout -k 10 300 python -u bench.py --force-shard --no-cpu ${BENCH_ARGS:-} > $O/bench_force_shard.json 2> $O/bench_force_shard.err ;;

@@ -47,9 +47,10 @@ GM_ERR_ESC = 128
 
 
 def test_escape_pool_overflow_fails_loudly(monkeypatch):
-    """The compact escape pool (gm_scaled.h): a cold start escapes every cell, so a pool smaller
+    """The compact escape storage (gm_scaled.h): a cold start escapes every cell, so a pool smaller
     than the cluster refuses the context; a warm start fits a tiny pool until a crash window
-    escapes the crashed nodes' entries (lag > 14 ticks), then the tick fails with GM_ERANGE."""
+    escapes the crashed nodes' entries (lag > 14 ticks) -- 64 of them per row, more than a
+    list's 16 inline cells -- then the tick fails with GM_ERANGE."""
     n = 1024
     monkeypatch.setenv("GM_ESC_CAP", str(n * n // 2))
     with pytest.raises(GmError) as e:
@@ -58,13 +59,14 @@ def test_escape_pool_overflow_fails_loudly(monkeypatch):
     monkeypatch.setenv("GM_ESC_CAP", "64")
     sim = Simulator(n, GM_MODE_SCALED, rd_seed=7, init_mode=1, init_t0=8, init_seed=11)
     assert first_error(sim, 3) == 0
-    sim.set_failed([5, 77, 300, 901])
-    code = first_error(sim, 30)  # 4 x 1020 observers escape ~10 ticks after the crash
+    crash = list(range(3, 1024, 16))  # 64 nodes
+    sim.set_failed(crash)
+    code = first_error(sim, 30)  # 64 x 960 observers' cells escape ~10 ticks after the crash
     assert code == GM_ERANGE
     sim.close()
     monkeypatch.delenv("GM_ESC_CAP")  # the default pool: the same run stays clean through the removals
     sim = Simulator(n, GM_MODE_SCALED, rd_seed=7, init_mode=1, init_t0=8, init_seed=11)
     assert first_error(sim, 3) == 0
-    sim.set_failed([5, 77, 300, 901])
+    sim.set_failed(crash)
     assert first_error(sim, 30) == 0 and sim.tick_stats()["err"] == 0
-    assert sim.event_totals()["removed"] == 4 * (n - 4)
+    assert sim.event_totals()["removed"] == 64 * (n - 64)

@@ -133,5 +133,9 @@ def test_column_shard_msgcount_matches_fused_kernel(world, drop, rccl, monkeypat
     assert want[0].sum() > 0 and want[1].sum() > 0
     for s in shards:
         got = s.msgcount(tmax)
-        assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1])
+        for t in range(tmax - ticks, tmax):
+            assert np.array_equal(got[0][:, t], want[0][:, t]), f"sent differs at tick {t}"
+            assert np.array_equal(got[1][:, t], want[1][:, t]), f"recv differs at tick {t}"
         assert s.tick_stats()["err"] == 0
+    if world == 1:
+        assert shards[0].dump_tables() == ref.dump_tables()
