@@ -1267,6 +1267,80 @@ extern "C" int gm_read_row(gm_ctx *c, int32_t r, int32_t c0, int32_t len, int32_
   return GM_OK;
 }
 
+// SCALED bulk readback: one copy of the table, the records, the row ticks and the last
+// tick's escape entries (inline + each stripe's used pool part), decoded row by row.
+struct ScaledSnapshot {
+  std::vector<uint8_t> tab, row;
+  std::vector<uint4> rec;
+  std::vector<uint32_t> pool, inl;
+  std::vector<uint16_t> esc;
+  std::vector<int32_t> wts;
+  int load(gm_ctx *c) {
+    const SState &s = c->s;
+    tab.resize((size_t)s.n * s.wp);
+    rec.resize((size_t)s.n * s.nb);
+    wts.resize(s.n);
+    std::vector<unsigned long long> cnt(s.esc_stripes);
+    HIPCHECK(hipMemcpy(tab.data(), s.table, tab.size(), hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(rec.data(), s.brec, sizeof(uint4) * rec.size(), hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(wts.data(), s.wtick, sizeof(int32_t) * s.n, hipMemcpyDeviceToHost));
+    const int par = (c->t - 1) & 1;
+    HIPCHECK(hipMemcpy(cnt.data(), s.tesc_cnt + (size_t)par * s.esc_stripes, sizeof(unsigned long long) * cnt.size(),
+                       hipMemcpyDeviceToHost));
+    inl.resize((size_t)s.n * s.nb * S_ESC_IN);
+    HIPCHECK(hipMemcpy(inl.data(), s.tesc_in[par], sizeof(uint32_t) * inl.size(), hipMemcpyDeviceToHost));
+    pool.resize(s.tesc_cap);  // each stripe's used part, at its absolute offsets
+    for (int k = 0; k < s.esc_stripes; k++) {
+      const size_t used = std::min<unsigned long long>(cnt[k], s.tesc_region);
+      if (used)
+        HIPCHECK(hipMemcpy(pool.data() + (size_t)k * s.tesc_region, s.tesc[par] + (size_t)k * s.tesc_region,
+                           sizeof(uint32_t) * used, hipMemcpyDeviceToHost));
+    }
+    row.resize(s.wp);
+    esc.resize(s.wp);
+    return GM_OK;
+  }
+  int decode(const gm_ctx *c, int i, std::vector<int32_t> &rh, std::vector<int32_t> &rt) {
+    const SState &s = c->s;
+    for (int b = 0; b < s.nb; b++) {
+      const uint8_t *pc = tab.data() + ((size_t)b * s.n + i) * s.band;
+      memcpy(row.data() + (size_t)b * s.band, pc, s.band);
+      size_t k = 0;
+      for (int j = 0; j < s.band; j++) k += s_is_esc(pc[j]);
+      if (!k) continue;
+      const uint32_t w = rec[(size_t)b * s.n + i].w;
+      const size_t in = std::min<size_t>(k, S_ESC_IN);
+      if (S_EW_TOT(w) != k || S_EW_OFF(w) + (k - in) > s.tesc_region) return GM_ESTATE;
+      const size_t stripe = ((size_t)b * s.n + i) & (size_t)(s.esc_stripes - 1);
+      TRY(place_entries(s, b, pc, inl.data() + ((size_t)b * s.n + i) * S_ESC_IN,
+                        pool.data() + stripe * s.tesc_region + S_EW_OFF(w), k, esc.data()));
+    }
+    decode_scaled_row(c, row.data(), esc.data(), wts[i], rh, rt);
+    return GM_OK;
+  }
+};
+
+extern "C" int gm_read_table(gm_ctx *c, int32_t r0, int32_t count, int32_t *hb, int32_t *ts) {
+  if (!c || r0 < 0 || count < 0 || r0 + (int64_t)count > c->n || (count > 0 && (!hb || !ts))) return GM_EINVAL;
+  TRY(f_settle(c));
+  HIPCHECK(hipStreamSynchronize(c->stream));
+  std::vector<int32_t> rh, rt;
+  ScaledSnapshot snap;
+  if (c->cfg.mode == GM_MODE_SCALED) TRY(snap.load(c));
+  for (int i = 0; i < count; i++) {
+    int w;
+    if (c->cfg.mode == GM_MODE_SCALED) {
+      TRY(snap.decode(c, r0 + i, rh, rt));
+      w = c->s.w;
+    } else {
+      TRY(read_table_row(c, r0 + i, rh, rt, w));
+    }
+    memcpy(hb + (size_t)i * w, rh.data(), sizeof(int32_t) * w);
+    memcpy(ts + (size_t)i * w, rt.data(), sizeof(int32_t) * w);
+  }
+  return GM_OK;
+}
+
 extern "C" int gm_read_views(gm_ctx *c, int32_t r0, int32_t count, uint64_t *out) {
   if (!c || count < 0 || (count > 0 && !out)) return GM_EINVAL;
   if (c->cfg.mode != GM_MODE_PARTIAL) return GM_EUNSUPPORTED;
@@ -1347,56 +1421,13 @@ extern "C" int gm_dump_tables(gm_ctx *c, char *buf, size_t cap, size_t *len) {
     return GM_OK;
   }
   std::vector<int32_t> rh, rt;
-  // SCALED: one copy of the table, the records and the last tick's pool, decoded row by row
-  std::vector<uint8_t> tab;
-  std::vector<uint4> rec;
-  std::vector<uint32_t> pool, inl;
-  std::vector<uint16_t> esc;
-  std::vector<int32_t> wts;
-  std::vector<uint8_t> row;
-  if (c->cfg.mode == GM_MODE_SCALED) {
-    const SState &s = c->s;
-    tab.resize((size_t)s.n * s.wp);
-    rec.resize((size_t)s.n * s.nb);
-    wts.resize(s.n);
-    std::vector<unsigned long long> cnt(s.esc_stripes);
-    HIPCHECK(hipMemcpy(tab.data(), s.table, tab.size(), hipMemcpyDeviceToHost));
-    HIPCHECK(hipMemcpy(rec.data(), s.brec, sizeof(uint4) * rec.size(), hipMemcpyDeviceToHost));
-    HIPCHECK(hipMemcpy(wts.data(), s.wtick, sizeof(int32_t) * s.n, hipMemcpyDeviceToHost));
-    const int par = (c->t - 1) & 1;
-    HIPCHECK(hipMemcpy(cnt.data(), s.tesc_cnt + (size_t)par * s.esc_stripes, sizeof(unsigned long long) * cnt.size(),
-                       hipMemcpyDeviceToHost));
-    inl.resize((size_t)s.n * s.nb * S_ESC_IN);
-    HIPCHECK(hipMemcpy(inl.data(), s.tesc_in[par], sizeof(uint32_t) * inl.size(), hipMemcpyDeviceToHost));
-    pool.resize(s.tesc_cap);  // each stripe's used part, at its absolute offsets
-    for (int k = 0; k < s.esc_stripes; k++) {
-      const size_t used = std::min<unsigned long long>(cnt[k], s.tesc_region);
-      if (used)
-        HIPCHECK(hipMemcpy(pool.data() + (size_t)k * s.tesc_region, s.tesc[par] + (size_t)k * s.tesc_region,
-                           sizeof(uint32_t) * used, hipMemcpyDeviceToHost));
-    }
-    row.resize(s.wp);
-    esc.resize(s.wp);
-  }
+  ScaledSnapshot snap;
+  if (c->cfg.mode == GM_MODE_SCALED) TRY(snap.load(c));
   for (int i = 0; i < c->n; i++) {
     int w;
     if (c->cfg.mode == GM_MODE_SCALED) {
-      const SState &s = c->s;
-      for (int b = 0; b < s.nb; b++) {
-        const uint8_t *pc = tab.data() + ((size_t)b * s.n + i) * s.band;
-        memcpy(row.data() + (size_t)b * s.band, pc, s.band);
-        size_t k = 0;
-        for (int j = 0; j < s.band; j++) k += s_is_esc(pc[j]);
-        if (!k) continue;
-        const uint32_t w = rec[(size_t)b * s.n + i].w;
-        const size_t in = std::min<size_t>(k, S_ESC_IN);
-        if (S_EW_TOT(w) != k || S_EW_OFF(w) + (k - in) > s.tesc_region) return GM_ESTATE;
-        const size_t stripe = ((size_t)b * s.n + i) & (size_t)(s.esc_stripes - 1);
-        TRY(place_entries(s, b, pc, inl.data() + ((size_t)b * s.n + i) * S_ESC_IN,
-                          pool.data() + stripe * s.tesc_region + S_EW_OFF(w), k, esc.data()));
-      }
-      decode_scaled_row(c, row.data(), esc.data(), wts[i], rh, rt);
-      w = s.w;
+      TRY(snap.decode(c, i, rh, rt));
+      w = c->s.w;
     } else {
       TRY(read_table_row(c, i, rh, rt, w));
     }

@@ -34,7 +34,7 @@ class GmEvent(ctypes.Structure):
 
 
 EXPORTS = ["gm_parse_conf", "gm_create", "gm_destroy", "gm_tick", "gm_sync", "gm_time", "gm_rand", "gm_set_failed",
-           "gm_set_dropmsg", "gm_drain_events", "gm_event_counts", "gm_msgcount", "gm_read_row", "gm_read_nodes",
+           "gm_set_dropmsg", "gm_drain_events", "gm_event_counts", "gm_msgcount", "gm_read_row", "gm_read_table", "gm_read_nodes",
            "gm_dump_tables", "gm_tick_stats", "gm_set_timing", "gm_last_kernel_ms", "gm_crash_set", "gm_strerror",
            "gm_comm_unique_id", "gm_comm_init", "gm_shard_layout", "gm_shard_merge", "gm_shard_draw",
            "gm_shard_accept", "gm_shard_end_tick", "gm_shard_loopback", "gm_partial_loopback_tick",
@@ -73,6 +73,7 @@ def load_library():
         "gm_msgcount": [ctypes.c_void_p, i32, P(i32), P(i32)],
         "gm_msgcount_record": [ctypes.c_void_p, i32],
         "gm_read_row": [ctypes.c_void_p, i32, i32, i32, P(i32), P(i32)],
+        "gm_read_table": [ctypes.c_void_p, i32, i32, P(i32), P(i32)],
         "gm_read_nodes": [ctypes.c_void_p, P(i32)],
         "gm_dump_tables": [ctypes.c_void_p, ctypes.c_char_p, sz, P(sz)],
         "gm_tick_stats": [ctypes.c_void_p, P(ctypes.c_int64)],
@@ -246,6 +247,15 @@ class Simulator:
         hb = np.zeros(length, dtype=np.int32)
         ts = np.zeros(length, dtype=np.int32)
         self._call("gm_read_row", self.h, r, c0, length, _ptr(hb), _ptr(ts))
+        return hb, ts
+
+    def read_table(self, r0=0, count=None):
+        """(hb, ts) int32 [count][w] of rows [r0, r0 + count) over this context's columns, -1 = absent."""
+        count = self.n - r0 if count is None else count
+        w = self.shard_layout()[1] if self.mode == GM_MODE_SCALED else self.n
+        hb = np.zeros((count, w), dtype=np.int32)
+        ts = np.zeros((count, w), dtype=np.int32)
+        self._call("gm_read_table", self.h, r0, count, _ptr(hb), _ptr(ts))
         return hb, ts
 
     def read_nodes(self):

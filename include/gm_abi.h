@@ -178,6 +178,9 @@ int gm_msgcount_record(gm_ctx *ctx, int32_t tmax);
 /* Dense readback of observer row r: hb/ts per subject column (absent -> -1),
  * columns [c0, c0+len) of this context's shard (c0 relative to the shard start). */
 int gm_read_row(gm_ctx *ctx, int32_t r, int32_t c0, int32_t len, int32_t *hb, int32_t *ts);
+/* Dense readback of observer rows [r0, r0+count): hb/ts [count][w] over this context's
+ * w columns (absent -> -1); one bulk copy of the table, for parity tests at larger N. */
+int gm_read_table(gm_ctx *ctx, int32_t r0, int32_t count, int32_t *hb, int32_t *ts);
 /* PARTIAL: the raw V-entry views (id << 32 | hb, 0 = empty, ascending id) of nodes
  * [r0, r0 + count) as of the last tick, [count][V]; a row shard reads its own nodes. */
 int gm_read_views(gm_ctx *ctx, int32_t r0, int32_t count, uint64_t *out);

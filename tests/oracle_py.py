@@ -148,6 +148,21 @@ class Oracle:
         self.L.oc_row(self.h, r, _i32p(hb), _i32p(ts))
         return hb, ts
 
+    def table(self):
+        """(hb, ts) int32 [n][n], -1 = absent: every observer's member list, dense"""
+        hb = np.empty((self.n, self.n), dtype=np.int32)
+        ts = np.empty((self.n, self.n), dtype=np.int32)
+        for r in range(self.n):
+            self.L.oc_row(self.h, r, _i32p(hb[r]), _i32p(ts[r]))
+        return hb, ts
+
+    def nodes(self):
+        """[n][4] inited / inGroup / failed / heartbeat"""
+        st = np.empty((self.n, 4), dtype=np.int32)
+        for r in range(self.n):
+            self.L.oc_node(self.h, r, _i32p(st[r]))
+        return st
+
     def node(self, r):
         st = np.zeros(4, dtype=np.int32)
         self.L.oc_node(self.h, r, _i32p(st))

@@ -11,6 +11,25 @@ from membership.sharded import loopback_tick
 pytestmark = pytest.mark.gpu
 
 
+def merged_state(shards, owners):
+    """Per-shard binary readbacks merged: (hb, ts) [n][n] by column concatenation (shards are
+    ordered by rank = ascending column ranges) and each row's node state from the shard that
+    owns the row's own column (only that shard bumps the row's self entry)."""
+    tabs = [s.read_table() for s in shards]
+    hb = np.concatenate([t[0] for t in tabs], axis=1)
+    ts = np.concatenate([t[1] for t in tabs], axis=1)
+    nodes = np.stack([s.read_nodes() for s in shards])  # [G][n][4]
+    st = nodes[owners, np.arange(len(owners))]
+    return hb, ts, st
+
+
+def assert_same_state(shards, owners, ref, what):
+    hb, ts, st = merged_state(shards, owners)
+    rhb, rts = ref.read_table()
+    assert np.array_equal(hb, rhb) and np.array_equal(ts, rts), f"tables differ {what}"
+    assert np.array_equal(st, ref.read_nodes()), f"node state differs {what}"
+
+
 def merge_dumps(dumps, owners):
     """Combine per-shard dumps (same rows, disjoint column ranges) into one dump."""
     per = [d.decode().splitlines() for d in dumps]
@@ -47,8 +66,8 @@ def test_shards_match_fused_kernel(n, world, drop, warm):
         assert all(s.time == ref.time for s in shards)
         ev = sorted(e for s in shards for e in s.drain_events())
         assert ev == sorted(ref.drain_events()), f"events differ at tick {t}"
-        got = merge_dumps([s.dump_tables() for s in shards], owners)
-        assert got == ref.dump_tables(), f"tables differ at tick {t}"
+        assert_same_state(shards, owners, ref, f"at tick {t}")
+    assert merge_dumps([s.dump_tables() for s in shards], owners) == ref.dump_tables()  # the text rendering too
     for s in shards:
         st = s.tick_stats()
         assert st["err"] == 0
@@ -88,7 +107,8 @@ def test_rccl_single_rank_matches_fused_kernel(n, drop, ncrash, rounds, monkeypa
             ref.set_failed(crash)
             sh.set_failed(crash)
         assert sorted(sh.drain_events()) == sorted(ref.drain_events()), f"events differ at tick {t}"
-        assert sh.dump_tables() == ref.dump_tables(), f"tables differ at tick {t}"
+        assert_same_state([sh], np.zeros(n, dtype=int), ref, f"at tick {t}")
+    assert sh.dump_tables() == ref.dump_tables()
     assert sh.tick_stats()["err"] == 0
 
 
@@ -128,8 +148,7 @@ def test_ramp_shards_match_fused_kernel(n, world, drop, intro):
         ev = sorted(e for s in shards for e in s.drain_events())
         assert ev == sorted(ref.drain_events()), f"events differ at tick {t}"
         if t % 4 == 0:
-            got = merge_dumps([s.dump_tables() for s in shards], owners)
-            assert got == ref.dump_tables(), f"tables differ at tick {t}"
+            assert_same_state(shards, owners, ref, f"at tick {t}")
     assert merge_dumps([s.dump_tables() for s in shards], owners) == ref.dump_tables()
     for s in shards:
         assert s.tick_stats()["err"] == 0
@@ -163,5 +182,6 @@ def test_rccl_single_rank_ramp_matches_fused_kernel(monkeypatch):
             ref.set_failed(crash)
             sh.set_failed(crash)
         assert sorted(sh.drain_events()) == sorted(ref.drain_events()), f"events differ at tick {t}"
-        assert sh.dump_tables() == ref.dump_tables(), f"tables differ at tick {t}"
+        assert_same_state([sh], np.zeros(n, dtype=int), ref, f"at tick {t}")
+    assert sh.dump_tables() == ref.dump_tables()
     assert sh.tick_stats()["err"] == 0
