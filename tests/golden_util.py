@@ -94,3 +94,12 @@ def parse_conf(text):
             k, v = line.split(":", 1)
             vals[k.strip()] = v.strip()
     return (int(vals["MAX_NNB"]), int(vals["SINGLE_FAILURE"]), int(vals["DROP_MSG"]), float(vals["MSG_DROP_PROB"]))
+
+
+def same_state(sim, ora):
+    """HIP context vs oracle by binary readbacks: every table cell (hb, ts) and every node's
+    state -- the content of the text dump, without rendering it (parity tests at larger N)."""
+    import numpy as np
+    hb, ts = sim.read_table()
+    ohb, ots = ora.table()
+    return np.array_equal(hb, ohb) and np.array_equal(ts, ots) and np.array_equal(sim.read_nodes(), ora.nodes())

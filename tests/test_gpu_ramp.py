@@ -8,11 +8,10 @@ init_mode 2), tick by tick: every table, node state (inited / inGroup / failed /
 heartbeat) and the join/remove event set -- through the ramp, a crash set that hits
 nodes before they start (nodeStart revives them, MP1Node.cpp:108), and the introducer
 crashing mid-ramp (later starters never join)."""
-import numpy as np
 import pytest
 
 import oracle_py
-from golden_util import digest64
+from golden_util import digest64, same_state
 from membership import GM_MODE_SCALED, Simulator, crash_set
 
 pytestmark = pytest.mark.gpu
@@ -24,13 +23,6 @@ def seed_with(n, count, want):
         if want in set(crash_set(n, count, seed).tolist()):
             return seed
     raise AssertionError("no seed")
-
-
-def same_state(sim, ora):
-    """binary readbacks: every table cell (hb, ts) and node state (the dump's content)"""
-    hb, ts = sim.read_table()
-    ohb, ots = ora.table()
-    return np.array_equal(hb, ohb) and np.array_equal(ts, ots) and np.array_equal(sim.read_nodes(), ora.nodes())
 
 
 def run_ramp(n, ticks, crash_tick=-1, crash_count=0, crash_seed=42, band=0, drop_pct=0, every=1, ora_out=None):
@@ -62,7 +54,7 @@ def run_ramp(n, ticks, crash_tick=-1, crash_count=0, crash_seed=42, band=0, drop
     return joins, removes
 
 
-@pytest.mark.parametrize("n,band", [(64, 64), (300, 128), pytest.param(1100, 0, marks=pytest.mark.slow)])
+@pytest.mark.parametrize("n,band", [(64, 64), (300, 128), (1100, 0)])
 def test_ramp_matches_oracle(n, band):
     joins, _ = run_ramp(n, n // 4 + 30, band=band)
     assert joins >= n * (n - 1)  # everyone learned everyone (plus re-joins)
