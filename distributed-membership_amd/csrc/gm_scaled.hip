@@ -324,6 +324,46 @@ __device__ __forceinline__ uint32_t nib_value(uint32_t nb, const SState &s, int 
   return nb == S_NIB_ESC ? pesc_value(s, pp, band, sn, li, q) : nb ? S_NIB_H(nb) : 0u;
 }
 
+// Keyed loss of the SCALED regime (build-defined; the reference drops whole messages with
+// rand() % 100 < MSG_DROP_PROB * 100, EmulNet.cpp:90-94): the entry of global column c in the list
+// src sent to dst at tick t_send is lost iff 16-bit chunk (c & 3) of mix64(pair + (c >> 2)) is
+// below T = ceil(pct * 65536 / 100) (s_drop_thresh), pair = mix64(seed ^ t_send << 48 ^ src << 24 ^ dst):
+// one hash per 4 columns (oracle/ref_cpu.c scaled_recv states the same function)
+__device__ __forceinline__ uint64_t s_drop_pair(const SState &s, int t, int sn, int r) {
+  return gm_mix64(s.drop_seed ^ ((uint64_t)(uint32_t)(t - 1) << 48) ^ ((uint64_t)(uint32_t)sn << 24) ^ (uint64_t)(uint32_t)r);
+}
+__device__ __forceinline__ bool s_keep(const SState &s, int t, int sn, int r, int c, uint32_t T) {
+  const uint64_t h = gm_mix64(s_drop_pair(s, t, sn, r) + (uint64_t)(uint32_t)(c >> 2));
+  return ((uint32_t)(h >> (16 * (c & 3))) & 0xFFFFu) >= T;
+}
+// payload nibble position of lane cell q (0..15) in its 8-byte slice (nib_max's order)
+__device__ __forceinline__ constexpr int nib_pos(int q) { return 32 * (q >> 3) + 16 * (q & 1) + 4 * (3 - ((q & 7) >> 1)); }
+// 0xF at the nibbles of the lane's kept cells in list sn -> row r (64 bits = the slice); agrp: the
+// lane's 16 columns are 4 whole hash groups (else one hash per cell, shards at odd offsets)
+__device__ __forceinline__ uint64_t s_keep_nibbles(const SState &s, int t, int sn, int r, int colb, uint32_t T,
+                                                   bool agrp) {
+  const uint64_t pair = s_drop_pair(s, t, sn, r);
+  const int c = s.c0 + colb;
+  uint64_t km = 0;
+  if (agrp) {
+#pragma unroll
+    for (int g = 0; g < 4; g++) {
+      const uint64_t h = gm_mix64(pair + (uint64_t)(uint32_t)((c >> 2) + g));
+#pragma unroll
+      for (int e = 0; e < 4; e++)
+        if (((uint32_t)(h >> (16 * e)) & 0xFFFFu) >= T) km |= 0xFull << nib_pos(4 * g + e);
+    }
+  } else {
+    for (int q = 0; q < 16; q++) {
+      const uint64_t h = gm_mix64(pair + (uint64_t)(uint32_t)((c + q) >> 2));
+      if (((uint32_t)(h >> (16 * ((c + q) & 3))) & 0xFFFFu) >= T) km |= 0xFull << nib_pos(q);
+    }
+  }
+  return km;
+}
+// bit 4i set where nibble i of x is non-zero
+__device__ __forceinline__ uint32_t nz_nibble_bits(uint32_t x) { return (x | (x >> 1) | (x >> 2) | (x >> 3)) & 0x11111111u; }
+
 // One work unit of the band sweep: unit u = (band u / U, rows [(u % U) * RPW, +RPW)).
 // unit_load issues the row metadata and the table slice; unit_gather the payload slices
 // (needs the sender ids); unit_finish merges, sweeps, stores and records the counts.
@@ -369,7 +409,7 @@ __device__ __forceinline__ void unit_gather(const SState &s, int t, const UnitIn
   const int k = min(in.k, S_KMAX);
 #pragma unroll
   for (int j = 0; j < S_SB; j++)
-    m[j] = __builtin_amdgcn_raw_buffer_load_b64(prs, (!DROP && j < k) ? poff + (uint32_t)in.snd[j] * B : GM_OOB, 0, 0);
+    m[j] = __builtin_amdgcn_raw_buffer_load_b64(prs, j < k ? poff + (uint32_t)in.snd[j] * B : GM_OOB, 0, 0);
 }
 
 template <int B, bool DROP>
@@ -430,16 +470,31 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
     // key5 = h' << 5 (the cell with age 0) in the u16 halves of each table word
     const int32_t *ib = s.inbox[par] + (size_t)r * S_KMAX;
     u16x2 key5[8];
-    if (!DROP) {
+    {
+      // DROP (keyed loss on this tick's deliveries): a list's lost entries are cleared from its
+      // nibbles before the max, per (list, lane) from 4 hashes of the pair key (s_keep_bits)
+      const uint32_t T = DROP ? s_drop_thresh(drop_pct) : 0u;
+      const bool agrp = ((s.c0 + colb) & 3) == 0;  // shard-uniform: the lane's cells in 4 whole hash groups
       u16x2 acc[8];
 #pragma unroll
       for (int i = 0; i < 8; i++) acc[i] = (u16x2)(0);
+      auto merge_list = [&](int sn, uint32_t x0, uint32_t x1) {
+        if (DROP) {
+          if (!(x0 | x1)) return;
+          const uint64_t km = s_keep_nibbles(s, t, sn, r, colb, T, agrp);
+          x0 &= (uint32_t)km;
+          x1 &= (uint32_t)(km >> 32);
+          if (s.mc_rdrop) nkept += __builtin_popcount(nz_nibble_bits(x0)) + __builtin_popcount(nz_nibble_bits(x1));
+        }
+        nib_max(acc, x0, x1);
+      };
 #pragma unroll
       for (int j = 0; j < S_SB; j++)
-        if (j < kw) nib_max(acc, m[j].x, m[j].y);
+        if (j < kw) merge_list(meta.snd[j], m[j].x, m[j].y);  // slots j >= k loaded zeros
       for (int j = S_SB; j < k; j++) {  // rare: more lists than prefetched ids
-        const u32x2 mm = __builtin_amdgcn_raw_buffer_load_b64(prs, poff + (uint32_t)ib[j] * B, 0, 0);
-        nib_max(acc, mm.x, mm.y);
+        const int sn = ib[j];
+        const u32x2 mv = __builtin_amdgcn_raw_buffer_load_b64(prs, poff + (uint32_t)sn * B, 0, 0);
+        merge_list(sn, mv.x, mv.y);
       }
       u16x2 nmax = (u16x2)(0);
 #pragma unroll
@@ -451,7 +506,7 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
       }
       if (__builtin_elementwise_max(nmax.x, nmax.y) == S_NIB_ESC) {
         // rare (cold start, JOINREQ entries, lag > 13 ticks): some list escaped a cell of
-        // this lane; the exact key of those cells = max over the lists' decoded values
+        // this lane; the exact key of those cells = max over the (kept) lists' decoded values
 #pragma unroll
         for (int i = 0; i < 8; i++) {
           const u16x2 nb = acc[i] >> (u16x2)(12);
@@ -462,6 +517,7 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
             uint32_t kv = 0;
             for (int j = 0; j < k; j++) {  // reloads (no dynamic register indexing: no scratch)
               const int sn = ib[j];
+              if (DROP && !s_keep(s, t, sn, r, s.c0 + colb + q, T)) continue;
               const u32x2 mm = __builtin_amdgcn_raw_buffer_load_b64(prs, poff + (uint32_t)sn * B, 0, 0);
               kv = max(kv, nib_value(nib_of(mm.x, mm.y, q), s, par ^ 1, band, sn, li, q));
             }
@@ -469,29 +525,6 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
           }
         }
       }
-    } else {
-      // per-entry drops keyed by (t_send, src, dst, global column) -- SCALED regime
-      uint32_t kk[Q];
-#pragma unroll
-      for (int q = 0; q < Q; q++) kk[q] = 0;
-      for (int j = 0; j < k; j++) {
-        const int sn = ib[j];
-        const u32x2 mv = __builtin_amdgcn_raw_buffer_load_b64(prs, poff + (uint32_t)sn * B, 0, 0);
-        if (!(mv.x | mv.y)) continue;
-        const uint64_t pair = gm_mix64(s.drop_seed ^ ((uint64_t)(uint32_t)(t - 1) << 48) ^
-                                       ((uint64_t)(uint32_t)sn << 24) ^ (uint64_t)(uint32_t)r);
-#pragma unroll
-        for (int q = 0; q < Q; q++) {
-          const uint32_t nb = nib_of(mv.x, mv.y, q);
-          if (!nb) continue;
-          const uint32_t h = (uint32_t)(gm_mix64(pair + (uint64_t)(s.c0 + colb + q)) >> 32);
-          if ((int)(h % 100u) < drop_pct) continue;
-          nkept++;
-          kk[q] = max(kk[q], nib_value(nb, s, par ^ 1, band, sn, li, q));
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < 8; i++) key5[i] = pk((kk[2 * i] << 5) | (kk[2 * i + 1] << 21));
     }
     if (s.ramp && r == 0) {  // the introducer takes the JOINREQs of the nodes that started at t-1:
       // entry {hb 0, ts t} = stored heartbeat 2t (offset 2(t-1+1)) = h 255 (MP1Node.cpp:226-251)

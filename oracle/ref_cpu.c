@@ -464,6 +464,12 @@ static void node_start(oc_ctx *c, int idx) {
   }
 }
 
+/* SCALED keyed loss threshold: an entry is lost iff its 16-bit chunk < ceil(pct * 65536 / 100)
+ * (gm_scaled.h s_drop_thresh) */
+static uint32_t scaled_drop_thresh(int pct) {
+  return pct <= 0 ? 0u : pct >= 100 ? 65536u : (uint32_t)((pct * 65536 + 99) / 100);
+}
+
 /* SCALED recv: every gossip list sent to this node at t-1, senders ascending,
  * entries ascending id, per-entry keyed drops. */
 static void scaled_recv(oc_ctx *c, int idx) {
@@ -475,9 +481,10 @@ static void scaled_recv(oc_ctx *c, int idx) {
       int dropping = c->cfg.drop_pct > 0 && t_send >= c->cfg.drop_from && t_send < c->cfg.drop_to;
       uint64_t pair = mix64(c->cfg.drop_seed ^ ((uint64_t)(uint32_t)t_send << 48) ^ ((uint64_t)s << 24) ^ (uint64_t)idx);
       for (int e = 0; e < p->n; e++) {
-        if (dropping) {
-          uint32_t h = (uint32_t)(mix64(pair + (uint64_t)(p->ids[e] - 1)) >> 32);
-          if ((int)(h % 100u) < c->cfg.drop_pct) continue;
+        if (dropping) { /* build-defined keyed loss: 16-bit chunk (col & 3) of one hash per 4 columns */
+          uint32_t col = (uint32_t)(p->ids[e] - 1);
+          uint32_t v = (uint32_t)(mix64(pair + (col >> 2)) >> (16 * (col & 3))) & 0xFFFFu;
+          if (v < scaled_drop_thresh(c->cfg.drop_pct)) continue;
         }
         if (c->mc_recv) c->mc_recv[idx]++;
         update_list(c, idx, p->ids[e], 0, p->hbs[e]);

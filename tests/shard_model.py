@@ -88,7 +88,8 @@ class ShardModel:
         if pct <= 0 or not (lo <= t_send < hi):
             return False
         pair = mix64(seed ^ (t_send << 48) ^ (s << 24) ^ r)
-        return ((mix64(pair + col) >> 32) % 100) < pct
+        thresh = 65536 if pct >= 100 else (pct * 65536 + 99) // 100  # gm_scaled.h s_drop_thresh
+        return ((mix64(pair + (col >> 2)) >> (16 * (col & 3))) & 0xFFFF) < thresh
 
     def tick(self, all_gather, all_reduce_max):
         n, t, w, c0 = self.n, self.t, self.w, self.c0
