@@ -41,6 +41,20 @@ __device__ __forceinline__ uint64_t gm_mix64(uint64_t z) {
   return z ^ (z >> 31);
 }
 
+// murmur3 finalizer: a bijection of uint32 (distinct inputs -> distinct outputs), 2 multiplies
+__host__ __device__ __forceinline__ uint32_t gm_fmix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  return h ^ (h >> 16);
+}
+// keyed-loss threshold on a 16-bit uniform chunk: lost iff chunk < ceil(pct * 65536 / 100)
+// (probability pct % to within 1.5e-5; SCALED and PARTIAL, oracle/ref_cpu.c the same)
+__host__ __device__ inline uint32_t gm_drop_thresh(int pct) {
+  return pct <= 0 ? 0u : pct >= 100 ? 65536u : (uint32_t)((pct * 65536 + 99) / 100);
+}
+
 // random_device replacement of the seed contract
 __device__ __forceinline__ uint32_t gm_rd_seed(uint64_t rd_seed, int32_t tick, int32_t id) {
   uint64_t z = rd_seed ^ (((uint64_t)(uint32_t)tick << 32) | (uint32_t)id);

@@ -58,6 +58,5 @@ struct PState {
   // entries sent (fresh entries x targets, before loss) / received (after loss, lists merged)
   uint32_t *mc_sent, *mc_recv;  // [mc_tmax][nloc]
   int mc_tmax;
-  int halfwave;                 // small nodes two per wave (gm_p_tick_half; GM_P_FULLWAVE=1: one per wave)
   int kcap;                     // inbox slots used (P_KMAX; lowered only by the diagnostics env GM_INBOX_CAP)
 };

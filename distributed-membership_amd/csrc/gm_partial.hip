@@ -74,11 +74,10 @@ __device__ __forceinline__ int p_age(int t, uint32_t hb) { return t - (int)((hb 
 // p_age(t, hb) >= A as one compare: t - floor((hb+1)/2) >= A <=> hb < 2(t-A)+1 (heartbeats < 2^31)
 __device__ __forceinline__ bool p_aged(int t, uint32_t hb, int A) { return (int)hb < 2 * (t - A) + 1; }
 
-// eviction tie-break key (oracle op_evict_key): distinct ids give distinct keys;
-// kseed = mix64(view_seed ^ t) is wave-uniform
-__device__ __forceinline__ uint64_t p_evict_key(uint64_t kseed, int obs, uint32_t id) {
-  return gm_mix64(kseed ^ (((uint64_t)(uint32_t)obs << 32) | id));
-}
+// eviction tie-break key (oracle op_evict_key): fmix32 of the id under a per-(tick, observer)
+// seed -- a bijection, so distinct ids give distinct keys; oseed = (uint32)mix64(mix64(view_seed
+// ^ t) ^ obs) is wave-uniform
+__device__ __forceinline__ uint32_t p_evict_key(uint32_t oseed, uint32_t id) { return gm_fmix32(id ^ oseed); }
 
 // wave-wide inclusive scan of ints on DPP: row_shr 1/2/4/8 scans each 16-lane row,
 // row_bcast15 / row_bcast31 carry the row totals upward (lanes a DPP source does not
@@ -239,10 +238,11 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
   const bool dropping = s.drop_pct >= 0;
   const bool mc = MC && t < s.mc_tmax;  // msgcount recording (wave-uniform)
   int nrecv = 0;                                           // delivered entries kept (msgcount)
-  uint64_t pairv = 0;
+  uint32_t pairv = 0;  // low word of mix64(seed ^ t_send << 48 ^ src << 24 ^ dst)
   if (dropping)
-    pairv = gm_mix64(s.drop_seed ^ ((uint64_t)(uint32_t)(t - 1) << 48) ^ ((uint64_t)(uint32_t)sg << 24) ^
-                     (uint64_t)(uint32_t)i);
+    pairv = (uint32_t)gm_mix64(s.drop_seed ^ ((uint64_t)(uint32_t)(t - 1) << 48) ^ ((uint64_t)(uint32_t)sg << 24) ^
+                               (uint64_t)(uint32_t)i);
+  const uint32_t dthr = gm_drop_thresh(s.drop_pct);
   PPROF(0);
   p_wsync();
   // ---- 2. merge: own entries first (they carry P_OWN), then the delivered lists
@@ -261,12 +261,10 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
       const uint64_t e = dv[st];
       bool take = e != 0 && (uint32_t)e >= tfresh;
       const uint32_t id = (uint32_t)(e >> 32);
-      if (dropping && __ballot(take)) {  // per-entry drops keyed by (t_send, src, dst, id-1)
-        const int j = min(st * per + jo, 63);
-        const uint32_t plo = __shfl((uint32_t)pairv, j, 64), phi = __shfl((uint32_t)(pairv >> 32), j, 64);
-        const uint64_t pair = ((uint64_t)phi << 32) | plo;
-        const uint32_t h = (uint32_t)(gm_mix64(pair + (uint64_t)(id - 1)) >> 32);
-        take = take && (int)(h % 100u) >= s.drop_pct;
+      if (dropping && __ballot(take)) {  // per-entry drops keyed by (t_send, src, dst, id-1): lost iff the
+        const int j = min(st * per + jo, 63);  // top 16 bits of fmix32(pair ^ (id-1)) are below the threshold
+        const uint32_t pair = __shfl(pairv, j, 64);
+        take = take && (gm_fmix32(pair ^ (id - 1)) >> 16) >= dthr;
       }
       if (take) (void)p_insert<H>(tid, thb, id, id, (uint32_t)e);
       if (mc) nrecv += __builtin_popcountll(__ballot(take));
@@ -402,19 +400,19 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
     } else {
       // the needb smallest eviction keys of the bucket: 6-bit radix on the top bits,
       // then exact min-selection inside the cut bin
-      const uint64_t kseed = gm_mix64(s.view_seed ^ (uint64_t)(uint32_t)t);
-      uint64_t key[DS];
+      const uint32_t oseed = (uint32_t)gm_mix64(gm_mix64(s.view_seed ^ (uint64_t)(uint32_t)t) ^ (uint64_t)(uint32_t)i);
+      uint32_t key[DS];
 #pragma unroll
       for (int q = 0; q < DS; q++) {
-        key[q] = ~0ull;
-        if (q < dm && __ballot((bucket >> q) & 1)) key[q] = ((bucket >> q) & 1) ? p_evict_key(kseed, i, dw[q] & P_IDMASK) : ~0ull;
+        key[q] = ~0u;
+        if (q < dm && __ballot((bucket >> q) & 1)) key[q] = ((bucket >> q) & 1) ? p_evict_key(oseed, dw[q] & P_IDMASK) : ~0u;
       }
       p_wsync();
       hist[lane] = 0;
       p_wsync();
 #pragma unroll
       for (int q = 0; q < DS; q++)
-        if (q < dm) atomicAdd(((bucket >> q) & 1) ? &hist[key[q] >> 58] : &tid[H - 64 + lane], 1u);
+        if (q < dm) atomicAdd(((bucket >> q) & 1) ? &hist[key[q] >> 26] : &tid[H - 64 + lane], 1u);
       p_wsync();
       c = (int)hist[lane];
       inc = p_scan(c, lane);
@@ -428,7 +426,7 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
       for (int q = 0; q < DS; q++) {
         if (q >= dm) continue;
         const uint32_t b = (bucket >> q) & 1;
-        const int bin = (int)(key[q] >> 58);
+        const int bin = (int)(key[q] >> 26);
         keep |= (b & (uint32_t)(bin < bcut)) << q;
         cand |= (b & (uint32_t)(bin == bcut)) << q;
       }
@@ -439,15 +437,12 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
         pp_[12] += needc;  // min-selection rounds
 #endif
         for (; needc > 0; needc--) {  // take the smallest remaining candidate key (keys are distinct)
-          uint64_t mn = ~0ull;
+          uint32_t mn = ~0u;
 #pragma unroll
           for (int q = 0; q < DS; q++)
             if (q < dm && ((cand >> q) & 1)) mn = min(mn, key[q]);
 #pragma unroll
-          for (int o = 32; o >= 1; o >>= 1) {
-            const uint32_t lo = __shfl_xor((uint32_t)mn, o, 64), hi = __shfl_xor((uint32_t)(mn >> 32), o, 64);
-            mn = min(mn, ((uint64_t)hi << 32) | lo);
-          }
+          for (int o = 32; o >= 1; o >>= 1) mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, 64));
 #pragma unroll
           for (int q = 0; q < DS; q++)
             if (q < dm && ((cand >> q) & 1) && key[q] == mn) {
@@ -690,557 +685,6 @@ __global__ __launch_bounds__(256) void gm_p_tick_small(PState s, int t, const ui
   p_node<P_HS, false, MC>(s, t, pre, li, lane, p_smem + (size_t)wave * PLds<P_HS>::bytes, chunk, r0);
 }
 
-// ------------------------------------------------------------------ half-wave node tick
-// Two nodes per wave, one per 32-lane half (the lists are <= P_VMAX = 32 entries: one entry per
-// lane of a half), for nodes with <= P_KSMALL delivered lists. The table is a 512-slot LDS hash of
-// 4-BYTE words, id << 6 | dist (dist = 2t-1 - hb, the heartbeat's distance below this tick's self
-// heartbeat: <= 40 for every entry alive after the sweep, <= 10 for a delivered fresh one), so the
-// updatelistCallBack merge (largest hb) is one atomicMin per id; "own" (the id was in the node's
-// list: no join record, removal records) is a 512-bit slot bitmap. Per wave 2 x 2 KB of table +
-// 2 x 192 B: 8 waves per SIMD = 16 nodes in flight, and every per-node step that used a whole
-// wave for <= 32 entries (own list, final list, histograms, draw) now serves two nodes.
-// Every half runs the same instruction stream; a half with no live node (crashed, deferred to the
-// big kernel, past the chunk) runs on empty inputs with its side effects masked (`act`).
-#define P_H2 512                  // table slots per node
-#define P_H2_LOG 9
-#define P_H2_MISC 48              // words per node: own bitmap (16) + histogram / targets (32)
-#define P_HALF_WAVE_BYTES (2 * P_H2 * 4 + 2 * P_H2_MISC * 4)
-#define P_DS2 (((1 + P_KSMALL) * P_VMAX + 31) / 32)  // dense entries per lane
-
-__device__ __forceinline__ uint32_t p_w_id(uint32_t w) { return (w >> 6) & P_IDMASK; }
-__device__ __forceinline__ uint32_t p_w_dist(uint32_t w) { return w & 63u; }
-// claim-or-compare the slot of `id`, keep the smaller word (= the larger heartbeat) of that id
-__device__ __forceinline__ int p_insert4(uint32_t *tab, uint32_t id, uint32_t w) {
-  uint32_t h = (id * 0x9E3779B1u) >> (32 - P_H2_LOG);
-  for (;;) {
-    const uint32_t cur = atomicCAS(&tab[h], 0u, w);
-    if (cur == 0) break;
-    if (p_w_id(cur) == id) {
-      if (w < cur) atomicMin(&tab[h], w);
-      break;
-    }
-    h = (h + 1) & (P_H2 - 1);
-  }
-  return (int)h;
-}
-// this half's 32 bits of a wave ballot
-__device__ __forceinline__ uint32_t h_bits(uint64_t bal, int hh) { return hh ? (uint32_t)(bal >> 32) : (uint32_t)bal; }
-__device__ __forceinline__ uint32_t h_ballot(bool p, int hh) { return h_bits(__ballot(p), hh); }
-__device__ __forceinline__ int h_below(uint32_t bits, int hl) { return __builtin_popcount(bits & ((1u << hl) - 1u)); }
-// value of lane l (uniform) of this lane's half
-__device__ __forceinline__ int h_at(int v, int l, int hh) {
-  const int a = __builtin_amdgcn_readlane(v, l), b = __builtin_amdgcn_readlane(v, 32 + l);
-  return hh ? b : a;
-}
-// inclusive scan within each half on DPP (row_shr 1/2/4/8, then row 0 -> 1 and row 2 -> 3 only)
-__device__ __forceinline__ int h_scan(int v) {
-  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);
-  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);
-  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);
-  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);
-  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
-  return v;
-}
-__device__ __forceinline__ uint64_t h_shfl64(uint64_t v, int src) {
-  const uint32_t lo = __shfl((uint32_t)v, src, 64), hi = __shfl((uint32_t)(v >> 32), src, 64);
-  return ((uint64_t)hi << 32) | lo;
-}
-
-template <bool MC>
-__device__ __forceinline__ void p_node_half(const PState &s, int t, const uint32_t *mtraw, int li, bool inr, int lane,
-                                            uint32_t *wbase, int chunk, int r0) {
-  const int hh = lane >> 5, hl = lane & 31;
-  const int V = s.V, par = t & 1;
-  const int lic = inr ? li : r0;  // loads stay in bounds for a half past the chunk
-  // ---- 1. loads, all issued before any branch on them
-  const int failed = s.failed[lic];
-  const int kq = s.inbox_cnt[par][lic];
-  const int hbctr = s.hbctr[lic];
-  const uint64_t own0 = hl < V ? s.lists[((size_t)(par ^ 1) * s.rows + lic) * V + hl] : 0ull;
-  const int sv0 = hl < P_KSMALL ? s.inbox[par][(size_t)lic * P_KMAX + hl] : 0;
-  const uint32_t raw0 = hl < 16 ? mtraw[(size_t)lic * 16 + hl] : 0u;
-  const bool act = inr && !failed && kq <= P_KSMALL;
-  uint32_t *tab = wbase + hh * P_H2;
-  uint32_t *misc = wbase + 2 * P_H2 + hh * P_H2_MISC;
-  uint32_t *bm = misc;        // own-slot bitmap, 16 words
-  uint32_t *hist = misc + 16; // 32 words: histograms, then the chosen targets
-  if (inr && failed) {  // crashed: frozen (its list carried to this tick's buffer), inbox dropped
-    if (hl < V) s.lists[((size_t)par * s.rows + li) * V + hl] = own0;
-    if (hl < 4) s.rowstat[(size_t)li * 4 + hl] = 0;
-    if (hl == 0) {
-      s.inbox_cnt[par][li] = 0;
-      s.ev_cnt[li] = 0;
-      if (s.G > 1) s.recmask[li] = 0;
-    }
-  } else if (inr && kq > P_KSMALL && hl == 0) {  // deferred to gm_p_tick_big
-    s.big[r0 + atomicAdd(&s.big_cnt[chunk], 1)] = li;
-  }
-  if (!__ballot(act)) return;  // wave-uniform
-  const int i = s.n0 + li;     // global node index (ids, keys, seeds, targets)
-  const int k = act ? kq : 0;
-  const uint64_t own = act ? own0 : 0ull;
-  const int sv = hl < k ? sv0 : 0;
-  if (act && hl == 0) s.inbox_cnt[par][li] = 0;  // consumed; the append target of tick t+1
-  const uint64_t *prev = s.lists + (size_t)(par ^ 1) * s.rows * V;
-  uint64_t *cur = s.lists + (size_t)par * s.rows * V;
-  // delivered lists: entry hl of list j on lane hl of the half
-  uint64_t dv[P_KSMALL];
-#pragma unroll
-  for (int j = 0; j < P_KSMALL; j++) {
-    const int sn = h_at(sv, j, hh);
-    uint64_t e = 0;
-    if (j < k && hl < V) {
-      if (sn < s.nloc) {
-        e = prev[(size_t)sn * V + hl];
-      } else {  // a list another shard sent at t-1: wire entry id | (2(t-1)-1 - hb) << 25
-        const uint32_t w = s.recv_list[par ^ 1][(size_t)(sn - s.nloc) * V + hl];
-        if (w) e = ((uint64_t)(w & ((1u << P_WIRE_IDBITS) - 1)) << 32) | (uint32_t)(2 * t - 3 - (int)(w >> P_WIRE_IDBITS));
-      }
-    }
-    dv[j] = e;
-  }
-  // global sender index of list hl (drop keys), one (t_send, src, dst) hash per list
-  const bool dropping = s.drop_pct >= 0;
-  uint64_t pairv = 0;
-  if (dropping && hl < k) {
-    const int sg = sv < s.nloc ? s.n0 + sv : s.rsrc[par ^ 1][sv - s.nloc];
-    pairv = gm_mix64(s.drop_seed ^ ((uint64_t)(uint32_t)(t - 1) << 48) ^ ((uint64_t)(uint32_t)sg << 24) ^
-                     (uint64_t)(uint32_t)i);
-  }
-  // clear this node's table and own bitmap
-  {
-    uint4 *z = (uint4 *)tab;
-#pragma unroll
-    for (int q = 0; q < P_H2 / 128; q++) z[hl + 32 * q] = make_uint4(0, 0, 0, 0);
-    if (hl < 16) bm[hl] = 0;
-  }
-  p_wsync();
-  // ---- 2. merge (order-free: min word per id; own-ness by slot)
-  const int top = 2 * t - 1;  // this tick's self heartbeat
-  const uint32_t self_id = (uint32_t)(i + 1);
-  int hslot = -1;
-  bool bad = false;  // an entry the 6-bit distance cannot hold (never in a PARTIAL run: loud)
-  if (own != 0) {
-    const uint32_t id = (uint32_t)(own >> 32);
-    const int dist = top - (int)(uint32_t)own;
-    bad |= dist < 0 || dist > 63;
-    hslot = p_insert4(tab, id, (id << 6) | (uint32_t)(dist & 63));
-    atomicOr(&bm[hslot >> 5], 1u << (hslot & 31));
-  }
-  const bool mc = MC && t < s.mc_tmax;
-  int nrecv = 0;
-  {
-    const uint32_t tfresh = (uint32_t)max(0, 2 * t - 11);  // hb >= 2t-11 <=> (t-1) - (hb+1)/2 < TFAIL
-#pragma unroll
-    for (int j = 0; j < P_KSMALL; j++) {
-      const uint64_t e = dv[j];
-      bool take = e != 0 && (uint32_t)e >= tfresh;
-      const uint32_t id = (uint32_t)(e >> 32);
-      if (dropping && __ballot(take)) {  // per-entry drops keyed by (t_send, src, dst, id-1)
-        const uint64_t pair = h_shfl64(pairv, 32 * hh + j);
-        const uint32_t h = (uint32_t)(gm_mix64(pair + (uint64_t)(id - 1)) >> 32);
-        take = take && (int)(h % 100u) >= s.drop_pct;
-      }
-      if (take) {
-        const int dist = top - (int)(uint32_t)e;
-        bad |= dist < 0 || dist > 63;
-        (void)p_insert4(tab, id, (id << 6) | (uint32_t)(dist & 63));
-      }
-      if (mc) nrecv += __builtin_popcount(h_ballot(take, hh));
-    }
-  }
-  p_wsync();
-  // ---- 3. self bump (heartbeat++; myPos->setheartbeat(heartbeat++))
-  const int hbnew = hbctr + 1;
-  {
-    const uint32_t sb = h_ballot(own != 0 && (uint32_t)(own >> 32) == self_id, hh);
-    int hs = __shfl(hslot, 32 * hh + (sb ? __builtin_ctz(sb) : 0), 64);
-    if (act && !sb) {  // cannot happen for a live node (the oracle aborts): flag, and re-insert self
-      if (hl == 0) {
-        atomicOr(s.err, GM_ERR_SELF);
-        hs = p_insert4(tab, self_id, self_id << 6);
-        atomicOr(&bm[hs >> 5], 1u << (hs & 31));
-      }
-      hs = __shfl(hs, 32 * hh, 64);
-    }
-    if (act && hl == 0) {
-      const int dist = top - hbnew;
-      bad |= dist < 0 || dist > 63;
-      tab[hs] = (self_id << 6) | (uint32_t)(dist & 63);
-      s.hbctr[li] = hbnew + 1;
-    }
-  }
-  p_wsync();
-  // ---- 4. sweep: TREMOVE removals (dist >= 2 TREMOVE - 1), compaction into a dense array
-  uint32_t *evr = s.ev + (size_t)(act ? li : 0) * 2 * V;
-  int m, removed, nrem;
-  {
-    uint32_t w[16];
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-      const uint4 a = ((const uint4 *)tab)[hl * 4 + q];
-      w[4 * q] = a.x; w[4 * q + 1] = a.y; w[4 * q + 2] = a.z; w[4 * q + 3] = a.w;
-    }
-    const uint32_t ob = (bm[hl >> 1] >> (16 * (hl & 1))) & 0xFFFFu;  // own bits of slots 16 hl ..
-    uint32_t alive = 0, rown = 0;
-    int rcount = 0;
-#pragma unroll
-    for (int u = 0; u < 16; u++) {
-      const uint32_t valid = w[u] != 0;
-      const uint32_t rem = valid & (uint32_t)(p_w_dist(w[u]) >= 2 * GM_TREMOVE - 1);
-      rcount += (int)rem;
-      rown |= (rem & (ob >> u)) << u;
-      alive |= (valid & ~rem) << u;
-      w[u] |= ((ob >> u) & 1u) << 31;  // the dense word carries the own bit
-    }
-    removed = nrem = 0;
-    if (__ballot(rcount != 0)) {  // rare: TREMOVE removals
-      const int ri = h_scan(rcount);
-      removed = h_at(ri, 31, hh);
-      const int ro = __builtin_popcount(rown);
-      const int oi = h_scan(ro);
-      nrem = h_at(oi, 31, hh);
-      int rpos = oi - ro;
-      if (act && rown) {  // REMOVE events of the node's own entries, from the back of its event row
-#pragma unroll
-        for (int u = 0; u < 16; u++)
-          if ((rown >> u) & 1) evr[2 * V - 1 - rpos++] = (P_EV_REMOVE << 30) | p_w_id(w[u]);
-      }
-    }
-    const int na = __builtin_popcount(alive);
-    const int ai = h_scan(na);
-    m = h_at(ai, 31, hh);
-    int pos = ai - na;
-    p_wsync();  // every slot is read: compact in place
-#pragma unroll
-    for (int u = 0; u < 16; u++)
-      if ((alive >> u) & 1) tab[pos++] = w[u];
-  }
-  p_wsync();
-  // ---- 5. dense entries e = q*32 + hl; eviction to V (self first, hb desc, key asc)
-  const int dm = (m + 31) >> 5;
-  const int dmw = max(__builtin_amdgcn_readlane(dm, 0), __builtin_amdgcn_readlane(dm, 32));
-  uint32_t dw[P_DS2];
-#pragma unroll
-  for (int q = 0; q < P_DS2; q++) {
-    dw[q] = 0u;
-    if (q < dmw) {
-      const int e = q * 32 + hl;
-      const uint32_t a = tab[min(e, P_H2 - 1)];
-      dw[q] = e < m ? a : 0u;
-    }
-  }
-  uint32_t keep = 0;
-#pragma unroll
-  for (int q = 0; q < P_DS2; q++)
-    if (q < dmw && dw[q]) keep |= 1u << q;
-  const bool evict = m > V;
-  if (__ballot(evict)) {
-    uint32_t ekeep = 0;
-    // distance histogram (dist is even: odd heartbeats only), self excluded
-    hist[hl] = 0;
-    p_wsync();
-#pragma unroll
-    for (int q = 0; q < P_DS2; q++)
-      if (q < dmw && evict && dw[q] && p_w_id(dw[q]) != self_id) {
-        bad |= (dw[q] & 1u) != 0;
-        atomicAdd(&hist[p_w_dist(dw[q]) >> 1], 1u);
-      }
-    p_wsync();
-    const int need = V - 1;  // self is always kept
-    int c = (int)hist[hl];
-    int inc = h_scan(c);
-    const uint32_t over = h_ballot(inc >= need, hh);
-    const int dcut = over ? __builtin_ctz(over) : 31;
-    const int before = __shfl(inc - c, 32 * hh + dcut, 64);
-    const int bsz = __shfl(c, 32 * hh + dcut, 64);
-    const int needb = need - before;  // 1 <= needb <= bsz
-    uint32_t bucket = 0;
-#pragma unroll
-    for (int q = 0; q < P_DS2; q++) {
-      if (q >= dmw) continue;
-      const uint32_t v = dw[q] != 0;
-      const bool self = p_w_id(dw[q]) == self_id;
-      const int d2 = (int)(p_w_dist(dw[q]) >> 1);
-      ekeep |= (v & (uint32_t)(self || d2 < dcut)) << q;
-      bucket |= (v & (uint32_t)(!self && d2 == dcut)) << q;
-    }
-    const bool kp = evict && needb != bsz;
-    if (!kp) ekeep |= bucket;
-    if (__ballot(kp)) {
-      // the needb smallest eviction keys of the cut bucket: 5-bit radix on the top key bits,
-      // then exact min-selection inside the cut bin
-      const uint64_t kseed = gm_mix64(s.view_seed ^ (uint64_t)(uint32_t)t);
-      uint64_t bins = 0;  // 5-bit top key bits of the bucket entries, slot q at bits 5q (keys are recomputed
-                          // for the rare exact selection instead of held in 2 x P_DS2 registers)
-#pragma unroll
-      for (int q = 0; q < P_DS2; q++)
-        if (q < dmw && __ballot(kp && ((bucket >> q) & 1)) && kp && ((bucket >> q) & 1))
-          bins |= (p_evict_key(kseed, i, p_w_id(dw[q])) >> 59) << (5 * q);
-      p_wsync();
-      hist[hl] = 0;
-      p_wsync();
-#pragma unroll
-      for (int q = 0; q < P_DS2; q++)
-        if (q < dmw && kp && ((bucket >> q) & 1)) atomicAdd(&hist[(bins >> (5 * q)) & 31u], 1u);
-      p_wsync();
-      c = (int)hist[hl];
-      inc = h_scan(c);
-      const uint32_t over2 = h_ballot(inc >= needb, hh);
-      const int bcut = over2 ? __builtin_ctz(over2) : 31;
-      const int before2 = __shfl(inc - c, 32 * hh + bcut, 64);
-      const int bsz2 = __shfl(c, 32 * hh + bcut, 64);
-      int needc = kp ? needb - before2 : 0;  // 1 <= needc <= bsz2
-      uint32_t cand = 0;
-#pragma unroll
-      for (int q = 0; q < P_DS2; q++) {
-        if (q >= dmw) continue;
-        const uint32_t b = kp && ((bucket >> q) & 1);
-        const int bin = (int)((bins >> (5 * q)) & 31u);
-        ekeep |= (b & (uint32_t)(bin < bcut)) << q;
-        cand |= (b & (uint32_t)(bin == bcut)) << q;
-      }
-      if (needc == bsz2) {
-        ekeep |= cand;
-        needc = 0;
-      }
-      while (__ballot(needc > 0)) {  // the smallest remaining candidate key of each half (keys are distinct)
-        uint64_t mn = ~0ull;
-        int qm = -1;
-#pragma unroll
-        for (int q = 0; q < P_DS2; q++)
-          if (q < dmw && __ballot(needc > 0 && ((cand >> q) & 1)) && needc > 0 && ((cand >> q) & 1)) {
-            const uint64_t kq = p_evict_key(kseed, i, p_w_id(dw[q]));
-            if (kq < mn) {
-              mn = kq;
-              qm = q;
-            }
-          }
-        uint64_t hm = mn;
-#pragma unroll
-        for (int o = 16; o >= 1; o >>= 1) hm = min(hm, h_shfl64(hm, lane ^ o));
-        if (needc > 0 && qm >= 0 && mn == hm) {
-          ekeep |= 1u << qm;
-          cand &= ~(1u << qm);
-        }
-        needc--;
-      }
-    }
-    if (evict) keep = ekeep;
-  }
-  // ---- 6. compact the kept entries (<= V), rank them by id, store the node's list
-  uint32_t *kid = tab, *kidr = tab + 32;
-  uint64_t *fin = (uint64_t *)(tab + 64);
-  p_wsync();  // the dense array is read
-  int cnt = 0;
-#pragma unroll
-  for (int q = 0; q < P_DS2; q++) {
-    if (q >= dmw) break;
-    const bool kb = (keep >> q) & 1;
-    const uint32_t bal = h_ballot(kb, hh);
-    if (kb) kid[cnt + h_below(bal, hl)] = dw[q];
-    cnt += __builtin_popcount(bal);
-  }
-  if (hl >= cnt) kid[hl] = 0x7FFFFFFFu;  // sentinels rank after every real entry
-  p_wsync();
-  uint64_t x = 0;
-  uint32_t f = 0;
-  {
-    const uint32_t mw = kid[hl];
-    const uint32_t mk = mw & 0x7FFFFFFFu;  // id << 6 | dist: ids are distinct, so this orders by id
-    int rank = 0;
-#pragma unroll
-    for (int q = 0; q < P_VMAX / 4; q++) {  // broadcast reads, 4 words each
-      const uint4 v = ((const uint4 *)kid)[q];
-      rank += ((v.x & 0x7FFFFFFFu) < mk) + ((v.y & 0x7FFFFFFFu) < mk) + ((v.z & 0x7FFFFFFFu) < mk) +
-              ((v.w & 0x7FFFFFFFu) < mk);
-    }
-    p_wsync();
-    if (hl < cnt) {
-      fin[rank] = ((uint64_t)p_w_id(mw) << 32) | (uint32_t)(top - (int)p_w_dist(mw));
-      kidr[rank] = mw;
-    }
-    p_wsync();
-    x = hl < cnt ? fin[hl] : 0ull;
-    f = hl < cnt ? kidr[hl] : 0u;
-  }
-  if (act && hl < V) cur[(size_t)li * V + hl] = x;
-  // joins (ascending id) from the front of the event row
-  const bool jn = hl < cnt && !(f >> 31);
-  const uint32_t jb = h_ballot(jn, hh);
-  const int nj = __builtin_popcount(jb);
-  if (act && jn) evr[h_below(jb, hl)] = (P_EV_ADD << 30) | (uint32_t)(x >> 32);
-  const bool aged = hl < cnt && (int)p_w_dist(f) >= 2 * GM_TFAIL - 1;
-  const int numfailed = removed + __builtin_popcount(h_ballot(aged, hh));
-  if (__ballot(act && bad) && lane == 0) atomicOr(s.err, GM_ERR_LAG);
-  // ---- 7. gossip draw over the final list (MP1Node.cpp:449-489)
-  const int numpot = cnt - 1 - numfailed;
-  const int target = act ? max(0, min(GM_FANOUT, numpot)) : 0;
-  int ng = 0;
-  uint32_t *gl = hist;  // the chosen targets in draw order (the histogram is dead)
-  p_wsync();
-  {  // the 16 precomputed outputs in parallel: output d = hl % 16 on both 16-lane groups of a half;
-     // group g tests d against the earlier outputs q in [8g, 8g + 8); the groups' verdicts are OR-ed
-    const uint32_t size = (uint32_t)max(cnt, 1);
-    const uint32_t thr = (0u - size) % size;
-    const int d = hl & 15, g8 = (hl >> 4) * 8;
-    const uint32_t rawd = __shfl(raw0, 32 * hh + d, 64);
-    const uint64_t prod = (uint64_t)rawd * size;
-    const int ixv = (int)(prod >> 32);
-    const uint64_t ent = h_shfl64(x, 32 * hh + ixv);
-    const int c = (int)(ent >> 32) - 1;
-    const bool okd = target > 0 && (uint32_t)prod >= thr && c != i && !p_aged(t, (uint32_t)ent, GM_TFAIL);
-    const int cv = okd ? c : -2;
-    int dup = 0;
-#pragma unroll
-    for (int j = 0; j < 8; j++) dup |= (g8 + j < d) & (__shfl(cv, 32 * hh + g8 + j, 64) == cv);
-    uint32_t db = h_ballot(dup, hh);
-    db |= db >> 16;
-    dup = (int)(db >> d) & 1;
-    const bool acc = hl < 16 && okd && !dup;
-    const uint32_t ab = h_ballot(acc, hh);
-    const int rk = h_below(ab, hl);
-    ng = min(__builtin_popcount(ab), target);
-    if (hl < 16) gl[acc && rk < target ? rk : 16 + hl] = (uint32_t)c;  // others: trash words past the targets
-  }
-  if (__ballot(ng < target)) {
-    // rare: more outputs, from a lazy generator (in the wave's dead table area), one half at a time
-    p_wsync();
-#pragma unroll 1
-    for (int h2 = 0; h2 < 2; h2++) {
-      if (__builtin_amdgcn_readlane(ng, 32 * h2) >= __builtin_amdgcn_readlane(target, 32 * h2)) continue;
-      const int tgt = __builtin_amdgcn_readlane(target, 32 * h2);
-      const uint32_t sz = (uint32_t)__builtin_amdgcn_readlane(cnt, 32 * h2);
-      const uint32_t th = (0u - sz) % sz;
-      const int ih = __builtin_amdgcn_readlane(i, 32 * h2);
-      uint32_t *glh = wbase + 2 * P_H2 + h2 * P_H2_MISC + 16;
-      int ngh = __builtin_amdgcn_readlane(ng, 32 * h2);
-      int g0 = -1, g1 = -1, g2 = -1, g3 = -1, g4 = -1;
-      if (ngh > 0) g0 = (int)__builtin_amdgcn_readfirstlane(glh[0]);
-      if (ngh > 1) g1 = (int)__builtin_amdgcn_readfirstlane(glh[1]);
-      if (ngh > 2) g2 = (int)__builtin_amdgcn_readfirstlane(glh[2]);
-      if (ngh > 3) g3 = (int)__builtin_amdgcn_readfirstlane(glh[3]);
-      GmLazyMT mt;
-      bool done = false;
-      for (int batch = 1; !done; batch++) {
-        if (batch > (1 << 16)) {
-          if (lane == 0) atomicOr(s.err, GM_ERR_DRAWS);
-          break;
-        }
-        if (lane == 0 && batch == 1) {
-          mt.seed(wbase, gm_rd_seed(s.rd_seed, t, ih + 1));
-          for (int q = 0; q < 16; q++) (void)mt.next();
-        }
-        uint32_t raw = 0;
-        for (int q = 0; q < 16; q++) {
-          uint32_t o = 0;
-          if (lane == 0) o = mt.next();
-          o = __builtin_amdgcn_readfirstlane(o);
-          if (lane == q) raw = o;
-        }
-        const uint64_t prod = (uint64_t)raw * sz;
-        const int ix = (int)(prod >> 32);
-        uint64_t mk = __ballot(lane < 16 && (uint32_t)prod >= th);
-        while (mk && !done) {
-          const int d = __builtin_ctzll(mk);
-          mk &= mk - 1;
-          const int ixd = __builtin_amdgcn_readlane(ix, d);
-          const uint64_t e = p_readlane64(x, 32 * h2 + ixd);
-          const int c = (int)(e >> 32) - 1;
-          if (c == ih) continue;                                    // "me"
-          if (p_aged(t, (uint32_t)e, GM_TFAIL)) continue;           // age >= TFAIL
-          if ((ngh > 0 && g0 == c) || (ngh > 1 && g1 == c) || (ngh > 2 && g2 == c) || (ngh > 3 && g3 == c)) continue;
-          if (ngh == 0) g0 = c;
-          else if (ngh == 1) g1 = c;
-          else if (ngh == 2) g2 = c;
-          else if (ngh == 3) g3 = c;
-          else g4 = c;
-          ngh++;
-          if (ngh >= tgt) done = true;
-        }
-      }
-      p_wsync();
-      if (lane < ngh) glh[lane] = (uint32_t)(lane == 0 ? g0 : lane == 1 ? g1 : lane == 2 ? g2 : lane == 3 ? g3 : g4);
-      if (hh == h2) ng = ngh;
-      p_wsync();
-    }
-  }
-  p_wsync();
-  // ---- sends: one parallel round of inbox appends, one lane per target; targets owned by
-  // another row shard get one record per (sender, shard): header + this tick's list
-  const int dst = hl < ng ? (int)gl[hl] : 0;
-  const int owner = (s.G > 1 && hl < ng) ? p_owner(s, dst) : s.rank;
-  if (act && hl < ng) {
-    s.targets[(size_t)li * GM_FANOUT + hl] = dst;
-    if (owner == s.rank) {
-      const int slot = atomicAdd(&s.inbox_cnt[par ^ 1][dst - s.n0], 1);
-      if (slot < s.kcap) s.inbox[par ^ 1][(size_t)(dst - s.n0) * P_KMAX + slot] = li;
-      else atomicOr(s.err, GM_ERR_INBOX);
-    }
-  }
-  uint32_t rmask = 0;  // shards this sender has a record for
-  if (s.G > 1 && __ballot(act && hl < ng && owner != s.rank)) {
-    bool first = act && hl < ng && owner != s.rank;
-#pragma unroll
-    for (int q = 0; q < GM_FANOUT - 1; q++) {
-      const int oq = __shfl(owner, 32 * hh + q, 64);  // outside the branch: a shuffle reads active lanes only
-      if (q < hl && oq == owner) first = false;
-    }
-    uint64_t fm = __ballot(first);
-    while (fm) {  // one record per (sender, shard) at its fixed sparse slot (rr, li)
-      const int fl = __builtin_ctzll(fm);
-      fm &= fm - 1;
-      const int h2 = fl >> 5;
-      const int rr = __builtin_amdgcn_readlane(owner, fl);
-      const int lih = __builtin_amdgcn_readlane(li, fl), ih = __builtin_amdgcn_readlane(i, fl);
-      const size_t rec = (size_t)rr * s.nloc + lih;
-      uint64_t tm = __ballot(hh == h2 && act && hl < ng && owner == rr);
-      const int nt = __builtin_popcountll(tm);
-      int tv0 = -1, tv1 = -1, tv2 = -1, tv3 = -1, tv4 = -1;
-      for (int q = 0; tm; q++) {
-        const int dd = __builtin_amdgcn_readlane(dst, __builtin_ctzll(tm));
-        tm &= tm - 1;
-        if (q == 0) tv0 = dd;
-        else if (q == 1) tv1 = dd;
-        else if (q == 2) tv2 = dd;
-        else if (q == 3) tv3 = dd;
-        else tv4 = dd;
-      }
-      if (hh == h2) {
-        rmask |= 1u << rr;
-        if (hl < 8)
-          s.sp_hdr[rec * 8 + hl] = hl == 0 ? ih : hl == 1 ? nt : hl == 2 ? tv0 : hl == 3 ? tv1
-                                 : hl == 4 ? tv2 : hl == 5 ? tv3 : hl == 6 ? tv4 : 0;
-        if (hl < V) {  // wire entry: fresh entries only, heartbeat as distance from this tick's 2t-1
-          const uint32_t hb = (uint32_t)x;
-          const bool fresh = hl < cnt && !p_aged(t, hb, GM_TFAIL);
-          s.sp_list[rec * V + hl] = fresh ? ((uint32_t)(x >> 32) | ((uint32_t)(2 * t - 1) - hb) << P_WIRE_IDBITS) : 0u;
-        }
-      }
-    }
-  }
-  if (act) {
-    if (s.G > 1 && hl == 0) s.recmask[li] = rmask;
-    if (hl < 4) s.rowstat[(size_t)li * 4 + hl] = hl == 0 ? k : hl == 1 ? cnt : hl == 2 ? numfailed : ng;
-    if (hl == 0) s.ev_cnt[li] = nj | (nrem << 16);
-    if (mc && hl == 0) {  // entries sent = fresh entries of the final list x targets (MP1Node.cpp:372-375)
-      s.mc_sent[(size_t)t * s.nloc + li] = (uint32_t)(ng * (cnt - (numfailed - removed)));
-      s.mc_recv[(size_t)t * s.nloc + li] = (uint32_t)nrecv;
-    }
-  }
-}
-
-// rows [r0, r1) = chunk `chunk` of this shard's nodes; two nodes per wave
-template <bool MC>
-__global__ __launch_bounds__(256) void gm_p_tick_half(PState s, int t, const uint32_t *mtraw, int chunk, int r0, int r1) {
-  extern __shared__ __align__(16) unsigned char p_smem[];
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int w0 = r0 + (blockIdx.x * 4 + wave) * 2;
-  if (w0 >= r1) return;  // whole wave; no workgroup barrier in this kernel
-  const int li = w0 + (lane >> 5);
-  p_node_half<MC>(s, t, mtraw, li, li < r1, lane, (uint32_t *)(p_smem + (size_t)wave * P_HALF_WAVE_BYTES), chunk, r0);
-}
-
 // drains the worklist gm_p_tick_small filled (a fixed grid; every wave exits when the list is done)
 template <bool MC>
 __global__ __launch_bounds__(256) void gm_p_tick_big(PState s, int t, const uint32_t *mtraw, int chunk, int r0) {
@@ -1393,10 +837,7 @@ hipError_t gm_launch_partial_reset(const PState &s, hipStream_t st) {
 hipError_t gm_launch_partial_chunk(const PState &s, int t, const uint32_t *mtraw, int c, hipStream_t st) {
   const int r0 = (int)((int64_t)s.nloc * c / s.nchunk), r1 = (int)((int64_t)s.nloc * (c + 1) / s.nchunk);
   const bool mc = s.mc_sent != nullptr && t < s.mc_tmax;
-  if (r1 > r0 && s.halfwave)  // two nodes per wave
-    hipLaunchKernelGGL(mc ? gm_p_tick_half<true> : gm_p_tick_half<false>, dim3((r1 - r0 + 7) / 8), dim3(256),
-                       4 * P_HALF_WAVE_BYTES, st, s, t, mtraw, c, r0, r1);
-  else if (r1 > r0)  // one node per wave (GM_P_FULLWAVE=1: the round-2 kernel, for comparisons)
+  if (r1 > r0)
     hipLaunchKernelGGL(mc ? gm_p_tick_small<true> : gm_p_tick_small<false>, dim3((r1 - r0 + 3) / 4), dim3(256),
                        4 * PLds<P_HS>::bytes, st, s, t, mtraw, c, r0, r1);
   hipLaunchKernelGGL(mc ? gm_p_tick_big<true> : gm_p_tick_big<false>, dim3(P_BIG_GRID), dim3(256),

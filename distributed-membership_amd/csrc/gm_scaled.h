@@ -78,11 +78,8 @@ __host__ __device__ inline bool s_ingroup(int ramp, int intro_until, int r, int 
 #define S_NIB_ESC 15u
 #define S_NIB_H(n) (S_NIB_BASE + 2u * (n))
 
-// keyed loss threshold on a 16-bit uniform chunk: lost iff chunk < ceil(pct * 65536 / 100)
-// (the probability is pct % to within 1.5e-5; gm_scaled.hip s_keep)
-__host__ __device__ inline uint32_t s_drop_thresh(int pct) {
-  return pct <= 0 ? 0u : pct >= 100 ? 65536u : (uint32_t)((pct * 65536 + 99) / 100);
-}
+// keyed loss threshold (gm_device.h gm_drop_thresh; gm_scaled.hip s_keep)
+__host__ __device__ inline uint32_t s_drop_thresh(int pct) { return gm_drop_thresh(pct); }
 
 #define S_EV_STRIPES 256
 #define S_EV_ADD 1u

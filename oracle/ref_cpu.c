@@ -900,12 +900,13 @@ int oc_bench_sample(int n, int lists, int max_nodes, double min_seconds, int *ou
  *  - self bump; sweep (MP1Node.cpp:426-444): age >= TFAIL counts toward numfailed,
  *    age >= TREMOVE removes (REMOVE event);
  *  - eviction to V: self first, then the largest hb (freshest), ties broken by a
- *    keyed hash (view_seed, t, observer, id); evictions are silent; ids present
+ *    keyed bijective hash of the id (op_evict_key: view_seed, t, observer); evictions are silent; ids present
  *    after the tick and absent before are joins (ADD events);
  *  - numfailed = removed + stale entries of the final list; gossip draw over the
  *    final list in id order exactly as MP1Node.cpp:449-489; the sent list is the
  *    final list's fresh entries (sendMemberList, MP1Node.cpp:360-395);
- *  - drops keyed by (t_send, src, dst, id-1) as in OC_SCALED; crash set at the end
+ *  - drops keyed by (t_send, src, dst, id-1): top 16 bits of fmix32 of the pair hash ^ (id-1)
+ *    below ceil(pct * 65536 / 100); crash set at the end
  *    of crash_tick; warm start at t0: self {2t0-1} plus V-1 distinct peers chosen by
  *    mix64(view_seed ^ i<<32 ^ j) % n, peer hb 2(t0-1-a)-1, a = mix64(init_seed ^
  *    i<<32 ^ p)>>40 % 4. */
@@ -939,8 +940,19 @@ static void op_emit(op_ctx *c, int logger, int kind, int32_t subject) {
   c->ev[c->nev++] = e;
 }
 
+static uint32_t fmix32(uint32_t h) { /* murmur3 finalizer: a bijection of uint32 */
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  return h ^ (h >> 16);
+}
+
+/* eviction tie-break: fmix32(id ^ (uint32)mix64(mix64(view_seed ^ t) ^ obs)) -- distinct ids,
+ * distinct keys (fmix32 is a bijection) */
 uint64_t op_evict_key(uint64_t view_seed, int32_t t, int32_t obs, int32_t id) {
-  return mix64(mix64(view_seed ^ (uint64_t)(uint32_t)t) ^ (((uint64_t)(uint32_t)obs << 32) | (uint32_t)id));
+  uint32_t s = (uint32_t)mix64(mix64(view_seed ^ (uint64_t)(uint32_t)t) ^ (uint64_t)(uint32_t)obs);
+  return fmix32((uint32_t)id ^ s);
 }
 
 op_ctx *op_create(const op_config *cfg) {
@@ -1045,11 +1057,11 @@ static void op_node(op_ctx *c, int i, pcand *m) {
   for (int q = 0; q < nrcv && q < OP_KP; q++) {
     const int s = c->rcv_src[c->rcv_off[i] + q];
     const snap *sp = &c->snaps[s];
-    uint64_t pair = mix64(c->cfg.drop_seed ^ ((uint64_t)(uint32_t)t_send << 48) ^ ((uint64_t)s << 24) ^ (uint64_t)i);
+    uint32_t pair = (uint32_t)mix64(c->cfg.drop_seed ^ ((uint64_t)(uint32_t)t_send << 48) ^ ((uint64_t)s << 24) ^ (uint64_t)i);
     for (int e = 0; e < sp->n; e++) {
-      if (dropping) {
-        uint32_t h = (uint32_t)(mix64(pair + (uint64_t)(sp->ids[e] - 1)) >> 32);
-        if ((int)(h % 100u) < c->cfg.drop_pct) continue;
+      if (dropping) { /* lost iff the top 16 bits of fmix32(pair ^ (id-1)) fall below ceil(pct*65536/100) */
+        uint32_t h = fmix32(pair ^ (uint32_t)(sp->ids[e] - 1));
+        if ((h >> 16) < scaled_drop_thresh(c->cfg.drop_pct)) continue;
       }
       m[cnt].id = sp->ids[e]; m[cnt].hb = sp->hbs[e]; m[cnt].own = 0; cnt++;
       c->mc_recv[i]++;
