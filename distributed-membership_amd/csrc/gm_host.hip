@@ -331,9 +331,15 @@ static int create_scaled(gm_ctx *c) {
   s.shard_count = G;
   // one forced shard (diagnostics/tests): the sharded tick + RCCL with a single rank
   s.sharded = G > 1 || (getenv("GM_FORCE_SHARD") && atoi(getenv("GM_FORCE_SHARD")) == 1);
-  // contiguous, balanced subject-column ranges
-  s.c0 = (int)((int64_t)n * rank / G);
-  s.w = (int)((int64_t)n * (rank + 1) / G) - s.c0;
+  // contiguous, balanced subject-column ranges whose boundaries are multiples of 4 (when n >= 8G):
+  // a start group of the join ramp (ids 4g..4g+3, gm_s_band's updateMyPos quirk) never straddles two
+  // shards, and the keyed loss's 4-column hash groups are whole on every shard
+  auto col0 = [n, G](int g) {
+    if (g >= G) return n;
+    return n >= 8 * G ? 4 * (int)((int64_t)n * g / (4 * G)) : (int)((int64_t)n * g / G);
+  };
+  s.c0 = col0(rank);
+  s.w = col0(rank + 1) - s.c0;
   s.wp = (s.w + S_ROW_ALIGN - 1) / S_ROW_ALIGN * S_ROW_ALIGN;
   s.band = pick_band(c, n, s.wp);
   if (s.band < 0) return GM_EINVAL;
@@ -407,12 +413,12 @@ static int create_scaled(gm_ctx *c) {
   const int t0 = warm ? c->cfg.init_t0 : 0;
   // join ramp (init_mode 2); with keyed drops a joiner can miss its own entry and take
   // updateMyPos's quirk path (MP1Node.cpp:316), handled in gm_s_band within the row's start
-  // group (ids 4g..4g+3): column shards must not split a group
+  // group (ids 4g..4g+3): column shards never split a group (col0 above)
   const bool ramp = c->cfg.init_mode == 2;
   if (c->cfg.init_mode < 0 || c->cfg.init_mode > 2 || (warm && (t0 < 5 || t0 > GM_T_LIMIT / 2))) return GM_EINVAL;
   if (ramp)
     for (int g = 1; g < G; g++)
-      if ((int64_t)n * g / G % 4 != 0) return GM_EUNSUPPORTED;
+      if (col0(g) % 4 != 0) return GM_EUNSUPPORTED;  // n < 8G only
   s.ramp = ramp ? 1 : 0;
   s.intro_until = 0x7FFFFFFF;
   if (ramp) {
@@ -509,6 +515,7 @@ static int create_partial(gm_ctx *c) {
   TRY(dalloc(c, &p.rowstat, (size_t)nl * 4));
   TRY(dalloc(c, &p.targets, (size_t)nl * GM_FANOUT));
   TRY(dalloc(c, &p.big, nl));
+  TRY(dalloc(c, &p.huge, nl));
   TRY(dalloc(c, &p.err, 1));
   TRY(dalloc(c, &c->p_mtraw, (size_t)nl * 16 * 2));
   HIPCHECK(hipStreamCreateWithFlags(&c->p_side, hipStreamNonBlocking));
@@ -522,6 +529,7 @@ static int create_partial(gm_ctx *c) {
   p.kcap = inbox_cap(P_KMAX);
   if (p.nchunk < 1 || p.nchunk > 64) return GM_EINVAL;
   TRY(dalloc(c, &p.big_cnt, p.nchunk));
+  TRY(dalloc(c, &p.huge_cnt, p.nchunk));
   if (c->p_sharded) {
     HIPCHECK(hipStreamCreateWithFlags(&c->p_comm, hipStreamNonBlocking));
     c->p_chev.assign(p.nchunk, nullptr);

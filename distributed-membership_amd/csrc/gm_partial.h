@@ -3,11 +3,12 @@
 #include <stdint.h>
 
 #define P_VMAX 32        // view capacity limit (a list is one half-wave of 8-byte entries)
-#define P_KP 16          // gossip lists merged per node and tick (oracle OP_KP)
 #define P_KSMALL 10      // nodes with <= P_KSMALL delivered lists take the small-table kernel
+#define P_KP 16          // nodes with P_KSMALL < k <= P_KP lists take the big-table kernel, more the huge one
 #define P_HS 512         // small kernel: LDS hash slots per wave (>= (1 + P_KSMALL) * P_VMAX / 0.69)
 #define P_HB 1024        // big kernel: LDS hash slots per wave (>= (1 + P_KP) * P_VMAX / 0.53)
-#define P_KMAX 64        // inbox capacity (lists queued per receiver per tick)
+#define P_HH 4096        // huge kernel: LDS hash slots per wave (>= (1 + P_KMAX) * P_VMAX / 0.51)
+#define P_KMAX 64        // inbox capacity (lists queued per receiver per tick); every list is merged
 #define P_EV_ADD 1u
 #define P_EV_REMOVE 2u
 // Wire entry of an exchanged list: id | (2t-1 - hb) << 25, only entries fresh at the
@@ -36,6 +37,8 @@ struct PState {
   int32_t *targets;      // [nloc][GM_FANOUT] (global node indices)
   int32_t *big;          // [nloc] worklists of nodes with > P_KSMALL lists (big-table kernel), chunk c at rows r0_c..
   int32_t *big_cnt;      // [K]
+  int32_t *huge;         // [nloc] worklists of nodes with > P_KP lists (huge-table kernel), chunk c at rows r0_c..
+  int32_t *huge_cnt;     // [K]
   // outgoing lists to the other row shards (sharded only): one record per (sender, remote rank)
   // The tick kernels write a sender's record to shard q at the fixed slot (q, li) of the
   // sparse buffers (no contended counters) and its shard bitmask to recmask[li]; per

@@ -31,10 +31,12 @@
 //      the wave (duplicates by shuffle-compares), the rare rest on scalars.
 // Nodes with more than P_KSMALL delivered lists (Poisson tail, ~1.4 %) do not fit
 // the small table: the small kernel defers them to a worklist that the big
-// kernel (1024-slot table, sender sort for > P_KP lists) drains.
+// kernel (1024-slot table) drains, and those with more than P_KP lists (~2e-5) to the
+// huge kernel's (4096 slots): every delivered list is merged, as EmulNet delivers them all.
 // Lists are double-buffered by tick parity: a receiver reads its senders' lists
 // of tick t-1 directly, so no separate payload copy is written.
 #include <algorithm>
+#include <type_traits>
 #include <cstdio>
 
 #include "gm_device.h"
@@ -169,9 +171,10 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
   int k = pre.k;
   const int i = s.n0 + li;  // global node index (ids, keys, seeds, targets)
   constexpr int TS = H / 64;                          // table slots per lane
-  constexpr int KK = BIG ? P_KP : P_KSMALL;           // lists merged at most
+  constexpr int KK = H == P_HH ? P_KMAX : BIG ? P_KP : P_KSMALL;  // lists merged at most
   constexpr int DS = ((1 + KK) * P_VMAX + 63) / 64;   // dense entries per lane
   constexpr int NSTEP = (KK + 1) / 2;                 // list-load steps (>= 2 lists per step)
+  using mask_t = typename std::conditional<(DS > 32), uint64_t, uint32_t>::type;  // one bit per dense slot
 #ifdef GM_P_PROFILE
   uint64_t pp_[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, pt_ = __builtin_amdgcn_s_memtime();
 #endif
@@ -187,9 +190,9 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
   uint64_t *cur = s.lists + (size_t)par * s.rows * V;
 
   if (lane == 0) s.inbox_cnt[par][li] = 0;  // consumed; the append target of tick t+1
-  if (BIG && k > P_KMAX) {
+  if (k > KK) {  // the huge kernel takes up to the inbox capacity; beyond it the tick is void
     if (lane == 0) atomicOr(s.err, GM_ERR_INBOX);
-    k = P_KMAX;
+    k = KK;
   }
   // ---- 1. loads (the independent ones arrived with `pre`)
   const uint64_t own = pre.own;
@@ -202,20 +205,6 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
     uint4 *z = (uint4 *)tid;
 #pragma unroll
     for (int q = 0; q < H / 128; q++) z[lane + 64 * q] = make_uint4(0, 0, 0, 0);
-  }
-  if (BIG && k > P_KP) {  // the P_KP lowest sender indices: bitonic sort of (sender, row) across the wave
-    uint64_t key = ((uint64_t)(uint32_t)sg << 32) | (uint32_t)sv;
-#pragma unroll
-    for (int k2 = 2; k2 <= 64; k2 <<= 1)
-#pragma unroll
-      for (int j2 = k2 >> 1; j2 > 0; j2 >>= 1) {
-        const uint32_t olo = __shfl_xor((uint32_t)key, j2, 64), ohi = __shfl_xor((uint32_t)(key >> 32), j2, 64);
-        const uint64_t o = ((uint64_t)ohi << 32) | olo;
-        const bool up = (lane & k2) == 0, lower = (lane & j2) == 0;
-        key = (lower == up) ? min(key, o) : max(key, o);
-      }
-    sv = (int)(uint32_t)key;
-    sg = (int)(key >> 32);
   }
   const int kk = min(k, KK);
   const int per = 64 / V, l = lane % V, jo = lane / V;
@@ -305,29 +294,31 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
       w[4 * q] = a.x; w[4 * q + 1] = a.y; w[4 * q + 2] = a.z; w[4 * q + 3] = a.w;
       hh[4 * q] = b.x; hh[4 * q + 1] = b.y; hh[4 * q + 2] = b.z; hh[4 * q + 3] = b.w;
     }
-    uint32_t alive = 0, rown = 0;
+    using tmask_t = typename std::conditional<(TS > 32), uint64_t, uint32_t>::type;  // one bit per table slot
+    constexpr int CB = TS <= 8 ? 4 : TS <= 16 ? 5 : TS <= 32 ? 6 : 7;               // bits of a per-lane slot count
+    tmask_t alive = 0, rown = 0;
     int rcount = 0;
 #pragma unroll
     for (int u = 0; u < TS; u++) {  // branch-free: exec-mask traffic is what this kernel spends SALU on
       const uint32_t valid = (w[u] & P_IDMASK) != 0;
       const uint32_t rem = valid & (uint32_t)p_aged(t, hh[u], GM_TREMOVE);
       rcount += (int)rem;
-      rown |= (rem & (w[u] >> 31)) << u;
-      alive |= (valid & ~rem) << u;
+      rown |= (tmask_t)(rem & (w[u] >> 31)) << u;
+      alive |= (tmask_t)(valid & ~rem) << u;
     }
     int tot;
     removed = nrem = 0;
     if (__ballot(rcount != 0)) {  // rare: TREMOVE removals in this row
-      (void)p_excl<TS == 8 ? 4 : 5>(rcount, &removed);
-      const int ro = __builtin_popcount(rown);
-      int rpos = p_excl<TS == 8 ? 4 : 5>(ro, &nrem);
+      (void)p_excl<CB>(rcount, &removed);
+      const int ro = __builtin_popcountll(rown);
+      int rpos = p_excl<CB>(ro, &nrem);
       if (nrem) {  // REMOVE events of the node's own entries, from the back of its event row
 #pragma unroll
         for (int u = 0; u < TS; u++)
           if ((rown >> u) & 1) evr[2 * V - 1 - rpos++] = (P_EV_REMOVE << 30) | (w[u] & P_IDMASK);
       }
     }
-    int pos = p_excl<TS == 8 ? 4 : 5>(__builtin_popcount(alive), &tot);
+    int pos = p_excl<CB>(__builtin_popcountll(alive), &tot);
     m = tot;
     // every slot is stored: dead ones to a per-lane slot of [H-64, H), past the dense
     // range (m <= (1+KK)V+1 < H-64) and free of bank conflicts
@@ -357,11 +348,11 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
       dh[q] = e < m ? b : 0u;
     }
   }
-  uint32_t keep = 0;
+  mask_t keep = 0;
   if (m <= V) {
 #pragma unroll
     for (int q = 0; q < DS; q++)
-      if (q < dm && dw[q]) keep |= 1u << q;
+      if (q < dm && dw[q]) keep |= (mask_t)1 << q;
   } else {
     // heartbeat distance from the top (2t-1 = this tick's self heartbeat); alive
     // entries have age < TREMOVE, i.e. distance <= 40 < 64
@@ -381,14 +372,14 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
     const int before = __builtin_amdgcn_readlane(inc - c, dcut);
     const int bsz = __builtin_amdgcn_readlane(c, dcut);
     const int needb = need - before;  // 1 <= needb <= bsz
-    uint32_t bucket = 0;
+    mask_t bucket = 0;
 #pragma unroll
     for (int q = 0; q < DS; q++) {
       if (q >= dm) continue;
       const int d = min(max(top - (int)dh[q], 0), 63);
-      const uint32_t v = dw[q] != 0;
-      keep |= (v & (uint32_t)(((dw[q] & P_SELF) != 0) | (d < dcut))) << q;
-      bucket |= (v & (uint32_t)(!(dw[q] & P_SELF) && d == dcut)) << q;
+      const mask_t v = dw[q] != 0;
+      keep |= (v & (mask_t)(((dw[q] & P_SELF) != 0) | (d < dcut))) << q;
+      bucket |= (v & (mask_t)(!(dw[q] & P_SELF) && d == dcut)) << q;
     }
 #ifdef GM_P_PROFILE
     pp_[10] += 1;  // evictions
@@ -421,14 +412,14 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
       const int before2 = __builtin_amdgcn_readlane(inc - c, bcut);
       const int bsz2 = __builtin_amdgcn_readlane(c, bcut);
       int needc = needb - before2;  // 1 <= needc <= bsz2
-      uint32_t cand = 0;
+      mask_t cand = 0;
 #pragma unroll
       for (int q = 0; q < DS; q++) {
         if (q >= dm) continue;
-        const uint32_t b = (bucket >> q) & 1;
+        const mask_t b = (bucket >> q) & 1;
         const int bin = (int)(key[q] >> 26);
-        keep |= (b & (uint32_t)(bin < bcut)) << q;
-        cand |= (b & (uint32_t)(bin == bcut)) << q;
+        keep |= (b & (mask_t)(bin < bcut)) << q;
+        cand |= (b & (mask_t)(bin == bcut)) << q;
       }
       if (needc == bsz2) {
         keep |= cand;
@@ -446,8 +437,8 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
 #pragma unroll
           for (int q = 0; q < DS; q++)
             if (q < dm && ((cand >> q) & 1) && key[q] == mn) {
-              keep |= 1u << q;
-              cand &= ~(1u << q);
+              keep |= (mask_t)1 << q;
+              cand &= ~((mask_t)1 << q);
             }
         }
       }
@@ -678,8 +669,11 @@ __global__ __launch_bounds__(256) void gm_p_tick_small(PState s, int t, const ui
     p_frozen(s, t, li, lane);
     return;
   }
-  if (pre.k > P_KSMALL) {  // deferred to gm_p_tick_big
-    if (lane == 0) s.big[r0 + atomicAdd(&s.big_cnt[chunk], 1)] = li;
+  if (pre.k > P_KSMALL) {  // deferred to gm_p_tick_big (<= P_KP lists) or gm_p_tick_huge
+    if (lane == 0) {
+      if (pre.k <= P_KP) s.big[r0 + atomicAdd(&s.big_cnt[chunk], 1)] = li;
+      else s.huge[r0 + atomicAdd(&s.huge_cnt[chunk], 1)] = li;
+    }
     return;
   }
   p_node<P_HS, false, MC>(s, t, pre, li, lane, p_smem + (size_t)wave * PLds<P_HS>::bytes, chunk, r0);
@@ -698,11 +692,25 @@ __global__ __launch_bounds__(256) void gm_p_tick_big(PState s, int t, const uint
   }
 }
 
+// drains the nodes with more than P_KP lists (Poisson tail: ~2e-5 of the nodes at S-C), one wave per
+// workgroup for the 33 KB table
+template <bool MC>
+__global__ __launch_bounds__(64) void gm_p_tick_huge(PState s, int t, const uint32_t *mtraw, int chunk, int r0) {
+  extern __shared__ __align__(16) unsigned char p_smem[];
+  const int lane = threadIdx.x & 63;
+  const int nh = s.huge_cnt[chunk];
+  for (int w = blockIdx.x; w < nh; w += gridDim.x) {
+    const int li = s.huge[r0 + w];
+    const PPre pre = p_preload(s, t, mtraw, li, lane, P_KMAX);
+    p_node<P_HH, true, MC>(s, t, pre, li, lane, p_smem, chunk, r0);
+  }
+}
+
 // first 16 S2 outputs of every node for tick t (see gm_mt_first16); resets the big
 // worklist and the outgoing record counts
 __global__ __launch_bounds__(256) void gm_p_mtgen(PState s, int t, uint32_t *mtraw, int reset) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (reset && r < s.nchunk) s.big_cnt[r] = 0;
+  if (reset && r < s.nchunk) s.big_cnt[r] = s.huge_cnt[r] = 0;
   if (reset && s.send_cnt && r < s.nchunk * s.G) s.send_cnt[r] = 0;
   if (r >= s.nloc) return;
   uint32_t out[16];
@@ -818,6 +826,7 @@ __global__ __launch_bounds__(P_PACK) void gm_p_pack_copy(PState s, int c, int r0
 }
 
 #define P_BIG_GRID 1024
+#define P_HUGE_GRID 256
 
 // S2 precompute for every row + reset of the per-chunk worklists and record counts
 hipError_t gm_launch_partial_mtgen(const PState &s, int t, uint32_t *mtraw, hipStream_t st, bool reset) {
@@ -829,6 +838,7 @@ hipError_t gm_launch_partial_mtgen(const PState &s, int t, uint32_t *mtraw, hipS
 // the per-tick resets gm_p_mtgen does when the S2 outputs were prefetched without them
 hipError_t gm_launch_partial_reset(const PState &s, hipStream_t st) {
   hipError_t e = hipMemsetAsync(s.big_cnt, 0, sizeof(int32_t) * s.nchunk, st);
+  if (e == hipSuccess) e = hipMemsetAsync(s.huge_cnt, 0, sizeof(int32_t) * s.nchunk, st);
   if (e == hipSuccess && s.send_cnt) e = hipMemsetAsync(s.send_cnt, 0, sizeof(int32_t) * s.nchunk * s.G, st);
   return e;
 }
@@ -842,6 +852,8 @@ hipError_t gm_launch_partial_chunk(const PState &s, int t, const uint32_t *mtraw
                        4 * PLds<P_HS>::bytes, st, s, t, mtraw, c, r0, r1);
   hipLaunchKernelGGL(mc ? gm_p_tick_big<true> : gm_p_tick_big<false>, dim3(P_BIG_GRID), dim3(256),
                      4 * PLds<P_HB>::bytes, st, s, t, mtraw, c, r0);
+  hipLaunchKernelGGL(mc ? gm_p_tick_huge<true> : gm_p_tick_huge<false>, dim3(P_HUGE_GRID), dim3(64),
+                     PLds<P_HH>::bytes, st, s, t, mtraw, c, r0);
   if (s.G > 1 && r1 > r0) {  // pack the chunk's records for the exchange
     const int nbq = (r1 - r0 + P_PACK - 1) / P_PACK;
     hipLaunchKernelGGL(gm_p_pack_count, dim3(s.G * nbq), dim3(P_PACK), 0, st, s, c, r0, r1, nbq);

@@ -895,8 +895,7 @@ int oc_bench_sample(int n, int lists, int max_nodes, double min_seconds, int *ou
  *    (a bounded view churns: stamping ts = receive tick, as the full list does,
  *    would let a crashed node's entry circulate forever as "fresh");
  *  - merge (updatelistCallBack, MP1Node.cpp:259-301): per id keep the largest hb;
- *    absent ids are inserted; a node merges at most OP_KP = 16 lists per tick (a node
- *    receiving more merges those of the 16 lowest sender indices);
+ *    absent ids are inserted; every list delivered to the node is merged (EmulNet.cpp:144-177);
  *  - self bump; sweep (MP1Node.cpp:426-444): age >= TFAIL counts toward numfailed,
  *    age >= TREMOVE removes (REMOVE event);
  *  - eviction to V: self first, then the largest hb (freshest), ties broken by a
@@ -910,7 +909,6 @@ int oc_bench_sample(int n, int lists, int max_nodes, double min_seconds, int *ou
  *    of crash_tick; warm start at t0: self {2t0-1} plus V-1 distinct peers chosen by
  *    mix64(view_seed ^ i<<32 ^ j) % n, peer hb 2(t0-1-a)-1, a = mix64(init_seed ^
  *    i<<32 ^ p)>>40 % 4. */
-#define OP_KP 16 /* lists merged per node and tick; more: those of the lowest sender indices */
 typedef struct pnode { int32_t *ids, *hbs; int cnt; int32_t hbctr; int failed; } pnode;
 struct op_ctx {
   op_config cfg;
@@ -1049,12 +1047,11 @@ static void op_node(op_ctx *c, int i, pcand *m) {
   pnode *p = &c->nd[i];
   int cnt = 0;
   for (int k = 0; k < p->cnt; k++) { m[cnt].id = p->ids[k]; m[cnt].hb = p->hbs[k]; m[cnt].own = 1; cnt++; }
-  /* lists delivered to i: every sender that targeted i at t-1 (BSP, order-free for the
-   * table); the OP_KP lowest sender indices when more arrived (rcv_* lists them ascending) */
+  /* lists delivered to i: every sender that targeted i at t-1 (BSP, order-free for the table) */
   const int t_send = t - 1;
   const int dropping = c->cfg.drop_pct > 0 && t_send >= c->cfg.drop_from && t_send < c->cfg.drop_to;
   const int nrcv = c->rcv_off[i + 1] - c->rcv_off[i];
-  for (int q = 0; q < nrcv && q < OP_KP; q++) {
+  for (int q = 0; q < nrcv; q++) {
     const int s = c->rcv_src[c->rcv_off[i] + q];
     const snap *sp = &c->snaps[s];
     uint32_t pair = (uint32_t)mix64(c->cfg.drop_seed ^ ((uint64_t)(uint32_t)t_send << 48) ^ ((uint64_t)s << 24) ^ (uint64_t)i);
@@ -1136,7 +1133,6 @@ static void op_node(op_ctx *c, int i, pcand *m) {
 
 int op_tick(op_ctx *c) {
   const int n = c->n;
-  pcand *m = (pcand *)malloc(sizeof(pcand) * (size_t)c->V * (OP_KP + 2));
   c->nev = 0;
   memset(c->mc_sent, 0, sizeof(int32_t) * (size_t)n);
   memset(c->mc_recv, 0, sizeof(int32_t) * (size_t)n);
@@ -1152,6 +1148,9 @@ int op_tick(op_ctx *c) {
       for (int q = 0; q < c->ntgt[s]; q++) c->rcv_src[fill[c->tgt[(size_t)s * FANOUT + q]]++] = s;
     free(fill);
   }
+  int kmax = 0; /* candidates of a node: its own list + every delivered list */
+  for (int i = 0; i < n; i++) kmax = c->rcv_off[i + 1] - c->rcv_off[i] > kmax ? c->rcv_off[i + 1] - c->rcv_off[i] : kmax;
+  pcand *m = (pcand *)malloc(sizeof(pcand) * (size_t)c->V * (size_t)(kmax + 2));
   for (int i = n - 1; i >= 0; i--) {
     c->ntgt_next[i] = 0;
     c->snaps_next[i].n = 0;

@@ -29,7 +29,7 @@ TAG=${1:?usage: scripts/gpu.sh <tag> <step>...}
 shift
 O=gpurun_out/$TAG
 mkdir -p "$O"
-PT="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
+PT="python -u -m pytest -x -v --timeout 150 --timeout-method thread"
 
 run_step() {
   case "$1" in

@@ -11,6 +11,7 @@ pytestmark = pytest.mark.gpu
 
 
 def run_pair(n, v, ticks, crash_tick=-1, crash_count=0, drop_pct=0, drop_from=0, drop_to=0, seed=42):
+    run_pair.max_inbox = 0
     kw = dict(rd_seed=7, view_seed=5, init_t0=8, init_seed=11)
     ora = oracle_py.PartialOracle(n, v=v, crash_tick=crash_tick, crash_count=crash_count, crash_seed=seed,
                                   drop_pct=drop_pct, drop_from=drop_from, drop_to=drop_to, drop_seed=seed, **kw)
@@ -31,6 +32,7 @@ def run_pair(n, v, ticks, crash_tick=-1, crash_count=0, drop_pct=0, drop_from=0,
         joins += sum(e[2] == 1 for e in ev)
         removes += sum(e[2] == 2 for e in ev)
         assert digest64(sim.dump_tables()) == digest64(ora.dump()), f"views differ at tick {t}"
+        run_pair.max_inbox = max(run_pair.max_inbox, sim.tick_stats()["max_inbox"])
     assert sim.tick_stats()["err"] == 0
     return joins, removes
 
@@ -43,6 +45,8 @@ def test_partial_matches_oracle(n, v):
 
 def test_partial_with_drops_matches_oracle():
     run_pair(400, 32, 40, crash_tick=10, crash_count=8, drop_pct=30, drop_from=5, drop_to=30)
+    # some node got more than P_KP = 16 lists in a tick: the huge-table kernel merged them all
+    assert run_pair.max_inbox > 16, run_pair.max_inbox
 
 
 def test_partial_sparse_views_remove_stale_entries():
@@ -53,7 +57,7 @@ def test_partial_sparse_views_remove_stale_entries():
 
 def test_partial_large_cluster_matches_oracle():
     # N = 131,072: ~1.4 % of the nodes receive more than P_KSMALL = 10 lists per tick
-    # (the big-table kernel), ~2 per tick more than P_KP = 16 (the lowest-sender rule);
+    # (the big-table kernel), ~2 per tick more than P_KP = 16 (the huge-table kernel, every list merged);
     # 5 % drops as in S-C, a crash set inside the window
     n, v = 131072, 32
     kw = dict(rd_seed=7, view_seed=5, init_t0=8, init_seed=11)
@@ -73,7 +77,7 @@ def test_partial_large_cluster_matches_oracle():
         if step in (2, 5):
             assert digest64(sim.dump_tables()) == digest64(ora.dump()), f"views differ at tick {t}"
     st = sim.tick_stats()
-    assert st["err"] == 0 and st["max_inbox"] == 16, st
+    assert st["err"] == 0 and st["max_inbox"] > 16, st  # the huge-table kernel merged all of them
 
 
 @pytest.mark.parametrize("n,v,world,drop,chunks", [(300, 16, 2, 0, 4), (1000, 32, 3, 30, 1), (4099, 32, 4, 5, 4),

@@ -120,7 +120,7 @@ def _crash_seed_with(n, count, want):
 
 
 @pytest.mark.parametrize("n,world,drop,intro", [(400, 2, 0, False), (600, 3, 30, False), (1024, 4, 10, False),
-                                                (256, 2, 0, True)])
+                                                (256, 2, 0, True), (602, 3, 20, False), (1001, 4, 10, False)])
 def test_ramp_shards_match_fused_kernel(n, world, drop, intro):
     """The join ramp (init_mode 2: JOINREQ / JOINREP / newNodes-first gossip) on G column
     shards equals the single context tick for tick: tables, node state, events. With keyed
@@ -155,11 +155,20 @@ def test_ramp_shards_match_fused_kernel(n, world, drop, intro):
     assert ref.tick_stats()["err"] == 0
 
 
-def test_ramp_shards_need_whole_start_groups():
-    """A column shard boundary inside a start group (ids 4g..4g+3) is refused."""
+def test_shard_boundaries_keep_start_groups_whole():
+    """Column shard boundaries are multiples of 4 for any n >= 8G (n = 602, 1001: n*g/G is not), so
+    no start group (ids 4g..4g+3) straddles two shards; a ramp whose tiny cluster cannot be cut that
+    way (n < 8G) is refused."""
     from membership.abi import GmError
+    for n, world in ((602, 3), (1001, 4), (4099, 8)):
+        cols = [Simulator(n, GM_MODE_SCALED, rd_seed=7, init_mode=2, shard_rank=g, shard_count=world).shard_layout()
+                for g in range(world)]
+        assert [c0 for c0, _ in cols] == sorted(c0 for c0, _ in cols) and cols[0][0] == 0
+        assert all(c0 % 4 == 0 for c0, _ in cols) and sum(w for _, w in cols) == n
+        assert all(cols[g][0] + cols[g][1] == cols[g + 1][0] for g in range(world - 1))
+        assert max(w for _, w in cols) - min(w for _, w in cols) <= 7
     with pytest.raises(GmError):
-        Simulator(602, GM_MODE_SCALED, rd_seed=7, init_mode=2, shard_rank=0, shard_count=3)
+        Simulator(20, GM_MODE_SCALED, rd_seed=7, init_mode=2, shard_rank=0, shard_count=3)
 
 
 def test_rccl_single_rank_ramp_matches_fused_kernel(monkeypatch):
