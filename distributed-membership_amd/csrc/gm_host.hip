@@ -535,16 +535,11 @@ static int create_partial(gm_ctx *c) {
     c->p_chev.assign(p.nchunk, nullptr);
     for (hipEvent_t &e : c->p_chev) HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIPCHECK(hipEventCreateWithFlags(&c->p_done, hipEventDisableTiming));
-    TRY(dalloc(c, &p.send_cnt, (size_t)p.nchunk * G));
-    TRY(dalloc(c, &p.recmask, std::max(nl, 1)));
     TRY(dalloc(c, &p.sp_hdr, (size_t)G * nl * 8));
     TRY(dalloc(c, &p.sp_list, (size_t)G * nl * p.V));
-    TRY(dalloc(c, &p.pack_blk, (size_t)G * (nl / 256 + 2)));
-    TRY(dalloc(c, &p.send_hdr, (size_t)G * nl * 8));
-    TRY(dalloc(c, &p.send_list, (size_t)G * nl * p.V));
+    HIPCHECK(hipMemset(p.sp_hdr, 0xFF, sizeof(int32_t) * G * nl * 8));  // stamp -1: no record yet
     TRY(dalloc(c, &p.recv_hdr, (size_t)std::max(R, 1) * 8));
     for (int q = 0; q < 2; q++) TRY(dalloc(c, &p.recv_list[q], (size_t)std::max(R, 1) * p.V));
-    TRY(dalloc(c, &p.recv_cnt, (size_t)p.nchunk * G));
     std::vector<int32_t> b(G + 1);
     for (int g = 0; g <= G; g++) b[g] = (int32_t)((int64_t)n * g / G);
     TRY(dalloc(c, &p.shard_n0, G + 1));
@@ -1807,42 +1802,63 @@ static int draw_settle(gm_ctx *c) {
 }
 
 // ------------------------------------------------------------ PARTIAL row shards
-// After the local kernels of tick t every shard holds, per remote shard q, the
-// records its nodes address to q (header + list). All-to-all of the record counts,
-// then all-to-allv of the headers and of the lists (wire format), which land in
-// recv_list[t&1] (where tick t+1 reads its senders' lists); gm_p_unpack appends
-// each received record to its targets' inboxes.
+// After chunk c's local kernels of tick t every shard holds, at the fixed slots (q, li) of
+// sp_hdr / sp_list, the records its nodes of rows [r0_c, r1_c) address to shard q. The exchange
+// sends each such block whole (no counts, no packing, no host round trip: every size is fixed by
+// the shard layout) with two all-to-allv -- headers, then lists (wire format) into recv_list[t&1],
+// where tick t+1 reads its senders' lists -- and gm_p_unpack appends each received record whose
+// stamp is t to its targets' inboxes (a slot without a record of this tick is skipped). A shard
+// thus moves its whole slot range per tick, ~2x the records it has (a sender addresses a given
+// peer with probability 1 - (1 - 1/G)^5: 0.49 at G = 8), over xGMI, while later chunks compute.
+struct XChunk {  // the block layout of chunk ch (rows of shard g in chunk ch: [nloc_g ch / K, nloc_g (ch+1) / K))
+  std::vector<size_t> sc, sd, rc, rd;  // send / receive row counts and row offsets per shard
+  size_t rbase = 0, rrows = 0;         // this chunk's first received row, rows received
+};
+static XChunk xchunk(const PState &p, int ch) {
+  const int G = p.G, K = p.nchunk;
+  auto nloc_of = [&](int g) { return (int64_t)p.n * (g + 1) / G - (int64_t)p.n * g / G; };
+  auto rows = [&](int g, int c) { return (size_t)(nloc_of(g) * (c + 1) / K - nloc_of(g) * c / K); };
+  XChunk x;
+  x.sc.assign(G, 0); x.sd.assign(G, 0); x.rc.assign(G, 0); x.rd.assign(G, 0);
+  for (int c = 0; c < ch; c++)
+    for (int g = 0; g < G; g++)
+      if (g != p.rank) x.rbase += rows(g, c);
+  const size_t r0 = (size_t)((int64_t)p.nloc * ch / K);
+  size_t off = x.rbase;
+  for (int q = 0; q < G; q++) {
+    if (q == p.rank) continue;
+    x.sc[q] = rows(p.rank, ch);
+    x.sd[q] = (size_t)q * p.nloc + r0;
+    x.rc[q] = rows(q, ch);
+    x.rd[q] = off;
+    off += x.rc[q];
+  }
+  x.rrows = off - x.rbase;
+  return x;
+}
+
 static int partial_exchange_chunk(gm_ctx *c, int ch, int64_t *roff) {
   PState &p = c->p;
-  const int G = p.G, V = p.V, nl = p.nloc;
-  const int r0 = (int)((int64_t)nl * ch / p.nchunk), r1 = (int)((int64_t)nl * (ch + 1) / p.nchunk);
+  const int G = p.G, V = p.V;
   hipStream_t cs = c->p_comm;
-  NCCLCHECK(ncclAllToAll(p.send_cnt + (size_t)ch * G, p.recv_cnt + (size_t)ch * G, 1, ncclInt32, c->comm, cs));
-  std::vector<int32_t> sc(G), rc(G);
-  HIPCHECK(hipMemcpyAsync(sc.data(), p.send_cnt + (size_t)ch * G, sizeof(int32_t) * G, hipMemcpyDeviceToHost, cs));
-  HIPCHECK(hipMemcpyAsync(rc.data(), p.recv_cnt + (size_t)ch * G, sizeof(int32_t) * G, hipMemcpyDeviceToHost, cs));
-  HIPCHECK(hipStreamSynchronize(cs));  // the compute stream keeps running the next chunks meanwhile
+  const XChunk x = xchunk(p, ch);
   std::vector<size_t> hs(G), hsd(G), hr(G), hrd(G), ls(G), lsd(G), lr(G), lrd(G);
-  size_t off = (size_t)*roff;
   for (int q = 0; q < G; q++) {
-    if (sc[q] < 0 || sc[q] > r1 - r0 || rc[q] < 0) return GM_ESTATE;
-    hs[q] = (size_t)sc[q] * 8;
-    hsd[q] = ((size_t)q * nl + r0) * 8;
-    ls[q] = (size_t)sc[q] * V;
-    lsd[q] = ((size_t)q * nl + r0) * V;
-    hr[q] = (size_t)rc[q] * 8;
-    hrd[q] = off * 8;
-    lr[q] = (size_t)rc[q] * V;
-    lrd[q] = off * V;
-    off += (size_t)rc[q];
+    hs[q] = x.sc[q] * 8;
+    hsd[q] = x.sd[q] * 8;
+    hr[q] = x.rc[q] * 8;
+    hrd[q] = x.rd[q] * 8;
+    ls[q] = x.sc[q] * V;
+    lsd[q] = x.sd[q] * V;
+    lr[q] = x.rc[q] * V;
+    lrd[q] = x.rd[q] * V;
   }
-  if (off > (size_t)(p.n - nl)) return GM_ESTATE;
-  NCCLCHECK(ncclAllToAllv(p.send_hdr, hs.data(), hsd.data(), p.recv_hdr, hr.data(), hrd.data(), ncclInt32, c->comm,
-                          cs));
-  NCCLCHECK(ncclAllToAllv(p.send_list, ls.data(), lsd.data(), p.recv_list[c->t & 1], lr.data(), lrd.data(), ncclUint32, c->comm,
-                          cs));
-  HIPCHECK(gm_launch_partial_unpack(p, c->t, (int)*roff, (int)(off - (size_t)*roff), cs));
-  *roff = (int64_t)off;
+  if (x.rbase + x.rrows > (size_t)(p.n - p.nloc)) return GM_ESTATE;
+  NCCLCHECK(ncclAllToAllv(p.sp_hdr, hs.data(), hsd.data(), p.recv_hdr, hr.data(), hrd.data(), ncclInt32, c->comm, cs));
+  NCCLCHECK(ncclAllToAllv(p.sp_list, ls.data(), lsd.data(), p.recv_list[c->t & 1], lr.data(), lrd.data(), ncclUint32,
+                          c->comm, cs));
+  HIPCHECK(gm_launch_partial_unpack(p, c->t, (int)x.rbase, (int)x.rrows, cs));
+  *roff = (int64_t)(x.rbase + x.rrows);
   return GM_OK;
 }
 
@@ -1868,34 +1884,29 @@ extern "C" int gm_partial_loopback_tick(gm_ctx **ctxs, int32_t G) {
     HIPCHECK(gm_launch_partial_tick(st, c->t, c->p_mtraw, c->stream, nullptr, nullptr));
   }
   const int K = ctxs[0]->p.nchunk;
-  std::vector<std::vector<int32_t>> sc(G, std::vector<int32_t>((size_t)K * G));
-  for (int g = 0; g < G; g++) {
+  for (int g = 0; g < G; g++)
     if (ctxs[g]->p.nchunk != K) return GM_EINVAL;
-    HIPCHECK(hipMemcpyAsync(sc[g].data(), ctxs[g]->p.send_cnt, sizeof(int32_t) * K * G, hipMemcpyDeviceToHost,
-                            ctxs[g]->stream));
-    HIPCHECK(hipStreamSynchronize(ctxs[g]->stream));
-  }
-  // the layout partial_exchange_chunk gives: per chunk, per source shard ascending
+  // the blocks partial_exchange_chunk's all-to-allv moves, by device copies
   const int V = ctxs[0]->p.V;
   std::vector<size_t> roff(G, 0);
+  for (int g = 0; g < G; g++) HIPCHECK(hipStreamSynchronize(ctxs[g]->stream));  // every shard's records are written
   for (int ch = 0; ch < K; ch++)
     for (int q = 0; q < G; q++) {
       PState &dq = ctxs[q]->p;
       hipStream_t st = ctxs[q]->stream;
-      const size_t base = roff[q];
+      const XChunk xq = xchunk(dq, ch);
       for (int g = 0; g < G; g++) {
+        if (g == q || !xq.rc[g]) continue;
+        const XChunk xg = xchunk(ctxs[g]->p, ch);
         const PState &sg = ctxs[g]->p;
-        const size_t cnt = (size_t)sc[g][(size_t)ch * G + q];
-        const size_t r0 = (size_t)((int64_t)sg.nloc * ch / K);
-        if (g == q || !cnt) continue;
-        if (cnt > (size_t)sg.nloc || roff[q] + cnt > (size_t)(dq.n - dq.nloc)) return GM_ESTATE;
-        HIPCHECK(hipMemcpyAsync(dq.recv_hdr + roff[q] * 8, sg.send_hdr + ((size_t)q * sg.nloc + r0) * 8,
-                                sizeof(int32_t) * 8 * cnt, hipMemcpyDeviceToDevice, st));
-        HIPCHECK(hipMemcpyAsync(dq.recv_list[ctxs[q]->t & 1] + roff[q] * V, sg.send_list + ((size_t)q * sg.nloc + r0) * V,
-                                sizeof(uint32_t) * V * cnt, hipMemcpyDeviceToDevice, st));
-        roff[q] += cnt;
+        if (xg.sc[q] != xq.rc[g]) return GM_ESTATE;
+        HIPCHECK(hipMemcpyAsync(dq.recv_hdr + xq.rd[g] * 8, sg.sp_hdr + xg.sd[q] * 8, sizeof(int32_t) * 8 * xq.rc[g],
+                                hipMemcpyDeviceToDevice, st));
+        HIPCHECK(hipMemcpyAsync(dq.recv_list[ctxs[q]->t & 1] + xq.rd[g] * V, sg.sp_list + xg.sd[q] * V,
+                                sizeof(uint32_t) * V * xq.rc[g], hipMemcpyDeviceToDevice, st));
       }
-      HIPCHECK(gm_launch_partial_unpack(dq, ctxs[q]->t, (int)base, (int)(roff[q] - base), st));
+      HIPCHECK(gm_launch_partial_unpack(dq, ctxs[q]->t, (int)xq.rbase, (int)xq.rrows, st));
+      roff[q] = xq.rbase + xq.rrows;
     }
   for (int q = 0; q < G; q++) ctxs[q]->p_recv_last = (int64_t)roff[q];
   for (int g = 0; g < G; g++) {
@@ -1911,7 +1922,7 @@ extern "C" int gm_partial_loopback_tick(gm_ctx **ctxs, int32_t G) {
 extern "C" int gm_shard_exchange_bytes(gm_ctx *c, int64_t *bytes) {
   if (!c || !bytes) return GM_EINVAL;
   *bytes = 0;
-  if (c->cfg.mode == GM_MODE_PARTIAL)  // received records of the last tick: 32 B header + the V-entry list
+  if (c->cfg.mode == GM_MODE_PARTIAL)  // record slots received in the last tick: 32 B header + the V-entry list
     *bytes = c->p_recv_last * (int64_t)(32 + 4 * c->p.V);
   return GM_OK;
 }

@@ -40,21 +40,15 @@ struct PState {
   int32_t *huge;         // [nloc] worklists of nodes with > P_KP lists (huge-table kernel), chunk c at rows r0_c..
   int32_t *huge_cnt;     // [K]
   // outgoing lists to the other row shards (sharded only): one record per (sender, remote rank)
-  // The tick kernels write a sender's record to shard q at the fixed slot (q, li) of the
-  // sparse buffers (no contended counters) and its shard bitmask to recmask[li]; per
-  // chunk, gm_p_pack_* compact them (counts, scan, copy) into the send buffers.
-  uint32_t *recmask;     // [nloc] shards li has a record for this tick
-  int32_t *sp_hdr;       // [G][nloc][8] sparse records: header
-  uint32_t *sp_list;     // [G][nloc][V] sparse records: list, wire entries (see P_WIRE below)
-  int32_t *pack_blk;     // [G][nloc/256 + 2] per-block record counts, then offsets
-  int32_t *send_cnt;     // [K][G] records of chunk c addressed to shard q
-  int32_t *send_hdr;     // [G][nloc][8]: sender global index, #targets on that rank, targets (global), 0;
-                         //   chunk c's records to q packed from slot q*nloc + r0_c on
-  uint32_t *send_list;   // [G][nloc][V]: the sender's fresh entries of the tick, wire format
-  int32_t *recv_hdr;     // [n - nloc][8] received headers
+  // at the fixed slot (q, li) of these buffers -- no contended counters, no packing: chunk c's
+  // slots to shard q, rows [r0_c, r1_c), go out as one fixed-size block of the all-to-allv (every
+  // size and offset is known on the host from the shard layout: no host round trip), and the
+  // header's stamp (word 7 = the tick) tells the receiver which slots hold a record of this tick
+  int32_t *sp_hdr;       // [G][nloc][8]: sender global index, #targets on that rank, targets (global), stamp t
+  uint32_t *sp_list;     // [G][nloc][V]: the sender's fresh entries of the tick, wire format
+  int32_t *recv_hdr;     // [n - nloc][8] received headers: chunk-major, source shard ascending
   uint32_t *recv_list[2]; // [n - nloc][V] received lists (wire format), by the parity of the tick that
                          //   sent them; the next tick's kernels decode them in place
-  int32_t *recv_cnt;     // [K][G] records received from each shard, per chunk
   int32_t *shard_n0;     // [G+1] first node of every row shard (shard_n0[G] = n)
   uint32_t *err;
   // msgcount analogue (gm_msgcount_record; nullptr = off): per tick and local node, view

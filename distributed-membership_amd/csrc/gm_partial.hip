@@ -592,7 +592,6 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
       else atomicOr(s.err, GM_ERR_INBOX);
     }
   }
-  uint32_t rmask = 0;  // shards this sender has a record for
   if (s.G > 1 && __ballot(lane < ng && owner != s.rank)) {
     bool first = lane < ng && owner != s.rank;
 #pragma unroll
@@ -603,7 +602,6 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
       const int fl = __builtin_ctzll(fm);
       fm &= fm - 1;
       const int rr = __builtin_amdgcn_readlane(owner, fl);
-      rmask |= 1u << rr;
       const size_t rec = (size_t)rr * s.nloc + li;
       uint64_t tm = __ballot(lane < ng && owner == rr);
       const int nt = __builtin_popcountll(tm);
@@ -619,7 +617,7 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
       }
       if (lane < 8)
         s.sp_hdr[rec * 8 + lane] = lane == 0 ? i : lane == 1 ? nt : lane == 2 ? tv0 : lane == 3 ? tv1
-                                 : lane == 4 ? tv2 : lane == 5 ? tv3 : lane == 6 ? tv4 : 0;
+                                 : lane == 4 ? tv2 : lane == 5 ? tv3 : lane == 6 ? tv4 : t;  // stamp: this tick's record
       if (lane < V) {  // wire entry: fresh entries only, heartbeat as distance from this tick's 2t-1
         const uint32_t hb = (uint32_t)x;
         const bool fresh = lane < cnt && !p_aged(t, hb, GM_TFAIL);
@@ -627,7 +625,6 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
       }
     }
   }
-  if (s.G > 1 && lane == 0) s.recmask[li] = rmask;
   if (lane < 4) s.rowstat[(size_t)li * 4 + lane] = lane == 0 ? kk : lane == 1 ? cnt : lane == 2 ? numfailed : ng;
   if (lane == 0) s.ev_cnt[li] = nj | (nrem << 16);
   if (mc && lane == 0) {  // entries sent = fresh entries of the final list x targets (MP1Node.cpp:372-375)
@@ -652,7 +649,6 @@ __device__ __forceinline__ void p_frozen(const PState &s, int t, int li, int lan
   if (lane == 0) {
     s.inbox_cnt[par][li] = 0;
     s.ev_cnt[li] = 0;
-    if (s.G > 1) s.recmask[li] = 0;
   }
 }
 
@@ -711,7 +707,6 @@ __global__ __launch_bounds__(64) void gm_p_tick_huge(PState s, int t, const uint
 __global__ __launch_bounds__(256) void gm_p_mtgen(PState s, int t, uint32_t *mtraw, int reset) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (reset && r < s.nchunk) s.big_cnt[r] = s.huge_cnt[r] = 0;
-  if (reset && s.send_cnt && r < s.nchunk * s.G) s.send_cnt[r] = 0;
   if (r >= s.nloc) return;
   uint32_t out[16];
   gm_mt_first16(gm_rd_seed(s.rd_seed, t, s.n0 + r + 1), out);
@@ -758,6 +753,7 @@ __global__ __launch_bounds__(256) void gm_p_unpack(PState s, int t, int base, in
   const int par = t & 1;
   const int4 h0 = ((const int4 *)s.recv_hdr)[2 * (size_t)j];
   const int4 h1 = ((const int4 *)s.recv_hdr)[2 * (size_t)j + 1];
+  if (h1.w != t) return;  // the sender's slot holds no record for this shard this tick (an older one, or none)
   s.rsrc[par][j] = h0.x;
   const int tg[GM_FANOUT] = {h0.z, h0.w, h1.x, h1.y, h1.z};
   for (int q = 0; q < h0.y && q < GM_FANOUT; q++) {
@@ -769,59 +765,6 @@ __global__ __launch_bounds__(256) void gm_p_unpack(PState s, int t, int base, in
     const int slot = atomicAdd(&s.inbox_cnt[par ^ 1][d], 1);
     if (slot < s.kcap) s.inbox[par ^ 1][(size_t)d * P_KMAX + slot] = s.nloc + j;
     else atomicOr(s.err, GM_ERR_INBOX);
-  }
-}
-
-// ---- row shards: compaction of chunk c's sparse records into the send buffers
-// (per (shard q, block of 256 senders): count; per q: exclusive scan of the block
-// counts -> send_cnt; per block: local scan + copy, one wave per record)
-#define P_PACK 256
-__device__ __forceinline__ int32_t *p_blk_row(const PState &s, int q) {  // [G][nloc/256 + 2]
-  return s.pack_blk + (size_t)q * (s.nloc / P_PACK + 2);
-}
-
-__global__ __launch_bounds__(P_PACK) void gm_p_pack_count(PState s, int c, int r0, int r1, int nbq) {
-  __shared__ int tmp[16];
-  const int q = blockIdx.x / nbq, b = blockIdx.x % nbq;
-  const int li = r0 + b * P_PACK + threadIdx.x;
-  const int f = (q != s.rank && li < r1) ? (int)((s.recmask[li] >> q) & 1u) : 0;
-  const int tot = gm_block_sum(f, tmp);
-  if (threadIdx.x == 0) p_blk_row(s, q)[b] = tot;
-}
-
-__global__ __launch_bounds__(1024) void gm_p_pack_scan(PState s, int c, int nbq) {
-  __shared__ int tmp[16];
-  const int q = blockIdx.x;
-  int32_t *blk = p_blk_row(s, q);
-  int base = 0;
-  for (int b0 = 0; b0 < nbq; b0 += 1024) {
-    const int b = b0 + threadIdx.x;
-    const int v = b < nbq ? blk[b] : 0;
-    int tot;
-    const int ex = gm_block_scan(v, tmp, &tot);
-    if (b < nbq) blk[b] = base + ex;
-    base += tot;
-  }
-  if (threadIdx.x == 0) s.send_cnt[c * s.G + q] = base;
-}
-
-__global__ __launch_bounds__(P_PACK) void gm_p_pack_copy(PState s, int c, int r0, int r1, int nbq) {
-  __shared__ int tmp[16];
-  __shared__ int lst[P_PACK];
-  const int q = blockIdx.x / nbq, b = blockIdx.x % nbq;
-  const int li = r0 + b * P_PACK + threadIdx.x;
-  const int f = (q != s.rank && li < r1) ? (int)((s.recmask[li] >> q) & 1u) : 0;
-  int m;
-  const int pos = gm_block_scan(f, tmp, &m);
-  if (f) lst[pos] = li;
-  __syncthreads();
-  const int base = p_blk_row(s, q)[b];
-  const int V = s.V, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (int k = wave; k < m; k += P_PACK / 64) {
-    const size_t src = (size_t)q * s.nloc + lst[k];
-    const size_t dst = (size_t)q * s.nloc + r0 + base + k;
-    if (lane < 4) ((uint2 *)(s.send_hdr + dst * 8))[lane] = ((const uint2 *)(s.sp_hdr + src * 8))[lane];
-    else if (lane < 4 + V) s.send_list[dst * V + lane - 4] = s.sp_list[src * V + lane - 4];  // wire entries
   }
 }
 
@@ -839,7 +782,6 @@ hipError_t gm_launch_partial_mtgen(const PState &s, int t, uint32_t *mtraw, hipS
 hipError_t gm_launch_partial_reset(const PState &s, hipStream_t st) {
   hipError_t e = hipMemsetAsync(s.big_cnt, 0, sizeof(int32_t) * s.nchunk, st);
   if (e == hipSuccess) e = hipMemsetAsync(s.huge_cnt, 0, sizeof(int32_t) * s.nchunk, st);
-  if (e == hipSuccess && s.send_cnt) e = hipMemsetAsync(s.send_cnt, 0, sizeof(int32_t) * s.nchunk * s.G, st);
   return e;
 }
 
@@ -854,14 +796,6 @@ hipError_t gm_launch_partial_chunk(const PState &s, int t, const uint32_t *mtraw
                      4 * PLds<P_HB>::bytes, st, s, t, mtraw, c, r0);
   hipLaunchKernelGGL(mc ? gm_p_tick_huge<true> : gm_p_tick_huge<false>, dim3(P_HUGE_GRID), dim3(64),
                      PLds<P_HH>::bytes, st, s, t, mtraw, c, r0);
-  if (s.G > 1 && r1 > r0) {  // pack the chunk's records for the exchange
-    const int nbq = (r1 - r0 + P_PACK - 1) / P_PACK;
-    hipLaunchKernelGGL(gm_p_pack_count, dim3(s.G * nbq), dim3(P_PACK), 0, st, s, c, r0, r1, nbq);
-    hipLaunchKernelGGL(gm_p_pack_scan, dim3(s.G), dim3(1024), 0, st, s, c, nbq);
-    hipLaunchKernelGGL(gm_p_pack_copy, dim3(s.G * nbq), dim3(P_PACK), 0, st, s, c, r0, r1, nbq);
-  } else if (s.G > 1) {
-    (void)hipMemsetAsync(s.send_cnt + (size_t)c * s.G, 0, sizeof(int32_t) * s.G, st);
-  }
   return hipGetLastError();
 }
 

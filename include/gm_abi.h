@@ -228,12 +228,13 @@ int gm_shard_stub(gm_ctx *ctx, int32_t on);
  * shard_count = G > 1 owns nodes [n*g/G, n*(g+1)/G) (gm_shard_layout returns the
  * range; gm_read_nodes / gm_dump_tables / gm_drain_events / gm_tick_stats report
  * its own nodes, with global indices). With RCCL attached (gm_comm_init) gm_tick
- * runs the local kernels, then ncclAllToAll of per-shard record counts and two
- * ncclAllToAllv (record headers; the lists' fresh entries, 4 bytes each, read in
- * place by the next tick), then appends the received records to their targets' inboxes.
- * gm_partial_loopback_tick does one such tick for G contexts on one device. */
+ * runs the local kernels in row chunks and, per chunk on a second stream, two
+ * ncclAllToAllv of fixed-size blocks (record headers stamped with the tick; the lists'
+ * fresh entries, 4 bytes each, read in place by the next tick) -- sizes come from the
+ * shard layout, so no host round trip -- then appends the received records to their
+ * targets' inboxes. gm_partial_loopback_tick does one such tick for G contexts on one device. */
 int gm_partial_loopback_tick(gm_ctx **ctxs, int32_t G);
-/* bytes this shard received from the other shards in the last tick's exchange */
+/* bytes this shard received from the other shards in the last tick's exchange (whole blocks) */
 int gm_shard_exchange_bytes(gm_ctx *ctx, int64_t *bytes);
 
 /* Crash set of the SCALED fault schedule: `count` node indices, ascending,

@@ -13,6 +13,7 @@
 #   sbshard    scripts/shard_profile.py --sb            -> $O/sb_shard.json
 #   prof_sa    rocprofv3 --kernel-trace --stats of S-A  -> $O/prof_sa/
 #   prof_sc    rocprofv3 --kernel-trace --stats of S-C  -> $O/prof_sc/
+#   prof_sb    rocprofv3 --kernel-trace --stats of S-B (N = 262,144, one GPU) -> $O/prof_sb/
 #   pmc_sa     FETCH_SIZE / WRITE_SIZE passes of S-A    -> $O/pmc_sa_{fetch,write}/ + traffic json
 #   mix_sa     SQ instruction mix of S-A (one --pmc pass)  -> $O/mix_sa/
 #   pmc_sc     FETCH_SIZE / WRITE_SIZE passes of S-C    -> $O/pmc_sc_{fetch,write}/ + traffic json
@@ -46,6 +47,8 @@ run_step() {
                python3 bench.py --no-cpu ${BENCH_ARGS:-} > $O/prof_sa.log 2>&1 ;;
     prof_sc) timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_sc -o sc -- \
                python3 bench.py --scenario S-C --no-cpu ${BENCH_ARGS:-} > $O/prof_sc.log 2>&1 ;;
+    prof_sb) timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_sb -o sb -- \
+               python3 bench.py --cluster 262144 --no-cpu ${BENCH_ARGS:-} > $O/prof_sb.log 2>&1 ;;
     pmc_sa) timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/pmc_sa_fetch -o p -- \
               python3 bench.py --no-cpu --steps 5 --warmup 1 > $O/pmc_sa_fetch.log 2>&1 &&
             timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/pmc_sa_write -o p -- \

@@ -29,10 +29,15 @@ def main():
     kw = dict(rd_seed=7, view=32, view_seed=5, init_mode=1, init_t0=8, init_seed=11, drop_pct=5, drop_from=0,
               drop_to=1 << 20, drop_seed=42)
     sims = [Simulator(n, GM_MODE_PARTIAL, shard_rank=g, shard_count=G, **kw) for g in range(G)]
+    for s in sims:
+        s.keep_events(0)  # join records are counted on the device, not staged on the host
+    print(f"created {G} shards of n={n}", file=sys.stderr, flush=True)
     crash = crash_set(n, n // 100, 42)
     while sims[0].time <= a.prologue:
         t = sims[0].time
+        w = time.perf_counter()
         partial_loopback_tick(sims)
+        print(f"prologue tick {t}: {(time.perf_counter() - w) * 1e3:.1f} ms", file=sys.stderr, flush=True)
         if t == 10:
             for s in sims:
                 s.set_failed(crash)
