@@ -326,38 +326,44 @@ __device__ __forceinline__ uint32_t nib_value(uint32_t nb, const SState &s, int 
 
 // Keyed loss of the SCALED regime (build-defined; the reference drops whole messages with
 // rand() % 100 < MSG_DROP_PROB * 100, EmulNet.cpp:90-94): the entry of global column c in the list
-// src sent to dst at tick t_send is lost iff 16-bit chunk (c & 3) of mix64(pair + (c >> 2)) is
-// below T = ceil(pct * 65536 / 100) (s_drop_thresh), pair = mix64(seed ^ t_send << 48 ^ src << 24 ^ dst):
-// one hash per 4 columns (oracle/ref_cpu.c scaled_recv states the same function)
-__device__ __forceinline__ uint64_t s_drop_pair(const SState &s, int t, int sn, int r) {
-  return gm_mix64(s.drop_seed ^ ((uint64_t)(uint32_t)(t - 1) << 48) ^ ((uint64_t)(uint32_t)sn << 24) ^ (uint64_t)(uint32_t)r);
+// src sent to dst at tick t_send is lost iff 16-bit half (c & 1) of fmix32(pair ^ (c >> 1) * phi) is
+// below T = ceil(pct * 65536 / 100) (s_drop_thresh), pair = low word of mix64(seed ^ t_send << 48 ^
+// src << 24 ^ dst): one 32-bit hash per column pair, whose halves are exactly the two u16 halves
+// of the packed nibble layout (oracle/ref_cpu.c scaled_recv states the same function)
+#define S_PHI 0x9E3779B9u
+__device__ __forceinline__ uint32_t s_drop_pair(const SState &s, int t, int sn, int r) {
+  return (uint32_t)gm_mix64(s.drop_seed ^ ((uint64_t)(uint32_t)(t - 1) << 48) ^ ((uint64_t)(uint32_t)sn << 24) ^
+                            (uint64_t)(uint32_t)r);
 }
 __device__ __forceinline__ bool s_keep(const SState &s, int t, int sn, int r, int c, uint32_t T) {
-  const uint64_t h = gm_mix64(s_drop_pair(s, t, sn, r) + (uint64_t)(uint32_t)(c >> 2));
-  return ((uint32_t)(h >> (16 * (c & 3))) & 0xFFFFu) >= T;
+  const uint32_t h = gm_fmix32(s_drop_pair(s, t, sn, r) ^ ((uint32_t)(c >> 1) * S_PHI));
+  return ((h >> (16 * (c & 1))) & 0xFFFFu) >= T;
 }
 // payload nibble position of lane cell q (0..15) in its 8-byte slice (nib_max's order)
 __device__ __forceinline__ constexpr int nib_pos(int q) { return 32 * (q >> 3) + 16 * (q & 1) + 4 * (3 - ((q & 7) >> 1)); }
-// 0xF at the nibbles of the lane's kept cells in list sn -> row r (64 bits = the slice); agrp: the
-// lane's 16 columns are 4 whole hash groups (else one hash per cell, shards at odd offsets)
+// 0xF at the nibbles of the lane's kept cells in list sn -> row r (64 bits = the slice). Even c0:
+// cells (2i, 2i+1) are a hash pair whose halves sit at the same nibble of the two u16 halves of
+// dword i / 4 -- one fmix32 and four packed ops per pair; else one hash per cell (odd offsets)
 __device__ __forceinline__ uint64_t s_keep_nibbles(const SState &s, int t, int sn, int r, int colb, uint32_t T,
                                                    bool agrp) {
-  const uint64_t pair = s_drop_pair(s, t, sn, r);
+  const uint32_t pair = s_drop_pair(s, t, sn, r);
   const int c = s.c0 + colb;
-  uint64_t km = 0;
+  if (T > 65535u) return 0;  // every entry lost
   if (agrp) {
+    const u16x2 t2 = (u16x2)((uint16_t)T);
+    uint32_t kw[2] = {0u, 0u};
 #pragma unroll
-    for (int g = 0; g < 4; g++) {
-      const uint64_t h = gm_mix64(pair + (uint64_t)(uint32_t)((c >> 2) + g));
-#pragma unroll
-      for (int e = 0; e < 4; e++)
-        if (((uint32_t)(h >> (16 * e)) & 0xFFFFu) >= T) km |= 0xFull << nib_pos(4 * g + e);
+    for (int i = 0; i < 8; i++) {
+      const uint32_t h = gm_fmix32(pair ^ ((uint32_t)((c >> 1) + i) * S_PHI));
+      const u16x2 drop = pmin1(__builtin_elementwise_sub_sat(t2, pk(h)));  // 1 where the half is < T
+      kw[i >> 2] |= unpk(((u16x2)(1) - drop) * (u16x2)(0xFu << (4 * (3 - (i & 3)))));
     }
-  } else {
-    for (int q = 0; q < 16; q++) {
-      const uint64_t h = gm_mix64(pair + (uint64_t)(uint32_t)((c + q) >> 2));
-      if (((uint32_t)(h >> (16 * ((c + q) & 3))) & 0xFFFFu) >= T) km |= 0xFull << nib_pos(q);
-    }
+    return (uint64_t)kw[0] | ((uint64_t)kw[1] << 32);
+  }
+  uint64_t km = 0;
+  for (int q = 0; q < 16; q++) {
+    const uint32_t h = gm_fmix32(pair ^ ((uint32_t)((c + q) >> 1) * S_PHI));
+    if (((h >> (16 * ((c + q) & 1))) & 0xFFFFu) >= T) km |= 0xFull << nib_pos(q);
   }
   return km;
 }
@@ -474,7 +480,7 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
       // DROP (keyed loss on this tick's deliveries): a list's lost entries are cleared from its
       // nibbles before the max, per (list, lane) from 4 hashes of the pair key (s_keep_bits)
       const uint32_t T = DROP ? s_drop_thresh(drop_pct) : 0u;
-      const bool agrp = ((s.c0 + colb) & 3) == 0;  // shard-uniform: the lane's cells in 4 whole hash groups
+      const bool agrp = ((s.c0 + colb) & 1) == 0;  // shard-uniform: the lane's cells are 8 whole hash pairs
       u16x2 acc[8];
 #pragma unroll
       for (int i = 0; i < 8; i++) acc[i] = (u16x2)(0);
@@ -832,8 +838,11 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
   }
 }
 
+#ifndef GM_DROP_MINW
+#define GM_DROP_MINW 8  // the keyed-loss instantiation at 8 waves per SIMD (64 VGPRs + 20 B of spills: 7.39 ms vs 7.63 at its own 79 VGPRs)
+#endif
 template <int B, bool DROP>
-__global__ __launch_bounds__(256) void gm_s_band(SState s, int t, int drop_pct) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DROP ? GM_DROP_MINW : 1, 8))) void gm_s_band(SState s, int t, int drop_pct) {
   constexpr int RPW = 64 / (B / S_COLS_PER_LANE);
   const int U = (s.n + RPW - 1) / RPW;
   // grid (units of a band / 4, bands): blockIdx.y is the band, so workgroups still dispatch

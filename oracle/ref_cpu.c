@@ -464,6 +464,14 @@ static void node_start(oc_ctx *c, int idx) {
   }
 }
 
+static uint32_t fmix32(uint32_t h) { /* murmur3 finalizer: a bijection of uint32 */
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  return h ^ (h >> 16);
+}
+
 /* SCALED keyed loss threshold: an entry is lost iff its 16-bit chunk < ceil(pct * 65536 / 100)
  * (gm_scaled.h s_drop_thresh) */
 static uint32_t scaled_drop_thresh(int pct) {
@@ -479,11 +487,11 @@ static void scaled_recv(oc_ctx *c, int idx) {
       snap *p = &c->snaps[s];
       int t_send = c->t - 1;
       int dropping = c->cfg.drop_pct > 0 && t_send >= c->cfg.drop_from && t_send < c->cfg.drop_to;
-      uint64_t pair = mix64(c->cfg.drop_seed ^ ((uint64_t)(uint32_t)t_send << 48) ^ ((uint64_t)s << 24) ^ (uint64_t)idx);
+      uint32_t pair = (uint32_t)mix64(c->cfg.drop_seed ^ ((uint64_t)(uint32_t)t_send << 48) ^ ((uint64_t)s << 24) ^ (uint64_t)idx);
       for (int e = 0; e < p->n; e++) {
-        if (dropping) { /* build-defined keyed loss: 16-bit chunk (col & 3) of one hash per 4 columns */
+        if (dropping) { /* build-defined keyed loss: 16-bit half (col & 1) of one fmix32 per column pair */
           uint32_t col = (uint32_t)(p->ids[e] - 1);
-          uint32_t v = (uint32_t)(mix64(pair + (col >> 2)) >> (16 * (col & 3))) & 0xFFFFu;
+          uint32_t v = (fmix32(pair ^ ((col >> 1) * 0x9E3779B9u)) >> (16 * (col & 1))) & 0xFFFFu;
           if (v < scaled_drop_thresh(c->cfg.drop_pct)) continue;
         }
         if (c->mc_recv) c->mc_recv[idx]++;
@@ -936,14 +944,6 @@ static void op_emit(op_ctx *c, int logger, int kind, int32_t subject) {
   }
   oc_event e = {c->t, logger, kind, subject};
   c->ev[c->nev++] = e;
-}
-
-static uint32_t fmix32(uint32_t h) { /* murmur3 finalizer: a bijection of uint32 */
-  h ^= h >> 16;
-  h *= 0x85EBCA6Bu;
-  h ^= h >> 13;
-  h *= 0xC2B2AE35u;
-  return h ^ (h >> 16);
 }
 
 /* eviction tie-break: fmix32(id ^ (uint32)mix64(mix64(view_seed ^ t) ^ obs)) -- distinct ids,

@@ -15,6 +15,14 @@ TFAIL, TREMOVE, FANOUT = 5, 20, 5
 M64 = (1 << 64) - 1
 
 
+def fmix32(h):
+    h ^= h >> 16
+    h = (h * 0x85EBCA6B) & 0xFFFFFFFF
+    h ^= h >> 13
+    h = (h * 0xC2B2AE35) & 0xFFFFFFFF
+    return h ^ (h >> 16)
+
+
 def mix64(z):
     z &= M64
     z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M64
@@ -87,9 +95,9 @@ class ShardModel:
         pct, lo, hi, seed = self.drop
         if pct <= 0 or not (lo <= t_send < hi):
             return False
-        pair = mix64(seed ^ (t_send << 48) ^ (s << 24) ^ r)
-        thresh = 65536 if pct >= 100 else (pct * 65536 + 99) // 100  # gm_scaled.h s_drop_thresh
-        return ((mix64(pair + (col >> 2)) >> (16 * (col & 3))) & 0xFFFF) < thresh
+        pair = mix64(seed ^ (t_send << 48) ^ (s << 24) ^ r) & 0xFFFFFFFF
+        thresh = 65536 if pct >= 100 else (pct * 65536 + 99) // 100  # gm_device.h gm_drop_thresh
+        return ((fmix32(pair ^ (((col >> 1) * 0x9E3779B9) & 0xFFFFFFFF)) >> (16 * (col & 1))) & 0xFFFF) < thresh
 
     def tick(self, all_gather, all_reduce_max):
         n, t, w, c0 = self.n, self.t, self.w, self.c0
