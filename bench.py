@@ -270,7 +270,7 @@ def main():
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        "dtype": "u8 cells (u16 escape plane) / 4-bit payload (integer)",
+        "dtype": "u8 cells (u16 escape lists) / 4-bit payload (integer)",
         "data": "synthetic (converged full-membership table, seeded crash set)",
         "config": {"workload": "S-A: SCALED full membership, 1% crash at tick 10, fanout 5, TFAIL 5, TREMOVE 20"
                    + (f", DIAGNOSTIC keyed {a.drop_pct}% per-entry drops" if a.drop_pct else ""),
@@ -379,13 +379,14 @@ def main_partial(a):
     # per delivered list the sender's list (8V B) + its inbox word
     b_alg = n_live * (16 * V + 120) + m_lists * (8 * V + 4)
     achieved = b_alg / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else None
-    traffic = None  # PMC FETCH_SIZE/WRITE_SIZE of the same tick pair (committed passes; N=16M, V=32 only)
+    traffic, traffic_src = None, None  # PMC FETCH_SIZE/WRITE_SIZE of the same tick (committed passes; N=16M, V=32 only)
     tpath = os.path.join(REPO, "profiles", f"traffic_sc_n{n}.json")
     if world == 1 and V == 32 and os.path.exists(tpath):
         with open(tpath) as f:
             tj = json.load(f)
         if tj.get("layout") == "partial-v32":
             traffic = tj.get("hbm_bytes_per_launch")
+            traffic_src = f"profiles/traffic_sc_n{n}.json ({tj.get('generated', 'r01')}, rocprofv3 --pmc passes by scripts/gpu.sh pmc_sc)"
     out = {
         "metric": "simulated node-ticks/sec (S-C partial view)",
         "value": n * a.steps / elapsed,
@@ -408,9 +409,10 @@ def main_partial(a):
                    "parallelism": f"row-shard x{world} (RCCL all-to-allv of lists)" if world > 1 else "single GPU"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                      "frac": (achieved / PEAK_HBM_GBPS) if achieved else None, "traffic": traffic,
+                     "traffic_source": traffic_src,
                      "kernel": "gm_p_tick", "kernel_ms": kernel_ms, "alg_bytes_per_launch": b_alg,
-                     "note": "instruction-issue bound, not HBM bound: ~960 VALU + ~570 SALU instructions per "
-                             "node (PMC, profiles/r01/partial_v3/pmc_instr_mix_n4m.txt; DESIGN.md PARTIAL); the "
+                     "note": "instruction-issue bound, not HBM bound: ~800 VALU + ~580 SALU instructions per "
+                             "node (PMC, profiles/r03/sc_hash32/mix_sc.txt; DESIGN.md PARTIAL); the "
                              "contract's bound field only offers hbm|mfma"},
     }
     if world > 1:
