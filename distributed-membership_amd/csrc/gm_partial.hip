@@ -677,7 +677,7 @@ __global__ __launch_bounds__(256) void gm_p_tick_small(PState s, int t, const ui
 
 // drains the worklist gm_p_tick_small filled (a fixed grid; every wave exits when the list is done)
 template <bool MC>
-__global__ __launch_bounds__(256) void gm_p_tick_big(PState s, int t, const uint32_t *mtraw, int chunk, int r0) {
+__global__ __launch_bounds__(256, 3) void gm_p_tick_big(PState s, int t, const uint32_t *mtraw, int chunk, int r0) {
   extern __shared__ __align__(16) unsigned char p_smem[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int nbig = s.big_cnt[chunk];
