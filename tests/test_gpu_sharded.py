@@ -44,8 +44,10 @@ def merge_dumps(dumps, owners):
 
 
 @pytest.mark.parametrize("n,world,drop,warm", [(256, 2, 0, 0), (600, 3, 0, 1), (512, 2, 25, 0), (1100, 4, 10, 1),
-                                               (2048, 8, 10, 1)])
+                                               (2048, 8, 10, 1), (21, 3, 30, 1)])
 def test_shards_match_fused_kernel(n, world, drop, warm):
+    # (21, 3): n < 8G, so shard starts 7 and 14 are odd -- the keyed loss hashes column pairs
+    # that straddle a shard boundary (gm_scaled.hip s_keep_nibbles' per-cell path)
     kw = dict(rd_seed=7, drop_pct=drop, drop_from=3, drop_to=25, drop_seed=42, init_mode=warm,
               init_t0=6 if warm else 0, init_seed=5)
     ref = Simulator(n, GM_MODE_SCALED, **kw)
