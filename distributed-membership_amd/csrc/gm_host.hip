@@ -518,7 +518,13 @@ static int create_partial(gm_ctx *c) {
   TRY(dalloc(c, &p.huge, nl));
   TRY(dalloc(c, &p.err, 1));
   TRY(dalloc(c, &c->p_mtraw, (size_t)nl * 16 * 2));
-  HIPCHECK(hipStreamCreateWithFlags(&c->p_side, hipStreamNonBlocking));
+  {  // the S2 prefetch for tick t+1 runs beside tick t's kernels: at the lowest stream priority it
+     // takes the CUs the tick leaves idle instead of competing for them (GM_SIDE_PRIO=0: default)
+    int lo = 0, hi = 0;
+    HIPCHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    const bool low = !(getenv("GM_SIDE_PRIO") && !atoi(getenv("GM_SIDE_PRIO")));
+    HIPCHECK(hipStreamCreateWithPriority(&c->p_side, hipStreamNonBlocking, low ? lo : 0));
+  }
   for (int q = 0; q < 2; q++) {
     HIPCHECK(hipEventCreateWithFlags(&c->p_tickev[q], hipEventDisableTiming));
     HIPCHECK(hipEventCreateWithFlags(&c->p_mtev[q], hipEventDisableTiming));
