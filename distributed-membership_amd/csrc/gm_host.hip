@@ -533,6 +533,7 @@ static int create_partial(gm_ctx *c) {
   // row shards pipeline their exchange over K chunks of their nodes (GM_CHUNKS, default 4)
   p.nchunk = c->p_sharded ? (getenv("GM_CHUNKS") ? atoi(getenv("GM_CHUNKS")) : 4) : 1;
   p.kcap = inbox_cap(P_KMAX);
+  p.npw = getenv("GM_P_NPW") ? std::max(1, atoi(getenv("GM_P_NPW"))) : P_NPW;
   if (p.nchunk < 1 || p.nchunk > 64) return GM_EINVAL;
   TRY(dalloc(c, &p.big_cnt, p.nchunk));
   TRY(dalloc(c, &p.huge_cnt, p.nchunk));

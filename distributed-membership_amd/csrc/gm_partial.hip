@@ -66,10 +66,14 @@ struct PLds {
   static constexpr int bytes = H * 8 + P_MISC_BYTES;
 };
 
+// LDS hand-off between the lanes of ONE wave (every LDS region here is private to its wave):
+// a wave's LDS instructions execute in issue order, so wavefront scope needs no lgkmcnt wait --
+// only the compiler must not move LDS accesses across it (workgroup scope waited lgkmcnt(0)
+// at each of the ~16 hand-offs of a node)
 __device__ __forceinline__ void p_wsync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 __device__ __forceinline__ int p_age(int t, uint32_t hb) { return t - (int)((hb + 1u) >> 1); }
@@ -148,7 +152,8 @@ struct PPre {
   int failed, k, hbctr;
   uint64_t own;
   int sv;
-  uint32_t raw0;
+  uint32_t raw0;  // S2 output d on lane roff + d
+  int roff;
 };
 __device__ __forceinline__ PPre p_preload(const PState &s, int t, const uint32_t *mtraw, int li, int lane, int nin) {
   const int par = t & 1, V = s.V;
@@ -159,13 +164,55 @@ __device__ __forceinline__ PPre p_preload(const PState &s, int t, const uint32_t
   p.own = lane < V ? s.lists[((size_t)(par ^ 1) * s.rows + li) * V + lane] : 0ull;
   p.sv = lane < nin ? s.inbox[par][(size_t)li * P_KMAX + lane] : 0;
   p.raw0 = lane < 16 ? mtraw[(size_t)li * 16 + lane] : 0u;
+  p.roff = 0;
+  return p;
+}
+
+// The small kernel's next node, prefetched while the wave works on the current one: ONE
+// packed word per lane -- inbox ids on lanes 0..15, S2 outputs on 16..31, crash flag / inbox
+// count / heartbeat counter on lanes 32 / 33 / 34 -- by an LDS-DMA load (global_load_lds:
+// no VGPR holds it across the node, and no register copy at the loop edge waits for it) into
+// the wave's P_PF_BYTES area. The compiler does not see this load (inline asm): every node
+// starts with vmcnt(0), which retires the DMA its predecessor issued.
+#define P_PF_LANES 40
+#define P_PF_BYTES (P_PF_LANES * 4)
+__device__ __forceinline__ void p_prefetch(const PState &s, int t, const uint32_t *mtraw, int li, int lane,
+                                           uint32_t lds) {
+  const int par = t & 1;
+  const uint32_t *a = lane < 16   ? (const uint32_t *)s.inbox[par] + (size_t)li * P_KMAX + lane
+                      : lane < 32 ? mtraw + (size_t)li * 16 + (lane - 16)
+                      : lane == 32 ? (const uint32_t *)s.failed + li
+                      : lane == 33 ? (const uint32_t *)s.inbox_cnt[par] + li
+                                   : (const uint32_t *)s.hbctr + li;
+  if (lane < P_PF_LANES) {
+    uint32_t keep;  // m0 = the LDS destination (lane l writes dword l); the reads of the area
+                    // by the node before are waited for first
+    asm volatile(
+        "s_waitcnt lgkmcnt(0)\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+        "global_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(a), "s"(lds)
+        : "memory");
+  }
+}
+__device__ __forceinline__ PPre p_unpack_next(const PState &s, int t, int li, uint32_t pv, int lane) {
+  PPre p;
+  p.failed = (int)__builtin_amdgcn_readlane(pv, 32);
+  p.k = (int)__builtin_amdgcn_readlane(pv, 33);
+  p.hbctr = (int)__builtin_amdgcn_readlane(pv, 34);
+  p.own = lane < s.V ? s.lists[((size_t)((t & 1) ^ 1) * s.rows + li) * s.V + lane] : 0ull;
+  p.sv = lane < 16 ? (int)pv : 0;
+  p.raw0 = pv;
+  p.roff = 16;
   return p;
 }
 
 // One node's tick on one wave. li: the node's local row (global index n0 + li);
 // pre.k: lists queued for it this tick.
 // MC: the msgcount-recording instantiation (gm_msgcount_record); the others carry no trace of it
-template <int H, bool BIG, bool MC>
+// RM: lists of other row shards may be delivered (sharded contexts); without, every sender is a
+// local row and the list loads carry no branch
+template <int H, bool BIG, bool MC, bool RM = true>
 __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, int li, int lane, unsigned char *base,
                                        int chunk, int r0) {
   int k = pre.k;
@@ -199,8 +246,6 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
   int sv = lane < k ? pre.sv : 0x7FFFFFFF;  // list rows
   const uint32_t raw0 = pre.raw0;
   const int hbnew = pre.hbctr + 1;
-  // global sender index of each row (drop keys, the lowest-sender rule)
-  int sg = lane < k ? (sv < s.nloc ? s.n0 + sv : s.rsrc[par ^ 1][sv - s.nloc]) : 0x7FFFFFFF;
   {  // clear the table (both word arrays are contiguous)
     uint4 *z = (uint4 *)tid;
 #pragma unroll
@@ -215,14 +260,16 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
     const bool ok = jo < per && j < kk;
     const int sn = __shfl(sv, ok ? j : 0, 64);
     uint64_t e = 0;
-    if (ok && sn < s.nloc) {
+    if (ok && (!RM || sn < s.nloc)) {
       e = prev[(size_t)sn * V + l];
-    } else if (ok) {  // a list another shard sent at t-1: wire entry id | (2(t-1)-1 - hb) << 25
+    } else if (RM && ok) {  // a list another shard sent at t-1: wire entry id | (2(t-1)-1 - hb) << 25
       const uint32_t w = s.recv_list[par ^ 1][(size_t)(sn - s.nloc) * V + l];
       if (w) e = ((uint64_t)(w & ((1u << P_WIRE_IDBITS) - 1)) << 32) | (uint32_t)(2 * t - 3 - (int)(w >> P_WIRE_IDBITS));
     }
     dv[st] = e;
   }
+  // global sender index of each list (the drop keys), after the list loads are in flight
+  const int sg = lane < k ? (!RM || sv < s.nloc ? s.n0 + sv : s.rsrc[par ^ 1][sv - s.nloc]) : 0x7FFFFFFF;
   // drop keys: one (t_send, src, dst) hash per delivered list, lane j for list j
   const bool dropping = s.drop_pct >= 0;
   const bool mc = MC && t < s.mc_tmax;  // msgcount recording (wave-uniform)
@@ -507,7 +554,7 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
       // every 16-lane group g evaluates all 16 outputs (output d = lane % 16) and tests
       // d against the earlier outputs q in [4g, 4g + 4); the groups' results are OR-ed
       const int d = lane & 15, g4 = (lane >> 4) * 4;
-      const uint32_t rawd = __shfl(raw0, d, 64);
+      const uint32_t rawd = __shfl(raw0, pre.roff + d, 64);
       const uint64_t prod = (uint64_t)rawd * size;
       const int ixv = (int)(prod >> 32);
       const uint32_t elo = __shfl((uint32_t)x, ixv, 64), ehi = __shfl((uint32_t)(x >> 32), ixv, 64);
@@ -653,14 +700,9 @@ __device__ __forceinline__ void p_frozen(const PState &s, int t, int li, int lan
 }
 
 // rows [r0, r1) = chunk `chunk` of this shard's nodes
-template <bool MC>
-__global__ __launch_bounds__(256) void gm_p_tick_small(PState s, int t, const uint32_t *mtraw, int chunk, int r0,
-                                                       int r1) {
-  extern __shared__ __align__(16) unsigned char p_smem[];
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int li = r0 + blockIdx.x * 4 + wave;
-  if (li >= r1) return;  // whole wave; no workgroup barrier in this kernel
-  const PPre pre = p_preload(s, t, mtraw, li, lane, P_KSMALL);
+template <bool MC, bool RM>
+__device__ __forceinline__ void p_small_node(const PState &s, int t, const PPre &pre, int li, int lane,
+                                             unsigned char *base, int chunk, int r0) {
   if (pre.failed) {
     p_frozen(s, t, li, lane);
     return;
@@ -672,7 +714,52 @@ __global__ __launch_bounds__(256) void gm_p_tick_small(PState s, int t, const ui
     }
     return;
   }
-  p_node<P_HS, false, MC>(s, t, pre, li, lane, p_smem + (size_t)wave * PLds<P_HS>::bytes, chunk, r0);
+  p_node<P_HS, false, MC, RM>(s, t, pre, li, lane, base, chunk, r0);
+}
+
+// NPW consecutive nodes per wave; with NPW > 1 each node's loads are prefetched during the
+// node before it (p_prefetch), so a node starts with one global round trip (its delivered
+// lists) instead of two
+template <bool MC, int NPW, bool RM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NPW > 1 ? 8 : 1, 8))) void gm_p_tick_small(PState s, int t, const uint32_t *mtraw, int chunk, int r0,
+                                                       int r1) {
+  extern __shared__ __align__(16) unsigned char p_smem[];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int l0 = r0 + (blockIdx.x * 4 + wave) * NPW;
+  if (l0 >= r1) return;  // whole wave; no workgroup barrier in this kernel
+  unsigned char *base = p_smem + (size_t)wave * PLds<P_HS>::bytes;
+  if constexpr (NPW == 1) {
+    const PPre pre = p_preload(s, t, mtraw, l0, lane, P_KSMALL);
+    p_small_node<MC, RM>(s, t, pre, l0, lane, base, chunk, r0);
+  } else {
+    const int l1 = min(r1, l0 + NPW);
+    uint32_t *pf = (uint32_t *)(p_smem + 4 * (size_t)PLds<P_HS>::bytes + (size_t)wave * P_PF_BYTES);
+    const uint32_t pfa =
+        __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(__attribute__((address_space(3))) uint32_t *)pf);
+    p_prefetch(s, t, mtraw, l0, lane, pfa);
+    for (int li = l0; li < l1; li++) {
+      // the kernel arguments and the lane index pass through empty asm each node, so the
+      // compiler re-derives what it needs per node instead of hoisting every address and
+      // lane-dependent value out of the loop (that held 120 VGPRs live: occupancy 4).
+      // (s is the first kernel argument: it sits at offset 0 of the kernarg segment)
+      const __attribute__((address_space(4))) PState *ka =
+          (const __attribute__((address_space(4))) PState *)__builtin_amdgcn_kernarg_segment_ptr();
+      asm volatile("" : "+s"(ka));
+      const PState &ss = *(const PState *)ka;
+      int ln = lane;
+      asm volatile("" : "+v"(ln));
+      const int tt = t, cc = chunk, rr = r0;
+      const uint32_t *mt = mtraw;
+      // the node before is done except for its stores: retire them (and, for the compiler's
+      // bookkeeping, every load it issued), so no stale pending load makes it wait on the DMA
+      // issued next
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+      const uint32_t pv = ln < P_PF_LANES ? pf[ln] : 0u;
+      if (li + 1 < l1) p_prefetch(ss, tt, mt, li + 1, ln, pfa);
+      const PPre pre = p_unpack_next(ss, tt, li, pv, ln);
+      p_small_node<MC, RM>(ss, tt, pre, li, ln, base, cc, rr);
+    }
+  }
 }
 
 // drains the worklist gm_p_tick_small filled (a fixed grid; every wave exits when the list is done)
@@ -789,9 +876,16 @@ hipError_t gm_launch_partial_reset(const PState &s, hipStream_t st) {
 hipError_t gm_launch_partial_chunk(const PState &s, int t, const uint32_t *mtraw, int c, hipStream_t st) {
   const int r0 = (int)((int64_t)s.nloc * c / s.nchunk), r1 = (int)((int64_t)s.nloc * (c + 1) / s.nchunk);
   const bool mc = s.mc_sent != nullptr && t < s.mc_tmax;
-  if (r1 > r0)
-    hipLaunchKernelGGL(mc ? gm_p_tick_small<true> : gm_p_tick_small<false>, dim3((r1 - r0 + 3) / 4), dim3(256),
-                       4 * PLds<P_HS>::bytes, st, s, t, mtraw, c, r0, r1);
+  if (r1 > r0) {
+    const int npw = s.npw > 1 ? P_NPW : 1;
+    const bool rm = s.rows != s.n || s.G > 1 || s.nloc != s.n;  // received lists possible
+    auto *small = rm ? (s.npw > 1 ? (mc ? gm_p_tick_small<true, P_NPW, true> : gm_p_tick_small<false, P_NPW, true>)
+                                  : (mc ? gm_p_tick_small<true, 1, true> : gm_p_tick_small<false, 1, true>))
+                     : (s.npw > 1 ? (mc ? gm_p_tick_small<true, P_NPW, false> : gm_p_tick_small<false, P_NPW, false>)
+                                  : (mc ? gm_p_tick_small<true, 1, false> : gm_p_tick_small<false, 1, false>));
+    hipLaunchKernelGGL(small, dim3((r1 - r0 + 4 * npw - 1) / (4 * npw)), dim3(256),
+                       4 * (PLds<P_HS>::bytes + (npw > 1 ? P_PF_BYTES : 0)), st, s, t, mtraw, c, r0, r1);
+  }
   hipLaunchKernelGGL(mc ? gm_p_tick_big<true> : gm_p_tick_big<false>, dim3(P_BIG_GRID), dim3(256),
                      4 * PLds<P_HB>::bytes, st, s, t, mtraw, c, r0);
   hipLaunchKernelGGL(mc ? gm_p_tick_huge<true> : gm_p_tick_huge<false>, dim3(P_HUGE_GRID), dim3(64),
