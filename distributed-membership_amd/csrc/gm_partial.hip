@@ -252,13 +252,27 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
     for (int q = 0; q < H / 128; q++) z[lane + 64 * q] = make_uint4(0, 0, 0, 0);
   }
   const int kk = min(k, KK);
-  const int per = 64 / V, l = lane % V, jo = lane / V;
+  // lists per load step (per), entry (l) and list slot (jo) of this lane; V = 32 (S-C) takes the
+  // shifts instead of three integer divisions. The step's per-list values come by ds_bpermute
+  // (the LDS port) rather than two readlanes + a select: VALU issue is what bounds this kernel
+  const bool v32 = V == P_VMAX;
+  int per, l, jo;
+  if (v32) {
+    per = 2;
+    l = lane & 31;
+    jo = lane >> 5;
+  } else {
+    per = 64 / V;
+    l = lane % V;
+    jo = lane / V;
+  }
+  auto step_val = [&](int v, int st) -> int { return __shfl(v, min(st * per + jo, 63), 64); };  // v of lane st * per + jo
   uint64_t dv[NSTEP];
 #pragma unroll
   for (int st = 0; st < NSTEP; st++) {
     const int j = st * per + jo;
     const bool ok = jo < per && j < kk;
-    const int sn = __shfl(sv, ok ? j : 0, 64);
+    const int sn = step_val(sv, st);
     uint64_t e = 0;
     if (ok && (!RM || sn < s.nloc)) {
       e = prev[(size_t)sn * V + l];
@@ -298,8 +312,8 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
       bool take = e != 0 && (uint32_t)e >= tfresh;
       const uint32_t id = (uint32_t)(e >> 32);
       if (dropping && __ballot(take)) {  // per-entry drops keyed by (t_send, src, dst, id-1): lost iff the
-        const int j = min(st * per + jo, 63);  // top 16 bits of fmix32(pair ^ (id-1)) are below the threshold
-        const uint32_t pair = __shfl(pairv, j, 64);
+        // top 16 bits of fmix32(pair ^ (id-1)) are below the threshold
+        const uint32_t pair = (uint32_t)step_val((int)pairv, st);
         take = take && (gm_fmix32(pair ^ (id - 1)) >> 16) >= dthr;
       }
       if (take) (void)p_insert<H>(tid, thb, id, id, (uint32_t)e);
