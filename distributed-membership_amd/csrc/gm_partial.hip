@@ -735,8 +735,8 @@ __device__ __forceinline__ void p_small_node(const PState &s, int t, const PPre 
 // node before it (p_prefetch), so a node starts with one global round trip (its delivered
 // lists) instead of two
 template <bool MC, int NPW, bool RM>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NPW > 1 ? 8 : 1, 8))) void gm_p_tick_small(PState s, int t, const uint32_t *mtraw, int chunk, int r0,
-                                                       int r1) {
+__device__ __forceinline__ void p_tick_small(const PState &s, int t, const uint32_t *mtraw, int chunk, int r0,
+                                             int r1) {
   extern __shared__ __align__(16) unsigned char p_smem[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int l0 = r0 + (blockIdx.x * 4 + wave) * NPW;
@@ -774,6 +774,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NPW > 1 ? 8
       p_small_node<MC, RM>(ss, tt, pre, li, ln, base, cc, rr);
     }
   }
+}
+template <bool MC, bool RM>
+__global__ __launch_bounds__(256) void gm_p_tick_small(PState s, int t, const uint32_t *mtraw, int chunk, int r0,
+                                                       int r1) {
+  p_tick_small<MC, 1, RM>(s, t, mtraw, chunk, r0, r1);
+}
+// P_NPW nodes per wave, held to 8 waves per SIMD (64 VGPRs; the loop keeps more live otherwise,
+// and some SGPRs spill to VGPR lanes: ~40 more VALU per node, still the faster variant)
+template <bool MC, bool RM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void gm_p_tick_small_pf(
+    PState s, int t, const uint32_t *mtraw, int chunk, int r0, int r1) {
+  p_tick_small<MC, P_NPW, RM>(s, t, mtraw, chunk, r0, r1);
 }
 
 // drains the worklist gm_p_tick_small filled (a fixed grid; every wave exits when the list is done)
@@ -893,10 +905,10 @@ hipError_t gm_launch_partial_chunk(const PState &s, int t, const uint32_t *mtraw
   if (r1 > r0) {
     const int npw = s.npw > 1 ? P_NPW : 1;
     const bool rm = s.rows != s.n || s.G > 1 || s.nloc != s.n;  // received lists possible
-    auto *small = rm ? (s.npw > 1 ? (mc ? gm_p_tick_small<true, P_NPW, true> : gm_p_tick_small<false, P_NPW, true>)
-                                  : (mc ? gm_p_tick_small<true, 1, true> : gm_p_tick_small<false, 1, true>))
-                     : (s.npw > 1 ? (mc ? gm_p_tick_small<true, P_NPW, false> : gm_p_tick_small<false, P_NPW, false>)
-                                  : (mc ? gm_p_tick_small<true, 1, false> : gm_p_tick_small<false, 1, false>));
+    auto *small = rm ? (s.npw > 1 ? (mc ? gm_p_tick_small_pf<true, true> : gm_p_tick_small_pf<false, true>)
+                                  : (mc ? gm_p_tick_small<true, true> : gm_p_tick_small<false, true>))
+                     : (s.npw > 1 ? (mc ? gm_p_tick_small_pf<true, false> : gm_p_tick_small_pf<false, false>)
+                                  : (mc ? gm_p_tick_small<true, false> : gm_p_tick_small<false, false>));
     hipLaunchKernelGGL(small, dim3((r1 - r0 + 4 * npw - 1) / (4 * npw)), dim3(256),
                        4 * (PLds<P_HS>::bytes + (npw > 1 ? P_PF_BYTES : 0)), st, s, t, mtraw, c, r0, r1);
   }
