@@ -3,9 +3,10 @@
 #include <stdint.h>
 
 #define P_VMAX 32        // view capacity limit (a list is one half-wave of 8-byte entries)
-#define P_KSMALL 10      // nodes with <= P_KSMALL delivered lists take the small-table kernel
+#define P_KSMALL 12      // nodes with <= P_KSMALL delivered lists take the small-table kernel
 #define P_KP 16          // nodes with P_KSMALL < k <= P_KP lists take the big-table kernel, more the huge one
-#define P_HS 512         // small kernel: LDS hash slots per wave (>= (1 + P_KSMALL) * P_VMAX / 0.69)
+#define P_HS 512         // small kernel: LDS hash slots per wave (union <= (1 + P_KSMALL) * P_VMAX + 1 < P_HS - 64:
+                         //   the sweep parks dead slots past the dense range; 12 lists = 0.2 % Poisson(5) tail left)
 #define P_HB 1024        // big kernel: LDS hash slots per wave (>= (1 + P_KP) * P_VMAX / 0.53)
 #define P_HH 4096        // huge kernel: LDS hash slots per wave (>= (1 + P_KMAX) * P_VMAX / 0.51)
 #define P_KMAX 64        // inbox capacity (lists queued per receiver per tick); every list is merged
@@ -15,6 +16,8 @@
 // Wire entry of an exchanged list: id | (2t-1 - hb) << 25, only entries fresh at the
 // sender's tick t (the receiver drops the others anyway), 0 = none: 4 bytes instead of 8.
 #define P_WIRE_IDBITS 25
+
+static_assert((1 + P_KSMALL) * P_VMAX + 1 < P_HS - 64, "small table: the dense range must end below the trash slots");
 
 struct PState {
   int n;                 // nodes of the whole cluster

@@ -29,7 +29,7 @@
 //      id-sorted list, stored as one coalesced row;
 //   6. the gossip draw: the 16 precomputed S2 outputs resolved in parallel across
 //      the wave (duplicates by shuffle-compares), the rare rest on scalars.
-// Nodes with more than P_KSMALL delivered lists (Poisson tail, ~1.4 %) do not fit
+// Nodes with more than P_KSMALL delivered lists (Poisson tail, ~0.2 % at 12) do not fit
 // the small table: the small kernel defers them to a worklist that the big
 // kernel (1024-slot table) drains, and those with more than P_KP lists (~2e-5) to the
 // huge kernel's (4096 slots): every delivered list is merged, as EmulNet delivers them all.
