@@ -161,17 +161,18 @@ __device__ __forceinline__ u16x2 narrow2(u16x2 v2, u16x2 pres, u16x2 &bad) {
   return enc * (pres - bad) + bad;
 }
 
-// bit q (0..15) set where byte q of a lane's 16 stored bytes is an escape code (1..15: low
-// nibble non-zero, high nibble zero), SWAR per dword (no carries cross a byte)
+// bit q (0..15) set where byte q of a lane's 16 stored bytes is the escape code S_B_ESC (the
+// narrowing writes no other code below 16): x = w ^ 0x01010101 has a zero byte exactly there,
+// found by the carry-free SWAR zero-byte test (no carries cross a byte)
 __device__ __forceinline__ uint32_t esc_mask16(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
+  static_assert(S_B_ESC == 1u, "esc_mask16 tests for the byte 0x01");
   const uint32_t w[4] = {w0, w1, w2, w3};
   uint32_t m = 0;
 #pragma unroll
   for (int i = 0; i < 4; i++) {
-    const uint32_t lo = ((w[i] & 0x0F0F0F0Fu) + 0x7F7F7F7Fu) & 0x80808080u;
-    const uint32_t hi = (((w[i] >> 1) & 0x78787878u) + 0x78787878u) & 0x80808080u;
-    const uint32_t e = (lo & ~hi) >> 7;                    // bits 0, 8, 16, 24
-    m |= (((e * 0x00204081u) >> 21) & 0xFu) << (4 * i);  // gathered to bits 21..24 (no two terms collide)
+    const uint32_t x = w[i] ^ 0x01010101u;
+    const uint32_t e = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;  // bit 7 of each zero byte
+    m |= ((((e >> 7) * 0x00204081u) >> 21) & 0xFu) << (4 * i);  // bits 0, 8, 16, 24 gathered to 21..24 (no two terms collide)
   }
   return m;
 }
@@ -278,14 +279,23 @@ __device__ __forceinline__ void esc_park(uint32_t *lds, int lane, const uint32_t
   mine[0] = (u32x4){cw[0], cw[1], cw[2], cw[3]};
   mine[1] = (u32x4){cw[4], cw[5], cw[6], cw[7]};
 }
-__device__ __forceinline__ void esc_emit(uint32_t *lds, int lane, const EscList &l, int eoff, uint32_t em, int colb) {
+// inl_only (row-uniform): the list fits its inline slot, so no entry needs the pool address.
+// An escaped cell that is present with h <= 2 sets GM_ERR_LAG (its next re-base would wrap);
+// only escaped cells can be that low (a stored byte holds h >= 226)
+__device__ __forceinline__ void esc_emit(uint32_t *lds, int lane, const EscList &l, int eoff, uint32_t em, int colb,
+                                         bool inl_only, uint32_t *err) {
   if (!em) return;
   const uint16_t *cells = (const uint16_t *)(lds + lane * 8);
   int j = eoff;
+  bool low = false;
   for (uint32_t m = em; m; m &= m - 1) {
     const int q = __builtin_ctz(m);
-    *l.at(j++) = (uint32_t)(colb + q) | ((uint32_t)cells[q] << 16);
+    const uint32_t c = cells[q];
+    low |= c < (uint32_t)S_CELL(3, 0);
+    *(inl_only ? l.inl + j : l.at(j)) = (uint32_t)(colb + q) | (c << 16);
+    j++;
   }
+  if (low) atomicOr(err, GM_ERR_LAG);
 }
 
 // Payload nibbles (gm_scaled.h S_NIB_*): dword w of a lane's 8-byte slice holds cells
@@ -663,11 +673,7 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
     const bool esc_row = row_any<LPR>(esc_st, sub);
     uint32_t em = 0;  // the lane's escaped cells (entries of this tick's list, emitted after the stores)
     if (esc_row) {  // rare: cells the byte cannot hold; the lane's cells wait in its LDS slot
-      if (esc_st) {
-        u16x2 lagmin = (u16x2)(0xFFFF);
-#pragma unroll
-        for (int i = 0; i < 8; i++) lagmin = __builtin_elementwise_min(lagmin, pk(cw[i]) - (u16x2)(32));
-        if (__builtin_elementwise_min(lagmin.x, lagmin.y) < 64) atomicOr(s.err, GM_ERR_LAG);  // present with h <= 2
+      if (esc_st) {  // (a present cell with h <= 2 escapes: esc_emit flags it)
         em = esc_mask16(bw[0], bw[1], bw[2], bw[3]);
         esc_park(lds, lane, cw);
       }
@@ -737,7 +743,7 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
       int etot;
       const int eoff = row_scan<LPR>(__builtin_popcount(em), li, lane, etot);
       eb_out = row_alloc<LPR>(s, par, slab, r, etot, li, lane);
-      if (eb_out != 0) esc_emit(lds, lane, esc_list(s, par, slab, r, eb_out), eoff, em, li * Q);
+      if (eb_out != 0) esc_emit(lds, lane, esc_list(s, par, slab, r, eb_out), eoff, em, li * Q, etot <= S_ESC_IN, s.err);
     }
   }
   if (DROP && s.mc_rdrop) {  // msgcount: the row's kept entries (wave-uniform test)
@@ -1519,7 +1525,7 @@ __global__ __launch_bounds__(256) void gm_s_init(SState s, int warm, int t0, uin
   __shared__ uint32_t lds_all[4 * S_LDS_WAVE_WORDS];
   uint32_t *lds = lds_all + (threadIdx.x >> 6) * S_LDS_WAVE_WORDS;
   if (em) esc_park(lds, lane, cw);
-  if (base != 0) esc_emit(lds, lane, esc_list(s, par, slab, r, base), eoff, em, li * Q);
+  if (base != 0) esc_emit(lds, lane, esc_list(s, par, slab, r, base), eoff, em, li * Q, etot <= S_ESC_IN, s.err);
   if (!row) return;
   *(u32x4 *)(s.table + (slab + r) * B + li * Q) = (u32x4){bw[0], bw[1], bw[2], bw[3]};
   if (li == 0) {
