@@ -33,7 +33,8 @@
 //                 (codes 2..15, h4 = 0, are unused)
 // Cells outside the byte's range (odd h of cold-start / JOINREQ entries, lag > 14 or age > 15,
 // e.g. a crashed node's entries in the ticks before TREMOVE) escape. The pool is COMPACT: per
-// (band, row) the escaped cells of the row's band slice, in column order, as consecutive u16
+// (band, row) the escaped cells of the row's band slice (lane by lane; entries carry their columns,
+// so the order is not significant), as consecutive u32
 // ENTRIES of the tick that wrote them (tick parity: written at t, read at t+1), one u32 per
 // escaped cell: its column in the band (low 16 bits) | its 16-bit cell << 16. The first S_ESC_IN
 // entries sit in the list's fixed inline slot (no allocation: a crash window escapes ~1 % of a

@@ -161,9 +161,11 @@ __device__ __forceinline__ u16x2 narrow2(u16x2 v2, u16x2 pres, u16x2 &bad) {
   return enc * (pres - bad) + bad;
 }
 
-// bit q (0..15) set where byte q of a lane's 16 stored bytes is the escape code S_B_ESC (the
-// narrowing writes no other code below 16): x = w ^ 0x01010101 has a zero byte exactly there,
-// found by the carry-free SWAR zero-byte test (no carries cross a byte)
+// The lane's escaped cells as a mask: bit 8j + i set where byte j of stored dword i (cell 4i + j)
+// is the escape code S_B_ESC (the narrowing writes no other code below 16). x = w ^ 0x01010101 has
+// a zero byte exactly there (carry-free SWAR zero-byte test); the four dwords' byte flags are
+// merged by shifts alone (no quarter-rate 32-bit multiply to gather them). esc_cell maps a bit
+// back to its cell; the list's entries carry their columns, so their order is not significant.
 __device__ __forceinline__ uint32_t esc_mask16(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
   static_assert(S_B_ESC == 1u, "esc_mask16 tests for the byte 0x01");
   const uint32_t w[4] = {w0, w1, w2, w3};
@@ -172,10 +174,11 @@ __device__ __forceinline__ uint32_t esc_mask16(uint32_t w0, uint32_t w1, uint32_
   for (int i = 0; i < 4; i++) {
     const uint32_t x = w[i] ^ 0x01010101u;
     const uint32_t e = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;  // bit 7 of each zero byte
-    m |= ((((e >> 7) * 0x00204081u) >> 21) & 0xFu) << (4 * i);  // bits 0, 8, 16, 24 gathered to 21..24 (no two terms collide)
+    m |= e >> (7 - i);
   }
   return m;
 }
+__device__ __forceinline__ int esc_cell(int p) { return ((p & 7) << 2) | (p >> 3); }
 
 // exclusive prefix of v over the LPR aligned lanes of this lane's row, and the row total;
 // every lane of the row is active (the callers branch on row-uniform conditions only)
@@ -271,8 +274,9 @@ __device__ __forceinline__ void esc_apply(uint32_t *lds, int lane, int li, const
 }
 
 // Writer: the lane's 16 swept cells wait in its LDS slot (esc_park, right after the sweep, so
-// they need no registers through the stores); its escaped cells (mask em) become entries eoff,
-// eoff + 1, ... of the list, a set bit's cell one dynamic LDS read (no register indexing).
+// they need no registers through the stores); its escaped cells (mask em, esc_mask16's bit order)
+// become entries eoff, eoff + 1, ... of the list, a set bit's cell one dynamic LDS read (no
+// register indexing).
 // colb = the lane's first column in the band.
 __device__ __forceinline__ void esc_park(uint32_t *lds, int lane, const uint32_t cw[8]) {
   u32x4 *mine = (u32x4 *)(lds + lane * 8);
@@ -289,7 +293,7 @@ __device__ __forceinline__ void esc_emit(uint32_t *lds, int lane, const EscList 
   int j = eoff;
   bool low = false;
   for (uint32_t m = em; m; m &= m - 1) {
-    const int q = __builtin_ctz(m);
+    const int q = esc_cell(__builtin_ctz(m));
     const uint32_t c = cells[q];
     low |= c < (uint32_t)S_CELL(3, 0);
     *(inl_only ? l.inl + j : l.at(j)) = (uint32_t)(colb + q) | (c << 16);
