@@ -651,27 +651,26 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
     int ngone = 0;
     uint32_t gmask = 0;  // lane cells removed this tick (bit q = cell q)
     if (__builtin_elementwise_max(amax.x, amax.y) >= GM_TREMOVE) {
-      // rare: age >= TREMOVE removes (MP1Node.cpp:429-444) -- the lane's cells again, with the
-      // removed ones absent (they sent nothing: stale, so the nibbles stand)
+      // rare: age >= TREMOVE removes (MP1Node.cpp:429-444): the removed cells' stored bytes
+      // become 0 (absent) and leave the present count. They sent nothing (stale: the nibbles
+      // stand) and were escaped (age > 15), so the lane's escape flag is re-taken from the stored
+      // bytes. cw keeps their old cells: only the escape mask's cells and fresh cells are read
+      // from it afterwards
       u16x2 ng2 = (u16x2)(0);
-      np2 = badv = (u16x2)(0);
+      uint32_t gprev = 0;
 #pragma unroll
       for (int i = 0; i < 8; i++) {
         const u16x2 v = pk(cw[i]);
         const u16x2 gone = ((v & (u16x2)(31)) + (u16x2)(32 - GM_TREMOVE)) >> (u16x2)(5);
         gmask |= ((unpk(gone) & 1u) | ((unpk(gone) >> 15) & 2u)) << (2 * i);
-        const u16x2 v2 = v * ((u16x2)(1) - gone);
-        const u16x2 pres = pmin1(v2);
-        np2 = padd(np2, pres);
         ng2 = padd(ng2, gone);
-        u16x2 bad;
-        const u16x2 b = narrow2(v2, pres, bad);
-        badv |= bad;
-        cw[i] = unpk(v2);
-        if (i & 1) bw[i >> 1] = __builtin_amdgcn_perm(unpk(b), bprev, 0x06040200u);
-        else bprev = unpk(b);
+        const uint32_t gb = unpk(gone * (u16x2)(0xFF));  // 0xFF in the low byte of a removed cell's half
+        if (i & 1) bw[i >> 1] &= ~__builtin_amdgcn_perm(gb, gprev, 0x06040200u);
+        else gprev = gb;
       }
+      np2 = np2 - ng2;
       ngone = (int)ng2.x + (int)ng2.y;
+      badv = (u16x2)(esc_mask16(bw[0], bw[1], bw[2], bw[3]) != 0 ? 1 : 0);
     }
     esc_st = unpk(badv) != 0;
     const bool esc_row = row_any<LPR>(esc_st, sub);
@@ -852,7 +851,10 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
 #define GM_DROP_MINW 8  // the keyed-loss instantiation at 8 waves per SIMD (64 VGPRs + 20 B of spills: 7.39 ms vs 7.63 at its own 79 VGPRs)
 #endif
 template <int B, bool DROP>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DROP ? GM_DROP_MINW : 1, 8))) void gm_s_band(SState s, int t, int drop_pct) {
+#ifndef GM_BAND_MINW
+#define GM_BAND_MINW 1
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DROP ? GM_DROP_MINW : GM_BAND_MINW, 8))) void gm_s_band(SState s, int t, int drop_pct) {
   constexpr int RPW = 64 / (B / S_COLS_PER_LANE);
   const int U = (s.n + RPW - 1) / RPW;
   // grid (units of a band / 4, bands): blockIdx.y is the band, so workgroups still dispatch
