@@ -502,9 +502,8 @@ static int create_partial(gm_ctx *c) {
   p.drop_pct = -1;
   TRY(dalloc(c, &p.lists, (size_t)2 * p.rows * p.V));
   for (int q = 0; q < 2; q++) {
-    TRY(dalloc(c, &p.inbox_cnt[q], nl));
     TRY(dalloc(c, &p.inbox[q], (size_t)nl * P_KMAX));
-    HIPCHECK(hipMemset(p.inbox_cnt[q], 0, sizeof(int32_t) * nl));
+    HIPCHECK(hipMemset(p.inbox[q], 0, sizeof(int32_t) * nl * P_KMAX));  // the counts (slot 0) start at 0
     if (G > 1) TRY(dalloc(c, &p.rsrc[q], R));
     if (G == 1) p.rsrc[q] = nullptr;
   }
@@ -532,7 +531,7 @@ static int create_partial(gm_ctx *c) {
   c->p_sharded = G > 1 || (getenv("GM_FORCE_SHARD") && atoi(getenv("GM_FORCE_SHARD")) == 1);
   // row shards pipeline their exchange over K chunks of their nodes (GM_CHUNKS, default 4)
   p.nchunk = c->p_sharded ? (getenv("GM_CHUNKS") ? atoi(getenv("GM_CHUNKS")) : 4) : 1;
-  p.kcap = inbox_cap(P_KMAX);
+  p.kcap = inbox_cap(P_KMAX - 1);
   p.npw = getenv("GM_P_NPW") ? std::max(1, atoi(getenv("GM_P_NPW"))) : P_NPW;
   if (p.nchunk < 1 || p.nchunk > 64) return GM_EINVAL;
   TRY(dalloc(c, &p.big_cnt, p.nchunk));

@@ -9,7 +9,7 @@
                          //   the sweep parks dead slots past the dense range; 12 lists = 0.2 % Poisson(5) tail left)
 #define P_HB 1024        // big kernel: LDS hash slots per wave (>= (1 + P_KP) * P_VMAX / 0.53)
 #define P_HH 4096        // huge kernel: LDS hash slots per wave (>= (1 + P_KMAX) * P_VMAX / 0.51)
-#define P_KMAX 64        // inbox capacity (lists queued per receiver per tick); every list is merged
+#define P_KMAX 64        // inbox row: count + P_KMAX - 1 = 63 lists queued per receiver per tick; every list is merged
 #define P_NPW 4          // small kernel: consecutive nodes per wave when prefetching (PState.npw > 1)
 #define P_EV_ADD 1u
 #define P_EV_REMOVE 2u
@@ -30,8 +30,9 @@ struct PState {
   int drop_pct;          // per-entry drop percentage for this tick's deliveries (-1: none)
   uint64_t rd_seed, view_seed, drop_seed;
   uint64_t *lists;       // [2][rows][V] entries (id << 32 | hb), 0 = empty, sorted by id; parity t&1 written at tick t
-  int32_t *inbox_cnt[2]; // [nloc] lists queued for each receiver, by delivery-tick parity
-  int32_t *inbox[2];     // [nloc][P_KMAX] senders: local row li, or nloc + j for received record j
+  int32_t *inbox[2];     // [nloc][P_KMAX] by delivery-tick parity: slot 0 = lists queued for the receiver (the
+                         //   append counter: it shares a line with the first slots), slots 1.. = senders: local
+                         //   row li, or nloc + j for received record j
   int32_t *rsrc[2];      // [n - nloc] global sender index of each received list row, by parity
   int32_t *hbctr;        // [nloc] heartbeat counter
   int32_t *failed;       // [nloc]
@@ -59,6 +60,6 @@ struct PState {
   // entries sent (fresh entries x targets, before loss) / received (after loss, lists merged)
   uint32_t *mc_sent, *mc_recv;  // [mc_tmax][nloc]
   int mc_tmax;
-  int kcap;                     // inbox slots used (P_KMAX; lowered only by the diagnostics env GM_INBOX_CAP)
+  int kcap;                     // inbox slots used (P_KMAX - 1; lowered only by the diagnostics env GM_INBOX_CAP)
   int npw;                      // small kernel: nodes per wave (P_NPW, prefetching; 1 = one node per wave: GM_P_NPW=1)
 };

@@ -159,10 +159,10 @@ __device__ __forceinline__ PPre p_preload(const PState &s, int t, const uint32_t
   const int par = t & 1, V = s.V;
   PPre p;
   p.failed = s.failed[li];
-  p.k = s.inbox_cnt[par][li];
+  p.k = s.inbox[par][(size_t)li * P_KMAX];
   p.hbctr = s.hbctr[li];
   p.own = lane < V ? s.lists[((size_t)(par ^ 1) * s.rows + li) * V + lane] : 0ull;
-  p.sv = lane < nin ? s.inbox[par][(size_t)li * P_KMAX + lane] : 0;
+  p.sv = lane < nin ? s.inbox[par][(size_t)li * P_KMAX + 1 + lane] : 0;
   p.raw0 = lane < 16 ? mtraw[(size_t)li * 16 + lane] : 0u;
   p.roff = 0;
   return p;
@@ -179,10 +179,10 @@ __device__ __forceinline__ PPre p_preload(const PState &s, int t, const uint32_t
 __device__ __forceinline__ void p_prefetch(const PState &s, int t, const uint32_t *mtraw, int li, int lane,
                                            uint32_t lds) {
   const int par = t & 1;
-  const uint32_t *a = lane < 16   ? (const uint32_t *)s.inbox[par] + (size_t)li * P_KMAX + lane
+  const uint32_t *a = lane < 16   ? (const uint32_t *)s.inbox[par] + (size_t)li * P_KMAX + 1 + lane
                       : lane < 32 ? mtraw + (size_t)li * 16 + (lane - 16)
                       : lane == 32 ? (const uint32_t *)s.failed + li
-                      : lane == 33 ? (const uint32_t *)s.inbox_cnt[par] + li
+                      : lane == 33 ? (const uint32_t *)s.inbox[par] + (size_t)li * P_KMAX
                                    : (const uint32_t *)s.hbctr + li;
   if (lane < P_PF_LANES) {
     uint32_t keep;  // m0 = the LDS destination (lane l writes dword l); the reads of the area
@@ -236,7 +236,7 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
   const uint64_t *prev = s.lists + (size_t)(par ^ 1) * s.rows * V;
   uint64_t *cur = s.lists + (size_t)par * s.rows * V;
 
-  if (lane == 0) s.inbox_cnt[par][li] = 0;  // consumed; the append target of tick t+1
+  if (lane == 0) s.inbox[par][(size_t)li * P_KMAX] = 0;  // consumed; the append target of tick t+1
   if (k > KK) {  // the huge kernel takes up to the inbox capacity; beyond it the tick is void
     if (lane == 0) atomicOr(s.err, GM_ERR_INBOX);
     k = KK;
@@ -648,8 +648,9 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
   if (lane < ng) {
     s.targets[(size_t)li * GM_FANOUT + lane] = dst;
     if (owner == s.rank) {
-      const int slot = atomicAdd(&s.inbox_cnt[par ^ 1][dst - s.n0], 1);
-      if (slot < s.kcap) s.inbox[par ^ 1][(size_t)(dst - s.n0) * P_KMAX + slot] = li;
+      int32_t *row = s.inbox[par ^ 1] + (size_t)(dst - s.n0) * P_KMAX;  // count and slots share a line
+      const int slot = atomicAdd(row, 1);
+      if (slot < s.kcap) row[1 + slot] = li;
       else atomicOr(s.err, GM_ERR_INBOX);
     }
   }
@@ -708,7 +709,7 @@ __device__ __forceinline__ void p_frozen(const PState &s, int t, int li, int lan
   if (lane < V) s.lists[((size_t)par * s.rows + li) * V + lane] = s.lists[((size_t)(par ^ 1) * s.rows + li) * V + lane];
   if (lane < 4) s.rowstat[(size_t)li * 4 + lane] = 0;
   if (lane == 0) {
-    s.inbox_cnt[par][li] = 0;
+    s.inbox[par][(size_t)li * P_KMAX] = 0;
     s.ev_cnt[li] = 0;
   }
 }
@@ -796,7 +797,7 @@ __global__ __launch_bounds__(256, 3) void gm_p_tick_big(PState s, int t, const u
   const int nbig = s.big_cnt[chunk];
   for (int w = blockIdx.x * 4 + wave; w < nbig; w += gridDim.x * 4) {
     const int li = s.big[r0 + w];
-    const PPre pre = p_preload(s, t, mtraw, li, lane, P_KMAX);
+    const PPre pre = p_preload(s, t, mtraw, li, lane, P_KMAX - 1);
     p_node<P_HB, true, MC>(s, t, pre, li, lane, p_smem + (size_t)wave * PLds<P_HB>::bytes, chunk, r0);
   }
 }
@@ -810,7 +811,7 @@ __global__ __launch_bounds__(64) void gm_p_tick_huge(PState s, int t, const uint
   const int nh = s.huge_cnt[chunk];
   for (int w = blockIdx.x; w < nh; w += gridDim.x) {
     const int li = s.huge[r0 + w];
-    const PPre pre = p_preload(s, t, mtraw, li, lane, P_KMAX);
+    const PPre pre = p_preload(s, t, mtraw, li, lane, P_KMAX - 1);
     p_node<P_HH, true, MC>(s, t, pre, li, lane, p_smem, chunk, r0);
   }
 }
@@ -875,8 +876,9 @@ __global__ __launch_bounds__(256) void gm_p_unpack(PState s, int t, int base, in
       atomicOr(s.err, GM_ERR_INBOX);
       continue;
     }
-    const int slot = atomicAdd(&s.inbox_cnt[par ^ 1][d], 1);
-    if (slot < s.kcap) s.inbox[par ^ 1][(size_t)d * P_KMAX + slot] = s.nloc + j;
+    int32_t *row = s.inbox[par ^ 1] + (size_t)d * P_KMAX;
+    const int slot = atomicAdd(row, 1);
+    if (slot < s.kcap) row[1 + slot] = s.nloc + j;
     else atomicOr(s.err, GM_ERR_INBOX);
   }
 }
