@@ -65,8 +65,13 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--scenario", choices=["S-A", "S-C"], default="S-A",
-                   help="S-A: full membership N=65,536 (headline); S-C: partial views V=32, N=16M, 5%% drop")
+    p.add_argument("--scenario", choices=["S-A", "S-B", "S-C"], default="S-A",
+                   help="S-A: full membership N=65,536 (headline); S-B: full membership N=262,144 (the "
+                        "north_star scaling cluster); S-C: partial views V=32, N=16M, 5%% drop")
+    p.add_argument("--dry-launch", action="store_true",
+                   help="start the ranks (--gpus G), rendezvous over gloo, print one JSON line with every rank's "
+                        "RANK / WORLD_SIZE / LOCAL_RANK and stop before libgm is loaded (no GPU call)")
+    p.add_argument("--master-port", type=int, default=0, help="--gpus G > 1 launch: rendezvous port (0: a free one)")
     p.add_argument("--cluster", type=int, default=0, help="N, simulated nodes (0: the scenario's)")
     p.add_argument("--view", type=int, default=32, help="S-C view capacity V")
     p.add_argument("--prologue", type=int, default=25)
@@ -143,17 +148,79 @@ def emit(out):
         os.write(_JSON_FD, line)
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(a):
+    """`bench.py --gpus G` (G > 1) started as a plain process: run G ranks of this same
+    command under torch.distributed.run (one rank per GPU, rendezvous on 127.0.0.1) as a
+    CHILD process and return its exit code. Called before anything loads libgm or touches
+    the GPU; the child's rank 0 prints the JSON line."""
+    import subprocess
+    port = a.master_port or free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this pool (RCCL across processes)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
+
+
+def rank_env(a):
+    """(rank, world, local_rank) of this process; exits non-zero when torch.distributed.run's
+    WORLD_SIZE disagrees with --gpus (the bench would otherwise time a different job)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus:
+        sys.stderr.write(f"bench.py: WORLD_SIZE={world} but --gpus {a.gpus}\n")
+        sys.exit(2)
+    return int(os.environ.get("RANK", "0")), world, int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def gather_ranks(dist, info):
+    """every rank's launch / RCCL facts, for rank 0's JSON line"""
+    if dist is None:
+        return [info]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, info)
+    return out
+
+
+def dry_launch(a):
+    rank, world, local = rank_env(a)
+    info = {"rank": rank, "world_size": world, "local_rank": local, "pid": os.getpid(),
+            "master": f"{os.environ.get('MASTER_ADDR', '')}:{os.environ.get('MASTER_PORT', '')}"}
+    dist = None
+    if world > 1:
+        import torch.distributed as tdist
+        tdist.init_process_group("gloo")
+        dist = tdist
+    ranks = gather_ranks(dist, info)
+    if rank == 0:
+        emit({"dry_launch": True, "n_gpus": a.gpus, "scenario": a.scenario, "ranks": ranks})
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     a = parse()
+    if a.gpus < 1:
+        sys.stderr.write("bench.py: --gpus must be >= 1\n")
+        sys.exit(2)
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(a))
     quiet_stdout()
+    if a.dry_launch:
+        return dry_launch(a)
     if a.scenario == "S-C":
         return main_partial(a)
-    a.cluster = a.cluster or 65536
+    a.cluster = a.cluster or (262144 if a.scenario == "S-B" else 65536)
     rtx = Roctx()
     rtx.pause()
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    rank, world, local = rank_env(a)
     if "GM_DEVICE_OVERRIDE" in os.environ:  # diagnostics only: pin every rank to one device
         local = int(os.environ["GM_DEVICE_OVERRIDE"])
     # libgm first: it binds the system ROCm HIP runtime and RCCL it was built
@@ -258,8 +325,11 @@ def main():
             traffic_src = f"profiles/traffic_n{n}.json ({tj.get('generated', 'r01')}, rocprofv3 --pmc passes by scripts/gpu.sh pmc_sa)"
 
     value = n * a.steps / elapsed
+    ranks = gather_ranks(dist, {"rank": rank, "local_rank": local, **sim.comm_info(), "kernel_ms": kernel_ms,
+                                "columns": W, "elapsed_s": t1 - t0})
     out = {
-        "metric": "simulated node-ticks/sec + achieved HBM GB/s at N=65,536 full-membership",
+        "metric": ("simulated node-ticks/sec + achieved HBM GB/s at N=65,536 full-membership" if a.scenario == "S-A"
+                   else "simulated node-ticks/sec (S-B N=262,144 full membership)"),
         "value": value,
         "unit": "node-ticks/s",
         "value_note": "all N simulated nodes per tick, the 1% crashed (frozen) ones included",
@@ -272,11 +342,12 @@ def main():
         "vs_baseline": None,
         "dtype": "u8 cells (u16 escape lists) / 4-bit payload (integer)",
         "data": "synthetic (converged full-membership table, seeded crash set)",
-        "config": {"workload": "S-A: SCALED full membership, 1% crash at tick 10, fanout 5, TFAIL 5, TREMOVE 20"
+        "config": {"workload": f"{a.scenario}: SCALED full membership, 1% crash at tick 10, fanout 5, TFAIL 5, TREMOVE 20"
                    + (f", DIAGNOSTIC keyed {a.drop_pct}% per-entry drops" if a.drop_pct else ""),
                    "n": n, "start": f"warm t0={a.t0}" if a.t0 > 0 else "cold", "prologue_to_tick": a.prologue, "crashed": ncrash, "live": n_live,
                    "lists_per_tick": m_lists, "parallelism": f"column-shard x{world}" if world > 1 else
                    ("column-shard x1 (RCCL, forced)" if a.force_shard else "single GPU")},
+        "ranks": ranks,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                      "frac": (achieved / PEAK_HBM_GBPS) if achieved else None, "traffic": traffic,
                      "traffic_source": traffic_src,
@@ -313,9 +384,7 @@ def main_partial(a):
     One step = one tick of gm_p_tick (+ the S2 precompute gm_p_mtgen)."""
     rtx = Roctx()
     rtx.pause()
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    rank, world, local = rank_env(a)
     from membership import GM_MODE_PARTIAL, Simulator, crash_set, load_library
     from membership.abi import comm_unique_id
     from membership.sharded import rendezvous_uid
@@ -362,6 +431,9 @@ def main_partial(a):
     st = sim.tick_stats()
     assert st["err"] == 0, st
     n_live, m_lists = st["live"], st["lists"]
+    ranks = gather_ranks(dist, {"rank": rank, "local_rank": local, **sim.comm_info(), "kernel_ms": kernel_ms,
+                                "nodes": sim.shard_layout()[1], "elapsed_s": elapsed,
+                                "exchange_bytes": sim.exchange_bytes() if (world > 1 or a.force_shard) else 0})
     if dist is not None:  # max time over ranks; this rank's kernel bytes, whole-cluster counts
         import torch
         dist.barrier()
@@ -407,6 +479,7 @@ def main_partial(a):
                    "n": n, "view": V, "start": f"warm t0={t0}", "prologue_to_tick": a.prologue, "crashed": ncrash,
                    "live": n_live_all, "lists_per_tick": m_lists_all, "max_inbox": st["max_inbox"],
                    "parallelism": f"row-shard x{world} (RCCL all-to-allv of lists)" if world > 1 else "single GPU"},
+        "ranks": ranks,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                      "frac": (achieved / PEAK_HBM_GBPS) if achieved else None, "traffic": traffic,
                      "traffic_source": traffic_src,

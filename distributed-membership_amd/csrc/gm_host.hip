@@ -50,6 +50,7 @@ void gm_partial_profile_dump();
 #define GM_D_MORE GM_D_MORE_ROUND  // S2 outputs per row in later rounds (transients with many stale entries)
 #define GM_MAX_ROUNDS 4096    // draw rounds per sharded tick (16 + 64 * 4096 S2 outputs per row)
 #define GM_D_LAST GM_D_LAST_ROUND  // bounded rounds: S2 outputs of round 2 (outputs [80, 336))
+#define GM_SIG_WORDS 16      // gm_comm_init: config words every rank must agree on
 
 struct gm_ctx {
   gm_config cfg;
@@ -1557,6 +1558,53 @@ extern "C" int gm_comm_init(gm_ctx *c, const uint8_t *id128, int32_t nranks, int
   memcpy(&id, id128, sizeof id);
   HIPCHECK(hipSetDevice(c->cfg.device));
   NCCLCHECK(ncclCommInitRank(&c->comm, nranks, id, rank));
+  // Every rank must run the same cluster: the collectives' sizes follow from n, the band width
+  // (column shards) and the chunk count (row shards, GM_CHUNKS), and the replayed draws from the
+  // seeds. One all-gather of a config signature; a rank that disagrees fails here (GM_EINVAL)
+  // instead of hanging or corrupting an all-to-allv later.
+  const gm_config &g = c->cfg;
+  const int64_t sig[GM_SIG_WORDS] = {g.mode, g.n, c->s.band, c->p.V, c->p.nchunk, (int64_t)g.rd_seed, g.drop_pct,
+                                     g.drop_from, g.drop_to, (int64_t)g.drop_seed, g.init_mode, g.init_t0,
+                                     (int64_t)g.init_seed, (int64_t)g.view_seed, c->p_sharded, GM_ABI_VERSION};
+  int64_t *dsig = nullptr;
+  HIPCHECK(hipMalloc(&dsig, sizeof(int64_t) * GM_SIG_WORDS * (nranks + 1)));
+  std::vector<int64_t> all((size_t)GM_SIG_WORDS * nranks);
+  int rc = GM_OK;
+  if (hipMemcpyAsync(dsig, sig, sizeof sig, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+      ncclAllGather(dsig, dsig + GM_SIG_WORDS, GM_SIG_WORDS, ncclInt64, c->comm, c->stream) != ncclSuccess ||
+      hipMemcpyAsync(all.data(), dsig + GM_SIG_WORDS, sizeof(int64_t) * all.size(), hipMemcpyDeviceToHost,
+                     c->stream) != hipSuccess ||
+      hipStreamSynchronize(c->stream) != hipSuccess) {
+    snprintf(g_errbuf, sizeof g_errbuf, "gm_comm_init: config all-gather failed");
+    rc = GM_ECOMM;
+  }
+  (void)hipFree(dsig);
+  for (int r = 0; rc == GM_OK && r < nranks; r++)
+    for (int k = 0; k < GM_SIG_WORDS; k++)
+      if (all[(size_t)r * GM_SIG_WORDS + k] != sig[k]) {
+        snprintf(g_errbuf, sizeof g_errbuf, "gm_comm_init: rank %d disagrees on config word %d (%lld vs %lld)", r,
+                 k, (long long)all[(size_t)r * GM_SIG_WORDS + k], (long long)sig[k]);
+        rc = GM_EINVAL;
+        break;
+      }
+  if (rc != GM_OK) {
+    (void)ncclCommDestroy(c->comm);
+    c->comm = nullptr;
+  }
+  return rc;
+}
+
+extern "C" int gm_comm_info(gm_ctx *c, int32_t info[4]) {
+  if (!c || !info) return GM_EINVAL;
+  if (!c->comm) {
+    info[0] = 0, info[1] = -1, info[2] = -1, info[3] = c->cfg.device;
+    return GM_OK;
+  }
+  int cnt = 0, rk = 0, dev = 0;
+  NCCLCHECK(ncclCommCount(c->comm, &cnt));
+  NCCLCHECK(ncclCommUserRank(c->comm, &rk));
+  NCCLCHECK(ncclCommCuDevice(c->comm, &dev));
+  info[0] = cnt, info[1] = rk, info[2] = dev, info[3] = c->cfg.device;
   return GM_OK;
 }
 

@@ -39,7 +39,7 @@ EXPORTS = ["gm_parse_conf", "gm_create", "gm_destroy", "gm_tick", "gm_sync", "gm
            "gm_comm_unique_id", "gm_comm_init", "gm_shard_layout", "gm_shard_merge", "gm_shard_draw",
            "gm_shard_accept", "gm_shard_end_tick", "gm_shard_loopback", "gm_partial_loopback_tick",
            "gm_shard_exchange_bytes", "gm_keep_events", "gm_event_totals", "gm_read_views", "gm_shard_stub",
-           "gm_msgcount_record"]
+           "gm_msgcount_record", "gm_comm_info"]
 
 _lib = None
 
@@ -81,6 +81,7 @@ def load_library():
         "gm_crash_set": [i32, i32, u64, P(i32)],
         "gm_comm_unique_id": [ctypes.c_char_p],
         "gm_comm_init": [ctypes.c_void_p, ctypes.c_char_p, i32, i32],
+        "gm_comm_info": [ctypes.c_void_p, P(i32)],
         "gm_shard_layout": [ctypes.c_void_p, P(i32), P(i32)],
         "gm_shard_loopback": [P(ctypes.c_void_p), i32, i32, i32],
         "gm_partial_loopback_tick": [P(ctypes.c_void_p), i32],
@@ -289,6 +290,12 @@ class Simulator:
     # ---- column shards (SCALED multi-GPU; see membership.sharded)
     def comm_init(self, uid, nranks, rank):
         self._call("gm_comm_init", self.h, uid, nranks, rank)
+
+    def comm_info(self):
+        """{"ranks", "rank", "rccl_device", "device"} of the attached RCCL communicator (ranks 0: none)"""
+        v = (ctypes.c_int32 * 4)()
+        self._call("gm_comm_info", self.h, v)
+        return {"ranks": v[0], "rank": v[1], "rccl_device": v[2], "device": v[3]}
 
     def shard_layout(self):
         c0, w = ctypes.c_int32(), ctypes.c_int32()

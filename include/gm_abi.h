@@ -210,7 +210,13 @@ int gm_last_kernel_ms(gm_ctx *ctx, float *ms);
  * rounds before the tick is read or the next one starts). No gossip payload crosses GPUs. The phase functions expose
  * the same steps for G contexts on one device (gm_shard_loopback collectives). */
 int gm_comm_unique_id(uint8_t *out128);   /* ncclGetUniqueId, on one rank */
+/* ncclCommInitRank, then an all-gather of the config words every rank must share (mode, n,
+ * band, view, GM_CHUNKS, seeds, drop schedule, init state): GM_EINVAL if any rank differs.
+ * The seam it replaces: every MP1Node shares one Params / EmulNet (Application.cpp:47-66). */
 int gm_comm_init(gm_ctx *ctx, const uint8_t *id128, int32_t nranks, int32_t rank);
+/* info = {ranks in the RCCL communicator (0 before gm_comm_init), this rank in it (-1),
+ * the device RCCL bound (-1), the context's HIP device} */
+int gm_comm_info(gm_ctx *ctx, int32_t info[4]);
 int gm_shard_layout(gm_ctx *ctx, int32_t *c0, int32_t *w);
 int gm_shard_merge(gm_ctx *ctx);
 int gm_shard_draw(gm_ctx *ctx, int32_t round, int32_t D);
