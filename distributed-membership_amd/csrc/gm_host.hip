@@ -27,7 +27,7 @@ __global__ void gm_f_sendscan(FState s, int t);
 __global__ void gm_f_sendemit(FState s);
 __global__ void gm_f_sendprep(FState s);
 __global__ void gm_f_s1expand(FState s);
-hipError_t gm_launch_tick(const SState &s, int t, int drop_pct, bool nt, hipStream_t st, hipEvent_t k0, hipEvent_t k1,
+hipError_t gm_launch_tick(const SState &s, int t, int drop_pct, hipStream_t st, hipEvent_t k0, hipEvent_t k1,
                           bool pick);
 hipError_t gm_launch_draw(const SState &s, int t, int round, int D, int listed, hipStream_t st);
 hipError_t gm_launch_accept(const SState &s, int t, int D, int in_list, int out, hipStream_t st);
@@ -60,7 +60,6 @@ struct gm_ctx {
   hipEvent_t k0 = nullptr, k1 = nullptr;  // per-tick band-kernel events (sharded)
   std::vector<hipEvent_t> tev;            // per-tick band-kernel event pairs (single context)
   double kernel_ms_sum = 0;
-  bool nt = true;                    // non-temporal table streams (env GM_NT=0 to disable)
   int shard_sync = -1;               // sharded tick draw rounds: 1 host-driven unbounded loop, 0 bounded
                                      // stream-ordered, -1 auto (env GM_SHARD_SYNC)
   int64_t nfailed = 0;               // nodes with failed_h set (gm_set_failed; nodeStart clears it)
@@ -349,39 +348,65 @@ static int create_scaled(gm_ctx *c) {
   s.evs = s.band / 32;
   // draw kernels' LDS: 4 waves x (chunk prefix + lazy MT state); N = 262,144 on one GPU: 42 KB
   if (sizeof(uint32_t) * 4 * ((size_t)(s.wp / S_CHUNK(s.band)) + 1 + 624) > 65536) return GM_EUNSUPPORTED;
-  s.ev_spill_cap = 1u << 24;
   s.rd_seed = c->cfg.rd_seed;
   s.drop_seed = c->cfg.drop_seed;
   const size_t cells = (size_t)n * s.wp;
   TRY(dalloc(c, &s.table, cells));   // stored cell bytes
-  c->nt = !(getenv("GM_NT") && !atoi(getenv("GM_NT")));  // non-temporal table streams, default on
-  s.pipe_waves = getenv("GM_BAND_PIPE") ? std::max(0, atoi(getenv("GM_BAND_PIPE"))) : 0;
   s.kcap = inbox_cap(S_KMAX);
+  s.lag_hmin = 3;  // h <= 2: the next re-base would wrap (lag > 125 ticks)
+  if (getenv("GM_LAG_CAP")) {  // diagnostics (tests): fail at a lag > L ticks (h = 254 - 2 lag), L >= 15
+    const int L = atoi(getenv("GM_LAG_CAP"));
+    if (L < 15 || L > 125) return GM_EINVAL;
+    s.lag_hmin = 254 - 2 * L;
+  }
   c->shard_sync = getenv("GM_SHARD_SYNC") ? (atoi(getenv("GM_SHARD_SYNC")) ? 1 : 0) : -1;
   TRY(dalloc(c, &s.msg, cells));        // nibbles: 2 parities x band/2 bytes per (band, row)
   // Escape storage (gm_scaled.h), one set per tick parity: a 16-cell inline slot per (band, row)
-  // list (1/32 B per cell at B = 1024) and the pools. Up to 2^31 cells the pools hold every cell
-  // (the dense equivalent: no run can overflow them); beyond, 1/64 of the cells and 1/16 of the
+  // list (1/32 B per cell at B = 1024) and the pools. The pools are DENSE-equivalent (every
+  // list's whole slice fits its stripe's region: no run can overflow them) when that fits the
+  // memory budget -- a quarter of the device's free HBM at create, split over the shard count
+  // (G column shards of one cluster may share a device: the loopback tests) -- or always up
+  // to 2^31 cells. S-A (N = 65,536): 43 GB of dense pools, so a crash of half the cluster (the
+  // reference's multifailure schedule, Application.cpp:188-195) escapes every cell it needs.
+  // Beyond the budget the pools take what it holds, at least 1/64 of the cells and 1/16 of the
   // payload lanes -- a warm cluster escapes only a crashed node's entries in the ticks before
   // their removal (~10 per list at a 1 % crash: inline) -- and an overflow fails loudly
   // (GM_ERR_ESC -> GM_ERANGE). GM_ESC_CAP (cells; diagnostics, tests) lowers the table pool.
-  // Striped: up to 1024 stripes, >= 64 (band, row) lists each; dense = every list's whole slice
-  // fits its stripe's region (ceil(lists / S) lists of `band` cells).
-  const bool dense = cells <= (1ull << 31);
+  // Striped: >= 64 (band, row) lists per stripe (up to 1024 stripes), more stripes while a
+  // stripe's region exceeds what the list word's offset field addresses (S_EW_REGION_MAX).
   const size_t lists = (size_t)n * s.nb;
   int S = 1024;
   while (S > 1 && lists / S < 64) S >>= 1;
-  while (dense && ((lists + S - 1) / S) * s.band > S_EW_REGION_MAX) S <<= 1;  // the list word's offset field
+  auto grow = [&](size_t per_stripe_cells_total) {  // stripes so that one region fits the offset field
+    while ((per_stripe_cells_total + S - 1) / S > S_EW_REGION_MAX) S <<= 1;
+  };
+  const size_t dense_t = ((lists + 1023) / 1024) * 1024 * s.band;  // table-pool entries, dense (rounded per stripe)
+  const size_t dense_p = dense_t / 16;                              // payload-pool 16-byte slots, dense
+  const double dense_bytes = 2.0 * ((double)dense_t * 4 + (double)dense_p * 16);
+  size_t free_b = 0, total_b = 0;
+  HIPCHECK(hipMemGetInfo(&free_b, &total_b));
+  double budget = (double)free_b / 4 / G;
+  if (getenv("GM_ESC_BUDGET_GB")) budget = atof(getenv("GM_ESC_BUDGET_GB")) * 1e9;  // diagnostics (tests)
+  const bool dense = cells <= (1ull << 31) || dense_bytes <= budget;
+  size_t tcells, pslots;
+  if (dense) {
+    while (((lists + S - 1) / S) * s.band > S_EW_REGION_MAX) S <<= 1;  // the list word's offset field
+    const size_t per = (lists + S - 1) / S;  // lists per stripe (at most)
+    tcells = per * s.band * S;
+    pslots = per * (s.band / 16) * S;
+  } else {
+    const double f = std::min(1.0, std::max(1.0 / 64, budget / dense_bytes));
+    tcells = std::max<size_t>((size_t)((double)cells * f), 4 * (size_t)s.band * S);
+    pslots = std::max<size_t>((size_t)((double)cells * std::min(1.0, 4 * f) / 256), 4 * (size_t)(s.band / 16) * S);
+    grow(tcells);
+  }
   s.esc_stripes = S;
-  const size_t per = (lists + S - 1) / S;  // lists per stripe (at most)
-  size_t treg = dense ? per * s.band : std::max<size_t>(cells / 64 / S, 4 * (size_t)s.band);
-  size_t preg = dense ? per * (s.band / 16) : std::max<size_t>(cells / 256 / S, 4 * (size_t)(s.band / 16));
-  treg = std::min<size_t>(treg, S_EW_REGION_MAX);
-  preg = std::min<size_t>(preg, 0xFFFFFFF0ull / S);
+  size_t treg = std::min<size_t>((tcells + S - 1) / S, S_EW_REGION_MAX);
+  size_t preg = std::min<size_t>((pslots + S - 1) / S, 0xFFFFFFF0ull / S);
   if (getenv("GM_ESC_CAP")) treg = std::max<size_t>(1, std::min<size_t>(atol(getenv("GM_ESC_CAP")) / S, treg));
   s.tesc_region = (uint32_t)treg;
   s.pesc_region = (uint32_t)preg;
-  s.tesc_cap = (uint32_t)(treg * S);
+  s.tesc_cap = treg * S;
   s.pesc_cap = (uint32_t)(preg * S);
   for (int p = 0; p < 2; p++) {
     TRY(dalloc(c, &s.tesc_in[p], lists * S_ESC_IN));
@@ -402,6 +427,13 @@ static int create_scaled(gm_ctx *c) {
   TRY(dalloc(c, &s.failed, n));
   TRY(dalloc(c, &s.brec, (size_t)n * s.nb));
   TRY(dalloc(c, &s.ev_band, (size_t)n * s.nb * s.evs));
+  {  // event spill ring (records past a (row, band)'s E slots): up to every cell of the shard, within a
+     // 1/32 share of the free HBM (the loopback shards of one device split it); at least 2^24 records.
+     // A half-cluster crash at S-A removes ~550 M entries in its peak tick (~420 M past the slots).
+    HIPCHECK(hipMemGetInfo(&free_b, &total_b));
+    const size_t want = std::min<size_t>((size_t)n * s.wp, free_b / 32 / G / sizeof(uint64_t));
+    s.ev_spill_cap = (uint32_t)std::min<size_t>(std::max<size_t>(want, 1u << 24), 1ull << 31);
+  }
   TRY(dalloc(c, &s.ev_spill, s.ev_spill_cap));
   TRY(dalloc(c, &s.ev_spill_cnt, 1 + S_EV_STRIPES));
   TRY(dalloc(c, &s.evcum, (size_t)n * s.nb));
@@ -439,7 +471,7 @@ static int create_scaled(gm_ctx *c) {
   uint32_t ierr = 0;
   HIPCHECK(hipMemcpy(&ierr, s.err, sizeof ierr, hipMemcpyDeviceToHost));
   if (ierr) {  // a cold start escapes every cell: beyond the dense-pool size it does not fit
-    snprintf(g_errbuf, sizeof g_errbuf, "initial state overflows the escape pool (%u cells)", s.tesc_cap);
+    snprintf(g_errbuf, sizeof g_errbuf, "initial state overflows the escape pool (%zu cells)", s.tesc_cap);
     return GM_ERANGE;
   }
   HIPCHECK(hipMemset(s.ev_spill_cnt, 0, (1 + S_EV_STRIPES) * sizeof(uint32_t)));
@@ -533,7 +565,6 @@ static int create_partial(gm_ctx *c) {
   // row shards pipeline their exchange over K chunks of their nodes (GM_CHUNKS, default 4)
   p.nchunk = c->p_sharded ? (getenv("GM_CHUNKS") ? atoi(getenv("GM_CHUNKS")) : 4) : 1;
   p.kcap = inbox_cap(P_KMAX - 1);
-  p.npw = getenv("GM_P_NPW") ? std::max(1, atoi(getenv("GM_P_NPW"))) : P_NPW;
   if (p.nchunk < 1 || p.nchunk > 64) return GM_EINVAL;
   TRY(dalloc(c, &p.big_cnt, p.nchunk));
   TRY(dalloc(c, &p.huge_cnt, p.nchunk));
@@ -786,7 +817,7 @@ static int tick_scaled(gm_ctx *c) {
   const bool drop = c->cfg.drop_pct > 0 && t_send >= c->cfg.drop_from && t_send < c->cfg.drop_to;
   hipEvent_t k0 = nullptr, k1 = nullptr;
   if (c->timing) TRY(timing_slot(c, &k0, &k1));
-  HIPCHECK(gm_launch_tick(c->s, c->t, drop ? c->cfg.drop_pct : -1, c->nt, c->stream, k0, k1, true));
+  HIPCHECK(gm_launch_tick(c->s, c->t, drop ? c->cfg.drop_pct : -1, c->stream, k0, k1, true));
   if (c->s.mc_sent && c->t < c->s.mc_tmax) {
     HIPCHECK(gm_launch_msgcount(c->s, c->t, drop, 0, c->stream));
     HIPCHECK(gm_launch_msgcount(c->s, c->t, drop, 1, c->stream));
@@ -1282,7 +1313,8 @@ extern "C" int gm_read_row(gm_ctx *c, int32_t r, int32_t c0, int32_t len, int32_
 struct ScaledSnapshot {
   std::vector<uint8_t> tab, row;
   std::vector<uint4> rec;
-  std::vector<uint32_t> pool, inl;
+  std::vector<std::vector<uint32_t>> pool;  // per stripe: its used part of the region
+  std::vector<uint32_t> inl;
   std::vector<uint16_t> esc;
   std::vector<int32_t> wts;
   int load(gm_ctx *c) {
@@ -1299,12 +1331,13 @@ struct ScaledSnapshot {
                        hipMemcpyDeviceToHost));
     inl.resize((size_t)s.n * s.nb * S_ESC_IN);
     HIPCHECK(hipMemcpy(inl.data(), s.tesc_in[par], sizeof(uint32_t) * inl.size(), hipMemcpyDeviceToHost));
-    pool.resize(s.tesc_cap);  // each stripe's used part, at its absolute offsets
+    pool.assign(s.esc_stripes, {});
     for (int k = 0; k < s.esc_stripes; k++) {
       const size_t used = std::min<unsigned long long>(cnt[k], s.tesc_region);
+      pool[k].resize(used);
       if (used)
-        HIPCHECK(hipMemcpy(pool.data() + (size_t)k * s.tesc_region, s.tesc[par] + (size_t)k * s.tesc_region,
-                           sizeof(uint32_t) * used, hipMemcpyDeviceToHost));
+        HIPCHECK(hipMemcpy(pool[k].data(), s.tesc[par] + (size_t)k * s.tesc_region, sizeof(uint32_t) * used,
+                           hipMemcpyDeviceToHost));
     }
     row.resize(s.wp);
     esc.resize(s.wp);
@@ -1320,10 +1353,10 @@ struct ScaledSnapshot {
       if (!k) continue;
       const uint32_t w = rec[(size_t)b * s.n + i].w;
       const size_t in = std::min<size_t>(k, S_ESC_IN);
-      if (S_EW_TOT(w) != k || S_EW_OFF(w) + (k - in) > s.tesc_region) return GM_ESTATE;
       const size_t stripe = ((size_t)b * s.n + i) & (size_t)(s.esc_stripes - 1);
+      if (S_EW_TOT(w) != k || S_EW_OFF(w) + (k - in) > pool[stripe].size()) return GM_ESTATE;
       TRY(place_entries(s, b, pc, inl.data() + ((size_t)b * s.n + i) * S_ESC_IN,
-                        pool.data() + stripe * s.tesc_region + S_EW_OFF(w), k, esc.data()));
+                        pool[stripe].data() + (k > in ? S_EW_OFF(w) : 0), k, esc.data()));
     }
     decode_scaled_row(c, row.data(), esc.data(), wts[i], rh, rt);
     return GM_OK;
@@ -1642,7 +1675,7 @@ extern "C" int gm_shard_merge(gm_ctx *c) {
                           c->stream));
   hipEvent_t k0 = nullptr, k1 = nullptr;
   if (c->timing) TRY(timing_slot(c, &k0, &k1));
-  HIPCHECK(gm_launch_tick(c->s, c->t, drop ? c->cfg.drop_pct : -1, c->nt, c->stream, k0, k1, false));
+  HIPCHECK(gm_launch_tick(c->s, c->t, drop ? c->cfg.drop_pct : -1, c->stream, k0, k1, false));
   // msgcount: this shard's fresh counts (its columns), SUM-allreduced before the draws
   if (mc_on(c, c->t)) HIPCHECK(gm_launch_msgcount(c->s, c->t, drop, 0, c->stream));
   return GM_OK;

@@ -10,7 +10,7 @@
 #define P_HB 1024        // big kernel: LDS hash slots per wave (>= (1 + P_KP) * P_VMAX / 0.53)
 #define P_HH 4096        // huge kernel: LDS hash slots per wave (>= (1 + P_KMAX) * P_VMAX / 0.51)
 #define P_KMAX 64        // inbox row: count + P_KMAX - 1 = 63 lists queued per receiver per tick; every list is merged
-#define P_NPW 8          // small kernel: consecutive nodes per wave when prefetching (PState.npw > 1; 8: 26.1 ms vs 4: 26.3)
+#define P_NPW 8          // small kernel: consecutive nodes per wave, prefetching (8: 26.1 ms vs 4: 26.3)
 #define P_EV_ADD 1u
 #define P_EV_REMOVE 2u
 // Wire entry of an exchanged list: id | (2t-1 - hb) << 25, only entries fresh at the
@@ -61,5 +61,4 @@ struct PState {
   uint32_t *mc_sent, *mc_recv;  // [mc_tmax][nloc]
   int mc_tmax;
   int kcap;                     // inbox slots used (P_KMAX - 1; lowered only by the diagnostics env GM_INBOX_CAP)
-  int npw;                      // small kernel: nodes per wave (P_NPW, prefetching; 1 = one node per wave: GM_P_NPW=1)
 };

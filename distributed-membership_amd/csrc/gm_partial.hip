@@ -237,9 +237,10 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
   uint64_t *cur = s.lists + (size_t)par * s.rows * V;
 
   if (lane == 0) s.inbox[par][(size_t)li * P_KMAX] = 0;  // consumed; the append target of tick t+1
-  if (k > KK) {  // the huge kernel takes up to the inbox capacity; beyond it the tick is void
+  const int kmax = min(KK, s.kcap);  // lists stored in the inbox row (the append counter may count more)
+  if (k > kmax) {  // the huge kernel takes up to the inbox capacity; beyond it the tick is void
     if (lane == 0) atomicOr(s.err, GM_ERR_INBOX);
-    k = KK;
+    k = kmax;  // never read sender slots that were not written
   }
   // ---- 1. loads (the independent ones arrived with `pre`)
   const uint64_t own = pre.own;
@@ -732,61 +733,46 @@ __device__ __forceinline__ void p_small_node(const PState &s, int t, const PPre 
   p_node<P_HS, false, MC, RM>(s, t, pre, li, lane, base, chunk, r0);
 }
 
-// NPW consecutive nodes per wave; with NPW > 1 each node's loads are prefetched during the
-// node before it (p_prefetch), so a node starts with one global round trip (its delivered
-// lists) instead of two
-template <bool MC, int NPW, bool RM>
-__device__ __forceinline__ void p_tick_small(const PState &s, int t, const uint32_t *mtraw, int chunk, int r0,
-                                             int r1) {
-  extern __shared__ __align__(16) unsigned char p_smem[];
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int l0 = r0 + (blockIdx.x * 4 + wave) * NPW;
-  if (l0 >= r1) return;  // whole wave; no workgroup barrier in this kernel
-  unsigned char *base = p_smem + (size_t)wave * PLds<P_HS>::bytes;
-  if constexpr (NPW == 1) {
-    const PPre pre = p_preload(s, t, mtraw, l0, lane, P_KSMALL);
-    p_small_node<MC, RM>(s, t, pre, l0, lane, base, chunk, r0);
-  } else {
-    const int l1 = min(r1, l0 + NPW);
-    uint32_t *pf = (uint32_t *)(p_smem + 4 * (size_t)PLds<P_HS>::bytes + (size_t)wave * P_PF_BYTES);
-    const uint32_t pfa =
-        __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(__attribute__((address_space(3))) uint32_t *)pf);
-    p_prefetch(s, t, mtraw, l0, lane, pfa);
-    for (int li = l0; li < l1; li++) {
-      // the kernel arguments and the lane index pass through empty asm each node, so the
-      // compiler re-derives what it needs per node instead of hoisting every address and
-      // lane-dependent value out of the loop (that held 120 VGPRs live: occupancy 4).
-      // (s is the first kernel argument: it sits at offset 0 of the kernarg segment)
-      const __attribute__((address_space(4))) PState *ka =
-          (const __attribute__((address_space(4))) PState *)__builtin_amdgcn_kernarg_segment_ptr();
-      asm volatile("" : "+s"(ka));
-      const PState &ss = *(const PState *)ka;
-      int ln = lane;
-      asm volatile("" : "+v"(ln));
-      const int tt = t, cc = chunk, rr = r0;
-      const uint32_t *mt = mtraw;
-      // the node before is done except for its stores: retire them (and, for the compiler's
-      // bookkeeping, every load it issued), so no stale pending load makes it wait on the DMA
-      // issued next
-      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-      const uint32_t pv = ln < P_PF_LANES ? pf[ln] : 0u;
-      if (li + 1 < l1) p_prefetch(ss, tt, mt, li + 1, ln, pfa);
-      const PPre pre = p_unpack_next(ss, tt, li, pv, ln);
-      p_small_node<MC, RM>(ss, tt, pre, li, ln, base, cc, rr);
-    }
-  }
-}
-template <bool MC, bool RM>
-__global__ __launch_bounds__(256) void gm_p_tick_small(PState s, int t, const uint32_t *mtraw, int chunk, int r0,
-                                                       int r1) {
-  p_tick_small<MC, 1, RM>(s, t, mtraw, chunk, r0, r1);
-}
-// P_NPW nodes per wave, held to 8 waves per SIMD (64 VGPRs; the loop keeps more live otherwise,
-// and some SGPRs spill to VGPR lanes: ~40 more VALU per node, still the faster variant)
+// P_NPW consecutive nodes per wave: each node's loads are prefetched during the node before it
+// (p_prefetch), so a node starts with one global round trip (its delivered lists) instead of two.
+// Held to 8 waves per SIMD (64 VGPRs; the loop keeps more live otherwise, and some SGPRs spill to
+// VGPR lanes: ~40 more VALU per node, still faster than one node per wave: 26.1 vs 27.5 ms)
 template <bool MC, bool RM>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void gm_p_tick_small_pf(
     PState s, int t, const uint32_t *mtraw, int chunk, int r0, int r1) {
-  p_tick_small<MC, P_NPW, RM>(s, t, mtraw, chunk, r0, r1);
+  extern __shared__ __align__(16) unsigned char p_smem[];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int l0 = r0 + (blockIdx.x * 4 + wave) * P_NPW;
+  if (l0 >= r1) return;  // whole wave; no workgroup barrier in this kernel
+  unsigned char *base = p_smem + (size_t)wave * PLds<P_HS>::bytes;
+  const int l1 = min(r1, l0 + P_NPW);
+  uint32_t *pf = (uint32_t *)(p_smem + 4 * (size_t)PLds<P_HS>::bytes + (size_t)wave * P_PF_BYTES);
+  const uint32_t pfa =
+      __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(__attribute__((address_space(3))) uint32_t *)pf);
+  p_prefetch(s, t, mtraw, l0, lane, pfa);
+  for (int li = l0; li < l1; li++) {
+    // the kernel arguments and the lane index pass through empty asm each node, so the
+    // compiler re-derives what it needs per node instead of hoisting every address and
+    // lane-dependent value out of the loop (that held 120 VGPRs live: occupancy 4).
+    // (s is the first kernel argument: it sits at offset 0 of the kernarg segment)
+    const __attribute__((address_space(4))) PState *ka =
+        (const __attribute__((address_space(4))) PState *)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(ka));
+    const PState &ss = *(const PState *)ka;
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int tt = t, cc = chunk, rr = r0;
+    const uint32_t *mt = mtraw;
+    // the node before is done except for its stores: retire them (and, for the compiler's
+    // bookkeeping, every load it issued), so no stale pending load makes it wait on the DMA
+    // issued next
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    asm volatile("" ::: "memory");       // the prefetch area is read only after the wait
+    const uint32_t pv = ln < P_PF_LANES ? pf[ln] : 0u;
+    if (li + 1 < l1) p_prefetch(ss, tt, mt, li + 1, ln, pfa);
+    const PPre pre = p_unpack_next(ss, tt, li, pv, ln);
+    p_small_node<MC, RM>(ss, tt, pre, li, ln, base, cc, rr);
+  }
 }
 
 // drains the worklist gm_p_tick_small filled (a fixed grid; every wave exits when the list is done)
@@ -905,14 +891,11 @@ hipError_t gm_launch_partial_chunk(const PState &s, int t, const uint32_t *mtraw
   const int r0 = (int)((int64_t)s.nloc * c / s.nchunk), r1 = (int)((int64_t)s.nloc * (c + 1) / s.nchunk);
   const bool mc = s.mc_sent != nullptr && t < s.mc_tmax;
   if (r1 > r0) {
-    const int npw = s.npw > 1 ? P_NPW : 1;
     const bool rm = s.rows != s.n || s.G > 1 || s.nloc != s.n;  // received lists possible
-    auto *small = rm ? (s.npw > 1 ? (mc ? gm_p_tick_small_pf<true, true> : gm_p_tick_small_pf<false, true>)
-                                  : (mc ? gm_p_tick_small<true, true> : gm_p_tick_small<false, true>))
-                     : (s.npw > 1 ? (mc ? gm_p_tick_small_pf<true, false> : gm_p_tick_small_pf<false, false>)
-                                  : (mc ? gm_p_tick_small<true, false> : gm_p_tick_small<false, false>));
-    hipLaunchKernelGGL(small, dim3((r1 - r0 + 4 * npw - 1) / (4 * npw)), dim3(256),
-                       4 * (PLds<P_HS>::bytes + (npw > 1 ? P_PF_BYTES : 0)), st, s, t, mtraw, c, r0, r1);
+    auto *small = rm ? (mc ? gm_p_tick_small_pf<true, true> : gm_p_tick_small_pf<false, true>)
+                     : (mc ? gm_p_tick_small_pf<true, false> : gm_p_tick_small_pf<false, false>);
+    hipLaunchKernelGGL(small, dim3((r1 - r0 + 4 * P_NPW - 1) / (4 * P_NPW)), dim3(256),
+                       4 * (PLds<P_HS>::bytes + P_PF_BYTES), st, s, t, mtraw, c, r0, r1);
   }
   hipLaunchKernelGGL(mc ? gm_p_tick_big<true> : gm_p_tick_big<false>, dim3(P_BIG_GRID), dim3(256),
                      4 * PLds<P_HB>::bytes, st, s, t, mtraw, c, r0);

@@ -113,7 +113,7 @@ struct SState {
   int esc_stripes;         // power of two
   unsigned long long *tesc_cnt;  // [2][esc_stripes] cells allocated per stripe this tick (zeroed a tick ahead)
   uint32_t tesc_region;    // entries per stripe
-  uint32_t tesc_cap;       // entries per pool = esc_stripes * tesc_region
+  size_t tesc_cap;         // entries per pool = esc_stripes * tesc_region
   uint8_t *msg;            // [nb][n][2][band/2] gossip payload nibbles, both tick parities of a (band, row) adjacent
   // escaped payload bytes (nibble 15): per (band, sender) of tick parity p the lanes holding escapes
   // write their 16 payload bytes h' into consecutive 16-byte slots of pesc[p] from the record's base,
@@ -145,7 +145,6 @@ struct SState {
   // rehearse the sharded protocol + RCCL on one GPU; see gm_s_draw / gm_s_accept)
   int shard_rank, shard_count;
   int sharded;
-  int pipe_waves;          // > 0: the software-pipelined band kernel with this many waves (env GM_BAND_PIPE)
   int stub;                // diagnostics (gm_shard_stub): one shard alone on a device; draws landing in
                            // other shards' columns resolve to fresh column ix (a symmetric stand-in)
   // ---- join ramp (gm_config.init_mode 2, single context): node j starts at tick j/4
@@ -178,4 +177,6 @@ struct SState {
   uint32_t *mc_rdrop;           // [n] entries a row received after keyed loss (DROP band kernel)
   int mc_tmax;
   int kcap;                     // inbox slots used (S_KMAX; lowered only by the diagnostics env GM_INBOX_CAP)
+  int lag_hmin;                 // a present cell with h < lag_hmin sets GM_ERR_LAG: 3 (lag > 125 ticks, the
+                                // encoding's limit); the diagnostics env GM_LAG_CAP=L (L >= 15) lowers it to lag > L
 };

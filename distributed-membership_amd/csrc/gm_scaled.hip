@@ -284,10 +284,10 @@ __device__ __forceinline__ void esc_park(uint32_t *lds, int lane, const uint32_t
   mine[1] = (u32x4){cw[4], cw[5], cw[6], cw[7]};
 }
 // inl_only (row-uniform): the list fits its inline slot, so no entry needs the pool address.
-// An escaped cell that is present with h <= 2 sets GM_ERR_LAG (its next re-base would wrap);
-// only escaped cells can be that low (a stored byte holds h >= 226)
+// An escaped cell that is present with h < hmin (3: h <= 2, its next re-base would wrap) sets
+// GM_ERR_LAG; only escaped cells can be that low (a stored byte holds h >= 226)
 __device__ __forceinline__ void esc_emit(uint32_t *lds, int lane, const EscList &l, int eoff, uint32_t em, int colb,
-                                         bool inl_only, uint32_t *err) {
+                                         bool inl_only, uint32_t *err, int hmin) {
   if (!em) return;
   const uint16_t *cells = (const uint16_t *)(lds + lane * 8);
   int j = eoff;
@@ -295,7 +295,7 @@ __device__ __forceinline__ void esc_emit(uint32_t *lds, int lane, const EscList 
   for (uint32_t m = em; m; m &= m - 1) {
     const int q = esc_cell(__builtin_ctz(m));
     const uint32_t c = cells[q];
-    low |= c < (uint32_t)S_CELL(3, 0);
+    low |= c < (uint32_t)S_CELL(hmin, 0);
     *(inl_only ? l.inl + j : l.at(j)) = (uint32_t)(colb + q) | (c << 16);
     j++;
   }
@@ -608,7 +608,7 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
       }
       if (s.ramp) s.mecol[r] = s.c0 + colb + tq;
       const int h = 255 - (2 * t - (hb + s_hbase(s.ramp, s.c0 + colb + tq)));
-      if (h < 3 || h > 255) atomicOr(s.err, GM_ERR_LAG);
+      if (h < s.lag_hmin || h > 255) atomicOr(s.err, GM_ERR_LAG);
 #pragma unroll
       for (int i = 0; i < 8; i++) {
         if ((tq >> 1) != i) continue;
@@ -746,7 +746,7 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
       int etot;
       const int eoff = row_scan<LPR>(__builtin_popcount(em), li, lane, etot);
       eb_out = row_alloc<LPR>(s, par, slab, r, etot, li, lane);
-      if (eb_out != 0) esc_emit(lds, lane, esc_list(s, par, slab, r, eb_out), eoff, em, li * Q, etot <= S_ESC_IN, s.err);
+      if (eb_out != 0) esc_emit(lds, lane, esc_list(s, par, slab, r, eb_out), eoff, em, li * Q, etot <= S_ESC_IN, s.err, s.lag_hmin);
     }
   }
   if (DROP && s.mc_rdrop) {  // msgcount: the row's kept entries (wave-uniform test)
@@ -874,40 +874,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DROP ? GM_D
       s.tesc_cnt[((t & 1) ^ 1) * S + i] = 0;
       s.pesc_cnt[((t & 1) ^ 1) * S + i] = 0;
     }
-  }
-}
-
-// Software-pipelined variant (GM_BAND_PIPE=<waves>): a fixed grid of waves strides over the
-// units in band-major rounds; each wave issues the next unit's metadata + table slice
-// before it merges the current one, and its payload gathers right after -- two units in
-// flight per wave instead of one dependent load chain per unit.
-template <int B>
-__global__ __launch_bounds__(256) void gm_s_band_pipe(SState s, int t, int nwaves) {
-  constexpr int RPW = 64 / (B / S_COLS_PER_LANE);
-  const int total = ((s.n + RPW - 1) / RPW) * s.nb;
-  int u = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
-  if (u >= total) return;
-  if (u == 0)
-    for (int i = threadIdx.x; i < s.esc_stripes; i += 64) {
-      s.tesc_cnt[((t & 1) ^ 1) * s.esc_stripes + i] = 0;
-      s.pesc_cnt[((t & 1) ^ 1) * s.esc_stripes + i] = 0;
-    }
-  UnitIn<B> cur, nxt;
-  u32x2 m[S_SB];
-  __shared__ uint32_t lds_all[4 * S_LDS_WAVE_WORDS];
-  const int U = (s.n + RPW - 1) / RPW;
-  unit_load<B>(s, t, u / U, u % U, cur);
-  uint32_t ent;
-  unit_gather<B, false>(s, t, cur, m, ent);
-  for (;;) {
-    const int un = u + nwaves;
-    const bool more = un < total;  // wave-uniform
-    if (more) unit_load<B>(s, t, un / U, un % U, nxt);
-    unit_finish<B, false>(s, t, -1, cur, m, ent, lds_all + (threadIdx.x >> 6) * S_LDS_WAVE_WORDS);
-    if (!more) break;
-    unit_gather<B, false>(s, t, nxt, m, ent);
-    cur = nxt;
-    u = un;
   }
 }
 
@@ -1531,7 +1497,7 @@ __global__ __launch_bounds__(256) void gm_s_init(SState s, int warm, int t0, uin
   __shared__ uint32_t lds_all[4 * S_LDS_WAVE_WORDS];
   uint32_t *lds = lds_all + (threadIdx.x >> 6) * S_LDS_WAVE_WORDS;
   if (em) esc_park(lds, lane, cw);
-  if (base != 0) esc_emit(lds, lane, esc_list(s, par, slab, r, base), eoff, em, li * Q, etot <= S_ESC_IN, s.err);
+  if (base != 0) esc_emit(lds, lane, esc_list(s, par, slab, r, base), eoff, em, li * Q, etot <= S_ESC_IN, s.err, s.lag_hmin);
   if (!row) return;
   *(u32x4 *)(s.table + (slab + r) * B + li * Q) = (u32x4){bw[0], bw[1], bw[2], bw[3]};
   if (li == 0) {
@@ -1546,7 +1512,7 @@ __global__ __launch_bounds__(256) void gm_s_init(SState s, int warm, int t0, uin
 // ------------------------------------------------------------ launch wrappers
 // (template dispatch over the band width; called by gm_host.hip)
 template <int B>
-static hipError_t launch_tick_b(const SState &s, int t, int drop_pct, bool nt, hipStream_t st, hipEvent_t k0,
+static hipError_t launch_tick_b(const SState &s, int t, int drop_pct, hipStream_t st, hipEvent_t k0,
                                 hipEvent_t k1, bool pick) {
   constexpr int RPW = 64 / (B / S_COLS_PER_LANE);
   const dim3 nblk((((s.n + RPW - 1) / RPW) + 3) / 4, s.nb);  // (units of a band / 4, bands)
@@ -1555,8 +1521,6 @@ static hipError_t launch_tick_b(const SState &s, int t, int drop_pct, bool nt, h
   hipLaunchKernelGGL(gm_s_mtgen, dim3((s.n + 255) / 256), dim3(256), 0, st, s, t);
   if (k0) (void)hipEventRecord(k0, st);
   if (drop_pct >= 0) hipLaunchKernelGGL((gm_s_band<B, true>), dim3(nblk), dim3(256), 0, st, s, t, drop_pct);
-  else if (s.pipe_waves > 0)
-    hipLaunchKernelGGL((gm_s_band_pipe<B>), dim3((s.pipe_waves + 3) / 4), dim3(256), 0, st, s, t, 4 * ((s.pipe_waves + 3) / 4));
   else hipLaunchKernelGGL((gm_s_band<B, false>), dim3(nblk), dim3(256), 0, st, s, t, drop_pct);
   if (k1) (void)hipEventRecord(k1, st);
   if (s.ramp) {
@@ -1568,14 +1532,14 @@ static hipError_t launch_tick_b(const SState &s, int t, int drop_pct, bool nt, h
   return hipGetLastError();
 }
 
-hipError_t gm_launch_tick(const SState &s, int t, int drop_pct, bool nt, hipStream_t st, hipEvent_t k0, hipEvent_t k1,
+hipError_t gm_launch_tick(const SState &s, int t, int drop_pct, hipStream_t st, hipEvent_t k0, hipEvent_t k1,
                           bool pick) {
   switch (s.band) {
-    case 64: return launch_tick_b<64>(s, t, drop_pct, nt, st, k0, k1, pick);
-    case 128: return launch_tick_b<128>(s, t, drop_pct, nt, st, k0, k1, pick);
-    case 256: return launch_tick_b<256>(s, t, drop_pct, nt, st, k0, k1, pick);
-    case 512: return launch_tick_b<512>(s, t, drop_pct, nt, st, k0, k1, pick);
-    case 1024: return launch_tick_b<1024>(s, t, drop_pct, nt, st, k0, k1, pick);
+    case 64: return launch_tick_b<64>(s, t, drop_pct, st, k0, k1, pick);
+    case 128: return launch_tick_b<128>(s, t, drop_pct, st, k0, k1, pick);
+    case 256: return launch_tick_b<256>(s, t, drop_pct, st, k0, k1, pick);
+    case 512: return launch_tick_b<512>(s, t, drop_pct, st, k0, k1, pick);
+    case 1024: return launch_tick_b<1024>(s, t, drop_pct, st, k0, k1, pick);
     default: return hipErrorInvalidValue;
   }
 }

@@ -87,8 +87,8 @@ typedef struct gm_config {
   uint64_t drop_seed;
   /* placement */
   int32_t device;          /* HIP device ordinal */
-  int32_t shard_rank;      /* column shard of this context (SCALED multi-GPU); 0 */
-  int32_t shard_count;     /* number of column shards; 1 */
+  int32_t shard_rank;      /* shard of this context: SCALED column shard / PARTIAL row shard; 0 */
+  int32_t shard_count;     /* number of shards (GPUs); 1 */
   /* SCALED initial state: 0 = cold converged start (every cell {hb 0, ts 0},
    * first tick 1); 1 = warm converged start at t0: own entry {2*t0-1, t0},
    * others {2*(t0-1-a)-1, t0-a} with a = splitmix64(init_seed, r, c) % 4,
@@ -149,7 +149,12 @@ int gm_set_dropmsg(gm_ctx *ctx, int32_t on);
 int gm_drain_events(gm_ctx *ctx, gm_event *out, size_t cap, size_t *n);
 /* on = 1 (default): keep every tick's records until drained. on = 0 (benchmarks):
  * a tick overwrites the previous tick's undrained records (no per-tick readback);
- * gm_drain_events then returns the last tick's records only. */
+ * gm_drain_events then returns the last tick's records only.
+ * Limits: with on = 1 the host stages at most 2^27 records between drains (GM_ERANGE
+ * beyond: a TREMOVE tick of S-B's 1 % crash removes ~687 M entries, of S-A's ~22 M);
+ * clusters that large run with on = 0 and read the device totals (gm_event_totals). The
+ * device keeps E = band/32 records per (row, band) plus a spill ring sized from free HBM
+ * (>= 2^24 records; GM_ERR_EVENTS -> GM_ERANGE past it). */
 int gm_keep_events(gm_ctx *ctx, int32_t on);
 /* counts[0] = records produced in the last tick (SCALED / PARTIAL telemetry; PARTIAL
  * also splits them per kind in counts[kind]; FAITHFUL: records pending per kind) */
@@ -164,8 +169,8 @@ int gm_event_totals(gm_ctx *ctx, uint64_t totals[6]);
  * SCALED / PARTIAL: the same per-entry-message counts in the list-gossip regime, recorded
  * once gm_msgcount_record was called (GM_ESTATE otherwise): sent = entries a node put on
  * the wire (its fresh entries x its targets, before loss: the loss is decided in flight),
- * recv = entries of the lists delivered to it that survived the loss (PARTIAL: of the <= 16
- * lists it merges). Gossip LIST entries only (the ramp's JOINREQ / JOINREP are not counted).
+ * recv = entries of the lists delivered to it that survived the loss (PARTIAL: of every
+ * delivered list; all are merged). Gossip LIST entries only (the ramp's JOINREQ / JOINREP are not counted).
  * A PARTIAL row shard reports its own nodes ([nloc][t]). */
 int gm_msgcount(gm_ctx *ctx, int32_t t, int32_t *sent, int32_t *recv);
 /* SCALED / PARTIAL: start recording the per-node counts of gm_msgcount for ticks < tmax

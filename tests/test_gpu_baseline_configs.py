@@ -190,3 +190,58 @@ def test_scaled_event_totals_match_drained_records():
     tot = sim.event_totals()
     assert seen[GM_EV_JOINED] > 0 and seen[GM_EV_REMOVED] > 0
     assert tot["joined"] == seen[GM_EV_JOINED] and tot["removed"] == seen[GM_EV_REMOVED], (tot, seen)
+
+
+def test_sa_half_cluster_crash_runs_clean():
+    """The reference's multifailure schedule at S-A size: half the cluster fails at
+    once (Application.cpp:188-195 fails nodes [s, s + N/2)). Every crashed node's entries escape
+    the byte cells in the ~10 ticks before their removal -- the escape pools are dense-equivalent
+    at N = 65,536 -- and ~550 M removal records of the peak tick overflow the per-(row, band)
+    slots into the spill ring. Every live observer removes exactly the crashed half, no error."""
+    n, crash_tick = 65536, 10
+    s0 = 12345
+    crash = np.arange(s0, s0 + n // 2, dtype=np.int32)
+    sim = Simulator(n, GM_MODE_SCALED, rd_seed=7, init_mode=1, init_t0=8, init_seed=11)
+    sim.keep_events(0)
+    while sim.time <= 50:
+        t = sim.time
+        sim.tick()
+        if t == crash_tick:
+            sim.set_failed(crash)
+    sim.sync()
+    st = sim.tick_stats()
+    n_live, ncrash = n - len(crash), len(crash)
+    assert st["err"] == 0 and st["live"] == n_live, st
+    tot = sim.event_totals()
+    assert tot["removed"] == n_live * ncrash and tot["joined"] == 0, tot
+    crashed = np.zeros(n, bool)
+    crashed[crash] = True
+    t = sim.time - 1
+    for r in (0, n - 1):
+        hb, ts = sim.read_row(r)
+        assert np.all(hb[crashed] == -1) and np.all(hb[~crashed] >= 0)
+        assert hb[r] == 2 * t - 1 and ts[r] == t
+    sim.close()
+
+
+def test_sa_cold_start_converges_without_false_removals():
+    """init_mode 0 at S-A size: every cell starts at {hb 0, ts 0} (odd-heartbeat cells: ALL of them
+    escape on the first ticks -- 4.3 G entries, held by the dense-equivalent pools). The epidemic
+    raises every entry long before its TREMOVE age, so nothing is removed or joined, and after
+    24 ticks every observer holds every subject with a raised heartbeat."""
+    n = 65536
+    sim = Simulator(n, GM_MODE_SCALED, rd_seed=7)
+    sim.keep_events(0)
+    while sim.time <= 24:
+        sim.tick()
+    sim.sync()
+    st = sim.tick_stats()
+    assert st["err"] == 0 and st["live"] == n, st
+    tot = sim.event_totals()
+    assert tot["removed"] == 0 and tot["joined"] == 0, tot
+    t = sim.time - 1
+    for r in (0, 4097, n - 1):
+        hb, ts = sim.read_row(r)
+        assert np.all(hb >= 1) and np.all(t - ts < TREMOVE)
+        assert hb[r] == 2 * t - 1
+    sim.close()

@@ -1,0 +1,156 @@
+"""The multi-GPU configurations of BASELINE.json at their FULL sizes, as G = 8 loopback shards on
+the one GPU of the box (VERDICT r3 missing 2), each checked against the single-context run of the
+same cluster -- which fits one 288 GB MI355X -- and by the size-independent properties:
+
+* S-B (configs[3]): N = 262,144 full membership as 8 COLUMN shards (32,768 subject columns each;
+  the multi-GPU layout of SURVEY §8(e)), the S-A schedule (warm start, 1 % crash at tick 10,
+  to tick 48 = bench.py's window). Removal totals sum to (N - 2,621) * 2,621, no joins, no error,
+  and spot rows read from the shards (columns concatenated) equal the single context's rows.
+  Reference: the TREMOVE sweep MP1Node.cpp:426-444.
+* S-C (configs[4]): N = 16,777,216, V = 32 partial views, 5 % keyed drops, as 8 ROW shards with
+  the all-to-allv exchange done by device copies (gm_partial_loopback_tick). Per-tick join /
+  removal counts and sampled views equal the single context's bit for bit; views stay full,
+  id-sorted, self-present and free of crashed ids after TFAIL.
+
+The single context runs first and is destroyed before the shards are created (both at once would
+not fit). keep_events(0): the device counts the records (gm_event_totals / gm_event_counts)."""
+import numpy as np
+import pytest
+
+from membership import GM_EV_JOINED, GM_EV_REMOVED, GM_MODE_PARTIAL, GM_MODE_SCALED, Simulator, crash_set
+from membership.abi import partial_loopback_tick
+from membership.sharded import loopback_tick
+
+pytestmark = pytest.mark.gpu
+
+G = 8
+
+
+def test_sb_full_size_column_shards_match_single_context():
+    n, crash_tick, last = 262144, 10, 48
+    ncrash = int(round(n * 0.01))
+    kw = dict(rd_seed=7, init_mode=1, init_t0=8, init_seed=11)
+    crash = crash_set(n, ncrash, 42)
+    crashed = np.zeros(n, bool)
+    crashed[crash] = True
+    rows = [r for r in (0, 1, 77777, n // 2 + 1, n - 1) if not crashed[r]]
+
+    ref = Simulator(n, GM_MODE_SCALED, **kw)
+    ref.keep_events(0)
+    while ref.time <= last:
+        t = ref.time
+        ref.tick()
+        if t == crash_tick:
+            ref.set_failed(crash)
+    ref.sync()
+    want_rows = {r: ref.read_row(r) for r in rows}
+    want_tot, want_st = ref.event_totals(), ref.tick_stats()
+    ref.close()
+    del ref
+    assert want_tot["removed"] == (n - ncrash) * ncrash and want_st["err"] == 0
+
+    shards = [Simulator(n, GM_MODE_SCALED, shard_rank=g, shard_count=G, **kw) for g in range(G)]
+    for s in shards:
+        s.keep_events(0)
+    lay = [s.shard_layout() for s in shards]
+    assert lay[0][0] == 0 and sum(w for _, w in lay) == n
+    while shards[0].time <= last:
+        t = shards[0].time
+        loopback_tick(shards)
+        if t == crash_tick:
+            for s in shards:
+                s.set_failed(crash)
+    removed = 0
+    for s, (c0, w) in zip(shards, lay):
+        st = s.tick_stats()
+        assert st["err"] == 0 and st["live"] == n - ncrash and st["lists"] == want_st["lists"]
+        tot = s.event_totals()
+        mine = int(((crash >= c0) & (crash < c0 + w)).sum())
+        assert tot["joined"] == 0 and tot["removed"] == (n - ncrash) * mine, (c0, tot)
+        removed += tot["removed"]
+    assert removed == (n - ncrash) * ncrash
+    for r in rows:
+        parts = [s.read_row(r) for s in shards]
+        hb = np.concatenate([p[0] for p in parts])
+        ts = np.concatenate([p[1] for p in parts])
+        assert np.array_equal(hb, want_rows[r][0]) and np.array_equal(ts, want_rows[r][1]), f"row {r} differs"
+        assert np.all(hb[crashed] == -1) and np.all(hb[~crashed] >= 0)
+    for s in shards:
+        s.close()
+
+
+def _check_views(views, r0, t, crashed_id, after_crash):
+    ids = (views >> np.uint64(32)).astype(np.int64)
+    hb = (views & np.uint64(0xFFFFFFFF)).astype(np.int64)
+    rows = np.arange(r0, r0 + len(views))
+    live = ~crashed_id[rows + 1]
+    ids, hb, rows = ids[live], hb[live], rows[live]
+    assert np.all(ids > 0), "a live view is not full"
+    assert np.all(np.diff(ids, axis=1) > 0), "a view is not strictly id-sorted"
+    own = ids == (rows + 1)[:, None]
+    assert np.all(own.sum(axis=1) == 1), "self missing from a view"
+    assert np.all(hb[own] == 2 * t - 1)
+    if after_crash:
+        assert not np.any(crashed_id[ids]), "a crashed node is still in a live view"
+
+
+def test_sc_full_size_row_shards_match_single_context():
+    n, v, crash_tick, last = 1 << 24, 32, 10, 30
+    ncrash = int(round(n * 0.01))
+    kw = dict(rd_seed=7, view=v, view_seed=5, init_mode=1, init_t0=8, init_seed=11, drop_pct=5, drop_from=0,
+              drop_to=1 << 20, drop_seed=42)
+    crash = crash_set(n, ncrash, 42)
+    crashed_id = np.zeros(n + 1, bool)
+    crashed_id[crash + 1] = True
+    blocks = [(0, 1 << 16), (n // 2 - 1000, 1 << 16), (n - (1 << 16), 1 << 16)]
+
+    ref = Simulator(n, GM_MODE_PARTIAL, **kw)
+    ref.keep_events(0)
+    want_counts = []
+    while ref.time <= last:
+        t = ref.time
+        ref.tick()
+        if t == crash_tick:
+            ref.set_failed(crash)
+        c = ref.event_counts()
+        want_counts.append((c[GM_EV_JOINED], c[GM_EV_REMOVED]))
+    want_views = [ref.read_views(r0, cnt) for r0, cnt in blocks]
+    want_st = ref.tick_stats()
+    ref.close()
+    del ref
+    assert want_st["err"] == 0
+
+    shards = [Simulator(n, GM_MODE_PARTIAL, shard_rank=g, shard_count=G, **kw) for g in range(G)]
+    for s in shards:
+        s.keep_events(0)
+    lay = [s.shard_layout() for s in shards]
+    assert lay[0][0] == 0 and sum(w for _, w in lay) == n
+    k = 0
+    while shards[0].time <= last:
+        t = shards[0].time
+        partial_loopback_tick(shards)
+        if t == crash_tick:
+            for s in shards:
+                s.set_failed(crash)
+        cs = [s.event_counts() for s in shards]
+        got = (sum(c[GM_EV_JOINED] for c in cs), sum(c[GM_EV_REMOVED] for c in cs))
+        assert got == want_counts[k], f"event counts differ at tick {t}: {got} vs {want_counts[k]}"
+        k += 1
+    t = shards[0].time - 1
+    for (r0, cnt), want in zip(blocks, want_views):
+        got = np.zeros_like(want)
+        for s, (a, w) in zip(shards, lay):  # the block's rows owned by each shard
+            lo, hi = max(r0, a), min(r0 + cnt, a + w)
+            if lo < hi:
+                got[lo - r0:hi - r0] = s.read_views(lo, hi - lo)  # global node indices
+        assert np.array_equal(got, want), f"views of rows [{r0}, {r0 + cnt}) differ"
+        _check_views(got, r0, t, crashed_id, after_crash=True)
+    lists = 0
+    for s in shards:
+        st = s.tick_stats()
+        assert st["err"] == 0
+        lists += st["lists"]
+        assert s.exchange_bytes() > 0  # lists really crossed the shard boundaries
+    assert lists == want_st["lists"]
+    for s in shards:
+        s.close()

@@ -2,9 +2,10 @@
 GM_ERR_INBOX and the context returns GM_ERANGE -- never a silent divergence. The
 diagnostics knob GM_INBOX_CAP lowers the compiled capacity (64 lists) so that an ordinary
 cluster overflows it on its first ticks; at the real capacity the same runs stay clean.
-(The other narrow-layout limit, GM_ERR_LAG -- a present entry lagging > ~126 ticks -- is
-not reachable under the protocol: the oracle's largest lag of a present entry at 90-98 %
-keyed loss over 300 ticks is 40 ticks)"""
+The other narrow-layout limit, GM_ERR_LAG -- a present entry lagging > 125 ticks -- is not
+reachable under the protocol (the oracle's largest lag at 95 / 98 % keyed loss over 1,000 ticks
+is 40 / 33 ticks, tests/test_oracle_limits.py); GM_LAG_CAP lowers it to show that it too fails
+loudly."""
 import pytest
 
 from membership import GM_MODE_PARTIAL, GM_MODE_SCALED, GmError, Simulator
@@ -70,3 +71,46 @@ def test_escape_pool_overflow_fails_loudly(monkeypatch):
     sim.set_failed(crash)
     assert first_error(sim, 30) == 0 and sim.tick_stats()["err"] == 0
     assert sim.event_totals()["removed"] == 64 * (n - 64)
+
+
+GM_ERR_LAG = 64
+
+
+@pytest.mark.parametrize("cap,fails", [(20, True), (45, False)])
+def test_lag_ceiling_fails_loudly(cap, fails, monkeypatch):
+    """The heartbeat-lag ceiling of the byte-cell layout (125 ticks, gm_scaled.h) lowered by the
+    diagnostics knob GM_LAG_CAP: a crashed node's entries lag L0 + age ticks until their TREMOVE
+    removal at age 20 (L0 <= ~5 at N = 1,024), so a 20-tick ceiling is crossed in the crash
+    window and the tick returns GM_ERANGE (GM_ERR_LAG), while a 45-tick one never is. The
+    protocol's own worst case is ~40 ticks at 95 % loss (tests/test_oracle_limits.py)."""
+    monkeypatch.setenv("GM_LAG_CAP", str(cap))
+    n = 1024
+    sim = Simulator(n, GM_MODE_SCALED, rd_seed=7, init_mode=1, init_t0=8, init_seed=11)
+    assert first_error(sim, 3) == 0
+    sim.set_failed(list(range(5, n, 64)))
+    code = first_error(sim, 30)
+    if fails:
+        assert code == GM_ERANGE
+    else:
+        assert code == 0 and sim.tick_stats()["err"] == 0
+        assert sim.event_totals()["removed"] == 16 * (n - 16)
+    sim.close()
+
+
+def test_heavy_loss_long_run_stays_inside_the_ceilings():
+    """95 % keyed loss for 400 ticks at N = 2,048: false removals and re-joins churn every row, the
+    lags and the escape pools stay bounded (no GM_ERR_LAG / GM_ERR_ESC) and no inbox nears 64."""
+    n = 2048
+    sim = Simulator(n, GM_MODE_SCALED, rd_seed=7, init_mode=1, init_t0=8, init_seed=11, drop_pct=95, drop_from=0,
+                    drop_to=1 << 20, drop_seed=5)
+    sim.keep_events(0)
+    worst_inbox = 0
+    for _ in range(400):
+        sim.tick()
+        worst_inbox = max(worst_inbox, sim.tick_stats()["max_inbox"])
+    st = sim.tick_stats()
+    tot = sim.event_totals()
+    assert st["err"] == 0, st
+    assert tot["removed"] > 0 and tot["joined"] > 0, tot
+    assert worst_inbox < 32, worst_inbox
+    sim.close()

@@ -56,7 +56,7 @@ def test_partial_sparse_views_remove_stale_entries():
 
 
 def test_partial_large_cluster_matches_oracle():
-    # N = 131,072: ~1.4 % of the nodes receive more than P_KSMALL = 10 lists per tick
+    # N = 131,072: ~0.2 % of the nodes receive more than P_KSMALL = 12 lists per tick
     # (the big-table kernel), ~2 per tick more than P_KP = 16 (the huge-table kernel, every list merged);
     # 5 % drops as in S-C, a crash set inside the window
     n, v = 131072, 32
@@ -114,9 +114,10 @@ def test_row_shards_match_oracle(n, v, world, drop, chunks, monkeypatch):
 
 
 def test_rccl_single_rank_row_shard_matches_oracle(monkeypatch):
-    """The RCCL exchange of the row-shard tick (ncclAllToAll of record counts, two
-    ncclAllToAllv) forced on with one rank: the multi-GPU call sequence on this box's
-    one GPU (every target is local, so the exchanged counts are zero)."""
+    """The RCCL exchange of the row-shard tick (per row chunk, two ncclAllToAllv of
+    fixed-size blocks: record headers, then the lists' fresh entries) forced on with one
+    rank: the multi-GPU call sequence on this box's one GPU (every target is local, so
+    the blocks to other ranks are empty)."""
     from membership.abi import comm_unique_id
     n, v = 2000, 32
     kw = dict(rd_seed=7, view_seed=5, init_t0=8, init_seed=11)
