@@ -1763,6 +1763,70 @@ extern "C" int gm_shard_loopback(gm_ctx **ctxs, int32_t G, int32_t what, int32_t
   return GM_OK;
 }
 
+// Host-collective hook: the phase exchange buffers of ONE shard context as plain host arrays, so
+// that any host-side collective (gloo across processes: membership.sharded.host_tick) can stand
+// in for RCCL / gm_shard_loopback. Layouts (n = cluster size, G = shard count):
+//   what 0  export: this rank's per-row (present, numfailed) int32[n][2]; import: all G slots
+//           int32[G][n][2] (the all-gather's result)
+//   what 1  export / import: the resolved draws int32[n][D]; import the MAX over the ranks
+//   what 2  (msgcount recording) export / import: uint32[n] fresh counts, plus uint32[n] kept
+//           entries on keyed-loss ticks; import the SUM over the ranks
+static int shard_buf(gm_ctx *c, int what, int D, std::vector<std::pair<void *, size_t>> &parts, bool import) {
+  const size_t n = (size_t)c->n;
+  SState &s = c->s;
+  parts.clear();
+  if (what == 0) {
+    if (import) parts.push_back({s.xcnt, sizeof(int32_t) * n * 2 * s.shard_count});
+    else parts.push_back({s.xcnt + (size_t)s.shard_rank * n * 2, sizeof(int32_t) * n * 2});
+  } else if (what == 1) {
+    if (D <= 0 || D > c->dmax) return GM_EINVAL;
+    parts.push_back({s.status, sizeof(int32_t) * n * D});
+  } else if (what == 2) {
+    if (!mc_on(c, c->t)) return GM_ESTATE;
+    parts.push_back({s.mc_fresh + (size_t)(c->t & 1) * n, sizeof(uint32_t) * n});
+    if (drop_tick(c, c->t)) parts.push_back({s.mc_rdrop, sizeof(uint32_t) * n});
+  } else {
+    return GM_EINVAL;
+  }
+  return GM_OK;
+}
+
+extern "C" int gm_shard_export(gm_ctx *c, int32_t what, int32_t D, void *out, size_t cap, size_t *bytes) {
+  if (!c || !bytes) return GM_EINVAL;
+  TRY(shard_ready(c));
+  std::vector<std::pair<void *, size_t>> parts;
+  TRY(shard_buf(c, what, D, parts, false));
+  size_t tot = 0;
+  for (auto &p : parts) tot += p.second;
+  *bytes = tot;
+  if (!out) return GM_OK;
+  if (cap < tot) return GM_ERANGE;
+  HIPCHECK(hipStreamSynchronize(c->stream));
+  size_t off = 0;
+  for (auto &p : parts) {
+    HIPCHECK(hipMemcpy((uint8_t *)out + off, p.first, p.second, hipMemcpyDeviceToHost));
+    off += p.second;
+  }
+  return GM_OK;
+}
+
+extern "C" int gm_shard_import(gm_ctx *c, int32_t what, int32_t D, const void *in, size_t bytes) {
+  if (!c || !in) return GM_EINVAL;
+  TRY(shard_ready(c));
+  std::vector<std::pair<void *, size_t>> parts;
+  TRY(shard_buf(c, what, D, parts, true));
+  size_t tot = 0;
+  for (auto &p : parts) tot += p.second;
+  if (bytes != tot) return GM_EINVAL;
+  HIPCHECK(hipStreamSynchronize(c->stream));
+  size_t off = 0;
+  for (auto &p : parts) {
+    HIPCHECK(hipMemcpy(p.first, (const uint8_t *)in + off, p.second, hipMemcpyHostToDevice));
+    off += p.second;
+  }
+  return GM_OK;
+}
+
 // Diagnostics: one column shard alone on a device (no RCCL, no peers): the all-gather of
 // per-row counts mirrors this shard's counts into every peer slot and the draw kernel
 // resolves draws landing in peer columns as fresh column ix (SState.stub) -- a symmetric

@@ -39,7 +39,7 @@ EXPORTS = ["gm_parse_conf", "gm_create", "gm_destroy", "gm_tick", "gm_sync", "gm
            "gm_comm_unique_id", "gm_comm_init", "gm_shard_layout", "gm_shard_merge", "gm_shard_draw",
            "gm_shard_accept", "gm_shard_end_tick", "gm_shard_loopback", "gm_partial_loopback_tick",
            "gm_shard_exchange_bytes", "gm_keep_events", "gm_event_totals", "gm_read_views", "gm_shard_stub",
-           "gm_msgcount_record", "gm_comm_info"]
+           "gm_msgcount_record", "gm_comm_info", "gm_shard_export", "gm_shard_import"]
 
 _lib = None
 
@@ -82,6 +82,8 @@ def load_library():
         "gm_comm_unique_id": [ctypes.c_char_p],
         "gm_comm_init": [ctypes.c_void_p, ctypes.c_char_p, i32, i32],
         "gm_comm_info": [ctypes.c_void_p, P(i32)],
+        "gm_shard_export": [ctypes.c_void_p, i32, i32, ctypes.c_void_p, sz, P(sz)],
+        "gm_shard_import": [ctypes.c_void_p, i32, i32, ctypes.c_void_p, sz],
         "gm_shard_layout": [ctypes.c_void_p, P(i32), P(i32)],
         "gm_shard_loopback": [P(ctypes.c_void_p), i32, i32, i32],
         "gm_partial_loopback_tick": [P(ctypes.c_void_p), i32],
@@ -321,6 +323,18 @@ class Simulator:
     def shard_stub(self, on):
         """Diagnostics: tick this column shard alone on its device (gm_shard_stub)."""
         self._call("gm_shard_stub", self.h, 1 if on else 0)
+
+    def shard_export(self, what, d=0):
+        """the phase exchange buffer `what` of this shard (gm_shard_export) as a flat int32 array"""
+        nb = ctypes.c_size_t()
+        self._call("gm_shard_export", self.h, what, d, None, 0, ctypes.byref(nb))
+        out = np.empty(nb.value // 4, dtype=np.int32)
+        self._call("gm_shard_export", self.h, what, d, out.ctypes.data_as(ctypes.c_void_p), nb.value, ctypes.byref(nb))
+        return out
+
+    def shard_import(self, what, arr, d=0):
+        a = np.ascontiguousarray(arr, dtype=np.int32)
+        self._call("gm_shard_import", self.h, what, d, a.ctypes.data_as(ctypes.c_void_p), a.nbytes)
 
     def shard_end_tick(self):
         self._call("gm_shard_end_tick", self.h)

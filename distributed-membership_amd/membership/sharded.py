@@ -52,6 +52,42 @@ def loopback_tick(sims):
     return rnd + 1
 
 
+def host_tick(sim, dist, group=None):
+    """One tick of THIS process's column shard with the exchanges done by a host collective
+    (torch.distributed, e.g. gloo between processes; gm_shard_export / gm_shard_import) in
+    place of RCCL: the same phases as loopback_tick, one rank per process. Returns the draw
+    rounds used."""
+    import torch
+    G = dist.get_world_size(group)
+    sim.shard_merge()
+    mine = torch.from_numpy(sim.shard_export(0))
+    slots = [torch.empty_like(mine) for _ in range(G)]
+    dist.all_gather(slots, mine, group=group)
+    sim.shard_import(0, torch.cat(slots).numpy())
+    if sim.msgcount_recording(sim.time):
+        x = torch.from_numpy(sim.shard_export(2))
+        dist.all_reduce(x, op=dist.ReduceOp.SUM, group=group)  # uint32 counts as int32: sums stay < 2^31
+        sim.shard_import(2, x.numpy())
+    rnd, d = 0, D_FIRST
+    while True:
+        sim.shard_draw(rnd, d)
+        x = torch.from_numpy(sim.shard_export(1, d))
+        dist.all_reduce(x, op=dist.ReduceOp.MAX, group=group)
+        sim.shard_import(1, x.numpy(), d)
+        pend = sim.shard_accept(d)
+        both = torch.tensor([pend, -pend], dtype=torch.int64)
+        dist.all_reduce(both, op=dist.ReduceOp.MAX, group=group)
+        if int(both[0]) != -int(both[1]):
+            raise RuntimeError(f"shards disagree on pending rows ({int(both[0])} vs {-int(both[1])})")
+        if pend == 0:
+            break
+        if rnd + 1 > MAX_ROUNDS:
+            raise RuntimeError(f"{pend} rows still drawing after {MAX_ROUNDS} rounds")
+        rnd, d = rnd + 1, D_MORE
+    sim.shard_end_tick()
+    return rnd + 1
+
+
 def rendezvous_uid(rank, world):
     """Share an RCCL unique id over the CPU (gloo) process group torchrun set up."""
     import torch.distributed as dist

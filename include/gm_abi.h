@@ -230,6 +230,16 @@ int gm_shard_end_tick(gm_ctx *ctx);
 /* what = 0: all-gather the per-row counts; what = 1: MAX-allreduce the first n*D draws;
  * what = 2 (msgcount recording, after what = 0): SUM-allreduce this tick's fresh counts */
 int gm_shard_loopback(gm_ctx **ctxs, int32_t G, int32_t what, int32_t D);
+/* Host-collective hook: the exchange buffers of ONE column-shard context as host arrays, so a
+ * host-side collective (e.g. gloo between processes) can stand in for RCCL or gm_shard_loopback
+ * between the phase calls. what = 0: export this rank's per-row counts int32[n][2], import all
+ * G slots int32[G][n][2]; what = 1: export / import the draws int32[n][D] (import their MAX over
+ * the ranks); what = 2 (msgcount recording): uint32[n] fresh counts (+ uint32[n] kept entries on
+ * keyed-loss ticks), import their SUM. gm_shard_export with out = NULL returns the size in *bytes;
+ * gm_shard_import requires exactly that many bytes. (The seam they replace is EmulNet's shared
+ * in-process buffer, EmulNet.cpp:87-177, which the reference's single process never had to cross.) */
+int gm_shard_export(gm_ctx *ctx, int32_t what, int32_t D, void *out, size_t cap, size_t *bytes);
+int gm_shard_import(gm_ctx *ctx, int32_t what, int32_t D, const void *in, size_t bytes);
 /* Diagnostics: tick ONE column shard alone on a device (no RCCL): peers' per-row counts
  * mirror this shard's and draws landing in peer columns resolve to fresh column ix --
  * the real kernels at the true shard shape, for measurement only (not a simulation). */
