@@ -7,6 +7,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cmath>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -37,6 +38,7 @@ hipError_t gm_launch_partial_tick(const PState &s, int t, uint32_t *mtraw, hipSt
                                   hipEvent_t k1);
 hipError_t gm_launch_partial_init(const PState &s, int t0, uint64_t init_seed, hipStream_t st);
 hipError_t gm_launch_partial_unpack(const PState &s, int t, int base, int nrecv, hipStream_t st);
+hipError_t gm_launch_partial_pack(const PState &s, int t, int c, int cap, hipStream_t st);
 hipError_t gm_launch_partial_mtgen(const PState &s, int t, uint32_t *mtraw, hipStream_t st, bool reset);
 hipError_t gm_launch_partial_reset(const PState &s, hipStream_t st);
 hipError_t gm_launch_partial_chunk(const PState &s, int t, const uint32_t *mtraw, int c, hipStream_t st);
@@ -50,7 +52,7 @@ void gm_partial_profile_dump();
 #define GM_D_MORE GM_D_MORE_ROUND  // S2 outputs per row in later rounds (transients with many stale entries)
 #define GM_MAX_ROUNDS 4096    // draw rounds per sharded tick (16 + 64 * 4096 S2 outputs per row)
 #define GM_D_LAST GM_D_LAST_ROUND  // bounded rounds: S2 outputs of round 2 (outputs [80, 336))
-#define GM_SIG_WORDS 16      // gm_comm_init: config words every rank must agree on
+#define GM_SIG_WORDS 17      // gm_comm_init: config words every rank must agree on
 
 struct gm_ctx {
   gm_config cfg;
@@ -576,6 +578,12 @@ static int create_partial(gm_ctx *c) {
     TRY(dalloc(c, &p.sp_hdr, (size_t)G * nl * 8));
     TRY(dalloc(c, &p.sp_list, (size_t)G * nl * p.V));
     HIPCHECK(hipMemset(p.sp_hdr, 0xFF, sizeof(int32_t) * G * nl * 8));  // stamp -1: no record yet
+    TRY(dalloc(c, &p.pk_hdr, (size_t)G * nl * 8));
+    TRY(dalloc(c, &p.pk_list, (size_t)G * nl * p.V));
+    HIPCHECK(hipMemset(p.pk_hdr, 0xFF, sizeof(int32_t) * G * nl * 8));
+    TRY(dalloc(c, &p.pk_cnt, (size_t)p.nchunk * G));
+    p.xcap_frac = getenv("GM_XCHG_CAP_FRAC") ? (float)atof(getenv("GM_XCHG_CAP_FRAC")) : 0.f;
+    if (p.xcap_frac < 0.f || p.xcap_frac > 1.f) return GM_EINVAL;
     TRY(dalloc(c, &p.recv_hdr, (size_t)std::max(R, 1) * 8));
     for (int q = 0; q < 2; q++) TRY(dalloc(c, &p.recv_list[q], (size_t)std::max(R, 1) * p.V));
     std::vector<int32_t> b(G + 1);
@@ -1598,7 +1606,8 @@ extern "C" int gm_comm_init(gm_ctx *c, const uint8_t *id128, int32_t nranks, int
   const gm_config &g = c->cfg;
   const int64_t sig[GM_SIG_WORDS] = {g.mode, g.n, c->s.band, c->p.V, c->p.nchunk, (int64_t)g.rd_seed, g.drop_pct,
                                      g.drop_from, g.drop_to, (int64_t)g.drop_seed, g.init_mode, g.init_t0,
-                                     (int64_t)g.init_seed, (int64_t)g.view_seed, c->p_sharded, GM_ABI_VERSION};
+                                     (int64_t)g.init_seed, (int64_t)g.view_seed, c->p_sharded, GM_ABI_VERSION,
+                                     (int64_t)(c->p.xcap_frac * 1e6f)};
   int64_t *dsig = nullptr;
   HIPCHECK(hipMalloc(&dsig, sizeof(int64_t) * GM_SIG_WORDS * (nranks + 1)));
   std::vector<int64_t> all((size_t)GM_SIG_WORDS * nranks);
@@ -1961,9 +1970,20 @@ static int draw_settle(gm_ctx *c) {
 // stamp is t to its targets' inboxes (a slot without a record of this tick is skipped). A shard
 // thus moves its whole slot range per tick, ~2x the records it has (a sender addresses a given
 // peer with probability 1 - (1 - 1/G)^5: 0.49 at G = 8), over xGMI, while later chunks compute.
+// Capacity of a packed block of `rows` slots (gm_p_pack): a sender addresses a given peer with
+// probability q = 1 - (1 - 1/G)^5 (5 targets drawn from a view of ids spread over the shards), so
+// its record count is ~Binomial(rows, q); the block holds the mean + 8 sigma + 64 (at most the
+// slots) and an overflow fails loudly (GM_ERR_XCHG). S-C at G = 8: 49 % of the slots.
+static size_t xcap(const PState &p, size_t rows) {
+  if (p.xcap_frac > 0.f) return std::min(rows, (size_t)std::ceil((double)rows * p.xcap_frac));
+  const double q = 1.0 - std::pow(1.0 - 1.0 / p.G, (double)GM_FANOUT);
+  const double m = (double)rows * q + 8.0 * std::sqrt((double)rows * q * (1.0 - q)) + 64.0;
+  return std::min(rows, (size_t)std::ceil(m));
+}
 struct XChunk {  // the block layout of chunk ch (rows of shard g in chunk ch: [nloc_g ch / K, nloc_g (ch+1) / K))
-  std::vector<size_t> sc, sd, rc, rd;  // send / receive row counts and row offsets per shard
+  std::vector<size_t> sc, sd, rc, rd;  // send / receive record counts (block capacities) and row offsets per shard
   size_t rbase = 0, rrows = 0;         // this chunk's first received row, rows received
+  size_t cap = 0;                      // capacity of this shard's outgoing blocks
 };
 static XChunk xchunk(const PState &p, int ch) {
   const int G = p.G, K = p.nchunk;
@@ -1973,14 +1993,15 @@ static XChunk xchunk(const PState &p, int ch) {
   x.sc.assign(G, 0); x.sd.assign(G, 0); x.rc.assign(G, 0); x.rd.assign(G, 0);
   for (int c = 0; c < ch; c++)
     for (int g = 0; g < G; g++)
-      if (g != p.rank) x.rbase += rows(g, c);
+      if (g != p.rank) x.rbase += xcap(p, rows(g, c));
   const size_t r0 = (size_t)((int64_t)p.nloc * ch / K);
+  x.cap = xcap(p, rows(p.rank, ch));
   size_t off = x.rbase;
   for (int q = 0; q < G; q++) {
     if (q == p.rank) continue;
-    x.sc[q] = rows(p.rank, ch);
-    x.sd[q] = (size_t)q * p.nloc + r0;
-    x.rc[q] = rows(q, ch);
+    x.sc[q] = x.cap;
+    x.sd[q] = (size_t)q * p.nloc + r0;  // the packed block (q, r0) of pk_hdr / pk_list
+    x.rc[q] = xcap(p, rows(q, ch));
     x.rd[q] = off;
     off += x.rc[q];
   }
@@ -2005,8 +2026,10 @@ static int partial_exchange_chunk(gm_ctx *c, int ch, int64_t *roff) {
     lrd[q] = x.rd[q] * V;
   }
   if (x.rbase + x.rrows > (size_t)(p.n - p.nloc)) return GM_ESTATE;
-  NCCLCHECK(ncclAllToAllv(p.sp_hdr, hs.data(), hsd.data(), p.recv_hdr, hr.data(), hrd.data(), ncclInt32, c->comm, cs));
-  NCCLCHECK(ncclAllToAllv(p.sp_list, ls.data(), lsd.data(), p.recv_list[c->t & 1], lr.data(), lrd.data(), ncclUint32,
+  if (ch == 0) HIPCHECK(hipMemsetAsync(p.pk_cnt, 0, sizeof(int32_t) * p.nchunk * G, cs));
+  HIPCHECK(gm_launch_partial_pack(p, c->t, ch, (int)x.cap, cs));
+  NCCLCHECK(ncclAllToAllv(p.pk_hdr, hs.data(), hsd.data(), p.recv_hdr, hr.data(), hrd.data(), ncclInt32, c->comm, cs));
+  NCCLCHECK(ncclAllToAllv(p.pk_list, ls.data(), lsd.data(), p.recv_list[c->t & 1], lr.data(), lrd.data(), ncclUint32,
                           c->comm, cs));
   HIPCHECK(gm_launch_partial_unpack(p, c->t, (int)x.rbase, (int)x.rrows, cs));
   *roff = (int64_t)(x.rbase + x.rrows);
@@ -2040,7 +2063,12 @@ extern "C" int gm_partial_loopback_tick(gm_ctx **ctxs, int32_t G) {
   // the blocks partial_exchange_chunk's all-to-allv moves, by device copies
   const int V = ctxs[0]->p.V;
   std::vector<size_t> roff(G, 0);
-  for (int g = 0; g < G; g++) HIPCHECK(hipStreamSynchronize(ctxs[g]->stream));  // every shard's records are written
+  for (int g = 0; g < G; g++) {  // every shard packs its records into its outgoing blocks (as on the comm stream)
+    PState &pg = ctxs[g]->p;
+    HIPCHECK(hipMemsetAsync(pg.pk_cnt, 0, sizeof(int32_t) * K * G, ctxs[g]->stream));
+    for (int ch = 0; ch < K; ch++) HIPCHECK(gm_launch_partial_pack(pg, ctxs[g]->t, ch, (int)xchunk(pg, ch).cap, ctxs[g]->stream));
+  }
+  for (int g = 0; g < G; g++) HIPCHECK(hipStreamSynchronize(ctxs[g]->stream));  // every shard's blocks are written
   for (int ch = 0; ch < K; ch++)
     for (int q = 0; q < G; q++) {
       PState &dq = ctxs[q]->p;
@@ -2051,9 +2079,9 @@ extern "C" int gm_partial_loopback_tick(gm_ctx **ctxs, int32_t G) {
         const XChunk xg = xchunk(ctxs[g]->p, ch);
         const PState &sg = ctxs[g]->p;
         if (xg.sc[q] != xq.rc[g]) return GM_ESTATE;
-        HIPCHECK(hipMemcpyAsync(dq.recv_hdr + xq.rd[g] * 8, sg.sp_hdr + xg.sd[q] * 8, sizeof(int32_t) * 8 * xq.rc[g],
+        HIPCHECK(hipMemcpyAsync(dq.recv_hdr + xq.rd[g] * 8, sg.pk_hdr + xg.sd[q] * 8, sizeof(int32_t) * 8 * xq.rc[g],
                                 hipMemcpyDeviceToDevice, st));
-        HIPCHECK(hipMemcpyAsync(dq.recv_list[ctxs[q]->t & 1] + xq.rd[g] * V, sg.sp_list + xg.sd[q] * V,
+        HIPCHECK(hipMemcpyAsync(dq.recv_list[ctxs[q]->t & 1] + xq.rd[g] * V, sg.pk_list + xg.sd[q] * V,
                                 sizeof(uint32_t) * V * xq.rc[g], hipMemcpyDeviceToDevice, st));
       }
       HIPCHECK(gm_launch_partial_unpack(dq, ctxs[q]->t, (int)xq.rbase, (int)xq.rrows, st));

@@ -648,7 +648,11 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
   const int owner = (s.G > 1 && lane < ng) ? p_owner(s, dst) : s.rank;
   if (lane < ng) {
     s.targets[(size_t)li * GM_FANOUT + lane] = dst;
+#ifdef GM_P_ROUTE  // the local appends are gm_p_route's, after the chunk's node kernels
+    if (false) {
+#else
     if (owner == s.rank) {
+#endif
       int32_t *row = s.inbox[par ^ 1] + (size_t)(dst - s.n0) * P_KMAX;  // count and slots share a line
       const int slot = atomicAdd(row, 1);
       if (slot < s.kcap) row[1 + slot] = li;
@@ -869,6 +873,82 @@ __global__ __launch_bounds__(256) void gm_p_unpack(PState s, int t, int base, in
   }
 }
 
+// Inbox appends of chunk c's local targets as a separate pass (GM_P_ROUTE): thread per node, its
+// <= 5 returning atomics issued back to back, no node work waiting on them
+__global__ __launch_bounds__(256) void gm_p_route(PState s, int t, int r0, int r1) {
+  const int li = r0 + blockIdx.x * blockDim.x + threadIdx.x;
+  if (li >= r1) return;
+  const int ng = s.rowstat[(size_t)li * 4 + 3];
+  int d[GM_FANOUT];
+#pragma unroll
+  for (int q = 0; q < GM_FANOUT; q++) d[q] = q < ng ? s.targets[(size_t)li * GM_FANOUT + q] - s.n0 : -1;
+  int32_t *ib = s.inbox[(t & 1) ^ 1];
+  int slot[GM_FANOUT];
+#pragma unroll
+  for (int q = 0; q < GM_FANOUT; q++)
+    slot[q] = d[q] >= 0 && d[q] < s.nloc ? atomicAdd(ib + (size_t)d[q] * P_KMAX, 1) : -1;
+#pragma unroll
+  for (int q = 0; q < GM_FANOUT; q++) {
+    if (slot[q] < 0) continue;
+    if (slot[q] < s.kcap) ib[(size_t)d[q] * P_KMAX + 1 + slot[q]] = li;
+    else atomicOr(s.err, GM_ERR_INBOX);
+  }
+}
+
+// Row shards: compact chunk c's records to shard q (slots (q, li), li in [r0, r1), stamped t) to the
+// front of the packed block (q, r0): one tile of 256 slots per workgroup and peer (blockIdx.y),
+// a workgroup scan of the stamp flags, one atomic per (tile, peer) for the block offset. The
+// records' order inside the block is the atomics' -- the receivers' merge is order-free. A block
+// that would exceed `cap` sets GM_ERR_XCHG (-> GM_ERANGE), never drops a record silently.
+__global__ __launch_bounds__(256) void gm_p_pack(PState s, int t, int c, int r0, int r1, int cap) {
+  const int q = (int)blockIdx.y + (blockIdx.y >= (unsigned)s.rank);  // the peer (own rank skipped)
+  const int li = r0 + blockIdx.x * 256 + threadIdx.x;
+  const size_t rec = (size_t)q * s.nloc + li;
+  const bool has = li < r1 && s.sp_hdr[rec * 8 + 7] == t;
+  __shared__ int wsum[4];
+  __shared__ int base;
+  __shared__ int srcs[256];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t bal = __ballot(has);
+  const int below = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+  if (lane == 0) wsum[wave] = __builtin_popcountll(bal);
+  __syncthreads();
+  int off = below, tot = 0;
+  for (int w = 0; w < 4; w++) {
+    off += w < wave ? wsum[w] : 0;
+    tot += wsum[w];
+  }
+  if (threadIdx.x == 0) base = tot ? atomicAdd(s.pk_cnt + (size_t)c * s.G + q, tot) : 0;
+  __syncthreads();
+  const int b = base;
+  if (has) {
+    const int d = b + off;
+    srcs[off] = li;
+    if (d < cap) {
+      const int4 *h = (const int4 *)(s.sp_hdr + rec * 8);
+      int4 *o = (int4 *)(s.pk_hdr + ((size_t)q * s.nloc + r0 + d) * 8);
+      o[0] = h[0];
+      o[1] = h[1];
+    } else {
+      atomicOr(s.err, GM_ERR_XCHG);
+    }
+  }
+  __syncthreads();
+  const int V = s.V, nw = tot * V;
+  for (int k = threadIdx.x; k < nw; k += 256) {  // the lists, V threads per record (coalesced rows)
+    const int j = k / V, e = k - j * V;
+    if (b + j < cap)
+      s.pk_list[((size_t)q * s.nloc + r0 + b + j) * V + e] = s.sp_list[((size_t)q * s.nloc + srcs[j]) * V + e];
+  }
+}
+
+hipError_t gm_launch_partial_pack(const PState &s, int t, int c, int cap, hipStream_t st) {
+  const int r0 = (int)((int64_t)s.nloc * c / s.nchunk), r1 = (int)((int64_t)s.nloc * (c + 1) / s.nchunk);
+  if (r1 > r0 && s.G > 1)
+    hipLaunchKernelGGL(gm_p_pack, dim3((r1 - r0 + 255) / 256, s.G - 1), dim3(256), 0, st, s, t, c, r0, r1, cap);
+  return hipGetLastError();
+}
+
 #define P_BIG_GRID 1024
 #define P_HUGE_GRID 256
 
@@ -901,6 +981,9 @@ hipError_t gm_launch_partial_chunk(const PState &s, int t, const uint32_t *mtraw
                      4 * PLds<P_HB>::bytes, st, s, t, mtraw, c, r0);
   hipLaunchKernelGGL(mc ? gm_p_tick_huge<true> : gm_p_tick_huge<false>, dim3(P_HUGE_GRID), dim3(64),
                      PLds<P_HH>::bytes, st, s, t, mtraw, c, r0);
+#ifdef GM_P_ROUTE
+  if (r1 > r0) hipLaunchKernelGGL(gm_p_route, dim3((r1 - r0 + 255) / 256), dim3(256), 0, st, s, t, r0, r1);
+#endif
   return hipGetLastError();
 }
 

@@ -3,5 +3,5 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
-VARIANTS="main nowait nodrop prof" bash scripts/sc_ablate.sh || exit 1
+VARIANTS="main defer nodrop prof nowait" bash scripts/sc_ablate.sh || exit 1
 TESTS="tests/test_gpu_gloo_shards.py tests/test_gpu_fullsize_shards.py tests/test_gpu_limits.py tests/test_gpu_baseline_configs.py tests/test_gpu_sharded.py tests/test_gpu_partial.py tests/test_gpu_scaled.py" bash scripts/gpu.sh r04b tests

@@ -70,7 +70,7 @@ def test_sb_full_size_column_shards_match_single_context():
         removed += tot["removed"]
     assert removed == (n - ncrash) * ncrash
     for r in rows:
-        parts = [s.read_row(r) for s in shards]
+        parts = [s.read_row(r, 0, w) for s, (_, w) in zip(shards, lay)]  # each shard's own columns
         hb = np.concatenate([p[0] for p in parts])
         ts = np.concatenate([p[1] for p in parts])
         assert np.array_equal(hb, want_rows[r][0]) and np.array_equal(ts, want_rows[r][1]), f"row {r} differs"

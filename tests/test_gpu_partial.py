@@ -139,3 +139,60 @@ def test_rccl_single_rank_row_shard_matches_oracle(monkeypatch):
         assert ev == ora.events(), f"events differ at tick {t}"
         assert sim.dump_tables() == ora.dump(), f"views differ at tick {t}"
     assert sim.tick_stats()["err"] == 0
+
+
+def test_row_shards_packed_blocks_match_oracle(monkeypatch):
+    """The exchange sends each (chunk, peer) block packed to its records (gm_p_pack) and only the
+    block's capacity travels. At S-C sizes the binomial bound keeps 49 % of the slots (G = 8); at
+    this size the bound is all of them, so GM_XCHG_CAP_FRAC = 0.9 forces blocks below the slot
+    count (records ~Binomial(256, 0.76) per block of 256 slots: capacity 231). Views, events and
+    the oracle still agree tick by tick, and the bytes received shrink with the capacity."""
+    from membership.abi import partial_loopback_tick
+    n, v, world = 4099, 32, 4
+    kw = dict(rd_seed=7, view_seed=5, init_t0=8, init_seed=11)
+    ora = oracle_py.PartialOracle(n, v=v, crash_tick=12, crash_count=n // 50, crash_seed=42, drop_pct=5,
+                                  drop_from=5, drop_to=30, drop_seed=42, **kw)
+
+    def shards(frac):
+        if frac:
+            monkeypatch.setenv("GM_XCHG_CAP_FRAC", str(frac))
+        else:
+            monkeypatch.delenv("GM_XCHG_CAP_FRAC", raising=False)
+        return [Simulator(n, GM_MODE_PARTIAL, rd_seed=7, view=v, view_seed=5, init_mode=1, init_t0=8, init_seed=11,
+                          drop_pct=5, drop_from=5, drop_to=30, drop_seed=42, shard_rank=g, shard_count=world)
+                for g in range(world)]
+    packed, whole = shards(0.9), shards(None)
+    monkeypatch.delenv("GM_XCHG_CAP_FRAC", raising=False)
+    crash = crash_set(n, n // 50, 42)
+    for _ in range(30):
+        t = packed[0].time
+        ora.tick()
+        partial_loopback_tick(packed)
+        partial_loopback_tick(whole)
+        if t == 12:
+            for s in packed + whole:
+                s.set_failed(crash)
+        ev = sorted((e[0], e[1], 1 if e[2] == GM_EV_JOINED else 2, e[3]) for s in packed for e in s.drain_events())
+        for s in whole:
+            s.drain_events()
+        assert ev == sorted(ora.events()), f"events differ at tick {t}"
+        assert b"".join(s.dump_tables() for s in packed) == ora.dump(), f"views differ at tick {t}"
+    for s in packed:
+        assert s.tick_stats()["err"] == 0
+    got, full = sum(s.exchange_bytes() for s in packed), sum(s.exchange_bytes() for s in whole)
+    assert 0.85 * full < got <= 0.91 * full, (got, full)
+
+
+def test_packed_block_overflow_fails_loudly(monkeypatch):
+    """A packed exchange block too small for its records sets GM_ERR_XCHG: the tick returns
+    GM_ERANGE instead of dropping lists (GM_XCHG_CAP_FRAC = 0.3 < the ~76 % of senders that
+    address each peer at G = 4)."""
+    from membership.abi import GmError, partial_loopback_tick
+    monkeypatch.setenv("GM_XCHG_CAP_FRAC", "0.3")
+    n, world = 2048, 4
+    sh = [Simulator(n, GM_MODE_PARTIAL, rd_seed=7, view=32, view_seed=5, init_mode=1, init_t0=8, init_seed=11,
+                    shard_rank=g, shard_count=world) for g in range(world)]
+    with pytest.raises(GmError) as e:
+        for _ in range(3):
+            partial_loopback_tick(sh)
+    assert e.value.code == -4
