@@ -84,9 +84,11 @@ def parse():
                    help="diagnostics (S-A): keyed per-entry drops on every tick (the drop path of gm_s_band)")
     p.add_argument("--force-shard", action="store_true",
                    help="diagnostics: at N=1 run the column-shard protocol with RCCL over one rank")
-    p.add_argument("--pmc", action="store_true",
-                   help="N=1: after the timed run, measure roofline.traffic live (two rocprofv3 --pmc passes "
-                        "of this workload, FETCH_SIZE and WRITE_SIZE, as scripts/gpu.sh pmc_sa / pmc_sc)")
+    p.add_argument("--no-pmc", dest="pmc", action="store_false",
+                   help="skip the live traffic measurement: by default (N=1) roofline.traffic is measured after "
+                        "the timed run by two rocprofv3 --pmc passes of this workload (FETCH_SIZE, WRITE_SIZE; as "
+                        "scripts/gpu.sh pmc_sa / pmc_sc), falling back to the committed profiles/traffic_*.json")
+    p.add_argument("--pmc", dest="pmc", action="store_true", help=argparse.SUPPRESS)  # the default; kept for old callers
     return p.parse_args()
 
 
@@ -98,7 +100,7 @@ def live_traffic(kernel, layout, n, extra):
     import subprocess
     import tempfile
     d = tempfile.mkdtemp(prefix="gm_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
-    child = [sys.executable, os.path.abspath(__file__), "--no-cpu", "--steps", "5", "--warmup", "1"] + extra
+    child = [sys.executable, os.path.abspath(__file__), "--no-cpu", "--no-pmc", "--steps", "5", "--warmup", "1"] + extra
     for ctr, sub in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
         cmd = ["rocprofv3", "--pmc", ctr, "--kernel-trace", "--output-format", "csv", "-d", os.path.join(d, sub),
                "-o", "p", "--"] + child
@@ -360,8 +362,11 @@ def main():
     }
     if a.pmc and world == 1:
         sim.close()  # the PMC passes are child processes with their own context
-        out["roofline"]["traffic"], out["roofline"]["traffic_source"] = live_traffic(
-            "gm_s_band", LAYOUT_SA, n, ["--cluster", str(n)] + (["--drop-pct", str(a.drop_pct)] if a.drop_pct else []))
+        try:
+            out["roofline"]["traffic"], out["roofline"]["traffic_source"] = live_traffic(
+                "gm_s_band", LAYOUT_SA, n, ["--cluster", str(n)] + (["--drop-pct", str(a.drop_pct)] if a.drop_pct else []))
+        except Exception as e:  # no profiler / counters on this host: the committed figure stands, said so
+            out["roofline"]["traffic_source"] = f"{traffic_src} (live PMC passes failed: {type(e).__name__})"
     if rank == 0 and world == 1 and not a.no_cpu:
         sys.path.insert(0, os.path.join(REPO, "tests"))
         import oracle_py  # the oracle is the CPU baseline here, never the measured path
@@ -492,8 +497,11 @@ def main_partial(a):
         out["roofline"]["note"] = "rank 0's local kernels (its n/G nodes)"
     if a.pmc and world == 1:
         sim.close()  # the PMC passes are child processes with their own context
-        out["roofline"]["traffic"], out["roofline"]["traffic_source"] = live_traffic(
-            "gm_p_tick", "partial-v32", n, ["--scenario", "S-C", "--cluster", str(n), "--view", str(V)])
+        try:
+            out["roofline"]["traffic"], out["roofline"]["traffic_source"] = live_traffic(
+                "gm_p_tick", "partial-v32", n, ["--scenario", "S-C", "--cluster", str(n), "--view", str(V)])
+        except Exception as e:  # no profiler / counters on this host: the committed figure stands, said so
+            out["roofline"]["traffic_source"] = f"{traffic_src} (live PMC passes failed: {type(e).__name__})"
     if rank == 0 and world == 1 and not a.no_cpu:
         sys.path.insert(0, os.path.join(REPO, "tests"))
         import oracle_py  # the oracle is the CPU baseline here, never the measured path

@@ -2049,13 +2049,18 @@ extern "C" int gm_partial_loopback_tick(gm_ctx **ctxs, int32_t G) {
     if (c->latched != GM_OK) return c->latched;
   }
   for (int g = 0; g < G; g++) TRY(before_tick_events(ctxs[g]));
+  // every shard's kernels on ONE stream, shard after shard: the sum of the shards' own costs (8
+  // concurrent streams on one device starve each other's small worklist kernels; on a node every
+  // shard has its GPU to itself)
+  for (int g = 0; g < G; g++) HIPCHECK(hipStreamSynchronize(ctxs[g]->stream));
+  hipStream_t ls = ctxs[0]->stream;
   for (int g = 0; g < G; g++) {
     gm_ctx *c = ctxs[g];
     const int t_send = c->t - 1;
     const bool drop = c->cfg.drop_pct > 0 && t_send >= c->cfg.drop_from && t_send < c->cfg.drop_to;
     PState st = c->p;
     st.drop_pct = drop ? c->cfg.drop_pct : -1;
-    HIPCHECK(gm_launch_partial_tick(st, c->t, c->p_mtraw, c->stream, nullptr, nullptr));
+    HIPCHECK(gm_launch_partial_tick(st, c->t, c->p_mtraw, ls, nullptr, nullptr));
   }
   const int K = ctxs[0]->p.nchunk;
   for (int g = 0; g < G; g++)
@@ -2065,14 +2070,13 @@ extern "C" int gm_partial_loopback_tick(gm_ctx **ctxs, int32_t G) {
   std::vector<size_t> roff(G, 0);
   for (int g = 0; g < G; g++) {  // every shard packs its records into its outgoing blocks (as on the comm stream)
     PState &pg = ctxs[g]->p;
-    HIPCHECK(hipMemsetAsync(pg.pk_cnt, 0, sizeof(int32_t) * K * G, ctxs[g]->stream));
-    for (int ch = 0; ch < K; ch++) HIPCHECK(gm_launch_partial_pack(pg, ctxs[g]->t, ch, (int)xchunk(pg, ch).cap, ctxs[g]->stream));
+    HIPCHECK(hipMemsetAsync(pg.pk_cnt, 0, sizeof(int32_t) * K * G, ls));
+    for (int ch = 0; ch < K; ch++) HIPCHECK(gm_launch_partial_pack(pg, ctxs[g]->t, ch, (int)xchunk(pg, ch).cap, ls));
   }
-  for (int g = 0; g < G; g++) HIPCHECK(hipStreamSynchronize(ctxs[g]->stream));  // every shard's blocks are written
   for (int ch = 0; ch < K; ch++)
     for (int q = 0; q < G; q++) {
       PState &dq = ctxs[q]->p;
-      hipStream_t st = ctxs[q]->stream;
+      hipStream_t st = ls;
       const XChunk xq = xchunk(dq, ch);
       for (int g = 0; g < G; g++) {
         if (g == q || !xq.rc[g]) continue;
@@ -2088,8 +2092,8 @@ extern "C" int gm_partial_loopback_tick(gm_ctx **ctxs, int32_t G) {
       roff[q] = xq.rbase + xq.rrows;
     }
   for (int q = 0; q < G; q++) ctxs[q]->p_recv_last = (int64_t)roff[q];
+  HIPCHECK(hipStreamSynchronize(ls));
   for (int g = 0; g < G; g++) {
-    HIPCHECK(hipStreamSynchronize(ctxs[g]->stream));
     TRY(check_err(ctxs[g]));
     ctxs[g]->t++;
     ctxs[g]->ticks_done++;
