@@ -84,6 +84,9 @@ def parse():
                    help="diagnostics (S-A): keyed per-entry drops on every tick (the drop path of gm_s_band)")
     p.add_argument("--force-shard", action="store_true",
                    help="diagnostics: at N=1 run the column-shard protocol with RCCL over one rank")
+    p.add_argument("--no-companion", dest="companion", action="store_false",
+                   help="S-A only: skip the companion S-B run (N=262,144, same schedule and ranks) whose line "
+                        "goes under \"companion\" -- the north_star scaling cluster measured by every --gpus G run")
     p.add_argument("--no-pmc", dest="pmc", action="store_false",
                    help="skip the live traffic measurement: by default (N=1) roofline.traffic is measured after "
                         "the timed run by two rocprofv3 --pmc passes of this workload (FETCH_SIZE, WRITE_SIZE; as "
@@ -202,44 +205,20 @@ def dry_launch(a):
         dist = tdist
     ranks = gather_ranks(dist, info)
     if rank == 0:
-        emit({"dry_launch": True, "n_gpus": a.gpus, "scenario": a.scenario, "ranks": ranks})
+        emit({"dry_launch": True, "n_gpus": a.gpus, "scenario": a.scenario, "ranks": ranks,
+              "companion": "S-B" if (a.companion and a.scenario == "S-A" and a.cluster in (0, 65536)
+                                     and not a.drop_pct and not a.force_shard) else None})
     if dist is not None:
         dist.destroy_process_group()
 
 
-def main():
-    a = parse()
-    if a.gpus < 1:
-        sys.stderr.write("bench.py: --gpus must be >= 1\n")
-        sys.exit(2)
-    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        sys.exit(launch_ranks(a))
-    quiet_stdout()
-    if a.dry_launch:
-        return dry_launch(a)
-    if a.scenario == "S-C":
-        return main_partial(a)
-    a.cluster = a.cluster or (262144 if a.scenario == "S-B" else 65536)
-    rtx = Roctx()
-    rtx.pause()
-    rank, world, local = rank_env(a)
-    if "GM_DEVICE_OVERRIDE" in os.environ:  # diagnostics only: pin every rank to one device
-        local = int(os.environ["GM_DEVICE_OVERRIDE"])
-    # libgm first: it binds the system ROCm HIP runtime and RCCL it was built
-    # against before torch (CPU-only here) brings its own copies into the process
-    from membership import GM_MODE_SCALED, Simulator, crash_set, load_library
+def scaled_run(a, n, rank, world, local, dist, rtx, profiled):
+    """One timed run of the SCALED tick at N = n on the S-A schedule (warm start at t0,
+    a.crash_frac crashed at a.crash_tick, prologue to a.prologue, a.warmup untimed ticks,
+    then exactly a.steps timed ticks between barriers), with the workload self-check
+    after the window. profiled: the timed ticks are the roctx-selected region."""
+    from membership import GM_MODE_SCALED, Simulator, crash_set
     from membership.sharded import distributed_shard
-    load_library()
-
-    dist = None
-    if world > 1:
-        # CPU-only process group: rendezvous, barrier and max-over-ranks timing.
-        # The GPU (and RCCL over xGMI) is driven by libgm alone.
-        import torch.distributed as tdist
-        tdist.init_process_group("gloo")
-        dist = tdist
-
-    n = a.cluster
     ncrash = int(round(n * a.crash_frac))
     init = dict(init_mode=1 if a.t0 > 0 else 0, init_t0=a.t0, init_seed=11)
     if a.drop_pct:
@@ -271,13 +250,15 @@ def main():
     barrier()
     sim.sync()
     sim.set_timing(1)
-    rtx.resume()
+    if profiled:
+        rtx.resume()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         sim.tick()
     sim.sync()
     t1 = time.perf_counter()
-    rtx.pause()
+    if profiled:
+        rtx.pause()
     barrier()
     elapsed = t1 - t0
     if dist is not None:
@@ -298,9 +279,65 @@ def main():
         c0, wl = sim.shard_layout() if world > 1 else (0, n)  # a column shard counts its own columns
         crash_here = int(((crash >= c0) & (crash < c0 + wl)).sum())
         assert tot["removed"] == (n - ncrash) * crash_here and tot["joined"] == 0, (tot, n - ncrash, crash_here)
-
-    n_live, m_lists = st["live"], st["lists"]
     W = sim.shard_layout()[1] if world > 1 else n  # this rank's subject columns
+    return dict(sim=sim, n=n, ncrash=ncrash, elapsed=elapsed, kernel_ms=kernel_ms, st=st, tot=tot,
+                removed_ok=removed_ok, W=W, t0=t0, t1=t1)
+
+
+def companion_sb(a, rank, world, local, dist, rtx):
+    """The north_star scaling cluster measured beside the headline: the same schedule at
+    N = 262,144 (S-B, BASELINE.json configs[3]) on the same G ranks, so that every
+    `bench.py --gpus G` line of a 1/2/4/8-GPU sweep also carries the S-B curve. Not the
+    headline value (that stays S-A); outside the roctx-selected region."""
+    try:
+        r = scaled_run(a, 262144, rank, world, local, dist, rtx, profiled=False)
+    except (AssertionError, RuntimeError, OSError) as e:  # reported, not fatal to the headline line
+        return {"scenario": "S-B", "error": f"{type(e).__name__}: {e}"}
+    n = r["n"]
+    out = {"scenario": "S-B", "metric": "simulated node-ticks/sec (S-B N=262,144 full membership)",
+           "value": n * a.steps / r["elapsed"], "unit": "node-ticks/s", "n_gpus": world,
+           "ms_per_step": r["elapsed"] / a.steps * 1e3, "kernel_ms_rank0": r["kernel_ms"],
+           "n": n, "crashed": r["ncrash"], "columns_per_gpu": r["W"], "scaling": "strong",
+           "check": {"removed_rank0": r["tot"]["removed"], "joined_rank0": r["tot"]["joined"]}}
+    r["sim"].close()
+    return out
+
+
+def main():
+    a = parse()
+    if a.gpus < 1:
+        sys.stderr.write("bench.py: --gpus must be >= 1\n")
+        sys.exit(2)
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(a))
+    quiet_stdout()
+    if a.dry_launch:
+        return dry_launch(a)
+    if a.scenario == "S-C":
+        return main_partial(a)
+    a.cluster = a.cluster or (262144 if a.scenario == "S-B" else 65536)
+    rtx = Roctx()
+    rtx.pause()
+    rank, world, local = rank_env(a)
+    if "GM_DEVICE_OVERRIDE" in os.environ:  # diagnostics only: pin every rank to one device
+        local = int(os.environ["GM_DEVICE_OVERRIDE"])
+    # libgm first: it binds the system ROCm HIP runtime and RCCL it was built
+    # against before torch (CPU-only here) brings its own copies into the process
+    from membership import load_library
+    load_library()
+
+    dist = None
+    if world > 1:
+        # CPU-only process group: rendezvous, barrier and max-over-ranks timing.
+        # The GPU (and RCCL over xGMI) is driven by libgm alone.
+        import torch.distributed as tdist
+        tdist.init_process_group("gloo")
+        dist = tdist
+
+    r = scaled_run(a, a.cluster, rank, world, local, dist, rtx, profiled=True)
+    sim, n, ncrash, elapsed, kernel_ms = r["sim"], r["n"], r["ncrash"], r["elapsed"], r["kernel_ms"]
+    st, tot, removed_ok, W, t0, t1 = r["st"], r["tot"], r["removed_ok"], r["W"], r["t0"], r["t1"]
+    n_live, m_lists = st["live"], st["lists"]
     # algorithmic bytes of one tick in this layout (DESIGN.md §3): per live row and
     # column 1 B cell read + 1 B cell write + 0.5 B payload write, plus 0.5 B per
     # delivered gossip list (payload read) -- the survey's formulation (SURVEY.md §8(d):
@@ -325,7 +362,6 @@ def main():
         if tj.get("layout") == LAYOUT_SA:
             traffic = tj.get("hbm_bytes_per_launch")
             traffic_src = f"profiles/traffic_n{n}.json ({tj.get('generated', 'r01')}, rocprofv3 --pmc passes by scripts/gpu.sh pmc_sa)"
-
     value = n * a.steps / elapsed
     ranks = gather_ranks(dist, {"rank": rank, "local_rank": local, **sim.comm_info(), "kernel_ms": kernel_ms,
                                 "columns": W, "elapsed_s": t1 - t0})
@@ -360,11 +396,14 @@ def main():
         "check": {"removed_rank0": tot["removed"], "joined_rank0": tot["joined"], "removed_all_expected":
                   (n - ncrash) * ncrash if removed_ok else None},
     }
+    sim.close()  # the companion run and the PMC passes (child processes) need the device memory
+    if a.companion and a.scenario == "S-A" and n == 65536 and not a.drop_pct and not a.force_shard:
+        out["companion"] = companion_sb(a, rank, world, local, dist, rtx)
     if a.pmc and world == 1:
-        sim.close()  # the PMC passes are child processes with their own context
         try:
             out["roofline"]["traffic"], out["roofline"]["traffic_source"] = live_traffic(
-                "gm_s_band", LAYOUT_SA, n, ["--cluster", str(n)] + (["--drop-pct", str(a.drop_pct)] if a.drop_pct else []))
+                "gm_s_band", LAYOUT_SA, n, ["--cluster", str(n), "--no-companion"] +
+                (["--drop-pct", str(a.drop_pct)] if a.drop_pct else []))
         except Exception as e:  # no profiler / counters on this host: the committed figure stands, said so
             out["roofline"]["traffic_source"] = f"{traffic_src} (live PMC passes failed: {type(e).__name__})"
     if rank == 0 and world == 1 and not a.no_cpu:

@@ -4,7 +4,7 @@
 #
 #   tests      python -m pytest tests -m gpu            -> $O/gpu_tests.txt
 #   smoke      __graft_entry__.smoke()                  -> $O/smoke.txt
-#   sa         bench.py (S-A, with cpu_baseline)        -> $O/bench_sa.json
+#   sa         bench.py (S-A, with cpu_baseline, live PMC traffic and the S-B companion run) -> $O/bench_sa.json
 #   sc         bench.py --scenario S-C                  -> $O/bench_sc.json
 #   ticks      scripts/tick_times.py: per-tick gm_s_band time of the S-A schedule -> $O/tick_times.txt
 #   sb         bench.py --cluster 262144 (S-B on one GPU) -> $O/bench_sb.json
@@ -41,22 +41,22 @@ run_step() {
     ticks) timeout -k 10 300 python -u scripts/tick_times.py ${TICKS_N:-65536} > $O/tick_times.txt 2>&1 ;;
     sb) timeout -k 10 400 python -u bench.py --cluster 262144 ${BENCH_ARGS:-} > $O/bench_sb.json 2> $O/bench_sb.err ;;
     sa_pmc) timeout -k 10 700 python -u bench.py --pmc --no-cpu ${BENCH_ARGS:-} > $O/bench_sa_pmc.json 2> $O/bench_sa_pmc.err ;;
-    shard) timeout -k 10 300 python -u bench.py --force-shard --no-cpu --no-pmc ${BENCH_ARGS:-} > $O/bench_force_shard.json 2> $O/bench_force_shard.err ;;
+    shard) timeout -k 10 300 python -u bench.py --force-shard --no-cpu --no-pmc --no-companion ${BENCH_ARGS:-} > $O/bench_force_shard.json 2> $O/bench_force_shard.err ;;
     sbshard) timeout -k 10 400 python -u scripts/shard_profile.py --sb > $O/sb_shard.json 2> $O/sb_shard.err ;;
     prof_sa) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_sa -o sa -- \
-               python3 bench.py --no-cpu --no-pmc ${BENCH_ARGS:-} > $O/prof_sa.log 2>&1 ;;
+               python3 bench.py --no-cpu --no-pmc --no-companion ${BENCH_ARGS:-} > $O/prof_sa.log 2>&1 ;;
     prof_sc) timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_sc -o sc -- \
                python3 bench.py --scenario S-C --no-cpu --no-pmc ${BENCH_ARGS:-} > $O/prof_sc.log 2>&1 ;;
     prof_sb) timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_sb -o sb -- \
                python3 bench.py --cluster 262144 --no-cpu --no-pmc ${BENCH_ARGS:-} > $O/prof_sb.log 2>&1 ;;
     pmc_sa) timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/pmc_sa_fetch -o p -- \
-              python3 bench.py --no-cpu --no-pmc --steps 5 --warmup 1 > $O/pmc_sa_fetch.log 2>&1 &&
+              python3 bench.py --no-cpu --no-pmc --no-companion --steps 5 --warmup 1 > $O/pmc_sa_fetch.log 2>&1 &&
             timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/pmc_sa_write -o p -- \
-              python3 bench.py --no-cpu --no-pmc --steps 5 --warmup 1 > $O/pmc_sa_write.log 2>&1 &&
+              python3 bench.py --no-cpu --no-pmc --no-companion --steps 5 --warmup 1 > $O/pmc_sa_write.log 2>&1 &&
             python3 scripts/pmc_traffic.py --kernel gm_s_band --fetch $O/pmc_sa_fetch --write $O/pmc_sa_write \
               --layout byte-band --out $O/traffic_n65536.json > $O/pmc_sa.txt 2>&1 ;;
     mix_sa) timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY \
-              --kernel-trace --output-format csv -d $O/mix_sa -o p -- python3 bench.py --no-cpu --no-pmc --steps 5 --warmup 1 > $O/mix_sa.log 2>&1 ;;
+              --kernel-trace --output-format csv -d $O/mix_sa -o p -- python3 bench.py --no-cpu --no-pmc --no-companion --steps 5 --warmup 1 > $O/mix_sa.log 2>&1 ;;
     mix_sc) timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
               --kernel-trace --output-format csv -d $O/mix_sc -o p -- python3 bench.py --scenario S-C --no-cpu --no-pmc --steps 3 --warmup 1 > $O/mix_sc.log 2>&1 ;;
     pmc_sc) timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/pmc_sc_fetch -o p -- \

@@ -36,6 +36,7 @@ def test_gpus_2_spawns_two_ranks():
     assert sorted(x["local_rank"] for x in ranks) == [0, 1]
     assert len({x["pid"] for x in ranks}) == 2  # two processes
     assert all(x["master"].startswith("127.0.0.1:") for x in ranks)
+    assert out["companion"] == "S-B"  # every S-A line of a --gpus sweep also measures the S-B cluster
 
 
 def test_gpus_1_stays_one_process():
@@ -45,6 +46,13 @@ def test_gpus_1_stays_one_process():
     assert out["n_gpus"] == 1 and out["scenario"] == "S-B"
     assert [x["world_size"] for x in out["ranks"]] == [1]
     assert out["ranks"][0]["pid"] != os.getpid()
+    assert out["companion"] is None  # S-B is the cluster itself
+
+
+def test_no_companion_flag():
+    r = _run(["--dry-launch", "--no-companion"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert json.loads(r.stdout.strip())["companion"] is None
 
 
 def test_world_size_mismatch_fails_loudly():
