@@ -428,6 +428,16 @@ static int create_scaled(gm_ctx *c) {
   TRY(dalloc(c, &s.wtick, n));
   TRY(dalloc(c, &s.failed, n));
   TRY(dalloc(c, &s.brec, (size_t)n * s.nb));
+  // the band kernel's fast path (B = 1024; gm_s_band_fast) and the list of units it hands back
+  // (at most every unit of a tick). GM_BAND_FAST=0 (diagnostics, A/B against the general path:
+  // tests/test_gpu_band_fast.py) leaves it off.
+  s.fb_cnt = nullptr;
+  s.fb_list = nullptr;
+  if (s.band == 1024 && !(getenv("GM_BAND_FAST") && atoi(getenv("GM_BAND_FAST")) == 0)) {
+    TRY(dalloc(c, &s.fb_cnt, 2));
+    HIPCHECK(hipMemset(s.fb_cnt, 0, 2 * sizeof(uint32_t)));
+    TRY(dalloc(c, &s.fb_list, (size_t)n * s.nb));
+  }
   TRY(dalloc(c, &s.ev_band, (size_t)n * s.nb * s.evs));
   {  // event spill ring (records past a (row, band)'s E slots): up to every cell of the shard, within a
      // 1/32 share of the free HBM (the loopback shards of one device split it); at least 2^24 records.

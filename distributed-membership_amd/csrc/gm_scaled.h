@@ -11,7 +11,8 @@
 #define S_SB 8                   // sender ids prefetched per row; payload loads in flight per lane
 #define S_MT_RAW 16              // mt19937 outputs precomputed per row and tick (gm_s_mtgen)
 #define S_SELFADD_CAP 65536      // join ramp: self appends verified per tick (gm_s_selfcheck)
-#define S_PLIST_CAP 4096         // sharded tick: rows a second (bounded) draw round takes
+#define S_PLIST_CAP 4096
+#define S_FB_BLOCKS 2048         // workgroups (4 waves) of gm_s_band's pass over the fast path's handed-back units         // sharded tick: rows a second (bounded) draw round takes
 #define GM_D_MORE_ROUND 64       // S2 outputs of bounded round 1 (= one host-driven round)
 #define GM_D_LAST_ROUND 256      // S2 outputs of bounded round 2 (= host-driven rounds 2..5)
 
@@ -27,11 +28,14 @@
 // Stored table cell: ONE BYTE per (observer, subject). The 16-bit cell above is the
 // working format in registers; in HBM a cell is
 //   0             absent
-//   h4 << 4 | a   h = 224 + 2 h4 (h4 in [1, 15]: even h in [226, 254], heartbeat lag <= 14
-//                 ticks), age a <= 15 -- every live entry of a warm, steady cluster
+//   h4 << 4 | a   h = 224 + 2 h4 (h4 in [3, 15]: even h in [230, 254], heartbeat lag <= 12
+//                 ticks), age a <= 14 -- every live entry of a warm, steady cluster. The range
+//                 is one short of the byte's at both ends, so that a stored byte re-based by one
+//                 tick (h4 - 1, a + 1) is again a byte: gm_s_band's fast path merges and sweeps
+//                 the stored bytes themselves and tests only its outputs
 //   1 (S_B_ESC)   escaped: the exact 16-bit cell is an entry of the (band, row)'s escape list
 //                 (codes 2..15, h4 = 0, are unused)
-// Cells outside the byte's range (odd h of cold-start / JOINREQ entries, lag > 14 or age > 15,
+// Cells outside the byte's range (odd h of cold-start / JOINREQ entries, lag > 12 or age > 14,
 // e.g. a crashed node's entries in the ticks before TREMOVE) escape. The pool is COMPACT: per
 // (band, row) the escaped cells of the row's band slice (lane by lane; entries carry their columns,
 // so the order is not significant), as consecutive u32
@@ -46,6 +50,8 @@
 // bounded (gm_host.hip: dense-equivalent for small clusters, a fraction of the cells beyond);
 // an overflow sets GM_ERR_ESC (-> GM_ERANGE) -- never a silent divergence.
 #define S_B_ESC 1u
+#define S_H4_MIN_H 230u  // smallest h a stored byte holds (h4 = 3)
+#define S_AGE_MAX_B 14u  // largest age a stored byte holds
 #define S_ESC_IN 16                 // entries of a (band, row) list held inline (64 B per list)
 #define S_EW_TOT(w) ((w) & 0x7FFu)  // escape-list word: entry count (<= band width)
 #define S_EW_OFF(w) ((w) >> 11)     // offset of entries S_ESC_IN.. in the stripe's pool region
@@ -57,7 +63,7 @@ __host__ __device__ inline uint32_t s_widen(uint32_t b) {  // byte -> 16-bit cel
 __host__ __device__ inline uint32_t s_narrow(uint32_t c) {  // 16-bit cell -> byte (an escape code if not representable)
   if (c == 0) return 0u;
   const uint32_t h = c >> 5, a = c & 31u;
-  if (h >= 226 && !(h & 1) && a <= 15) return (((h - 224) >> 1) << 4) | a;
+  if (h >= S_H4_MIN_H && !(h & 1) && a <= S_AGE_MAX_B) return (((h - 224) >> 1) << 4) | a;
   return S_B_ESC;
 }
 __host__ __device__ inline int s_start(int j) { return j >> 2; }  // (int)(0.25 * j) for j >= 0
@@ -177,6 +183,10 @@ struct SState {
   uint32_t *mc_rdrop;           // [n] entries a row received after keyed loss (DROP band kernel)
   int mc_tmax;
   int kcap;                     // inbox slots used (S_KMAX; lowered only by the diagnostics env GM_INBOX_CAP)
+  // fast path (B = 1024, gm_s_band_fast): the units it hands back to the general path this tick,
+  // by tick parity (the count of tick t+1 is zeroed during tick t); nullptr: fast path off
+  uint32_t *fb_cnt;             // [2]
+  int2 *fb_list;                // [nb * n]: (band, row)
   int lag_hmin;                 // a present cell with h < lag_hmin sets GM_ERR_LAG: 3 (lag > 125 ticks, the
                                 // encoding's limit); the diagnostics env GM_LAG_CAP=L (L >= 15) lowers it to lag > L
 };

@@ -64,6 +64,7 @@ struct RowMeta {
   int k;           // lists delivered to the row (-1: no such row, or a crashed node)
   int snd[S_SB];   // first S_SB senders
   uint32_t ebase;  // the (band, row) record's escape-list word of the last tick (S_EW_*, 0: no escaped cells)
+  uint32_t bz;     // the record's count word of the last tick (S_BC_*: the slice's present cells as stored)
 };
 
 // Every load of the row's metadata issues at once, none behind a branch on another (one
@@ -77,7 +78,9 @@ __device__ __forceinline__ RowMeta<B> row_meta(const SState &s, int r, int par, 
   int4 b = *(const int4 *)(ib + 4);
   int k = s.inbox_cnt[par][rc];
   int failed = s.failed[rc];
-  m.ebase = s.brec[slab + rc].w;
+  const uint4 rec = s.brec[slab + rc];
+  m.ebase = rec.w;
+  m.bz = rec.z;
   // empty asm statements that read the values here: without them the compiler sinks the
   // inbox-count load into a branch on `failed` and the sender ids behind that, two more
   // round trips before the gathers (one row per wave: scalar registers)
@@ -150,14 +153,16 @@ __device__ __forceinline__ int dpp_scan(int v) {
   return v;
 }
 
-// Stored bytes of two swept cells (pres = min(v2, 1)): tt = v2 - S_CELL(226, 0) (wraps below
-// h = 226) = (h - 226) << 5 | age; representable iff nothing above the h4 field (h <= 254, no
-// wrap), h even (bit 5) and age <= 15 (bit 4) -> h4 << 4 | age, else S_B_ESC (bad = 1); absent 0
+// Stored bytes of two swept cells (pres = min(v2, 1)): tt = v2 - (S_CELL(230, 0) - 1) (wraps below
+// h = 230) = (h - 230) << 5 | (age + 1); representable iff nothing above the h field (h <= 254, no
+// wrap), h even (bit 5) and age <= 14 (bit 4 of age + 1) -> h4 << 4 | age (h4 = (h - 224) / 2 =
+// the tt field + 3), else S_B_ESC (bad = 1); absent 0. gm_scaled.h: a stored byte is always one
+// re-base away from another byte, which the fast path of gm_s_band relies on.
 __device__ __forceinline__ u16x2 narrow2(u16x2 v2, u16x2 pres, u16x2 &bad) {
-  const u16x2 tt = v2 - (u16x2)(7232);
+  const u16x2 tt = v2 - (u16x2)(S_CELL(S_H4_MIN_H, 0) - 1);
   bad = pmin1(tt & (u16x2)(0xFC30)) & pres;
   const uint32_t tu = unpk(tt);
-  const u16x2 enc = pk((tu & 0x000F000Fu) | ((tu >> 2) & 0x00F000F0u)) + (u16x2)(16);
+  const u16x2 enc = pk((tu & 0x000F000Fu) | ((tu >> 2) & 0x00F000F0u)) + (u16x2)(0x2F);
   return enc * (pres - bad) + bad;
 }
 
@@ -393,6 +398,7 @@ struct UnitIn {
   int snd[S_SB];
   u32x4 ta;        // the row's 16 cell bytes of this lane (as loaded)
   uint32_t ebase;  // the row slice's escape list in the pool of tick t-1 (S_PESC_NONE: none)
+  uint32_t bz;     // the (band, row) record's count word of tick t-1 (S_BC_PRES: present cells as loaded)
 };
 
 // UNI: the row is wave-uniform and known to be (one row per wave, a grid-derived unit)
@@ -413,6 +419,7 @@ __device__ __forceinline__ void unit_load(const SState &s, int t, int band, int 
   for (int j = 0; j < S_SB; j++) in.snd[j] = meta.snd[j];
   in.k = meta.k;
   in.ebase = meta.ebase;
+  in.bz = meta.bz;
 }
 
 // every payload slice at once; slots j >= k read out of range (zeros = "not sent"); with them,
@@ -430,6 +437,147 @@ __device__ __forceinline__ void unit_gather(const SState &s, int t, const UnitIn
 #pragma unroll
   for (int j = 0; j < S_SB; j++)
     m[j] = __builtin_amdgcn_raw_buffer_load_b64(prs, j < k ? poff + (uint32_t)in.snd[j] * B : GM_OOB, 0, 0);
+}
+
+// The unit's commit, shared by both paths of unit_finish. unit_stores (a merged row's lanes): the
+// swept slice's table bytes and payload nibbles, and its escape list; returns the list's word.
+template <int B>
+__device__ __forceinline__ uint32_t unit_stores(const SState &s, int t, const UnitIn<B> &in, const uint32_t bw[4],
+                                                uint32_t ov0, uint32_t ov1, bool esc_row, uint32_t em, uint32_t *lds) {
+  constexpr int LPR = B / S_COLS_PER_LANE;  // lanes per row
+  constexpr int Q = S_COLS_PER_LANE;        // cells per lane
+  const int lane = threadIdx.x & 63;
+  const int par = t & 1;
+  const int li = lane % LPR;
+  const int band = in.band, r = in.r;
+  const size_t slab = (size_t)band * s.n;
+  const __amdgpu_buffer_rsrc_t trs = gm_rsrc(s.table + slab * B, (uint32_t)(s.n * B));
+  const __amdgpu_buffer_rsrc_t prs = gm_rsrc(s.msg + slab * B, (uint32_t)(s.n * B));
+  const uint32_t toff = (uint32_t)(r * B + li * Q);  // bytes
+  uint32_t eb_out = 0;
+  const u32x4 nb4 = {bw[0], bw[1], bw[2], bw[3]};
+  __builtin_amdgcn_raw_buffer_store_b128(nb4, trs, toff, 0, GM_AUX_NT);
+  const u32x2 ov = {ov0, ov1};
+  __builtin_amdgcn_raw_buffer_store_b64(ov, prs, (uint32_t)(r * B + par * (B / 2) + li * 8), 0, GM_AUX_NT);
+  if (band == 0 && li == 0) s.wtick[r] = t;
+  if (esc_row) {  // the escaped cells as entries of this tick's list (the record's .w)
+    int etot;
+    const int eoff = row_scan<LPR>(__builtin_popcount(em), li, lane, etot);
+    eb_out = row_alloc<LPR>(s, par, slab, r, etot, li, lane);
+    if (eb_out != 0) esc_emit(lds, lane, esc_list(s, par, slab, r, eb_out), eoff, em, li * Q, etot <= S_ESC_IN, s.err, s.lag_hmin);
+  }
+  return eb_out;
+}
+
+// unit_records (every lane): the (band, row) record (rank-select chunk counts, the row's present /
+// numfailed / event counts, the escape-list word eb_out), the events, a column shard's exchange
+// slot. live: the row was merged and swept (else only its record is written).
+template <int B, bool DROP>
+__device__ __forceinline__ void unit_records(const SState &s, int t, const UnitIn<B> &in, bool live, uint32_t eb_out,
+                                             int npres, int nfail, int nev, uint32_t evk, int nkept) {
+  constexpr int LPR = B / S_COLS_PER_LANE;  // lanes per row
+  constexpr int Q = S_COLS_PER_LANE;        // cells per lane
+  const int lane = threadIdx.x & 63;
+  const int sub = lane / LPR, li = lane % LPR;
+  const int band = in.band, r = in.r;
+  const int colb = band * B + li * Q;  // shard-local column of this lane's first cell
+  const size_t slab = (size_t)band * s.n;
+  if (DROP && s.mc_rdrop) {  // msgcount: the row's kept entries (wave-uniform test)
+    int v = nkept;
+#pragma unroll
+    for (int o = 1; o < LPR; o <<= 1) v += __shfl_xor(v, o, 64);
+    if (live && li == 0 && v) atomicAdd(&s.mc_rdrop[r], (uint32_t)v);
+  }
+  // present cells per 64-column chunk (4 lanes) for the draw's rank-select, gathered
+  // into the row's first lane: bytes 0..B/64-1 of the (band, row) record
+  constexpr int CH = S_CHUNK(B), LPC = CH / Q;  // columns / lanes per rank-select chunk
+  // per-row reductions over the row's LPR lanes (aligned lane segments): counts packed
+  // as present | numfailed << 16 (each <= B)
+  int pf = npres | (nfail << 16);
+  uint64_t piece = 0;
+  if (LPR == 64 && LPC == 8) {
+    // one row per wave: 8-lane chunk sums on DPP (xor 1, xor 2 by quad_perm, then + the
+    // mirrored lane of the other quad), then the 8 chunk words by readlane on the scalar side
+    pf += __builtin_amdgcn_update_dpp(0, pf, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    pf += __builtin_amdgcn_update_dpp(0, pf, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+    pf += __builtin_amdgcn_update_dpp(0, pf, 0x141, 0xF, 0xF, false);  // row_half_mirror
+    int tsum = 0;
+#pragma unroll
+    for (int c = 0; c < 8; c++) {
+      const int v = __builtin_amdgcn_readlane(pf, 8 * c);
+      piece |= (uint64_t)(v & 0xFF) << (8 * c);
+      tsum += v;
+    }
+    pf = tsum;
+  } else {
+    int cc = npres;
+#pragma unroll
+    for (int o = 1; o < LPC; o <<= 1) cc += __shfl_xor(cc, o, 64);
+#pragma unroll
+    for (int c = 0; c < B / CH; c++) piece |= (uint64_t)(__shfl(cc, sub * LPR + LPC * c, 64) & 0xFF) << (8 * c);
+#pragma unroll
+    for (int o = LPR / 2; o >= 1; o >>= 1) pf += __shfl_xor(pf, o, 64);
+  }
+  int x = 0, tot = 0;
+  if (__builtin_amdgcn_ballot_w64(nev != 0)) {  // wave-uniform: events anywhere in this wave
+    // cumulative (joins, removals) of this (row, band): ADD kinds are 01, REMOVE kinds 10
+    int jr = __builtin_popcount(evk & 0x55555555u) | (__builtin_popcount(evk & 0xAAAAAAAAu) << 16);
+    x = nev;
+    if (LPR == 64) {  // one row per wave: inclusive scans on DPP, totals from lane 63
+      x = dpp_scan(x);
+      jr = dpp_scan(jr);
+      tot = __builtin_amdgcn_readlane(x, 63);
+      jr = __builtin_amdgcn_readlane(jr, 63);
+    } else {
+#pragma unroll
+      for (int o = 1; o < LPR; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (li >= o) x += y;
+      }
+      tot = __shfl(x, sub * LPR + LPR - 1, 64);
+#pragma unroll
+      for (int o = LPR / 2; o >= 1; o >>= 1) jr += __shfl_xor(jr, o, 64);
+    }
+    // single writer per (row, band); a no-return atomic keeps the wave from waiting on a load
+    if (live && li == 0 && jr)
+      atomicAdd((unsigned long long *)&s.evcum[(size_t)r * s.nb + band],
+                (unsigned long long)(jr & 0xFFFF) | ((unsigned long long)(jr >> 16) << 32));
+  }
+  const int E = s.evs;
+  uint32_t sbase = 0;  // one spill-ring reservation per (row, band) that overflows its slots
+  if (live && li == 0 && tot > E) sbase = atomicAdd(s.ev_spill_cnt, (uint32_t)(tot - E));
+  if (live && li == 0 && tot)  // the tick's total (host staging), striped partial sums
+    atomicAdd(s.ev_spill_cnt + 1 + ((slab + (size_t)r) & (S_EV_STRIPES - 1)), (uint32_t)tot);
+  sbase = LPR == 64 ? __builtin_amdgcn_readfirstlane(sbase) : __shfl(sbase, sub * LPR, 64);
+  if (live && nev) {
+    int slot = x - nev;
+    uint32_t *slots = s.ev_band + ((size_t)r * s.nb + band) * E;
+    for (uint32_t ek = evk; ek; ek &= ek - 1) {
+      const int bit = __builtin_ctz(ek);  // low bit of a set 2-bit kind field (ADD=1, REMOVE=2)
+      const int q = bit >> 1;
+      const uint32_t kind = (evk >> (2 * q)) & 3u;
+      const uint32_t rec = (kind << 30) | (uint32_t)(s.c0 + colb + q + 1);
+      if (slot < E) {
+        slots[slot] = rec;
+      } else {
+        const uint32_t sp = sbase + (uint32_t)(slot - E);
+        if (sp < s.ev_spill_cap) s.ev_spill[sp] = ((uint64_t)(uint32_t)r << 32) | rec;
+        else atomicOr(s.err, GM_ERR_EVENTS);
+      }
+      slot++;
+    }
+  }
+  if (li == 0 && r < s.n) {
+    // one 16-byte record per (band, row), consecutive rows adjacent: whole-line writes
+    const uint32_t bc = (uint32_t)(pf & 0xFFFF) | ((uint32_t)(pf >> 16) << 11) | ((uint32_t)min(tot, 1023) << 22);
+    s.brec[slab + r] = live ? make_uint4((uint32_t)piece, (uint32_t)(piece >> 32), bc, eb_out)
+                            : make_uint4(0u, 0u, 0u, eb_out);
+    // column shard: this shard's row totals (present, numfailed) for the all-gather,
+    // accumulated as one packed 64-bit add per (row, band) into the zeroed slot
+    if (s.sharded && live)
+      atomicAdd((unsigned long long *)(s.xcnt + ((size_t)s.shard_rank * s.n + r) * 2),
+                (unsigned long long)(pf & 0xFFFF) | ((unsigned long long)(pf >> 16) << 32));
+  }
 }
 
 template <int B, bool DROP>
@@ -621,7 +769,7 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
     // sweep (MP1Node.cpp:426-444), one packed pass: age >= TFAIL counts toward numfailed,
     // age >= TREMOVE removes; fresh entries (age < TFAIL) form the payload sent at tick t.
     // The swept cell is narrowed to its stored byte (S_B_ESC where the byte cannot hold it).
-    // A fresh stored byte h4 << 4 | a sends h' = h - 2, i.e. the nibble h4 - 1; h4 = 1 and
+    // A fresh stored byte h4 << 4 | a sends h' = h - 2, i.e. the nibble h4 - 1 (>= 2: h4 >= 3);
     // escaped cells send the escape nibble 15 (their byte h' goes to the payload's wide plane).
     u16x2 np2 = (u16x2)(0), nf2 = (u16x2)(0), badv = (u16x2)(0), nmx = (u16x2)(0), amax = (u16x2)(0);
     u16x2 nwv[2] = {(u16x2)(0), (u16x2)(0)};
@@ -737,128 +885,268 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
       }
       nev = __builtin_popcount((evk | (evk >> 1)) & 0x55555555u);
     }
-    const u32x4 nb4 = {bw[0], bw[1], bw[2], bw[3]};
-    __builtin_amdgcn_raw_buffer_store_b128(nb4, trs, toff, 0, GM_AUX_NT);
-    const u32x2 ov = {unpk(nwv[0]), unpk(nwv[1])};
-    __builtin_amdgcn_raw_buffer_store_b64(ov, prs, (uint32_t)(r * B + par * (B / 2) + li * 8), 0, GM_AUX_NT);
-    if (band == 0 && li == 0) s.wtick[r] = t;
-    if (esc_row) {  // the escaped cells as entries of this tick's list (the record's .w)
-      int etot;
-      const int eoff = row_scan<LPR>(__builtin_popcount(em), li, lane, etot);
-      eb_out = row_alloc<LPR>(s, par, slab, r, etot, li, lane);
-      if (eb_out != 0) esc_emit(lds, lane, esc_list(s, par, slab, r, eb_out), eoff, em, li * Q, etot <= S_ESC_IN, s.err, s.lag_hmin);
+    eb_out = unit_stores<B>(s, t, in, bw, unpk(nwv[0]), unpk(nwv[1]), esc_row, em, lds);
+  }
+  unit_records<B, DROP>(s, t, in, live, eb_out, npres, nfail, nev, evk, nkept);
+}
+
+// ------------------------------------------------------------ gm_s_band fast path
+// Lane-mask bit p in esc_mask16's order is cell esc_cell(p); esc_bit is the inverse.
+__device__ __forceinline__ int esc_bit(int q) { return ((q & 3) << 3) | (q >> 2); }
+// byte q of a lane's four stored dwords; the same with byte q replaced. q is dynamic: the dword is
+// chosen by masks, not by an index (which the compiler turns into a scratch array)
+__device__ __forceinline__ uint32_t lane_sel(int j, int i) { return (uint32_t)-(int)(j == i); }
+__device__ __forceinline__ uint32_t lane_byte(const uint32_t w[4], int q) {
+  const int j = q >> 2;
+  const uint32_t x = (w[0] & lane_sel(j, 0)) | (w[1] & lane_sel(j, 1)) | (w[2] & lane_sel(j, 2)) | (w[3] & lane_sel(j, 3));
+  return (x >> (8 * (q & 3))) & 0xFFu;
+}
+__device__ __forceinline__ void lane_set_byte(uint32_t w[4], int q, uint32_t v) {
+  const int j = q >> 2, sh = 8 * (q & 3);
+  const uint32_t m = 0xFFu << sh, b = v << sh;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint32_t si = lane_sel(j, i);
+    w[i] = (w[i] & ~(m & si)) | (b & si);
+  }
+}
+// payload nibble of lane cell q (nib_of's position) replaced in the lane's two payload words
+__device__ __forceinline__ void lane_set_nib(uint32_t &x0, uint32_t &x1, int q, uint32_t v) {
+  const int c = q & 7;
+  const int sh = 16 * (c & 1) + 4 * (3 - (c >> 1));
+  const uint32_t m = 0xFu << sh, b = v << sh;
+  if (q < 8) x0 = (x0 & ~m) | b;
+  else x1 = (x1 & ~m) | b;
+}
+
+// gm_s_band's fast path (one row per wave; no keyed loss, no join ramp): the merge and the sweep on
+// the stored bytes themselves. A stored byte x = h4 << 4 | a (h4 >= 3, a <= 14: gm_scaled.h) re-based
+// by one tick is x - 15 (h4 - 1, a + 1) and a delivered nibble n is the byte n << 4 (h' = 224 + 2n,
+// age 0); bytes order as their cells do, so the merge of updatelistCallBack (MP1Node.cpp:278-299) is
+// max(sat(x - 15), n << 4), and the sweep's counts (MP1Node.cpp:426-444) and the payload nibbles of
+// sendMemberList (MP1Node.cpp:360-395: the fresh cells' h4 - 1) come from SWAR over the packed
+// result, four cells per instruction. The rare cells are marked and redone one by one with the 16-bit
+// cell, as the general path computes them: escaped cells (their value is the row slice's escape
+// list's), results a byte cannot hold (age 15, h4 <= 2: they escape, or are removed at TREMOVE), and
+// the row's own cell (heartbeat bump). A delivered escape nibble, or a fresh cell whose payload needs
+// the wide plane, sends the whole wave to the general path: the function then returns false before
+// any global store. Returns true when the unit is done.
+template <int B>
+__device__ __forceinline__ bool unit_fast(const SState &s, int t, const UnitIn<B> &in, const u32x2 m[S_SB],
+                                          uint32_t ent, uint32_t *lds) {
+  static_assert(B / S_COLS_PER_LANE == 64, "the fast path takes one row per wave");
+  constexpr int Q = S_COLS_PER_LANE;
+  const int lane = threadIdx.x & 63, li = lane;
+  const int par = t & 1;
+  const int band = in.band, r = in.r;
+  const int colb = band * B + li * Q;  // shard-local column of this lane's first cell
+  const size_t slab = (size_t)band * s.n;
+  const int k = in.k;  // wave-uniform
+  if (k < 0 || k > S_KMAX || s.ramp) return false;  // not merged / inbox error / join ramp: general path
+  // 1. the delivered lists: per cell pair the largest nibble, in the top nibble of each u16 (nib_max)
+  u16x2 acc[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) acc[i] = (u16x2)(0);
+#pragma unroll
+  for (int j = 0; j < S_SB; j++)
+    if (j < k) nib_max(acc, m[j].x, m[j].y);  // slots j >= k loaded zeros
+  if (k > S_SB) {  // more lists than prefetched ids (a Poisson tail: ~7 % of rows at fanout 5)
+    const __amdgpu_buffer_rsrc_t prs = gm_rsrc(s.msg + slab * B, (uint32_t)(s.n * B));
+    const uint32_t poff = (uint32_t)((par ^ 1) * (B / 2) + li * 8);
+    const int32_t *ib = s.inbox[par] + (size_t)r * S_KMAX;
+    for (int j = S_SB; j < k; j++) {
+      const int sn = ib[j];
+      const u32x2 mv = __builtin_amdgcn_raw_buffer_load_b64(prs, poff + (uint32_t)sn * B, 0, 0);
+      nib_max(acc, mv.x, mv.y);
     }
   }
-  if (DROP && s.mc_rdrop) {  // msgcount: the row's kept entries (wave-uniform test)
-    int v = nkept;
+  {
+    u16x2 amx = acc[0];
 #pragma unroll
-    for (int o = 1; o < LPR; o <<= 1) v += __shfl_xor(v, o, 64);
-    if (live && li == 0 && v) atomicAdd(&s.mc_rdrop[r], (uint32_t)v);
+    for (int i = 1; i < 8; i++) amx = __builtin_elementwise_max(amx, acc[i]);
+    if (__builtin_amdgcn_ballot_w64(__builtin_elementwise_max(amx.x, amx.y) >= (uint16_t)(S_NIB_ESC << 12)))
+      return false;  // a delivered escape nibble: its value is in the sender's wide plane
   }
-  // present cells per 64-column chunk (4 lanes) for the draw's rank-select, gathered
-  // into the row's first lane: bytes 0..B/64-1 of the (band, row) record
-  constexpr int CH = S_CHUNK(B), LPC = CH / Q;  // columns / lanes per rank-select chunk
-  // per-row reductions over the row's LPR lanes (aligned lane segments): counts packed
-  // as present | numfailed << 16 (each <= B)
-  int pf = npres | (nfail << 16);
-  uint64_t piece = 0;
-  if (LPR == 64 && LPC == 8) {
-    // one row per wave: 8-lane chunk sums on DPP (xor 1, xor 2 by quad_perm, then + the
-    // mirrored lane of the other quad), then the 8 chunk words by readlane on the scalar side
-    pf += __builtin_amdgcn_update_dpp(0, pf, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
-    pf += __builtin_amdgcn_update_dpp(0, pf, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
-    pf += __builtin_amdgcn_update_dpp(0, pf, 0x141, 0xF, 0xF, false);  // row_half_mirror
-    int tsum = 0;
+  // 2. re-base and merge, two cells per u16x2, packed back to bytes
+  const uint32_t tb4[4] = {in.ta.x, in.ta.y, in.ta.z, in.ta.w};
+  uint32_t bw[4], yprev = 0;
 #pragma unroll
-    for (int c = 0; c < 8; c++) {
-      const int v = __builtin_amdgcn_readlane(pf, 8 * c);
-      piece |= (uint64_t)(v & 0xFF) << (8 * c);
-      tsum += v;
-    }
-    pf = tsum;
-  } else {
-    int cc = npres;
-#pragma unroll
-    for (int o = 1; o < LPC; o <<= 1) cc += __shfl_xor(cc, o, 64);
-#pragma unroll
-    for (int c = 0; c < B / CH; c++) piece |= (uint64_t)(__shfl(cc, sub * LPR + LPC * c, 64) & 0xFF) << (8 * c);
-#pragma unroll
-    for (int o = LPR / 2; o >= 1; o >>= 1) pf += __shfl_xor(pf, o, 64);
+  for (int i = 0; i < 8; i++) {
+    const u16x2 x = pk(byte_pair(tb4[i >> 1], i & 1));
+    const u16x2 kb = (acc[i] >> (u16x2)(8)) & (u16x2)(0xF0);
+    const u16x2 y = __builtin_elementwise_max(__builtin_elementwise_sub_sat(x, (u16x2)(15)), kb);
+    if (i & 1) bw[i >> 1] = __builtin_amdgcn_perm(unpk(y), yprev, 0x06040200u);
+    else yprev = unpk(y);
   }
-  int x = 0, tot = 0;
-  if (__builtin_amdgcn_ballot_w64(nev != 0)) {  // wave-uniform: events anywhere in this wave
-    // cumulative (joins, removals) of this (row, band): ADD kinds are 01, REMOVE kinds 10
-    int jr = __builtin_popcount(evk & 0x55555555u) | (__builtin_popcount(evk & 0xAAAAAAAAu) << 16);
-    x = nev;
-    if (LPR == 64) {  // one row per wave: inclusive scans on DPP, totals from lane 63
-      x = dpp_scan(x);
-      jr = dpp_scan(jr);
-      tot = __builtin_amdgcn_readlane(x, 63);
-      jr = __builtin_amdgcn_readlane(jr, 63);
-    } else {
+  // 3. SWAR over the merged bytes: present (h4 >= 1) and stale (age >= TFAIL) counts, payload nibbles
+  // (fresh present cells: h4 - 1, in the byte's high nibble), and the cells to redo
+  int npres = 0, nfail = 0;
+  uint32_t nb[4], spm = 0;
 #pragma unroll
-      for (int o = 1; o < LPR; o <<= 1) {
-        const int y = __shfl_up(x, o, 64);
-        if (li >= o) x += y;
+  for (int w = 0; w < 4; w++) {
+    const uint32_t v = bw[w];
+    const uint32_t lo = v & 0x0F0F0F0Fu;
+    const uint32_t st = (lo + 0x01010101u * (16 - GM_TFAIL)) & 0x10101010u;  // age >= TFAIL
+    const uint32_t a15 = (lo + 0x01010101u) & 0x10101010u;                   // age 15: not a byte next tick
+    const uint32_t hi = v & 0xF0F0F0F0u;
+    const uint32_t hs = hi >> 1;
+    const uint32_t pr = (hs + 0x78787878u) & 0x80808080u;  // h4 >= 1: present
+    const uint32_t g3 = (hs + 0x68686868u) & 0x80808080u;  // h4 >= 3
+    nfail += __builtin_popcount(st);
+    npres += __builtin_popcount(pr);
+    spm |= ((pr & ~g3) | (a15 << 3)) >> (7 - w);  // esc_mask16's bit order
+    nb[w] = (hi - (pr >> 3)) & ~((st << 4) - st);
+  }
+  // payload words in nib_max's order: the high nibbles of cells [4, 0, 5, 1] | those of [6, 2, 7, 3]
+  // shifted down, for cells 0..7 and likewise 8..15
+  uint32_t ov0 = __builtin_amdgcn_perm(nb[1], nb[0], 0x01050004u) | (__builtin_amdgcn_perm(nb[1], nb[0], 0x03070206u) >> 4);
+  uint32_t ov1 = __builtin_amdgcn_perm(nb[3], nb[2], 0x01050004u) | (__builtin_amdgcn_perm(nb[3], nb[2], 0x03070206u) >> 4);
+  if (in.ebase != 0) spm |= esc_mask16(tb4[0], tb4[1], tb4[2], tb4[3]);  // row-uniform: escaped cells
+  const int selfc = (r >= s.c0 && r < s.c0 + s.w) ? r - s.c0 - colb : -1;
+  const bool selflane = selfc >= 0 && selfc < Q;
+  int hbself = 0;
+  if (selflane) {
+    spm |= 1u << esc_bit(selfc);
+    hbself = s.hbctr[r] + 1;
+  }
+  // 4. the marked cells, exactly (16-bit cell; the general path's arithmetic)
+  int ngone = 0;
+  uint32_t gmask = 0, em = 0;
+  bool esc_row = false;
+  if (__builtin_amdgcn_ballot_w64(spm != 0)) {
+    uint16_t *row16 = (uint16_t *)lds;  // the wave's LDS: a 16-bit cell per column (lane li: [16 li, +16))
+    if (in.ebase != 0) {  // the row slice's escape list, by column (its entries carry their columns)
+      const int tot = (int)S_EW_TOT(in.ebase);
+      if (li < min(tot, S_ESC_IN)) row16[ent & 0xFFFFu] = (uint16_t)(ent >> 16);
+      if (tot > S_ESC_IN) {
+        const EscList l = esc_list(s, par ^ 1, slab, r, in.ebase);
+        for (int i = S_ESC_IN + li; i < tot; i += 64) {
+          const uint32_t e = *l.at(i);
+          row16[e & 0xFFFFu] = (uint16_t)(e >> 16);
+        }
       }
-      tot = __shfl(x, sub * LPR + LPR - 1, 64);
-#pragma unroll
-      for (int o = LPR / 2; o >= 1; o >>= 1) jr += __shfl_xor(jr, o, 64);
+      lds_wave_sync();
     }
-    // single writer per (row, band); a no-return atomic keeps the wave from waiting on a load
-    if (live && li == 0 && jr)
-      atomicAdd((unsigned long long *)&s.evcum[(size_t)r * s.nb + band],
-                (unsigned long long)(jr & 0xFFFF) | ((unsigned long long)(jr >> 16) << 32));
-  }
-  const int E = s.evs;
-  uint32_t sbase = 0;  // one spill-ring reservation per (row, band) that overflows its slots
-  if (live && li == 0 && tot > E) sbase = atomicAdd(s.ev_spill_cnt, (uint32_t)(tot - E));
-  if (live && li == 0 && tot)  // the tick's total (host staging), striped partial sums
-    atomicAdd(s.ev_spill_cnt + 1 + ((slab + (size_t)r) & (S_EV_STRIPES - 1)), (uint32_t)tot);
-  sbase = LPR == 64 ? __builtin_amdgcn_readfirstlane(sbase) : __shfl(sbase, sub * LPR, 64);
-  if (live && nev) {
-    int slot = x - nev;
-    uint32_t *slots = s.ev_band + ((size_t)r * s.nb + band) * E;
-    for (uint32_t ek = evk; ek; ek &= ek - 1) {
-      const int bit = __builtin_ctz(ek);  // low bit of a set 2-bit kind field (ADD=1, REMOVE=2)
-      const int q = bit >> 1;
-      const uint32_t kind = (evk >> (2 * q)) & 3u;
-      const uint32_t rec = (kind << 30) | (uint32_t)(s.c0 + colb + q + 1);
-      if (slot < E) {
-        slots[slot] = rec;
-      } else {
-        const uint32_t sp = sbase + (uint32_t)(slot - E);
-        if (sp < s.ev_spill_cap) s.ev_spill[sp] = ((uint64_t)(uint32_t)r << 32) | rec;
-        else atomicOr(s.err, GM_ERR_EVENTS);
+    bool bail = false;
+    for (uint32_t mm = spm; mm; mm &= mm - 1) {
+      const int p = __builtin_ctz(mm), q = esc_cell(p);
+      const uint32_t x = lane_byte(tb4, q), y = lane_byte(bw, q);
+      // re-based cell max delivered key: y is exact unless x escaped (then y = the key: sat(1 - 15) = 0)
+      uint32_t c = s_widen(y);
+      if (x == S_B_ESC) {
+        const uint32_t e = row16[li * Q + q];
+        c = max(e ? e - 63u : 0u, c);
       }
-      slot++;
+      if (q == selfc) {  // heartbeat++; myPos->setheartbeat(heartbeat++) (MP1Node.cpp:412-415)
+        if (c == 0) atomicOr(s.err, GM_ERR_SELF);  // converged start: the own entry is always present
+        const int h = 255 - (2 * t - hbself);
+        if (h < s.lag_hmin || h > 255) atomicOr(s.err, GM_ERR_LAG);
+        c = (uint32_t)S_CELL(h, 0) & 0xFFFFu;
+      }
+      const uint32_t age = c & 31u;
+      const bool pres = c != 0, stale = pres && age >= GM_TFAIL, gone = pres && age >= GM_TREMOVE;
+      uint32_t nbyte = 0, nib = 0;
+      if (gone) {  // TREMOVE (MP1Node.cpp:429-444): absent; it sent nothing (stale)
+        gmask |= 1u << q;
+        ngone++;
+      } else if (pres) {
+        nbyte = s_narrow(c);
+        if (nbyte == S_B_ESC) {  // an entry of this tick's list (unit_stores: esc_emit reads it here)
+          em |= 1u << p;
+          row16[li * Q + q] = (uint16_t)c;
+        }
+        if (!stale) {  // fresh: the nibble of h' = h - 2, or the wide plane (general path)
+          const uint32_t hp = (c >> 5) - 2u;
+          if ((hp & 1u) || hp < S_NIB_H(1) || hp > S_NIB_H(14)) bail = true;
+          else nib = (hp - S_NIB_BASE) >> 1;
+        }
+      }
+      // the fast pass's counts of this cell, replaced
+      const bool fpres = y >= 16u, fstale = fpres && (y & 15u) >= GM_TFAIL;
+      npres += (int)(pres && !gone) - (int)fpres;
+      nfail += (int)stale - (int)fstale;
+      lane_set_byte(bw, q, nbyte);
+      lane_set_nib(ov0, ov1, q, nib);
     }
+    if (__builtin_amdgcn_ballot_w64(bail)) return false;
+    esc_row = __builtin_amdgcn_ballot_w64(em != 0) != 0;
   }
-  if (li == 0 && r < s.n) {
-    // one 16-byte record per (band, row), consecutive rows adjacent: whole-line writes
-    const uint32_t bc = (uint32_t)(pf & 0xFFFF) | ((uint32_t)(pf >> 16) << 11) | ((uint32_t)min(tot, 1023) << 22);
-    s.brec[slab + r] = live ? make_uint4((uint32_t)piece, (uint32_t)(piece >> 32), bc, eb_out)
-                            : make_uint4(0u, 0u, 0u, eb_out);
-    // column shard: this shard's row totals (present, numfailed) for the all-gather,
-    // accumulated as one packed 64-bit add per (row, band) into the zeroed slot
-    if (s.sharded && live)
-      atomicAdd((unsigned long long *)(s.xcnt + ((size_t)s.shard_rank * s.n + r) * 2),
-                (unsigned long long)(pf & 0xFFFF) | ((unsigned long long)(pf >> 16) << 32));
+  // 5. events: removals = gmask; joins = cells present now but absent as loaded -- there are some iff
+  // the slice's present cells before the sweep (npres + ngone over the row) differ from the count
+  // the record kept of the last tick (first tick after gm_s_init: no count kept, so the cells are
+  // compared; they are always compared where any differ)
+  int nev = 0;
+  uint32_t evk = 0;
+  int tot = npres + ngone;
+  tot += __builtin_amdgcn_update_dpp(0, tot, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+  tot += __builtin_amdgcn_update_dpp(0, tot, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+  tot += __builtin_amdgcn_update_dpp(0, tot, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  tot += __builtin_amdgcn_update_dpp(0, tot, 0x140, 0xF, 0xF, false);  // row_mirror
+  tot = __builtin_amdgcn_readlane(tot, 0) + __builtin_amdgcn_readlane(tot, 16) + __builtin_amdgcn_readlane(tot, 32) +
+        __builtin_amdgcn_readlane(tot, 48);
+  if (tot != (int)S_BC_PRES(in.bz)) {
+#pragma unroll
+    for (int q = 0; q < Q; q++) {
+      const uint32_t before = (tb4[q >> 2] >> (8 * (q & 3))) & 0xFFu;
+      const uint32_t after = (bw[q >> 2] >> (8 * (q & 3))) & 0xFFu;  // 0 = absent
+      const uint32_t ev = !before ? (after ? S_EV_ADD : 0u) : (!after ? S_EV_REMOVE : 0u);
+      evk |= ev << (2 * q);
+    }
+    nev = __builtin_popcount((evk | (evk >> 1)) & 0x55555555u);
+  } else if (ngone) {  // removals only (the crash case): REMOVE kinds (10) at the removed cells
+    uint32_t x = gmask;
+    x = (x | (x << 8)) & 0x00FF00FFu;
+    x = (x | (x << 4)) & 0x0F0F0F0Fu;
+    x = (x | (x << 2)) & 0x33333333u;
+    x = (x | (x << 1)) & 0x55555555u;
+    evk = x << 1;
+    nev = ngone;
   }
+  // 6. commit (the general path's)
+  if (selflane) s.hbctr[r] = hbself + 1;
+  const uint32_t eb_out = unit_stores<B>(s, t, in, bw, ov0, ov1, esc_row, em, lds);
+  unit_records<B, false>(s, t, in, true, eb_out, npres, nfail, nev, evk, 0);
+  return true;
 }
 
 #ifndef GM_DROP_MINW
 #define GM_DROP_MINW 8  // the keyed-loss instantiation at 8 waves per SIMD (64 VGPRs + 20 B of spills: 7.39 ms vs 7.63 at its own 79 VGPRs)
 #endif
+// One unit of the general path (every band width, keyed loss, the join ramp, and the units the
+// fast path hands back).
+// UNI: the grid's own unit (its row metadata in scalar registers); the listed pass loads its units'
+// rows through vector registers.
+template <int B, bool DROP, bool UNI>
+__device__ __forceinline__ void band_unit(const SState &s, int t, int drop_pct, int band, int ub, uint32_t *lds) {
+  UnitIn<B> in;
+  unit_load<B, UNI>(s, t, band, ub, in);
+  u32x2 m[S_SB];
+  uint32_t ent;
+  unit_gather<B, DROP>(s, t, in, m, ent);
+  unit_finish<B, DROP>(s, t, drop_pct, in, m, ent, lds);
+}
+// the pools of tick t+1 start empty (the tick t-1 lists in them are read through their bases,
+// never through the counters), and so does the fast path's hand-back list of tick t+1 (whichever
+// kernel ran tick t: a keyed-loss tick between two fast ticks must not leave a count behind); one
+// wave of the tick's first band kernel
+__device__ __forceinline__ void band_reset_pools(const SState &s, int t) {
+  const int S = s.esc_stripes;
+  for (int i = threadIdx.x; i < S; i += 64) {
+    s.tesc_cnt[((t & 1) ^ 1) * S + i] = 0;
+    s.pesc_cnt[((t & 1) ^ 1) * S + i] = 0;
+  }
+  if (s.fb_cnt && threadIdx.x == 0) s.fb_cnt[(t & 1) ^ 1] = 0;
+}
+
 template <int B, bool DROP>
 #ifndef GM_BAND_MINW
 #define GM_BAND_MINW 1
 #endif
+// grid (units of a band / 4, bands): blockIdx.y is the band, so workgroups still dispatch
+// band-major, and the wave-uniform unit index needs no division
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DROP ? GM_DROP_MINW : GM_BAND_MINW, 8))) void gm_s_band(SState s, int t, int drop_pct) {
   constexpr int RPW = 64 / (B / S_COLS_PER_LANE);
   const int U = (s.n + RPW - 1) / RPW;
-  // grid (units of a band / 4, bands): blockIdx.y is the band, so workgroups still dispatch
-  // band-major, and the wave-uniform unit index needs no division
   const int ub = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
   if (ub >= U) return;  // whole wave
   UnitIn<B> in;
@@ -868,13 +1156,42 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DROP ? GM_D
   unit_gather<B, DROP>(s, t, in, m, ent);
   __shared__ uint32_t lds_all[4 * S_LDS_WAVE_WORDS];  // escaped rows only (esc_apply / esc_emit)
   unit_finish<B, DROP>(s, t, drop_pct, in, m, ent, lds_all + (threadIdx.x >> 6) * S_LDS_WAVE_WORDS);
-  if (ub == 0 && blockIdx.y == 0) {  // the pools of tick t+1 start empty (the tick t-1 lists in them are
-    const int S = s.esc_stripes;       // read through their bases, never through the counters)
-    for (int i = threadIdx.x; i < S; i += 64) {
-      s.tesc_cnt[((t & 1) ^ 1) * S + i] = 0;
-      s.pesc_cnt[((t & 1) ^ 1) * S + i] = 0;
-    }
+  if (ub == 0 && blockIdx.y == 0) band_reset_pools(s, t);
+}
+
+// The general path over the units gm_s_band_fast handed back this tick (s.fb_list): a fixed grid of
+// waves striding over the list (rows through vector registers: the units come from memory).
+template <int B>
+__global__ __launch_bounds__(256) void gm_s_band_listed(SState s, int t) {
+  __shared__ uint32_t lds_all[4 * S_LDS_WAVE_WORDS];
+  uint32_t *lds = lds_all + (threadIdx.x >> 6) * S_LDS_WAVE_WORDS;
+  const uint32_t cnt = s.fb_cnt[t & 1];
+  const uint32_t nw = gridDim.x * 4;
+  for (uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6); i < cnt; i += nw) {
+    const int2 u = s.fb_list[i];
+    band_unit<B, false, false>(s, t, -1, __builtin_amdgcn_readfirstlane(u.x), __builtin_amdgcn_readfirstlane(u.y), lds);
   }
+}
+
+// The fast path's kernel (B = 1024, no keyed loss, no join ramp): every unit takes unit_fast; a
+// unit it hands back (not merged, a delivered escape nibble, a payload for the wide plane) goes to
+// s.fb_list for gm_s_band's listed pass right after, untouched. The list of tick t+1 starts empty.
+template <int B>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GM_BAND_MINW, 8))) void gm_s_band_fast(SState s, int t) {
+  const int ub = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  if (ub >= s.n) return;  // whole wave (one row per wave)
+  __shared__ uint32_t lds_all[4 * S_LDS_WAVE_WORDS];
+  uint32_t *lds = lds_all + (threadIdx.x >> 6) * S_LDS_WAVE_WORDS;
+  UnitIn<B> in;
+  unit_load<B, true>(s, t, (int)blockIdx.y, ub, in);
+  u32x2 m[S_SB];
+  uint32_t ent;
+  unit_gather<B, false>(s, t, in, m, ent);
+  if (!unit_fast<B>(s, t, in, m, ent, lds) && (threadIdx.x & 63) == 0) {
+    const uint32_t slot = atomicAdd(&s.fb_cnt[t & 1], 1u);  // < the units of a tick: the list's size
+    s.fb_list[slot] = make_int2((int)blockIdx.y, ub);
+  }
+  if (ub == 0 && blockIdx.y == 0) band_reset_pools(s, t);
 }
 
 // --------------------------------------------------------------- gm_s_selfcheck
@@ -1520,8 +1837,14 @@ static hipError_t launch_tick_b(const SState &s, int t, int drop_pct, hipStream_
   (void)hipMemsetAsync(s.ev_spill_cnt, 0, (1 + S_EV_STRIPES) * sizeof(uint32_t), st);
   hipLaunchKernelGGL(gm_s_mtgen, dim3((s.n + 255) / 256), dim3(256), 0, st, s, t);
   if (k0) (void)hipEventRecord(k0, st);
-  if (drop_pct >= 0) hipLaunchKernelGGL((gm_s_band<B, true>), dim3(nblk), dim3(256), 0, st, s, t, drop_pct);
-  else hipLaunchKernelGGL((gm_s_band<B, false>), dim3(nblk), dim3(256), 0, st, s, t, drop_pct);
+  if (drop_pct >= 0) {
+    hipLaunchKernelGGL((gm_s_band<B, true>), dim3(nblk), dim3(256), 0, st, s, t, drop_pct);
+  } else if (B == 1024 && !s.ramp && s.fb_list) {  // the fast path, then the units it handed back
+    hipLaunchKernelGGL((gm_s_band_fast<B == 1024 ? B : 1024>), dim3(nblk), dim3(256), 0, st, s, t);
+    hipLaunchKernelGGL((gm_s_band_listed<B == 1024 ? B : 1024>), dim3(S_FB_BLOCKS), dim3(256), 0, st, s, t);
+  } else {
+    hipLaunchKernelGGL((gm_s_band<B, false>), dim3(nblk), dim3(256), 0, st, s, t, drop_pct);
+  }
   if (k1) (void)hipEventRecord(k1, st);
   if (s.ramp) {
     hipLaunchKernelGGL(gm_s_selfcheck, dim3(16), dim3(256), 0, st, s);
