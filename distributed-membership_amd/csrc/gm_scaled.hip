@@ -549,7 +549,11 @@ __device__ __forceinline__ void unit_records(const SState &s, int t, const UnitI
   if (live && li == 0 && tot)  // the tick's total (host staging), striped partial sums
     atomicAdd(s.ev_spill_cnt + 1 + ((slab + (size_t)r) & (S_EV_STRIPES - 1)), (uint32_t)tot);
   sbase = LPR == 64 ? __builtin_amdgcn_readfirstlane(sbase) : __shfl(sbase, sub * LPR, 64);
+#ifdef GM_ABL_NO_EVREC  // measurement builds only (scripts/r04 ablation): the event records not written
+  if (false) {
+#else
   if (live && nev) {
+#endif
     int slot = x - nev;
     uint32_t *slots = s.ev_band + ((size_t)r * s.nb + band) * E;
     for (uint32_t ek = evk; ek; ek &= ek - 1) {
@@ -893,32 +897,6 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
 // ------------------------------------------------------------ gm_s_band fast path
 // Lane-mask bit p in esc_mask16's order is cell esc_cell(p); esc_bit is the inverse.
 __device__ __forceinline__ int esc_bit(int q) { return ((q & 3) << 3) | (q >> 2); }
-// byte q of a lane's four stored dwords; the same with byte q replaced. q is dynamic: the dword is
-// chosen by masks, not by an index (which the compiler turns into a scratch array)
-__device__ __forceinline__ uint32_t lane_sel(int j, int i) { return (uint32_t)-(int)(j == i); }
-__device__ __forceinline__ uint32_t lane_byte(const uint32_t w[4], int q) {
-  const int j = q >> 2;
-  const uint32_t x = (w[0] & lane_sel(j, 0)) | (w[1] & lane_sel(j, 1)) | (w[2] & lane_sel(j, 2)) | (w[3] & lane_sel(j, 3));
-  return (x >> (8 * (q & 3))) & 0xFFu;
-}
-__device__ __forceinline__ void lane_set_byte(uint32_t w[4], int q, uint32_t v) {
-  const int j = q >> 2, sh = 8 * (q & 3);
-  const uint32_t m = 0xFFu << sh, b = v << sh;
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    const uint32_t si = lane_sel(j, i);
-    w[i] = (w[i] & ~(m & si)) | (b & si);
-  }
-}
-// payload nibble of lane cell q (nib_of's position) replaced in the lane's two payload words
-__device__ __forceinline__ void lane_set_nib(uint32_t &x0, uint32_t &x1, int q, uint32_t v) {
-  const int c = q & 7;
-  const int sh = 16 * (c & 1) + 4 * (3 - (c >> 1));
-  const uint32_t m = 0xFu << sh, b = v << sh;
-  if (q < 8) x0 = (x0 & ~m) | b;
-  else x1 = (x1 & ~m) | b;
-}
-
 // gm_s_band's fast path (one row per wave; no keyed loss, no join ramp): the merge and the sweep on
 // the stored bytes themselves. A stored byte x = h4 << 4 | a (h4 >= 3, a <= 14: gm_scaled.h) re-based
 // by one tick is x - 15 (h4 - 1, a + 1) and a delivered nibble n is the byte n << 4 (h' = 224 + 2n,
@@ -933,7 +911,7 @@ __device__ __forceinline__ void lane_set_nib(uint32_t &x0, uint32_t &x1, int q, 
 // any global store. Returns true when the unit is done.
 template <int B>
 __device__ __forceinline__ bool unit_fast(const SState &s, int t, const UnitIn<B> &in, const u32x2 m[S_SB],
-                                          uint32_t ent, uint32_t *lds) {
+                                          uint32_t ent, uint32_t *lds, uint32_t *park) {
   static_assert(B / S_COLS_PER_LANE == 64, "the fast path takes one row per wave");
   constexpr int Q = S_COLS_PER_LANE;
   const int lane = threadIdx.x & 63, li = lane;
@@ -995,13 +973,13 @@ __device__ __forceinline__ bool unit_fast(const SState &s, int t, const UnitIn<B
     nfail += __builtin_popcount(st);
     npres += __builtin_popcount(pr);
     spm |= ((pr & ~g3) | (a15 << 3)) >> (7 - w);  // esc_mask16's bit order
-    nb[w] = (hi - (pr >> 3)) & ~((st << 4) - st);
+    uint32_t st4 = st << 4;
+    asm volatile("" : "+v"(st4));  // else (st << 4) - st becomes a quarter-rate multiply by 15
+    nb[w] = (hi - (pr >> 3)) & ~(st4 - st);
   }
-  // payload words in nib_max's order: the high nibbles of cells [4, 0, 5, 1] | those of [6, 2, 7, 3]
-  // shifted down, for cells 0..7 and likewise 8..15
-  uint32_t ov0 = __builtin_amdgcn_perm(nb[1], nb[0], 0x01050004u) | (__builtin_amdgcn_perm(nb[1], nb[0], 0x03070206u) >> 4);
-  uint32_t ov1 = __builtin_amdgcn_perm(nb[3], nb[2], 0x01050004u) | (__builtin_amdgcn_perm(nb[3], nb[2], 0x03070206u) >> 4);
-  if (in.ebase != 0) spm |= esc_mask16(tb4[0], tb4[1], tb4[2], tb4[3]);  // row-uniform: escaped cells
+  uint32_t escm = 0;  // escaped cells (esc-order bits): their value is in the row slice's escape list
+  if (in.ebase != 0) escm = esc_mask16(tb4[0], tb4[1], tb4[2], tb4[3]);  // row-uniform
+  spm |= escm;
   const int selfc = (r >= s.c0 && r < s.c0 + s.w) ? r - s.c0 - colb : -1;
   const bool selflane = selfc >= 0 && selfc < Q;
   int hbself = 0;
@@ -1009,12 +987,18 @@ __device__ __forceinline__ bool unit_fast(const SState &s, int t, const UnitIn<B
     spm |= 1u << esc_bit(selfc);
     hbself = s.hbctr[r] + 1;
   }
-  // 4. the marked cells, exactly (16-bit cell; the general path's arithmetic)
+  // 4. the marked cells, exactly (16-bit cell; the general path's arithmetic). The lane's merged
+  // bytes and nibble bytes wait in LDS (park: 32 B per lane), so that a cell is one byte read and
+  // two byte writes there, not register selects
   int ngone = 0;
   uint32_t gmask = 0, em = 0;
   bool esc_row = false;
   if (__builtin_amdgcn_ballot_w64(spm != 0)) {
     uint16_t *row16 = (uint16_t *)lds;  // the wave's LDS: a 16-bit cell per column (lane li: [16 li, +16))
+    u32x4 *pk4 = (u32x4 *)(park + li * 8);
+    pk4[0] = (u32x4){bw[0], bw[1], bw[2], bw[3]};
+    pk4[1] = (u32x4){nb[0], nb[1], nb[2], nb[3]};
+    uint8_t *pb = (uint8_t *)(park + li * 8);  // [0, 16): the bytes, [16, 32): the nibbles (high-nibble form)
     if (in.ebase != 0) {  // the row slice's escape list, by column (its entries carry their columns)
       const int tot = (int)S_EW_TOT(in.ebase);
       if (li < min(tot, S_ESC_IN)) row16[ent & 0xFFFFu] = (uint16_t)(ent >> 16);
@@ -1025,15 +1009,14 @@ __device__ __forceinline__ bool unit_fast(const SState &s, int t, const UnitIn<B
           row16[e & 0xFFFFu] = (uint16_t)(e >> 16);
         }
       }
-      lds_wave_sync();
     }
+    lds_wave_sync();
     bool bail = false;
     for (uint32_t mm = spm; mm; mm &= mm - 1) {
       const int p = __builtin_ctz(mm), q = esc_cell(p);
-      const uint32_t x = lane_byte(tb4, q), y = lane_byte(bw, q);
-      // re-based cell max delivered key: y is exact unless x escaped (then y = the key: sat(1 - 15) = 0)
+      const uint32_t y = pb[q];  // the merged byte: exact unless the stored cell escaped (then the key)
       uint32_t c = s_widen(y);
-      if (x == S_B_ESC) {
+      if ((escm >> p) & 1u) {
         const uint32_t e = row16[li * Q + q];
         c = max(e ? e - 63u : 0u, c);
       }
@@ -1065,12 +1048,19 @@ __device__ __forceinline__ bool unit_fast(const SState &s, int t, const UnitIn<B
       const bool fpres = y >= 16u, fstale = fpres && (y & 15u) >= GM_TFAIL;
       npres += (int)(pres && !gone) - (int)fpres;
       nfail += (int)stale - (int)fstale;
-      lane_set_byte(bw, q, nbyte);
-      lane_set_nib(ov0, ov1, q, nib);
+      pb[q] = (uint8_t)nbyte;
+      pb[16 + q] = (uint8_t)(nib << 4);
     }
     if (__builtin_amdgcn_ballot_w64(bail)) return false;
     esc_row = __builtin_amdgcn_ballot_w64(em != 0) != 0;
+    const u32x4 b0 = pk4[0], b1 = pk4[1];
+    bw[0] = b0.x; bw[1] = b0.y; bw[2] = b0.z; bw[3] = b0.w;
+    nb[0] = b1.x; nb[1] = b1.y; nb[2] = b1.z; nb[3] = b1.w;
   }
+  // payload words in nib_max's order: the high nibbles of cells [4, 0, 5, 1] | those of [6, 2, 7, 3]
+  // shifted down, for cells 0..7 and likewise 8..15
+  const uint32_t ov0 = __builtin_amdgcn_perm(nb[1], nb[0], 0x01050004u) | (__builtin_amdgcn_perm(nb[1], nb[0], 0x03070206u) >> 4);
+  const uint32_t ov1 = __builtin_amdgcn_perm(nb[3], nb[2], 0x01050004u) | (__builtin_amdgcn_perm(nb[3], nb[2], 0x03070206u) >> 4);
   // 5. events: removals = gmask; joins = cells present now but absent as loaded -- there are some iff
   // the slice's present cells before the sweep (npres + ngone over the row) differ from the count
   // the record kept of the last tick (first tick after gm_s_init: no count kept, so the cells are
@@ -1180,14 +1170,14 @@ template <int B>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GM_BAND_MINW, 8))) void gm_s_band_fast(SState s, int t) {
   const int ub = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
   if (ub >= s.n) return;  // whole wave (one row per wave)
-  __shared__ uint32_t lds_all[4 * S_LDS_WAVE_WORDS];
-  uint32_t *lds = lds_all + (threadIdx.x >> 6) * S_LDS_WAVE_WORDS;
+  __shared__ uint32_t lds_all[4 * 2 * S_LDS_WAVE_WORDS];  // per wave: escape cells by column, then the park
+  uint32_t *lds = lds_all + (threadIdx.x >> 6) * 2 * S_LDS_WAVE_WORDS;
   UnitIn<B> in;
   unit_load<B, true>(s, t, (int)blockIdx.y, ub, in);
   u32x2 m[S_SB];
   uint32_t ent;
   unit_gather<B, false>(s, t, in, m, ent);
-  if (!unit_fast<B>(s, t, in, m, ent, lds) && (threadIdx.x & 63) == 0) {
+  if (!unit_fast<B>(s, t, in, m, ent, lds, lds + S_LDS_WAVE_WORDS) && (threadIdx.x & 63) == 0) {
     const uint32_t slot = atomicAdd(&s.fb_cnt[t & 1], 1u);  // < the units of a tick: the list's size
     s.fb_list[slot] = make_int2((int)blockIdx.y, ub);
   }
