@@ -1006,8 +1006,8 @@ static int place_entries(const SState &s, int b, const uint8_t *piece, const uin
 // SCALED: the last tick's join + remove records (the band kernel's striped partial sums) and
 // how many of them spilled to the ring
 static int tick_event_total(gm_ctx *c, uint64_t *total, uint32_t *spilled) {
-  uint32_t cnt[1 + S_EV_STRIPES];
-  HIPCHECK(hipMemcpyAsync(cnt, c->s.ev_spill_cnt, sizeof cnt, hipMemcpyDeviceToHost, c->stream));
+  std::vector<uint32_t> cnt(1 + S_EV_STRIPES);
+  HIPCHECK(hipMemcpyAsync(cnt.data(), c->s.ev_spill_cnt, sizeof(uint32_t) * cnt.size(), hipMemcpyDeviceToHost, c->stream));
   HIPCHECK(hipStreamSynchronize(c->stream));
   *spilled = cnt[0];
   *total = 0;

@@ -88,7 +88,7 @@ __host__ __device__ inline bool s_ingroup(int ramp, int intro_until, int r, int 
 // keyed loss threshold (gm_device.h gm_drop_thresh; gm_scaled.hip s_keep)
 __host__ __device__ inline uint32_t s_drop_thresh(int pct) { return gm_drop_thresh(pct); }
 
-#define S_EV_STRIPES 256
+#define S_EV_STRIPES 16384  // the tick's event total in partial sums (a TREMOVE tick adds ~4 M of them)
 #define S_EV_ADD 1u
 #define S_EV_REMOVE 2u
 

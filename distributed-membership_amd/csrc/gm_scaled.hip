@@ -65,12 +65,13 @@ struct RowMeta {
   int snd[S_SB];   // first S_SB senders
   uint32_t ebase;  // the (band, row) record's escape-list word of the last tick (S_EW_*, 0: no escaped cells)
   uint32_t bz;     // the record's count word of the last tick (S_BC_*: the slice's present cells as stored)
+  uint64_t evc;    // EVC: the (row, band)'s cumulative events (evcum), read with the metadata
 };
 
 // Every load of the row's metadata issues at once, none behind a branch on another (one
 // memory round trip before the payload gathers can issue, not a chain of three).
-template <int B, bool UNI>
-__device__ __forceinline__ RowMeta<B> row_meta(const SState &s, int r, int par, int t, size_t slab) {
+template <int B, bool UNI, bool EVC = false>
+__device__ __forceinline__ RowMeta<B> row_meta(const SState &s, int r, int par, int t, size_t slab, int band) {
   RowMeta<B> m;
   const int rc = min(r, s.n - 1);  // r >= n (a partial unit): loads stay in bounds, k = -1
   const int32_t *ib = s.inbox[par] + (size_t)rc * S_KMAX;
@@ -81,6 +82,10 @@ __device__ __forceinline__ RowMeta<B> row_meta(const SState &s, int r, int par, 
   const uint4 rec = s.brec[slab + rc];
   m.ebase = rec.w;
   m.bz = rec.z;
+  // the fast path (one row per wave): the unit is the only writer of its evcum cell this tick, so it is read
+  // here (in flight with the rest) and written back plainly -- no device-scope atomic per unit with
+  // events (at the TREMOVE peak ~4 M of them held the fast path's waves: +2 ms per tick)
+  m.evc = EVC ? s.evcum[(size_t)rc * s.nb + band] : 0ull;
   // empty asm statements that read the values here: without them the compiler sinks the
   // inbox-count load into a branch on `failed` and the sender ids behind that, two more
   // round trips before the gathers (one row per wave: scalar registers)
@@ -399,10 +404,12 @@ struct UnitIn {
   u32x4 ta;        // the row's 16 cell bytes of this lane (as loaded)
   uint32_t ebase;  // the row slice's escape list in the pool of tick t-1 (S_PESC_NONE: none)
   uint32_t bz;     // the (band, row) record's count word of tick t-1 (S_BC_PRES: present cells as loaded)
+  uint64_t evc;    // evcum of the (row, band) as of tick t-1 (uni: read by unit_load)
+  bool uni;        // the fast path's unit: its evcum cell is written back plainly, not by an atomic
 };
 
 // UNI: the row is wave-uniform and known to be (one row per wave, a grid-derived unit)
-template <int B, bool UNI = false>
+template <int B, bool UNI = false, bool EVC = false>
 __device__ __forceinline__ void unit_load(const SState &s, int t, int band, int ub, UnitIn<B> &in) {
   constexpr int LPR = B / S_COLS_PER_LANE, RPW = 64 / LPR, Q = S_COLS_PER_LANE;
   const int lane = threadIdx.x & 63;
@@ -414,12 +421,14 @@ __device__ __forceinline__ void unit_load(const SState &s, int t, int band, int 
   const uint32_t toff = (uint32_t)(in.r * B + li * Q);  // r >= n: out of range -> zeros, dropped
   // the table slice first: it is independent of the metadata, both in flight together
   in.ta = __builtin_amdgcn_raw_buffer_load_b128(trs, toff, 0, GM_AUX_NT);
-  const RowMeta<B> meta = row_meta<B, UNI>(s, in.r, t & 1, t, slab);
+  const RowMeta<B> meta = row_meta<B, UNI, EVC>(s, in.r, t & 1, t, slab, band);
 #pragma unroll
   for (int j = 0; j < S_SB; j++) in.snd[j] = meta.snd[j];
   in.k = meta.k;
   in.ebase = meta.ebase;
   in.bz = meta.bz;
+  in.evc = meta.evc;
+  in.uni = EVC;
 }
 
 // every payload slice at once; slots j >= k read out of range (zeros = "not sent"); with them,
@@ -538,10 +547,13 @@ __device__ __forceinline__ void unit_records(const SState &s, int t, const UnitI
 #pragma unroll
       for (int o = LPR / 2; o >= 1; o >>= 1) jr += __shfl_xor(jr, o, 64);
     }
-    // single writer per (row, band); a no-return atomic keeps the wave from waiting on a load
-    if (live && li == 0 && jr)
-      atomicAdd((unsigned long long *)&s.evcum[(size_t)r * s.nb + band],
-                (unsigned long long)(jr & 0xFFFF) | ((unsigned long long)(jr >> 16) << 32));
+    // single writer per (row, band): one row per wave writes back the value row_meta read; otherwise
+    // a no-return atomic (no wave waits on a load)
+    if (live && li == 0 && jr) {
+      const unsigned long long add = (unsigned long long)(jr & 0xFFFF) | ((unsigned long long)(jr >> 16) << 32);
+      if (in.uni) s.evcum[(size_t)r * s.nb + band] = in.evc + add;  // the only writer of the cell (row_meta)
+      else atomicAdd((unsigned long long *)&s.evcum[(size_t)r * s.nb + band], add);
+    }
   }
   const int E = s.evs;
   uint32_t sbase = 0;  // one spill-ring reservation per (row, band) that overflows its slots
@@ -1173,7 +1185,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GM_BAND_MIN
   __shared__ uint32_t lds_all[4 * 2 * S_LDS_WAVE_WORDS];  // per wave: escape cells by column, then the park
   uint32_t *lds = lds_all + (threadIdx.x >> 6) * 2 * S_LDS_WAVE_WORDS;
   UnitIn<B> in;
-  unit_load<B, true>(s, t, (int)blockIdx.y, ub, in);
+  unit_load<B, true, true>(s, t, (int)blockIdx.y, ub, in);
   u32x2 m[S_SB];
   uint32_t ent;
   unit_gather<B, false>(s, t, in, m, ent);
