@@ -389,7 +389,8 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                      "frac": (achieved / PEAK_HBM_GBPS) if achieved else None, "traffic": traffic,
                      "traffic_source": traffic_src,
-                     "kernel": "gm_s_band", "kernel_ms": kernel_ms,
+                     "kernel": "gm_s_band" if a.drop_pct else "gm_s_band_fast + gm_s_band_listed",
+                     "kernel_ms": kernel_ms,
                      "alg_bytes_per_launch": b_alg, "survey_int32_bytes_per_launch": b_survey,
                      "dram_bytes_est": dram_est, "frac_dram": frac_dram,
                      "columns_per_gpu": W},

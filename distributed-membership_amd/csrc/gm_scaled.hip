@@ -932,7 +932,21 @@ __device__ __forceinline__ bool unit_fast(const SState &s, int t, const UnitIn<B
   const int colb = band * B + li * Q;  // shard-local column of this lane's first cell
   const size_t slab = (size_t)band * s.n;
   const int k = in.k;  // wave-uniform
-  if (k < 0 || k > S_KMAX || s.ramp) return false;  // not merged / inbox error / join ramp: general path
+  if (k > S_KMAX || s.ramp) return false;  // inbox error / join ramp: general path
+  if (k < 0) {  // a row not merged this tick (crashed): its cells stay as they are, its escape list moves
+    uint32_t eb_out = 0;  // to this tick's storage (entries carry their columns), its record is written
+    if (in.ebase != 0) {
+      const int etot = (int)S_EW_TOT(in.ebase);
+      eb_out = row_alloc<64>(s, par, slab, r, etot, li, lane);
+      if (eb_out != 0) {
+        const EscList src = esc_list(s, par ^ 1, slab, r, in.ebase), dst = esc_list(s, par, slab, r, eb_out);
+        if (li < min(etot, S_ESC_IN)) *dst.at(li) = ent;
+        for (int i = S_ESC_IN + li; i < etot; i += 64) *dst.at(i) = *src.at(i);
+      }
+    }
+    unit_records<B, false>(s, t, in, false, eb_out, 0, 0, 0, 0u, 0);
+    return true;
+  }
   // 1. the delivered lists: per cell pair the largest nibble, in the top nibble of each u16 (nib_max)
   u16x2 acc[8];
 #pragma unroll
