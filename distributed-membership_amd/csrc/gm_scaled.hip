@@ -1399,7 +1399,9 @@ __device__ __forceinline__ uint32_t gm_mt_batch(GmLazyMT &mt, uint32_t *mts, uin
 // ------------------------------------------------------------------- gm_s_pick
 // Single-context tick, phase 2: one wave per observer row.
 template <int B>
-__global__ __launch_bounds__(256) void gm_s_pick(SState s, int t) {
+// 6 waves per SIMD (80 VGPRs, no spills) rather than the compiler's 5 (89): the kernel waits on
+// dependent loads, 141 -> 125 us per S-A tick (profiles/r04/pick_occupancy/)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) void gm_s_pick(SState s, int t) {
   extern __shared__ __align__(16) uint32_t p_smem[];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = blockIdx.x * 4 + wave;
