@@ -909,6 +909,46 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
 // ------------------------------------------------------------ gm_s_band fast path
 // Lane-mask bit p in esc_mask16's order is cell esc_cell(p); esc_bit is the inverse.
 __device__ __forceinline__ int esc_bit(int q) { return ((q & 3) << 3) | (q >> 2); }
+// set bits of a wave mask below this lane
+__device__ __forceinline__ int p_lanes_below(uint64_t b) {
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+}
+// One marked cell of the fast path, exactly (16-bit cell c: the merged byte y widened, or the escaped
+// cell re-based and merged; the general path's arithmetic): its stored byte, payload nibble (high-
+// nibble form), whether it is removed (TREMOVE) or needs the wide payload plane (bail), and the
+// corrections of the SWAR pass's present / stale counts, which counted the byte y.
+struct FastCell {
+  uint32_t nbyte, nib, c;
+  bool gone, bail;
+  int dpres, dfail;
+};
+__device__ __forceinline__ FastCell fast_cell(const SState &s, int t, uint32_t y, uint32_t c, bool self, int hbself) {
+  FastCell o;
+  if (self) {  // heartbeat++; myPos->setheartbeat(heartbeat++) (MP1Node.cpp:412-415)
+    if (c == 0) atomicOr(s.err, GM_ERR_SELF);  // converged start: the own entry is always present
+    const int h = 255 - (2 * t - hbself);
+    if (h < s.lag_hmin || h > 255) atomicOr(s.err, GM_ERR_LAG);
+    c = (uint32_t)S_CELL(h, 0) & 0xFFFFu;
+  }
+  const uint32_t age = c & 31u;
+  const bool pres = c != 0, stale = pres && age >= GM_TFAIL;
+  o.gone = pres && age >= GM_TREMOVE;  // TREMOVE (MP1Node.cpp:429-444): absent; it sent nothing (stale)
+  o.nbyte = o.nib = 0;
+  o.bail = false;
+  if (pres && !o.gone) {
+    o.nbyte = s_narrow(c);
+    if (!stale) {  // fresh: the nibble of h' = h - 2, or the wide plane (general path)
+      const uint32_t hp = (c >> 5) - 2u;
+      if ((hp & 1u) || hp < S_NIB_H(1) || hp > S_NIB_H(14)) o.bail = true;
+      else o.nib = ((hp - S_NIB_BASE) >> 1) << 4;
+    }
+  }
+  o.c = c;
+  const bool fpres = y >= 16u, fstale = fpres && (y & 15u) >= GM_TFAIL;
+  o.dpres = (int)(pres && !o.gone) - (int)fpres;
+  o.dfail = (int)stale - (int)fstale;
+  return o;
+}
 // gm_s_band's fast path (one row per wave; no keyed loss, no join ramp): the merge and the sweep on
 // the stored bytes themselves. A stored byte x = h4 << 4 | a (h4 >= 3, a <= 14: gm_scaled.h) re-based
 // by one tick is x - 15 (h4 - 1, a + 1) and a delivered nibble n is the byte n << 4 (h' = 224 + 2n,
@@ -1003,9 +1043,6 @@ __device__ __forceinline__ bool unit_fast(const SState &s, int t, const UnitIn<B
     asm volatile("" : "+v"(st4));  // else (st << 4) - st becomes a quarter-rate multiply by 15
     nb[w] = (hi - (pr >> 3)) & ~(st4 - st);
   }
-  uint32_t escm = 0;  // escaped cells (esc-order bits): their value is in the row slice's escape list
-  if (in.ebase != 0) escm = esc_mask16(tb4[0], tb4[1], tb4[2], tb4[3]);  // row-uniform
-  spm |= escm;
   const int selfc = (r >= s.c0 && r < s.c0 + s.w) ? r - s.c0 - colb : -1;
   const bool selflane = selfc >= 0 && selfc < Q;
   int hbself = 0;
@@ -1013,75 +1050,103 @@ __device__ __forceinline__ bool unit_fast(const SState &s, int t, const UnitIn<B
     spm |= 1u << esc_bit(selfc);
     hbself = s.hbctr[r] + 1;
   }
-  // 4. the marked cells, exactly (16-bit cell; the general path's arithmetic). The lane's merged
-  // bytes and nibble bytes wait in LDS (park: 32 B per lane), so that a cell is one byte read and
-  // two byte writes there, not register selects
+#ifdef GM_ABL_SPECIAL_ALWAYS  // measurement builds only: every unit takes the per-cell pass (cell 0 of lane 0, exact anyway)
+  if (li == 0) spm |= 1u;
+#endif
+  // 4. the marked cells, exactly (fast_cell). The lane's merged bytes and nibble bytes wait in LDS
+  // (park: 32 B per lane), so that a cell is one byte read and two byte writes there, not register
+  // selects. Escaped cells go entry-parallel: lane j takes entry j of the row slice's escape list (the
+  // entries carry their columns) and that column's parked byte, whichever lane holds it; what the
+  // holding lane needs back (that its cell was escaped, its removal bits, its count corrections) meets
+  // in that lane's three words `cor` (LDS or / add). The other marked cells (age 15, h4 <= 2, the own
+  // cell) are taken one by one in their own lane. An escaped cell that stays escaped is this tick's
+  // list entry straight from its entry lane (sv / sent: VALU issue is what these ticks spend, and
+  // the wave pays every instruction of a per-lane loop at its longest lane); past 64 entries (a cold
+  // start) they go through the row's 16-bit cells like the per-lane loop's new ones.
   int ngone = 0;
-  uint32_t gmask = 0, em = 0;
-  bool esc_row = false;
-  if (__builtin_amdgcn_ballot_w64(spm != 0)) {
+  uint32_t gmask = 0, em = 0, sent = 0;
+  bool sv = false, epar = true;
+  const bool eslice = in.ebase != 0;  // row-uniform
+  if (eslice || __builtin_amdgcn_ballot_w64(spm != 0)) {
     uint16_t *row16 = (uint16_t *)lds;  // the wave's LDS: a 16-bit cell per column (lane li: [16 li, +16))
     u32x4 *pk4 = (u32x4 *)(park + li * 8);
     pk4[0] = (u32x4){bw[0], bw[1], bw[2], bw[3]};
     pk4[1] = (u32x4){nb[0], nb[1], nb[2], nb[3]};
-    uint8_t *pb = (uint8_t *)(park + li * 8);  // [0, 16): the bytes, [16, 32): the nibbles (high-nibble form)
-    if (in.ebase != 0) {  // the row slice's escape list, by column (its entries carry their columns)
-      const int tot = (int)S_EW_TOT(in.ebase);
-      if (li < min(tot, S_ESC_IN)) row16[ent & 0xFFFFu] = (uint16_t)(ent >> 16);
-      if (tot > S_ESC_IN) {
-        const EscList l = esc_list(s, par ^ 1, slab, r, in.ebase);
-        for (int i = S_ESC_IN + li; i < tot; i += 64) {
-          const uint32_t e = *l.at(i);
-          row16[e & 0xFFFFu] = (uint16_t)(e >> 16);
-        }
-      }
-    }
+    uint8_t *pall = (uint8_t *)park;  // lane l's cell q: byte 32 l + q, its nibble byte 32 l + 16 + q
+    uint8_t *pb = pall + li * 32;
+    // per lane: cor[li] = its escaped cells as loaded (esc order), cor[64 + li] = removal bits (cell
+    // order), cor[128 + li] = the present / stale corrections, packed as dpres + dfail << 16
+    uint32_t *cor = park + S_LDS_WAVE_WORDS;
+    if (eslice) cor[li] = cor[64 + li] = cor[128 + li] = 0u;
     lds_wave_sync();
     bool bail = false;
-    for (uint32_t mm = spm; mm; mm &= mm - 1) {
+    uint32_t escm = 0;  // this lane's escaped cells (esc order): the entry lanes took them
+    if (eslice) {
+      const int tot = (int)S_EW_TOT(in.ebase);
+      epar = tot <= 64;
+      const int selfb = r - s.c0 - band * B;  // the own column in the band (row-uniform), if in [0, B)
+      const int hbs = (selfb >= 0 && selfb < B) ? __builtin_amdgcn_readlane(hbself, selfb / Q) : 0;
+      const EscList l = esc_list(s, par ^ 1, slab, r, in.ebase);
+      for (int j0 = 0; j0 < tot; j0 += 64) {
+        const int j = j0 + li;
+        if (j < tot) {
+          const uint32_t e = j < S_ESC_IN ? ent : *l.at(j);  // lane li < S_ESC_IN prefetched entry li
+          const int col = (int)(e & 0xFFFFu), q = col % Q, ol = col / Q;
+          uint8_t *cb = pall + ol * 32 + q;
+          const uint32_t y = cb[0];  // the merged byte of an escaped cell: the delivered key alone
+          const uint32_t ev = e >> 16;
+          const FastCell o = fast_cell(s, t, y, max(ev ? ev - 63u : 0u, s_widen(y)), col == selfb, hbs);
+          bail |= o.bail;
+          atomicOr(cor + ol, 1u << esc_bit(q));
+          if (o.nbyte == S_B_ESC) {  // an entry of this tick's list
+            if (epar) {
+              sv = true;
+              sent = (uint32_t)col | (o.c << 16);
+            } else {
+              row16[col] = (uint16_t)o.c;  // esc_emit reads it here (em: the escape bytes, below)
+            }
+          }
+          if (o.gone) atomicOr(cor + 64 + ol, 1u << q);
+          cb[0] = (uint8_t)o.nbyte;
+          cb[16] = (uint8_t)o.nib;
+          if (o.dpres | o.dfail) atomicAdd(cor + 128 + ol, (uint32_t)(o.dpres + o.dfail * 65536));
+        }
+      }
+      lds_wave_sync();
+      escm = cor[li];
+    }
+    for (uint32_t mm = spm & ~escm; mm; mm &= mm - 1) {
       const int p = __builtin_ctz(mm), q = esc_cell(p);
-      const uint32_t y = pb[q];  // the merged byte: exact unless the stored cell escaped (then the key)
-      uint32_t c = s_widen(y);
-      if ((escm >> p) & 1u) {
-        const uint32_t e = row16[li * Q + q];
-        c = max(e ? e - 63u : 0u, c);
-      }
-      if (q == selfc) {  // heartbeat++; myPos->setheartbeat(heartbeat++) (MP1Node.cpp:412-415)
-        if (c == 0) atomicOr(s.err, GM_ERR_SELF);  // converged start: the own entry is always present
-        const int h = 255 - (2 * t - hbself);
-        if (h < s.lag_hmin || h > 255) atomicOr(s.err, GM_ERR_LAG);
-        c = (uint32_t)S_CELL(h, 0) & 0xFFFFu;
-      }
-      const uint32_t age = c & 31u;
-      const bool pres = c != 0, stale = pres && age >= GM_TFAIL, gone = pres && age >= GM_TREMOVE;
-      uint32_t nbyte = 0, nib = 0;
-      if (gone) {  // TREMOVE (MP1Node.cpp:429-444): absent; it sent nothing (stale)
+      const uint32_t y = pb[q];  // the merged byte (exact: the stored cell did not escape)
+      const FastCell o = fast_cell(s, t, y, s_widen(y), q == selfc, hbself);
+      bail |= o.bail;
+      if (o.gone) {
         gmask |= 1u << q;
         ngone++;
-      } else if (pres) {
-        nbyte = s_narrow(c);
-        if (nbyte == S_B_ESC) {  // an entry of this tick's list (unit_stores: esc_emit reads it here)
-          em |= 1u << p;
-          row16[li * Q + q] = (uint16_t)c;
-        }
-        if (!stale) {  // fresh: the nibble of h' = h - 2, or the wide plane (general path)
-          const uint32_t hp = (c >> 5) - 2u;
-          if ((hp & 1u) || hp < S_NIB_H(1) || hp > S_NIB_H(14)) bail = true;
-          else nib = (hp - S_NIB_BASE) >> 1;
-        }
       }
-      // the fast pass's counts of this cell, replaced
-      const bool fpres = y >= 16u, fstale = fpres && (y & 15u) >= GM_TFAIL;
-      npres += (int)(pres && !gone) - (int)fpres;
-      nfail += (int)stale - (int)fstale;
-      pb[q] = (uint8_t)nbyte;
-      pb[16 + q] = (uint8_t)(nib << 4);
+      if (o.nbyte == S_B_ESC) {
+        em |= 1u << p;
+        row16[li * Q + q] = (uint16_t)o.c;
+      }
+      npres += o.dpres;
+      nfail += o.dfail;
+      pb[q] = (uint8_t)o.nbyte;
+      pb[16 + q] = (uint8_t)o.nib;
     }
     if (__builtin_amdgcn_ballot_w64(bail)) return false;
-    esc_row = __builtin_amdgcn_ballot_w64(em != 0) != 0;
+    lds_wave_sync();  // other lanes' entries wrote into this lane's park and words
+    if (eslice) {
+      const uint32_t ge = cor[64 + li], cd = cor[128 + li];
+      gmask |= ge;
+      ngone += __builtin_popcount(ge);
+      const int dp = (int)(int16_t)(cd & 0xFFFFu);
+      npres += dp;
+      nfail += ((int)cd - dp) >> 16;
+    }
     const u32x4 b0 = pk4[0], b1 = pk4[1];
     bw[0] = b0.x; bw[1] = b0.y; bw[2] = b0.z; bw[3] = b0.w;
     nb[0] = b1.x; nb[1] = b1.y; nb[2] = b1.z; nb[3] = b1.w;
+    if (!epar) em = esc_mask16(bw[0], bw[1], bw[2], bw[3]);  // every escape byte: row16 holds its cell
   }
   // payload words in nib_max's order: the high nibbles of cells [4, 0, 5, 1] | those of [6, 2, 7, 3]
   // shifted down, for cells 0..7 and likewise 8..15
@@ -1118,9 +1183,29 @@ __device__ __forceinline__ bool unit_fast(const SState &s, int t, const UnitIn<B
     evk = x << 1;
     nev = ngone;
   }
-  // 6. commit (the general path's)
+  // 6. commit: the table and payload stores (the general path's), then this tick's escape list --
+  // the entry lanes' survivors first (ballot rank), the lanes' escape bytes after them (esc_emit)
   if (selflane) s.hbctr[r] = hbself + 1;
-  const uint32_t eb_out = unit_stores<B>(s, t, in, bw, ov0, ov1, esc_row, em, lds);
+  uint32_t eb_out = unit_stores<B>(s, t, in, bw, ov0, ov1, false, 0u, lds);
+  const uint64_t svb = __builtin_amdgcn_ballot_w64(sv);
+  const bool emany = __builtin_amdgcn_ballot_w64(em != 0) != 0;
+  if (svb || emany) {
+    const int ns = __builtin_popcountll(svb);
+    int etot = ns, eoff = 0;
+    if (emany) {
+      eoff = row_scan<64>(__builtin_popcount(em), li, lane, etot);
+      etot += ns;
+    }
+    eb_out = row_alloc<64>(s, par, slab, r, etot, li, lane);
+    if (eb_out != 0) {
+      const EscList l = esc_list(s, par, slab, r, eb_out);
+      if (sv) {
+        *l.at(p_lanes_below(svb)) = sent;
+        if ((sent >> 16) < (uint32_t)S_CELL(s.lag_hmin, 0)) atomicOr(s.err, GM_ERR_LAG);
+      }
+      if (emany) esc_emit(lds, lane, l, ns + eoff, em, li * Q, etot <= S_ESC_IN, s.err, s.lag_hmin);
+    }
+  }
   unit_records<B, false>(s, t, in, true, eb_out, npres, nfail, nev, evk, 0);
   return true;
 }
@@ -1196,8 +1281,10 @@ template <int B>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GM_BAND_MINW, 8))) void gm_s_band_fast(SState s, int t) {
   const int ub = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
   if (ub >= s.n) return;  // whole wave (one row per wave)
-  __shared__ uint32_t lds_all[4 * 2 * S_LDS_WAVE_WORDS];  // per wave: escape cells by column, then the park
-  uint32_t *lds = lds_all + (threadIdx.x >> 6) * 2 * S_LDS_WAVE_WORDS;
+  // per wave: escape cells by column, the park, the per-lane words of the escaped cells' outcomes
+  constexpr int W = 2 * S_LDS_WAVE_WORDS + 192;
+  __shared__ uint32_t lds_all[4 * W];
+  uint32_t *lds = lds_all + (threadIdx.x >> 6) * W;
   UnitIn<B> in;
   unit_load<B, true, true>(s, t, (int)blockIdx.y, ub, in);
   u32x2 m[S_SB];
