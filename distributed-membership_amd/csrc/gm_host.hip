@@ -109,6 +109,19 @@ struct gm_ctx {
   hipEvent_t p_done = nullptr;         // the tick's exchange + unpacks are done (comm stream)
 };
 
+// Every copy and fill of a context goes through its own stream. That stream is non-blocking, so the
+// legacy null stream that hipMemcpy / hipMemset use neither waits for its kernels nor is waited for by
+// them: a fill at creation could still be running when the init kernel writes (seen as an own entry
+// missing from an S-C view after a 8.6 GB fill of the lists), and a host-to-device copy may return
+// before its DMA lands. Fills are enqueued in order; copies wait for the stream (the host buffers are
+// the caller's).
+static inline hipError_t ctx_memset(gm_ctx *c, void *p, int v, size_t n) { return hipMemsetAsync(p, v, n, c->stream); }
+static inline hipError_t ctx_memcpy(gm_ctx *c, void *d, const void *src, size_t n, hipMemcpyKind k) {
+  const hipError_t e = hipMemcpyAsync(d, src, n, k, c->stream);
+  return e == hipSuccess ? hipStreamSynchronize(c->stream) : e;
+}
+
+
 static thread_local char g_errbuf[256];
 
 #define HIPCHECK(x)                                                                   \
@@ -275,24 +288,24 @@ static int create_faithful(gm_ctx *c) {
   lap("faithful allocations");
   if (hipHostMalloc(&c->f_mail, 16 + sizeof(FEvent) * GM_F_MAILBOX, hipHostMallocDefault) != hipSuccess) return GM_ENOMEM;
   lap("pinned mailbox");
-  HIPCHECK(hipMemset(f.table, 0xFF, sizeof(uint32_t) * (size_t)n * f.np));
+  HIPCHECK(ctx_memset(c, f.table, 0xFF, sizeof(uint32_t) * (size_t)n * f.np));
   std::vector<int32_t> start(n);
   for (int i = 0; i < n; i++) start[i] = (int)(0.25 * i);  // (int)(STEP_RATE*i), Application.cpp:143
-  HIPCHECK(hipMemcpy(f.start, start.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice));
+  HIPCHECK(ctx_memcpy(c, f.start, start.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice));
   for (int32_t *p : {f.failed, f.inited, f.ingroup, f.hbctr, f.started_now, f.q_off, f.q_cnt,
                      f.scount, f.jcnt, f.gcnt, f.fcnt})
-    HIPCHECK(hipMemset(p, 0, sizeof(int32_t) * (size_t)n));
-  HIPCHECK(hipMemset(f.sent, 0, sizeof(int32_t) * (size_t)(n + 1) * f.tmax));
-  HIPCHECK(hipMemset(f.recv, 0, sizeof(int32_t) * (size_t)(n + 1) * f.tmax));
-  HIPCHECK(hipMemset(f.bufsize, 0, sizeof(int32_t)));
-  HIPCHECK(hipMemset(f.ev_count, 0, sizeof(unsigned long long)));
-  HIPCHECK(hipMemset(f.err, 0, sizeof(uint32_t)));
+    HIPCHECK(ctx_memset(c, p, 0, sizeof(int32_t) * (size_t)n));
+  HIPCHECK(ctx_memset(c, f.sent, 0, sizeof(int32_t) * (size_t)(n + 1) * f.tmax));
+  HIPCHECK(ctx_memset(c, f.recv, 0, sizeof(int32_t) * (size_t)(n + 1) * f.tmax));
+  HIPCHECK(ctx_memset(c, f.bufsize, 0, sizeof(int32_t)));
+  HIPCHECK(ctx_memset(c, f.ev_count, 0, sizeof(unsigned long long)));
+  HIPCHECK(ctx_memset(c, f.err, 0, sizeof(uint32_t)));
   int32_t st[33];
   s1_seed(c->cfg.time_seed, st);  // srand(time(NULL)) at Application.cpp:50 and :96
-  HIPCHECK(hipMemcpy(f.s1, st, sizeof st, hipMemcpyHostToDevice));
+  HIPCHECK(ctx_memcpy(c, f.s1, st, sizeof st, hipMemcpyHostToDevice));
   lap("faithful memsets");
   const std::vector<uint32_t> pm = s1_round_powers();
-  HIPCHECK(hipMemcpy(f.s1mat, pm.data(), sizeof(uint32_t) * pm.size(), hipMemcpyHostToDevice));
+  HIPCHECK(ctx_memcpy(c, f.s1mat, pm.data(), sizeof(uint32_t) * pm.size(), hipMemcpyHostToDevice));
   lap("S1 powers");
   HIPCHECK(hipFuncSetAttribute((const void *)gm_f_recv, hipFuncAttributeMaxDynamicSharedMemorySize, F_RECV_LDS));
   lap("kernel attributes");
@@ -418,8 +431,8 @@ static int create_scaled(gm_ctx *c) {
   }
   TRY(dalloc(c, &s.tesc_cnt, 2 * (size_t)S));
   TRY(dalloc(c, &s.pesc_cnt, 2 * (size_t)S));
-  HIPCHECK(hipMemset(s.tesc_cnt, 0, 2 * S * sizeof(unsigned long long)));
-  HIPCHECK(hipMemset(s.pesc_cnt, 0, 2 * S * sizeof(unsigned long long)));
+  HIPCHECK(ctx_memset(c, s.tesc_cnt, 0, 2 * S * sizeof(unsigned long long)));
+  HIPCHECK(ctx_memset(c, s.pesc_cnt, 0, 2 * S * sizeof(unsigned long long)));
   for (int p = 0; p < 2; p++) {
     TRY(dalloc(c, &s.inbox_cnt[p], n));
     TRY(dalloc(c, &s.inbox[p], (size_t)n * S_KMAX));
@@ -435,7 +448,7 @@ static int create_scaled(gm_ctx *c) {
   s.fb_list = nullptr;
   if (s.band == 1024 && !(getenv("GM_BAND_FAST") && atoi(getenv("GM_BAND_FAST")) == 0)) {
     TRY(dalloc(c, &s.fb_cnt, 2));
-    HIPCHECK(hipMemset(s.fb_cnt, 0, 2 * sizeof(uint32_t)));
+    HIPCHECK(ctx_memset(c, s.fb_cnt, 0, 2 * sizeof(uint32_t)));
     TRY(dalloc(c, &s.fb_list, (size_t)n * s.nb));
   }
   TRY(dalloc(c, &s.ev_band, (size_t)n * s.nb * s.evs));
@@ -468,27 +481,26 @@ static int create_scaled(gm_ctx *c) {
   s.intro_until = 0x7FFFFFFF;
   if (ramp) {
     TRY(dalloc(c, &s.mecol, n));
-    HIPCHECK(hipMemset(s.mecol, 0xFF, sizeof(int32_t) * n));  // -1: written by the rank owning the row's column
+    HIPCHECK(ctx_memset(c, s.mecol, 0xFF, sizeof(int32_t) * n));  // -1: written by the rank owning the row's column
     TRY(dalloc(c, &s.selfadd, S_SELFADD_CAP));
     TRY(dalloc(c, &s.selfadd_cnt, 1));
-    HIPCHECK(hipMemset(s.selfadd_cnt, 0, sizeof(uint32_t)));
+    HIPCHECK(ctx_memset(c, s.selfadd_cnt, 0, sizeof(uint32_t)));
   }
-  HIPCHECK(hipMemset(s.msg, 0, sizeof(uint8_t) * cells));
-  for (int p = 0; p < 2; p++) HIPCHECK(hipMemset(s.inbox_cnt[p], 0, sizeof(int32_t) * n));
-  HIPCHECK(hipMemset(s.failed, 0, sizeof(int32_t) * n));
-  HIPCHECK(hipMemset(s.err, 0, sizeof(uint32_t)));
-  HIPCHECK(hipDeviceSynchronize());  // the memsets above are done before the init kernel runs on c->stream
+  HIPCHECK(ctx_memset(c, s.msg, 0, sizeof(uint8_t) * cells));
+  for (int p = 0; p < 2; p++) HIPCHECK(ctx_memset(c, s.inbox_cnt[p], 0, sizeof(int32_t) * n));
+  HIPCHECK(ctx_memset(c, s.failed, 0, sizeof(int32_t) * n));
+  HIPCHECK(ctx_memset(c, s.err, 0, sizeof(uint32_t)));
   HIPCHECK(gm_launch_init(s, ramp ? 2 : warm ? 1 : 0, t0, c->cfg.init_seed, c->stream));  // table, records, pool
   HIPCHECK(hipStreamSynchronize(c->stream));
   uint32_t ierr = 0;
-  HIPCHECK(hipMemcpy(&ierr, s.err, sizeof ierr, hipMemcpyDeviceToHost));
+  HIPCHECK(ctx_memcpy(c, &ierr, s.err, sizeof ierr, hipMemcpyDeviceToHost));
   if (ierr) {  // a cold start escapes every cell: beyond the dense-pool size it does not fit
     snprintf(g_errbuf, sizeof g_errbuf, "initial state overflows the escape pool (%zu cells)", s.tesc_cap);
     return GM_ERANGE;
   }
-  HIPCHECK(hipMemset(s.ev_spill_cnt, 0, (1 + S_EV_STRIPES) * sizeof(uint32_t)));
-  HIPCHECK(hipMemset(s.evcum, 0, sizeof(uint64_t) * (size_t)n * s.nb));
-  HIPCHECK(hipMemset(s.rowstat, 0, sizeof(int32_t) * n * 4));
+  HIPCHECK(ctx_memset(c, s.ev_spill_cnt, 0, (1 + S_EV_STRIPES) * sizeof(uint32_t)));
+  HIPCHECK(ctx_memset(c, s.evcum, 0, sizeof(uint64_t) * (size_t)n * s.nb));
+  HIPCHECK(ctx_memset(c, s.rowstat, 0, sizeof(int32_t) * n * 4));
   if (s.sharded) {
     TRY(dalloc(c, &s.acc, (size_t)n * 8));
     TRY(dalloc(c, &s.pending, n));
@@ -510,8 +522,8 @@ static int create_scaled(gm_ctx *c) {
       TRY(dalloc(c, &s.plist_cnt[l], 1));
       TRY(dalloc(c, &s.statusl[l], (size_t)s.plist_cap[l] * (l == 1 ? GM_D_MORE : GM_D_LAST)));
     }
-    HIPCHECK(hipMemset(s.pending, 0, sizeof(int32_t) * n));
-    HIPCHECK(hipMemset(s.xcnt, 0, sizeof(int32_t) * (size_t)G * n * 2));
+    HIPCHECK(ctx_memset(c, s.pending, 0, sizeof(int32_t) * n));
+    HIPCHECK(ctx_memset(c, s.xcnt, 0, sizeof(int32_t) * (size_t)G * n * 2));
   }
   c->t = t0 + 1;  // the converged table is the state "as of tick t0"
   return GM_OK;
@@ -548,7 +560,7 @@ static int create_partial(gm_ctx *c) {
   TRY(dalloc(c, &p.lists, (size_t)2 * p.rows * p.V));
   for (int q = 0; q < 2; q++) {
     TRY(dalloc(c, &p.inbox[q], (size_t)nl * P_KMAX));
-    HIPCHECK(hipMemset(p.inbox[q], 0, sizeof(int32_t) * nl * P_KMAX));  // the counts (slot 0) start at 0
+    HIPCHECK(ctx_memset(c, p.inbox[q], 0, sizeof(int32_t) * nl * P_KMAX));  // the counts (slot 0) start at 0
     if (G > 1) TRY(dalloc(c, &p.rsrc[q], R));
     if (G == 1) p.rsrc[q] = nullptr;
   }
@@ -587,10 +599,10 @@ static int create_partial(gm_ctx *c) {
     HIPCHECK(hipEventCreateWithFlags(&c->p_done, hipEventDisableTiming));
     TRY(dalloc(c, &p.sp_hdr, (size_t)G * nl * 8));
     TRY(dalloc(c, &p.sp_list, (size_t)G * nl * p.V));
-    HIPCHECK(hipMemset(p.sp_hdr, 0xFF, sizeof(int32_t) * G * nl * 8));  // stamp -1: no record yet
+    HIPCHECK(ctx_memset(c, p.sp_hdr, 0xFF, sizeof(int32_t) * G * nl * 8));  // stamp -1: no record yet
     TRY(dalloc(c, &p.pk_hdr, (size_t)G * nl * 8));
     TRY(dalloc(c, &p.pk_list, (size_t)G * nl * p.V));
-    HIPCHECK(hipMemset(p.pk_hdr, 0xFF, sizeof(int32_t) * G * nl * 8));
+    HIPCHECK(ctx_memset(c, p.pk_hdr, 0xFF, sizeof(int32_t) * G * nl * 8));
     TRY(dalloc(c, &p.pk_cnt, (size_t)p.nchunk * G));
     p.xcap_frac = getenv("GM_XCHG_CAP_FRAC") ? (float)atof(getenv("GM_XCHG_CAP_FRAC")) : 0.f;
     if (p.xcap_frac < 0.f || p.xcap_frac > 1.f) return GM_EINVAL;
@@ -599,13 +611,13 @@ static int create_partial(gm_ctx *c) {
     std::vector<int32_t> b(G + 1);
     for (int g = 0; g <= G; g++) b[g] = (int32_t)((int64_t)n * g / G);
     TRY(dalloc(c, &p.shard_n0, G + 1));
-    HIPCHECK(hipMemcpy(p.shard_n0, b.data(), sizeof(int32_t) * (G + 1), hipMemcpyHostToDevice));
+    HIPCHECK(ctx_memcpy(c, p.shard_n0, b.data(), sizeof(int32_t) * (G + 1), hipMemcpyHostToDevice));
   }
-  HIPCHECK(hipMemset(p.lists, 0, sizeof(uint64_t) * 2 * p.rows * p.V));
-  HIPCHECK(hipMemset(p.failed, 0, sizeof(int32_t) * nl));
-  HIPCHECK(hipMemset(p.ev_cnt, 0, sizeof(int32_t) * nl));
-  HIPCHECK(hipMemset(p.rowstat, 0, sizeof(int32_t) * nl * 4));
-  HIPCHECK(hipMemset(p.err, 0, sizeof(uint32_t)));
+  HIPCHECK(ctx_memset(c, p.lists, 0, sizeof(uint64_t) * 2 * p.rows * p.V));
+  HIPCHECK(ctx_memset(c, p.failed, 0, sizeof(int32_t) * nl));
+  HIPCHECK(ctx_memset(c, p.ev_cnt, 0, sizeof(int32_t) * nl));
+  HIPCHECK(ctx_memset(c, p.rowstat, 0, sizeof(int32_t) * nl * 4));
+  HIPCHECK(ctx_memset(c, p.err, 0, sizeof(uint32_t)));
   HIPCHECK(gm_launch_partial_init(p, t0, c->cfg.init_seed, c->stream));
   HIPCHECK(hipStreamSynchronize(c->stream));
   c->t = t0 + 1;
@@ -731,7 +743,7 @@ static int f_collect(gm_ctx *c) {
     std::vector<FEvent> ev(nev);
     memcpy(ev.data(), (const uint8_t *)c->f_mail + 16, sizeof(FEvent) * std::min<size_t>(nev, GM_F_MAILBOX));
     if (nev > GM_F_MAILBOX) {
-      HIPCHECK(hipMemcpy(ev.data() + GM_F_MAILBOX, c->f.ev + GM_F_MAILBOX, sizeof(FEvent) * (nev - GM_F_MAILBOX),
+      HIPCHECK(ctx_memcpy(c, ev.data() + GM_F_MAILBOX, c->f.ev + GM_F_MAILBOX, sizeof(FEvent) * (nev - GM_F_MAILBOX),
                          hipMemcpyDeviceToHost));
     }
     std::sort(ev.begin(), ev.end(), ev_order);
@@ -942,7 +954,7 @@ extern "C" int gm_rand(gm_ctx *c, int32_t *out) {
   st[f] = (int32_t)v;
   st[31] = (f + 1) % 31;
   st[32] = (r + 1) % 31;
-  HIPCHECK(hipMemcpy(c->f.s1, st, sizeof st, hipMemcpyHostToDevice));
+  HIPCHECK(ctx_memcpy(c, c->f.s1, st, sizeof st, hipMemcpyHostToDevice));
   *out = (int32_t)(v >> 1);
   return GM_OK;
 }
@@ -962,7 +974,7 @@ extern "C" int gm_set_failed(gm_ctx *c, const int32_t *idx, int32_t n) {
   int32_t *dst = c->cfg.mode == GM_MODE_FAITHFUL ? c->f.failed : c->cfg.mode == GM_MODE_SCALED ? c->s.failed : c->p.failed;
   const bool part = c->cfg.mode == GM_MODE_PARTIAL;  // a row shard holds its own nodes' flags only
   HIPCHECK(hipStreamSynchronize(c->stream));
-  HIPCHECK(hipMemcpy(dst, c->failed_h.data() + (part ? c->p.n0 : 0), sizeof(int32_t) * (part ? c->p.nloc : c->n),
+  HIPCHECK(ctx_memcpy(c, dst, c->failed_h.data() + (part ? c->p.n0 : 0), sizeof(int32_t) * (part ? c->p.nloc : c->n),
                      hipMemcpyHostToDevice));
   return GM_OK;
 }
@@ -1034,7 +1046,7 @@ static int drain_scaled(gm_ctx *c, std::vector<gm_event> &out) {
   for (uint32_t v : bc) any |= S_BC_NEV(v) != 0;
   if (any) {
     std::vector<uint32_t> ev(nrb * s.evs);
-    HIPCHECK(hipMemcpy(ev.data(), s.ev_band, sizeof(uint32_t) * ev.size(), hipMemcpyDeviceToHost));
+    HIPCHECK(ctx_memcpy(c, ev.data(), s.ev_band, sizeof(uint32_t) * ev.size(), hipMemcpyDeviceToHost));
     for (size_t i = 0; i < nrb; i++) {
       const int k = std::min<int>((int)S_BC_NEV(bc[i]), s.evs);
       for (int q = 0; q < k; q++) push((int)(i / s.nb), ev[i * s.evs + q]);
@@ -1043,7 +1055,7 @@ static int drain_scaled(gm_ctx *c, std::vector<gm_event> &out) {
   nsp = std::min(nsp, s.ev_spill_cap);
   if (nsp) {
     std::vector<uint64_t> sp(nsp);
-    HIPCHECK(hipMemcpy(sp.data(), s.ev_spill, sizeof(uint64_t) * nsp, hipMemcpyDeviceToHost));
+    HIPCHECK(ctx_memcpy(c, sp.data(), s.ev_spill, sizeof(uint64_t) * nsp, hipMemcpyDeviceToHost));
     for (uint64_t v : sp) push((int)(v >> 32), (uint32_t)v);
   }
   return GM_OK;
@@ -1068,7 +1080,7 @@ static int drain_partial(gm_ctx *c, std::vector<gm_event> &out) {
   if (!tot) return GM_OK;
   const size_t row = 2 * (size_t)p.V;  // joins from the front, removals from the back
   std::vector<uint32_t> ev((size_t)p.nloc * row);
-  HIPCHECK(hipMemcpy(ev.data(), p.ev, sizeof(uint32_t) * ev.size(), hipMemcpyDeviceToHost));
+  HIPCHECK(ctx_memcpy(c, ev.data(), p.ev, sizeof(uint32_t) * ev.size(), hipMemcpyDeviceToHost));
   const int t = c->t - 1;
   out.reserve(out.size() + tot);
   for (int r = 0; r < p.nloc; r++) {
@@ -1205,8 +1217,8 @@ extern "C" int gm_msgcount(gm_ctx *c, int32_t t, int32_t *sent, int32_t *recv) {
     HIPCHECK(hipStreamSynchronize(c->stream));
     std::vector<uint32_t> hs((size_t)t * rows), hr(hs.size());
     if (t > 0) {
-      HIPCHECK(hipMemcpy(hs.data(), ms, sizeof(uint32_t) * hs.size(), hipMemcpyDeviceToHost));
-      HIPCHECK(hipMemcpy(hr.data(), mr, sizeof(uint32_t) * hr.size(), hipMemcpyDeviceToHost));
+      HIPCHECK(ctx_memcpy(c, hs.data(), ms, sizeof(uint32_t) * hs.size(), hipMemcpyDeviceToHost));
+      HIPCHECK(ctx_memcpy(c, hr.data(), mr, sizeof(uint32_t) * hr.size(), hipMemcpyDeviceToHost));
     }
     for (size_t i = 0; i < rows; i++)
       for (int j = 0; j < t; j++) {
@@ -1219,8 +1231,8 @@ extern "C" int gm_msgcount(gm_ctx *c, int32_t t, int32_t *sent, int32_t *recv) {
   TRY(f_settle(c));
   HIPCHECK(hipStreamSynchronize(c->stream));
   std::vector<int32_t> hs((size_t)(c->n + 1) * c->f.tmax), hr(hs.size());
-  HIPCHECK(hipMemcpy(hs.data(), c->f.sent, sizeof(int32_t) * hs.size(), hipMemcpyDeviceToHost));
-  HIPCHECK(hipMemcpy(hr.data(), c->f.recv, sizeof(int32_t) * hr.size(), hipMemcpyDeviceToHost));
+  HIPCHECK(ctx_memcpy(c, hs.data(), c->f.sent, sizeof(int32_t) * hs.size(), hipMemcpyDeviceToHost));
+  HIPCHECK(ctx_memcpy(c, hr.data(), c->f.recv, sizeof(int32_t) * hr.size(), hipMemcpyDeviceToHost));
   for (int i = 0; i < c->n; i++)
     for (int j = 0; j < t; j++) {
       sent[(size_t)i * t + j] = hs[(size_t)(i + 1) * c->f.tmax + j];
@@ -1250,7 +1262,7 @@ static int read_table_row(gm_ctx *c, int r, std::vector<int32_t> &hb, std::vecto
     TRY(f_settle(c));
     w = c->n;
     std::vector<uint32_t> row(w);
-    HIPCHECK(hipMemcpy(row.data(), c->f.table + (size_t)r * c->f.np, sizeof(uint32_t) * w, hipMemcpyDeviceToHost));
+    HIPCHECK(ctx_memcpy(c, row.data(), c->f.table + (size_t)r * c->f.np, sizeof(uint32_t) * w, hipMemcpyDeviceToHost));
     hb.resize(w);
     ts.resize(w);
     for (int j = 0; j < w; j++) {
@@ -1263,7 +1275,7 @@ static int read_table_row(gm_ctx *c, int r, std::vector<int32_t> &hb, std::vecto
     const PState &p = c->p;
     if (r < p.n0 || r >= p.n0 + p.nloc) return GM_EINVAL;  // another row shard's node
     std::vector<uint64_t> lst(p.V);
-    HIPCHECK(hipMemcpy(lst.data(), p.lists + ((size_t)((c->t - 1) & 1) * p.rows + (r - p.n0)) * p.V,
+    HIPCHECK(ctx_memcpy(c, lst.data(), p.lists + ((size_t)((c->t - 1) & 1) * p.rows + (r - p.n0)) * p.V,
                        sizeof(uint64_t) * p.V, hipMemcpyDeviceToHost));
     w = c->n;
     hb.assign(w, -1);
@@ -1287,7 +1299,7 @@ static int read_table_row(gm_ctx *c, int r, std::vector<int32_t> &hb, std::vecto
                        hipMemcpyDeviceToHost));
   HIPCHECK(hipMemcpy2D(eb.data(), sizeof(uint32_t), (const uint8_t *)(s.brec + r) + 12, sizeof(uint4) * s.n,
                        sizeof(uint32_t), s.nb, hipMemcpyDeviceToHost));
-  HIPCHECK(hipMemcpy(&wt, s.wtick + r, sizeof wt, hipMemcpyDeviceToHost));
+  HIPCHECK(ctx_memcpy(c, &wt, s.wtick + r, sizeof wt, hipMemcpyDeviceToHost));
   std::vector<uint16_t> esc(s.wp);  // escaped cells by column (the entries of the row's band lists)
   const int par = (c->t - 1) & 1;
   std::vector<uint32_t> ent;
@@ -1299,11 +1311,11 @@ static int read_table_row(gm_ctx *c, int r, std::vector<int32_t> &hb, std::vecto
     const size_t in = std::min<size_t>(k, S_ESC_IN);
     if (S_EW_TOT(eb[b]) != k || S_EW_OFF(eb[b]) + (k - in) > s.tesc_region) return GM_ESTATE;
     ent.resize(k);
-    HIPCHECK(hipMemcpy(ent.data(), s.tesc_in[par] + ((size_t)b * s.n + r) * S_ESC_IN, sizeof(uint32_t) * in,
+    HIPCHECK(ctx_memcpy(c, ent.data(), s.tesc_in[par] + ((size_t)b * s.n + r) * S_ESC_IN, sizeof(uint32_t) * in,
                        hipMemcpyDeviceToHost));
     const size_t stripe = ((size_t)b * s.n + r) & (size_t)(s.esc_stripes - 1);
     if (k > in)
-      HIPCHECK(hipMemcpy(ent.data() + in, s.tesc[par] + stripe * s.tesc_region + S_EW_OFF(eb[b]),
+      HIPCHECK(ctx_memcpy(c, ent.data() + in, s.tesc[par] + stripe * s.tesc_region + S_EW_OFF(eb[b]),
                          sizeof(uint32_t) * (k - in), hipMemcpyDeviceToHost));
     TRY(place_entries(s, b, piece, ent.data(), ent.data() + S_ESC_IN, k, esc.data()));
   }
@@ -1341,20 +1353,20 @@ struct ScaledSnapshot {
     rec.resize((size_t)s.n * s.nb);
     wts.resize(s.n);
     std::vector<unsigned long long> cnt(s.esc_stripes);
-    HIPCHECK(hipMemcpy(tab.data(), s.table, tab.size(), hipMemcpyDeviceToHost));
-    HIPCHECK(hipMemcpy(rec.data(), s.brec, sizeof(uint4) * rec.size(), hipMemcpyDeviceToHost));
-    HIPCHECK(hipMemcpy(wts.data(), s.wtick, sizeof(int32_t) * s.n, hipMemcpyDeviceToHost));
+    HIPCHECK(ctx_memcpy(c, tab.data(), s.table, tab.size(), hipMemcpyDeviceToHost));
+    HIPCHECK(ctx_memcpy(c, rec.data(), s.brec, sizeof(uint4) * rec.size(), hipMemcpyDeviceToHost));
+    HIPCHECK(ctx_memcpy(c, wts.data(), s.wtick, sizeof(int32_t) * s.n, hipMemcpyDeviceToHost));
     const int par = (c->t - 1) & 1;
-    HIPCHECK(hipMemcpy(cnt.data(), s.tesc_cnt + (size_t)par * s.esc_stripes, sizeof(unsigned long long) * cnt.size(),
+    HIPCHECK(ctx_memcpy(c, cnt.data(), s.tesc_cnt + (size_t)par * s.esc_stripes, sizeof(unsigned long long) * cnt.size(),
                        hipMemcpyDeviceToHost));
     inl.resize((size_t)s.n * s.nb * S_ESC_IN);
-    HIPCHECK(hipMemcpy(inl.data(), s.tesc_in[par], sizeof(uint32_t) * inl.size(), hipMemcpyDeviceToHost));
+    HIPCHECK(ctx_memcpy(c, inl.data(), s.tesc_in[par], sizeof(uint32_t) * inl.size(), hipMemcpyDeviceToHost));
     pool.assign(s.esc_stripes, {});
     for (int k = 0; k < s.esc_stripes; k++) {
       const size_t used = std::min<unsigned long long>(cnt[k], s.tesc_region);
       pool[k].resize(used);
       if (used)
-        HIPCHECK(hipMemcpy(pool[k].data(), s.tesc[par] + (size_t)k * s.tesc_region, sizeof(uint32_t) * used,
+        HIPCHECK(ctx_memcpy(c, pool[k].data(), s.tesc[par] + (size_t)k * s.tesc_region, sizeof(uint32_t) * used,
                            hipMemcpyDeviceToHost));
     }
     row.resize(s.wp);
@@ -1409,7 +1421,7 @@ extern "C" int gm_read_views(gm_ctx *c, int32_t r0, int32_t count, uint64_t *out
   if (r0 < p.n0 || r0 + (int64_t)count > (int64_t)p.n0 + p.nloc) return GM_EINVAL;  // this shard's nodes only
   HIPCHECK(hipStreamSynchronize(c->stream));
   if (count)
-    HIPCHECK(hipMemcpy(out, p.lists + ((size_t)((c->t - 1) & 1) * p.rows + (r0 - p.n0)) * p.V,
+    HIPCHECK(ctx_memcpy(c, out, p.lists + ((size_t)((c->t - 1) & 1) * p.rows + (r0 - p.n0)) * p.V,
                        sizeof(uint64_t) * p.V * (size_t)count, hipMemcpyDeviceToHost));
   return GM_OK;
 }
@@ -1421,10 +1433,10 @@ extern "C" int gm_read_nodes(gm_ctx *c, int32_t *st4) {
   const int n = c->cfg.mode == GM_MODE_PARTIAL ? c->p.nloc : c->n;  // a row shard reports its own nodes
   std::vector<int32_t> a(n), b(n), f(n), h(n);
   if (c->cfg.mode == GM_MODE_FAITHFUL) {
-    HIPCHECK(hipMemcpy(a.data(), c->f.inited, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
-    HIPCHECK(hipMemcpy(b.data(), c->f.ingroup, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
-    HIPCHECK(hipMemcpy(f.data(), c->f.failed, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
-    HIPCHECK(hipMemcpy(h.data(), c->f.hbctr, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+    HIPCHECK(ctx_memcpy(c, a.data(), c->f.inited, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+    HIPCHECK(ctx_memcpy(c, b.data(), c->f.ingroup, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+    HIPCHECK(ctx_memcpy(c, f.data(), c->f.failed, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+    HIPCHECK(ctx_memcpy(c, h.data(), c->f.hbctr, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
   } else {
     const bool part = c->cfg.mode == GM_MODE_PARTIAL;
     std::fill(a.begin(), a.end(), 1);
@@ -1437,8 +1449,8 @@ extern "C" int gm_read_nodes(gm_ctx *c, int32_t *st4) {
         b[i] = i == 0 ? a[i] : s_ingroup(1, c->s.intro_until, i, t) && c->fail_t[i] >= s_start(i) + 2;
       }
     }
-    HIPCHECK(hipMemcpy(f.data(), part ? c->p.failed : c->s.failed, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
-    HIPCHECK(hipMemcpy(h.data(), part ? c->p.hbctr : c->s.hbctr, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+    HIPCHECK(ctx_memcpy(c, f.data(), part ? c->p.failed : c->s.failed, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+    HIPCHECK(ctx_memcpy(c, h.data(), part ? c->p.hbctr : c->s.hbctr, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
   }
   for (int i = 0; i < n; i++) {
     st4[4 * i] = a[i];
@@ -1459,7 +1471,7 @@ extern "C" int gm_dump_tables(gm_ctx *c, char *buf, size_t cap, size_t *len) {
   if (c->cfg.mode == GM_MODE_PARTIAL) {  // the V-entry lists (id order) of the last tick, one copy
     const PState &p = c->p;          // a row shard renders its own nodes (global indices)
     std::vector<uint64_t> all((size_t)p.nloc * p.V);
-    HIPCHECK(hipMemcpy(all.data(), p.lists + (size_t)(t & 1) * p.rows * p.V, sizeof(uint64_t) * all.size(),
+    HIPCHECK(ctx_memcpy(c, all.data(), p.lists + (size_t)(t & 1) * p.rows * p.V, sizeof(uint64_t) * all.size(),
                        hipMemcpyDeviceToHost));
     for (int i = 0; i < p.nloc; i++) {
       const uint64_t *row = all.data() + (size_t)i * p.V;
@@ -1823,7 +1835,7 @@ extern "C" int gm_shard_export(gm_ctx *c, int32_t what, int32_t D, void *out, si
   HIPCHECK(hipStreamSynchronize(c->stream));
   size_t off = 0;
   for (auto &p : parts) {
-    HIPCHECK(hipMemcpy((uint8_t *)out + off, p.first, p.second, hipMemcpyDeviceToHost));
+    HIPCHECK(ctx_memcpy(c, (uint8_t *)out + off, p.first, p.second, hipMemcpyDeviceToHost));
     off += p.second;
   }
   return GM_OK;
@@ -1840,7 +1852,7 @@ extern "C" int gm_shard_import(gm_ctx *c, int32_t what, int32_t D, const void *i
   HIPCHECK(hipStreamSynchronize(c->stream));
   size_t off = 0;
   for (auto &p : parts) {
-    HIPCHECK(hipMemcpy(p.first, (const uint8_t *)in + off, p.second, hipMemcpyHostToDevice));
+    HIPCHECK(ctx_memcpy(c, p.first, (const uint8_t *)in + off, p.second, hipMemcpyHostToDevice));
     off += p.second;
   }
   return GM_OK;
@@ -1928,7 +1940,7 @@ static int tick_sharded(gm_ctx *c) {
     if (pend == 0) break;
     if (++round > GM_MAX_ROUNDS) {  // a row that never finds its targets: same guard as gm_s_pick
       uint32_t e = GM_ERR_DRAWS;
-      HIPCHECK(hipMemcpy(c->s.err, &e, sizeof e, hipMemcpyHostToDevice));
+      HIPCHECK(ctx_memcpy(c, c->s.err, &e, sizeof e, hipMemcpyHostToDevice));
       c->latched = GM_ERANGE;
       return c->latched;
     }
@@ -1955,7 +1967,7 @@ static int draw_settle(gm_ctx *c) {
     if (getenv("GM_DEBUG_ROUNDS")) fprintf(stderr, "[gm] t=%d settle round %d: %d rows still drawing\n", t, round, pend);
     if (round >= GM_MAX_ROUNDS) {
       uint32_t e = GM_ERR_DRAWS;
-      HIPCHECK(hipMemcpy(c->s.err, &e, sizeof e, hipMemcpyHostToDevice));
+      HIPCHECK(ctx_memcpy(c, c->s.err, &e, sizeof e, hipMemcpyHostToDevice));
       c->latched = GM_ERANGE;
       return c->latched;
     }
