@@ -930,19 +930,18 @@ __device__ __forceinline__ FastCell fast_cell(const SState &s, int t, uint32_t y
     if (h < s.lag_hmin || h > 255) atomicOr(s.err, GM_ERR_LAG);
     c = (uint32_t)S_CELL(h, 0) & 0xFFFFu;
   }
-  const uint32_t age = c & 31u;
+  // branch-free (selects, not exec-mask branches: the scalar unit is what a divergent branch costs)
+  const uint32_t age = c & 31u, h = c >> 5, hp = h - 2u;
   const bool pres = c != 0, stale = pres && age >= GM_TFAIL;
   o.gone = pres && age >= GM_TREMOVE;  // TREMOVE (MP1Node.cpp:429-444): absent; it sent nothing (stale)
-  o.nbyte = o.nib = 0;
-  o.bail = false;
-  if (pres && !o.gone) {
-    o.nbyte = s_narrow(c);
-    if (!stale) {  // fresh: the nibble of h' = h - 2, or the wide plane (general path)
-      const uint32_t hp = (c >> 5) - 2u;
-      if ((hp & 1u) || hp < S_NIB_H(1) || hp > S_NIB_H(14)) o.bail = true;
-      else o.nib = ((hp - S_NIB_BASE) >> 1) << 4;
-    }
-  }
+  const bool keep = pres && !o.gone;
+  const bool fits = h >= S_H4_MIN_H && !(h & 1u) && age <= S_AGE_MAX_B;  // s_narrow's test
+  o.nbyte = keep ? (fits ? ((((h - 224u) >> 1) << 4) | age) : S_B_ESC) : 0u;
+  // fresh: the nibble of h' = h - 2, or the wide plane (general path)
+  const bool fresh = keep && !stale;
+  const bool nibok = !(hp & 1u) && hp >= S_NIB_H(1) && hp <= S_NIB_H(14);
+  o.bail = fresh && !nibok;
+  o.nib = fresh && nibok ? ((hp - S_NIB_BASE) >> 1) << 4 : 0u;
   o.c = c;
   const bool fpres = y >= 16u, fstale = fpres && (y & 15u) >= GM_TFAIL;
   o.dpres = (int)(pres && !o.gone) - (int)fpres;
@@ -1097,19 +1096,19 @@ __device__ __forceinline__ bool unit_fast(const SState &s, int t, const UnitIn<B
           const uint32_t ev = e >> 16;
           const FastCell o = fast_cell(s, t, y, max(ev ? ev - 63u : 0u, s_widen(y)), col == selfb, hbs);
           bail |= o.bail;
+          // the holding lane's words, unconditionally (LDS ops with zero operands, no branches)
           atomicOr(cor + ol, 1u << esc_bit(q));
-          if (o.nbyte == S_B_ESC) {  // an entry of this tick's list
-            if (epar) {
-              sv = true;
-              sent = (uint32_t)col | (o.c << 16);
-            } else {
-              row16[col] = (uint16_t)o.c;  // esc_emit reads it here (em: the escape bytes, below)
-            }
-          }
-          if (o.gone) atomicOr(cor + 64 + ol, 1u << q);
+          atomicOr(cor + 64 + ol, o.gone ? 1u << q : 0u);
+          atomicAdd(cor + 128 + ol, (uint32_t)(o.dpres + o.dfail * 65536));
           cb[0] = (uint8_t)o.nbyte;
           cb[16] = (uint8_t)o.nib;
-          if (o.dpres | o.dfail) atomicAdd(cor + 128 + ol, (uint32_t)(o.dpres + o.dfail * 65536));
+          const bool eout = o.nbyte == S_B_ESC;  // an entry of this tick's list
+          if (epar) {
+            sv = eout;
+            sent = (uint32_t)col | (o.c << 16);
+          } else if (eout) {
+            row16[col] = (uint16_t)o.c;  // esc_emit reads it here (em: the escape bytes, below)
+          }
         }
       }
       lds_wave_sync();
