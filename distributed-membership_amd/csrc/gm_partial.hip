@@ -125,8 +125,10 @@ __device__ __forceinline__ uint64_t p_readlane64(uint64_t v, int l) {
 // claim or find the slot of `id` (idw = id | flags on claim), raise its heartbeat word
 template <int H>
 __device__ __forceinline__ int p_insert(uint32_t *tid, uint32_t *thb, uint32_t id, uint32_t idw, uint32_t hb) {
-  constexpr int LOGH = H == 512 ? 9 : 10;
-  uint32_t h = (id * 0x9E3779B1u) >> (32 - LOGH);
+  // slot = low bits of id ^ id >> 9: view ids are uniform node indices, so this spreads them like a
+  // multiplicative hash without its quarter-rate 32-bit multiply (the slot never shows in a result:
+  // the table is compacted and ranked by id)
+  uint32_t h = (id ^ (id >> 9)) & (H - 1);
   for (;;) {  // claim-or-compare in one LDS op
     const uint32_t cur = atomicCAS(&tid[h], 0u, idw);
     if (cur == 0 || (cur & P_IDMASK) == id) break;
@@ -195,12 +197,14 @@ __device__ __forceinline__ void p_prefetch(const PState &s, int t, const uint32_
         : "memory");
   }
 }
+template <int VF>
 __device__ __forceinline__ PPre p_unpack_next(const PState &s, int t, int li, uint32_t pv, int lane) {
+  const int V = VF ? VF : s.V;
   PPre p;
   p.failed = (int)__builtin_amdgcn_readlane(pv, 32);
   p.k = (int)__builtin_amdgcn_readlane(pv, 33);
   p.hbctr = (int)__builtin_amdgcn_readlane(pv, 34);
-  p.own = lane < s.V ? s.lists[((size_t)((t & 1) ^ 1) * s.rows + li) * s.V + lane] : 0ull;
+  p.own = lane < V ? s.lists[((size_t)((t & 1) ^ 1) * s.rows + li) * V + lane] : 0ull;
   p.sv = lane < 16 ? (int)pv : 0;
   p.raw0 = pv;
   p.roff = 16;
@@ -212,7 +216,8 @@ __device__ __forceinline__ PPre p_unpack_next(const PState &s, int t, int li, ui
 // MC: the msgcount-recording instantiation (gm_msgcount_record); the others carry no trace of it
 // RM: lists of other row shards may be delivered (sharded contexts); without, every sender is a
 // local row and the list loads carry no branch
-template <int H, bool BIG, bool MC, bool RM = true>
+// VF: the view width when known at compile time (32: S-C), 0 = s.V at run time
+template <int H, bool BIG, bool MC, bool RM = true, int VF = 0>
 __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, int li, int lane, unsigned char *base,
                                        int chunk, int r0) {
   int k = pre.k;
@@ -231,7 +236,7 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
   uint32_t *kid = hist + 64;
   uint32_t *khb = kid + P_VMAX;
   uint64_t *fin = (uint64_t *)(khb + P_VMAX);
-  const int V = s.V;
+  const int V = VF ? VF : s.V;
   const int par = t & 1;
   const uint64_t *prev = s.lists + (size_t)(par ^ 1) * s.rows * V;
   uint64_t *cur = s.lists + (size_t)par * s.rows * V;
@@ -720,7 +725,7 @@ __device__ __forceinline__ void p_frozen(const PState &s, int t, int li, int lan
 }
 
 // rows [r0, r1) = chunk `chunk` of this shard's nodes
-template <bool MC, bool RM>
+template <bool MC, bool RM, int VF>
 __device__ __forceinline__ void p_small_node(const PState &s, int t, const PPre &pre, int li, int lane,
                                              unsigned char *base, int chunk, int r0) {
   if (pre.failed) {
@@ -734,14 +739,14 @@ __device__ __forceinline__ void p_small_node(const PState &s, int t, const PPre 
     }
     return;
   }
-  p_node<P_HS, false, MC, RM>(s, t, pre, li, lane, base, chunk, r0);
+  p_node<P_HS, false, MC, RM, VF>(s, t, pre, li, lane, base, chunk, r0);
 }
 
 // P_NPW consecutive nodes per wave: each node's loads are prefetched during the node before it
 // (p_prefetch), so a node starts with one global round trip (its delivered lists) instead of two.
 // Held to 8 waves per SIMD (64 VGPRs; the loop keeps more live otherwise, and some SGPRs spill to
 // VGPR lanes: ~40 more VALU per node, still faster than one node per wave: 26.1 vs 27.5 ms)
-template <bool MC, bool RM>
+template <bool MC, bool RM, int VF>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void gm_p_tick_small_pf(
     PState s, int t, const uint32_t *mtraw, int chunk, int r0, int r1) {
   extern __shared__ __align__(16) unsigned char p_smem[];
@@ -774,8 +779,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     asm volatile("" ::: "memory");       // the prefetch area is read only after the wait
     const uint32_t pv = ln < P_PF_LANES ? pf[ln] : 0u;
     if (li + 1 < l1) p_prefetch(ss, tt, mt, li + 1, ln, pfa);
-    const PPre pre = p_unpack_next(ss, tt, li, pv, ln);
-    p_small_node<MC, RM>(ss, tt, pre, li, ln, base, cc, rr);
+    const PPre pre = p_unpack_next<VF>(ss, tt, li, pv, ln);
+    p_small_node<MC, RM, VF>(ss, tt, pre, li, ln, base, cc, rr);
   }
 }
 
@@ -972,8 +977,12 @@ hipError_t gm_launch_partial_chunk(const PState &s, int t, const uint32_t *mtraw
   const bool mc = s.mc_sent != nullptr && t < s.mc_tmax;
   if (r1 > r0) {
     const bool rm = s.rows != s.n || s.G > 1 || s.nloc != s.n;  // received lists possible
-    auto *small = rm ? (mc ? gm_p_tick_small_pf<true, true> : gm_p_tick_small_pf<false, true>)
-                     : (mc ? gm_p_tick_small_pf<true, false> : gm_p_tick_small_pf<false, false>);
+    // V = 32 (S-C) takes the instantiation with the view width folded in (shifts, not multiplies)
+    auto *small = s.V == P_VMAX
+                      ? (rm ? (mc ? gm_p_tick_small_pf<true, true, P_VMAX> : gm_p_tick_small_pf<false, true, P_VMAX>)
+                            : (mc ? gm_p_tick_small_pf<true, false, P_VMAX> : gm_p_tick_small_pf<false, false, P_VMAX>))
+                      : (rm ? (mc ? gm_p_tick_small_pf<true, true, 0> : gm_p_tick_small_pf<false, true, 0>)
+                            : (mc ? gm_p_tick_small_pf<true, false, 0> : gm_p_tick_small_pf<false, false, 0>));
     hipLaunchKernelGGL(small, dim3((r1 - r0 + 4 * P_NPW - 1) / (4 * P_NPW)), dim3(256),
                        4 * (PLds<P_HS>::bytes + P_PF_BYTES), st, s, t, mtraw, c, r0, r1);
   }
