@@ -363,19 +363,23 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
     }
     using tmask_t = typename std::conditional<(TS > 32), uint64_t, uint32_t>::type;  // one bit per table slot
     constexpr int CB = TS <= 8 ? 4 : TS <= 16 ? 5 : TS <= 32 ? 6 : 7;               // bits of a per-lane slot count
+    // alive <=> present and not aged past TREMOVE <=> hb >= xa: every present entry has hb >= 1
+    // (heartbeats start at 2t-1 >= 1; hb < 2^31) and an empty slot holds hb 0, so one compare per
+    // slot gives the alive bit; removals = present - alive (rare: tested once per row)
+    const uint32_t xa = (uint32_t)max(2 * (t - GM_TREMOVE) + 1, 1);
     tmask_t alive = 0, rown = 0;
     int rcount = 0;
 #pragma unroll
     for (int u = 0; u < TS; u++) {  // branch-free: exec-mask traffic is what this kernel spends SALU on
-      const uint32_t valid = (w[u] & P_IDMASK) != 0;
-      const uint32_t rem = valid & (uint32_t)p_aged(t, hh[u], GM_TREMOVE);
-      rcount += (int)rem;
-      rown |= (tmask_t)(rem & (w[u] >> 31)) << u;
-      alive |= (tmask_t)(valid & ~rem) << u;
+      alive |= (tmask_t)((xa - 1u - hh[u]) >> 31) << u;
+      rcount += (int)min(w[u], 1u);
     }
+    rcount -= __builtin_popcountll(alive);
     int tot;
     removed = nrem = 0;
     if (__ballot(rcount != 0)) {  // rare: TREMOVE removals in this row
+#pragma unroll
+      for (int u = 0; u < TS; u++) rown |= (tmask_t)((w[u] >> 31) & (uint32_t)!((alive >> u) & 1)) << u;
       (void)p_excl<CB>(rcount, &removed);
       const int ro = __builtin_popcountll(rown);
       int rpos = p_excl<CB>(ro, &nrem);
