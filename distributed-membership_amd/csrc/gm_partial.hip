@@ -61,6 +61,16 @@ __device__ unsigned long long g_pprof[16];
 #define P_SELF 0x40000000u    // table id-word flag: the node's own entry
 #define P_MISC_BYTES (64 * 4 + P_VMAX * 4 + P_VMAX * 4 + P_VMAX * 8)
 
+// Lemire's rejection threshold 2^32 mod size for every list size 1..P_VMAX (a final list holds at
+// most V <= P_VMAX entries), read by a scalar load instead of a 32-bit remainder per node
+struct PThrTab {
+  uint32_t v[P_VMAX + 1];
+  constexpr PThrTab() : v() {
+    for (uint32_t n = 1; n <= P_VMAX; n++) v[n] = (0u - n) % n;
+  }
+};
+__constant__ PThrTab p_thr_tab = PThrTab();
+
 template <int H>
 struct PLds {
   static constexpr int bytes = H * 8 + P_MISC_BYTES;
@@ -576,7 +586,7 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
   uint32_t *gl = hist;  // the chosen targets in draw order (hist is free after the compaction)
   if (numpot > 0) {
     const uint32_t size = (uint32_t)cnt;
-    const uint32_t thr = (0u - size) % size;
+    const uint32_t thr = p_thr_tab.v[size];  // size = cnt <= V <= P_VMAX
     {  // the 16 precomputed outputs in parallel, output d on lane d: it is taken iff Lemire
        // accepts it, the drawn entry is not "me" and not aged, and no earlier such output drew
        // the same id (that one was taken, or repeated a taken one) -- the reference's loop
