@@ -4,4 +4,4 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
-bash scripts/gpu.sh r04zl tests smoke sa sc sb prof_sa ticks || exit 1
+bash scripts/gpu.sh r04zp tests smoke sa sc sb prof_sa ticks || exit 1
