@@ -38,13 +38,13 @@ hipError_t gm_launch_partial_tick(const PState &s, int t, uint32_t *mtraw, hipSt
                                   hipEvent_t k1);
 hipError_t gm_launch_partial_init(const PState &s, int t0, uint64_t init_seed, hipStream_t st);
 hipError_t gm_launch_partial_unpack(const PState &s, int t, int base, int nrecv, hipStream_t st);
-hipError_t gm_launch_partial_pack(const PState &s, int t, int c, int cap, hipStream_t st);
+hipError_t gm_launch_partial_pack(const PState &s, int t, int c, hipStream_t st);
 hipError_t gm_launch_partial_mtgen(const PState &s, int t, uint32_t *mtraw, hipStream_t st, bool reset);
 hipError_t gm_launch_partial_reset(const PState &s, hipStream_t st);
 hipError_t gm_launch_partial_chunk(const PState &s, int t, const uint32_t *mtraw, int c, hipStream_t st);
 hipError_t gm_launch_msgcount(const SState &s, int t, bool dropped, int phase, hipStream_t st);
 size_t gm_partial_lds_bytes();
-void gm_partial_profile_dump();
+void gm_partial_profile_dump(hipStream_t st);
 
 #define GM_T_LIMIT 32766  // packed 16-bit hb/ts stay exact: hb <= 2t+1 < 0xFFFF
 #define GM_F_MAILBOX 4096  // FAITHFUL events copied back with the count and error flags
@@ -107,6 +107,7 @@ struct gm_ctx {
   hipStream_t p_comm = nullptr;        // row shards: RCCL exchange stream (overlaps the next chunk's kernels)
   std::vector<hipEvent_t> p_chev;      // per chunk: its node ticks are done (compute stream)
   hipEvent_t p_done = nullptr;         // the tick's exchange + unpacks are done (comm stream)
+  std::vector<double> p_xq;            // per row shard q: probability that a sender addresses q (xcap)
 };
 
 // Every copy and fill of a context goes through its own stream. That stream is non-blocking, so the
@@ -120,7 +121,11 @@ static inline hipError_t ctx_memcpy(gm_ctx *c, void *d, const void *src, size_t 
   const hipError_t e = hipMemcpyAsync(d, src, n, k, c->stream);
   return e == hipSuccess ? hipStreamSynchronize(c->stream) : e;
 }
-
+static inline hipError_t ctx_memcpy2d(gm_ctx *c, void *d, size_t dpitch, const void *src, size_t spitch, size_t width,
+                                      size_t height, hipMemcpyKind k) {
+  const hipError_t e = hipMemcpy2DAsync(d, dpitch, src, spitch, width, height, k, c->stream);
+  return e == hipSuccess ? hipStreamSynchronize(c->stream) : e;
+}
 
 static thread_local char g_errbuf[256];
 
@@ -400,7 +405,10 @@ static int create_scaled(gm_ctx *c) {
   const double dense_bytes = 2.0 * ((double)dense_t * 4 + (double)dense_p * 16);
   size_t free_b = 0, total_b = 0;
   HIPCHECK(hipMemGetInfo(&free_b, &total_b));
-  double budget = (double)free_b / 4 / G;
+  // the free HBM is split over the contexts of this cluster on this device: every shard on one
+  // device (loopback) unless the caller says each has its own GPU (device_share = 1, RCCL ranks)
+  const int gdev = c->cfg.device_share > 0 ? std::min(c->cfg.device_share, G) : G;
+  double budget = (double)free_b / 4 / gdev;
   if (getenv("GM_ESC_BUDGET_GB")) budget = atof(getenv("GM_ESC_BUDGET_GB")) * 1e9;  // diagnostics (tests)
   const bool dense = cells <= (1ull << 31) || dense_bytes <= budget;
   size_t tcells, pslots;
@@ -410,11 +418,19 @@ static int create_scaled(gm_ctx *c) {
     tcells = per * s.band * S;
     pslots = per * (s.band / 16) * S;
   } else {
-    const double f = std::min(1.0, std::max(1.0 / 64, budget / dense_bytes));
-    tcells = std::max<size_t>((size_t)((double)cells * f), 4 * (size_t)s.band * S);
-    pslots = std::max<size_t>((size_t)((double)cells * std::min(1.0, 4 * f) / 256), 4 * (size_t)(s.band / 16) * S);
+    // the table pool takes the fraction f of its dense size and the payload pool min(1, 4f) of its
+    // dense count (cells / 16 slots), so at least 1/16 of the payload lanes at the floor f = 1/64
+    // (a / 256 here gave 1/256); both parities together fit the budget:
+    // 8 f cells + 2 min(1, 4f) cells bytes
+    const double cb = (double)cells;
+    double f = budget / (16.0 * cb);
+    if (f > 0.25) f = (budget - 2.0 * cb) / (8.0 * cb);
+    f = std::min(1.0, std::max(1.0 / 64, f));
+    tcells = std::max<size_t>((size_t)(cb * f), 4 * (size_t)s.band * S);
+    pslots = std::max<size_t>((size_t)(cb * std::min(1.0, 4 * f) / 16), 4 * (size_t)(s.band / 16) * S);
     grow(tcells);
   }
+  s.esc_dense = dense ? 1 : 0;
   s.esc_stripes = S;
   size_t treg = std::min<size_t>((tcells + S - 1) / S, S_EW_REGION_MAX);
   size_t preg = std::min<size_t>((pslots + S - 1) / S, 0xFFFFFFF0ull / S);
@@ -456,7 +472,7 @@ static int create_scaled(gm_ctx *c) {
      // 1/32 share of the free HBM (the loopback shards of one device split it); at least 2^24 records.
      // A half-cluster crash at S-A removes ~550 M entries in its peak tick (~420 M past the slots).
     HIPCHECK(hipMemGetInfo(&free_b, &total_b));
-    const size_t want = std::min<size_t>((size_t)n * s.wp, free_b / 32 / G / sizeof(uint64_t));
+    const size_t want = std::min<size_t>((size_t)n * s.wp, free_b / 32 / gdev / sizeof(uint64_t));
     s.ev_spill_cap = (uint32_t)std::min<size_t>(std::max<size_t>(want, 1u << 24), 1ull << 31);
   }
   TRY(dalloc(c, &s.ev_spill, s.ev_spill_cap));
@@ -534,6 +550,8 @@ static int create_scaled(gm_ctx *c) {
 // exchanges the lists its nodes send to other shards every tick (gm_tick with RCCL
 // attached: all-to-all of record counts + two all-to-allv; gm_partial_loopback for
 // G contexts on one device).
+static int partial_caps(gm_ctx *c);
+
 static int create_partial(gm_ctx *c) {
   const int n = c->n;
   PState &p = c->p;
@@ -604,6 +622,7 @@ static int create_partial(gm_ctx *c) {
     TRY(dalloc(c, &p.pk_list, (size_t)G * nl * p.V));
     HIPCHECK(ctx_memset(c, p.pk_hdr, 0xFF, sizeof(int32_t) * G * nl * 8));
     TRY(dalloc(c, &p.pk_cnt, (size_t)p.nchunk * G));
+    TRY(dalloc(c, &p.pk_cap, (size_t)p.nchunk * G));
     p.xcap_frac = getenv("GM_XCHG_CAP_FRAC") ? (float)atof(getenv("GM_XCHG_CAP_FRAC")) : 0.f;
     if (p.xcap_frac < 0.f || p.xcap_frac > 1.f) return GM_EINVAL;
     TRY(dalloc(c, &p.recv_hdr, (size_t)std::max(R, 1) * 8));
@@ -612,6 +631,7 @@ static int create_partial(gm_ctx *c) {
     for (int g = 0; g <= G; g++) b[g] = (int32_t)((int64_t)n * g / G);
     TRY(dalloc(c, &p.shard_n0, G + 1));
     HIPCHECK(ctx_memcpy(c, p.shard_n0, b.data(), sizeof(int32_t) * (G + 1), hipMemcpyHostToDevice));
+    TRY(partial_caps(c));
   }
   HIPCHECK(ctx_memset(c, p.lists, 0, sizeof(uint64_t) * 2 * p.rows * p.V));
   HIPCHECK(ctx_memset(c, p.failed, 0, sizeof(int32_t) * nl));
@@ -686,7 +706,7 @@ extern "C" int gm_destroy(gm_ctx *c) {
   for (hipEvent_t e : c->p_chev) (void)hipEventDestroy(e);
   if (c->p_done) (void)hipEventDestroy(c->p_done);
   if (c->p_comm) (void)hipStreamDestroy(c->p_comm);
-  if (c->cfg.mode == GM_MODE_PARTIAL) gm_partial_profile_dump();
+  if (c->cfg.mode == GM_MODE_PARTIAL) gm_partial_profile_dump(c->stream);
   if (c->p_side) {
     (void)hipStreamSynchronize(c->p_side);
     (void)hipStreamDestroy(c->p_side);
@@ -976,6 +996,7 @@ extern "C" int gm_set_failed(gm_ctx *c, const int32_t *idx, int32_t n) {
   HIPCHECK(hipStreamSynchronize(c->stream));
   HIPCHECK(ctx_memcpy(c, dst, c->failed_h.data() + (part ? c->p.n0 : 0), sizeof(int32_t) * (part ? c->p.nloc : c->n),
                      hipMemcpyHostToDevice));
+  if (part && c->p_sharded) TRY(partial_caps(c));  // the exchange blocks follow the live nodes per shard
   return GM_OK;
 }
 
@@ -1295,10 +1316,10 @@ static int read_table_row(gm_ctx *c, int r, std::vector<int32_t> &hb, std::vecto
   std::vector<uint32_t> eb(s.nb);
   int32_t wt = 0;
   const size_t piece = s.band;  // bytes of one (band, row) piece of the stored cells
-  HIPCHECK(hipMemcpy2D(row.data(), piece, s.table + (size_t)r * s.band, piece * s.n, piece, s.nb,
-                       hipMemcpyDeviceToHost));
-  HIPCHECK(hipMemcpy2D(eb.data(), sizeof(uint32_t), (const uint8_t *)(s.brec + r) + 12, sizeof(uint4) * s.n,
-                       sizeof(uint32_t), s.nb, hipMemcpyDeviceToHost));
+  HIPCHECK(ctx_memcpy2d(c, row.data(), piece, s.table + (size_t)r * s.band, piece * s.n, piece, s.nb,
+                        hipMemcpyDeviceToHost));
+  HIPCHECK(ctx_memcpy2d(c, eb.data(), sizeof(uint32_t), (const uint8_t *)(s.brec + r) + 12, sizeof(uint4) * s.n,
+                        sizeof(uint32_t), s.nb, hipMemcpyDeviceToHost));
   HIPCHECK(ctx_memcpy(c, &wt, s.wtick + r, sizeof wt, hipMemcpyDeviceToHost));
   std::vector<uint16_t> esc(s.wp);  // escaped cells by column (the entries of the row's band lists)
   const int par = (c->t - 1) & 1;
@@ -1543,6 +1564,16 @@ extern "C" int gm_tick_stats(gm_ctx *c, int64_t stats[4]) {
   stats[1] = live;
   stats[2] = mx;
   stats[3] = e;
+  return GM_OK;
+}
+
+extern "C" int gm_pool_info(gm_ctx *c, int64_t info[4]) {
+  if (!c || !info) return GM_EINVAL;
+  if (c->cfg.mode != GM_MODE_SCALED) return GM_EUNSUPPORTED;
+  info[0] = c->s.esc_dense;
+  info[1] = (int64_t)c->s.tesc_cap;
+  info[2] = (int64_t)c->s.pesc_cap;
+  info[3] = (int64_t)c->s.ev_spill_cap;
   return GM_OK;
 }
 
@@ -1992,38 +2023,45 @@ static int draw_settle(gm_ctx *c) {
 // stamp is t to its targets' inboxes (a slot without a record of this tick is skipped). A shard
 // thus moves its whole slot range per tick, ~2x the records it has (a sender addresses a given
 // peer with probability 1 - (1 - 1/G)^5: 0.49 at G = 8), over xGMI, while later chunks compute.
-// Capacity of a packed block of `rows` slots (gm_p_pack): a sender addresses a given peer with
-// probability q = 1 - (1 - 1/G)^5 (5 targets drawn from a view of ids spread over the shards), so
-// its record count is ~Binomial(rows, q); the block holds the mean + 8 sigma + 64 (at most the
-// slots) and an overflow fails loudly (GM_ERR_XCHG). S-C at G = 8: 49 % of the slots.
-static size_t xcap(const PState &p, size_t rows) {
+// Capacity of a packed block (gm_p_pack): the records one chunk of `rows` senders addresses to
+// shard q. A sender's five targets are drawn from its view; with a fraction f_q of the view's
+// entries on shard q it addresses q with probability 1 - (1 - f_q)^5, so the block's record count is
+// a sum of Bernoullis whose mean is at most rows * (1 - (1 - E f_q)^5) (the map is concave) and
+// whose variance is at most the binomial's. E f_q: views follow the live nodes once the crashed
+// ones are swept out, and hold the static shares before -- so f_q = max(n_q / n, live_q / live) (a
+// crashed shard keeps its static share; ADVICE r4: a contiguous half-cluster crash, the
+// reference's multifailure schedule, Application.cpp:189-192, leaves the survivors addressing each
+// surviving shard with ~76 % at G = 8, past the static 49 %). The block holds the mean + 8 sigma +
+// 64 (at most the slots); every rank derives the same capacities from the same crash set, and an
+// overflow fails loudly (GM_ERR_XCHG).
+static size_t xcap(const gm_ctx *c, size_t rows, int q) {
+  const PState &p = c->p;
   if (p.xcap_frac > 0.f) return std::min(rows, (size_t)std::ceil((double)rows * p.xcap_frac));
-  const double q = 1.0 - std::pow(1.0 - 1.0 / p.G, (double)GM_FANOUT);
-  const double m = (double)rows * q + 8.0 * std::sqrt((double)rows * q * (1.0 - q)) + 64.0;
+  const double pq = c->p_xq[q];
+  const double m = (double)rows * pq + 8.0 * std::sqrt((double)rows * pq * (1.0 - pq)) + 64.0;
   return std::min(rows, (size_t)std::ceil(m));
 }
 struct XChunk {  // the block layout of chunk ch (rows of shard g in chunk ch: [nloc_g ch / K, nloc_g (ch+1) / K))
   std::vector<size_t> sc, sd, rc, rd;  // send / receive record counts (block capacities) and row offsets per shard
   size_t rbase = 0, rrows = 0;         // this chunk's first received row, rows received
-  size_t cap = 0;                      // capacity of this shard's outgoing blocks
 };
-static XChunk xchunk(const PState &p, int ch) {
+static XChunk xchunk(const gm_ctx *c, int ch) {
+  const PState &p = c->p;
   const int G = p.G, K = p.nchunk;
   auto nloc_of = [&](int g) { return (int64_t)p.n * (g + 1) / G - (int64_t)p.n * g / G; };
-  auto rows = [&](int g, int c) { return (size_t)(nloc_of(g) * (c + 1) / K - nloc_of(g) * c / K); };
+  auto rows = [&](int g, int cc) { return (size_t)(nloc_of(g) * (cc + 1) / K - nloc_of(g) * cc / K); };
   XChunk x;
   x.sc.assign(G, 0); x.sd.assign(G, 0); x.rc.assign(G, 0); x.rd.assign(G, 0);
-  for (int c = 0; c < ch; c++)
+  for (int cc = 0; cc < ch; cc++)
     for (int g = 0; g < G; g++)
-      if (g != p.rank) x.rbase += xcap(p, rows(g, c));
+      if (g != p.rank) x.rbase += xcap(c, rows(g, cc), p.rank);
   const size_t r0 = (size_t)((int64_t)p.nloc * ch / K);
-  x.cap = xcap(p, rows(p.rank, ch));
   size_t off = x.rbase;
   for (int q = 0; q < G; q++) {
     if (q == p.rank) continue;
-    x.sc[q] = x.cap;
+    x.sc[q] = xcap(c, rows(p.rank, ch), q);
     x.sd[q] = (size_t)q * p.nloc + r0;  // the packed block (q, r0) of pk_hdr / pk_list
-    x.rc[q] = xcap(p, rows(q, ch));
+    x.rc[q] = xcap(c, rows(q, ch), p.rank);
     x.rd[q] = off;
     off += x.rc[q];
   }
@@ -2031,11 +2069,38 @@ static XChunk xchunk(const PState &p, int ch) {
   return x;
 }
 
+// the address probabilities per shard from the crash set (every rank holds the whole set), and the
+// outgoing block capacities per (chunk, peer) on the device (gm_p_pack reads them)
+static int partial_caps(gm_ctx *c) {
+  const PState &p = c->p;
+  const int G = p.G;
+  std::vector<int64_t> live(G, 0);
+  int64_t tot = 0;
+  for (int g = 0; g < G; g++) {
+    const int a = (int)((int64_t)p.n * g / G), b = (int)((int64_t)p.n * (g + 1) / G);
+    for (int i = a; i < b; i++) live[g] += c->failed_h[i] ? 0 : 1;
+    tot += live[g];
+  }
+  c->p_xq.assign(G, 0.0);
+  for (int g = 0; g < G; g++) {
+    const double fs = (double)((int64_t)p.n * (g + 1) / G - (int64_t)p.n * g / G) / p.n;
+    const double fl = tot > 0 ? (double)live[g] / tot : 0.0;
+    c->p_xq[g] = 1.0 - std::pow(1.0 - std::max(fs, fl), (double)GM_FANOUT);
+  }
+  std::vector<int32_t> cap((size_t)p.nchunk * G, 0);
+  for (int ch = 0; ch < p.nchunk; ch++) {
+    const XChunk x = xchunk(c, ch);
+    for (int q = 0; q < G; q++) cap[(size_t)ch * G + q] = (int32_t)x.sc[q];
+  }
+  HIPCHECK(ctx_memcpy(c, p.pk_cap, cap.data(), sizeof(int32_t) * cap.size(), hipMemcpyHostToDevice));
+  return GM_OK;
+}
+
 static int partial_exchange_chunk(gm_ctx *c, int ch, int64_t *roff) {
   PState &p = c->p;
   const int G = p.G, V = p.V;
   hipStream_t cs = c->p_comm;
-  const XChunk x = xchunk(p, ch);
+  const XChunk x = xchunk(c, ch);
   std::vector<size_t> hs(G), hsd(G), hr(G), hrd(G), ls(G), lsd(G), lr(G), lrd(G);
   for (int q = 0; q < G; q++) {
     hs[q] = x.sc[q] * 8;
@@ -2049,7 +2114,7 @@ static int partial_exchange_chunk(gm_ctx *c, int ch, int64_t *roff) {
   }
   if (x.rbase + x.rrows > (size_t)(p.n - p.nloc)) return GM_ESTATE;
   if (ch == 0) HIPCHECK(hipMemsetAsync(p.pk_cnt, 0, sizeof(int32_t) * p.nchunk * G, cs));
-  HIPCHECK(gm_launch_partial_pack(p, c->t, ch, (int)x.cap, cs));
+  HIPCHECK(gm_launch_partial_pack(p, c->t, ch, cs));
   NCCLCHECK(ncclAllToAllv(p.pk_hdr, hs.data(), hsd.data(), p.recv_hdr, hr.data(), hrd.data(), ncclInt32, c->comm, cs));
   NCCLCHECK(ncclAllToAllv(p.pk_list, ls.data(), lsd.data(), p.recv_list[c->t & 1], lr.data(), lrd.data(), ncclUint32,
                           c->comm, cs));
@@ -2093,16 +2158,16 @@ extern "C" int gm_partial_loopback_tick(gm_ctx **ctxs, int32_t G) {
   for (int g = 0; g < G; g++) {  // every shard packs its records into its outgoing blocks (as on the comm stream)
     PState &pg = ctxs[g]->p;
     HIPCHECK(hipMemsetAsync(pg.pk_cnt, 0, sizeof(int32_t) * K * G, ls));
-    for (int ch = 0; ch < K; ch++) HIPCHECK(gm_launch_partial_pack(pg, ctxs[g]->t, ch, (int)xchunk(pg, ch).cap, ls));
+    for (int ch = 0; ch < K; ch++) HIPCHECK(gm_launch_partial_pack(pg, ctxs[g]->t, ch, ls));
   }
   for (int ch = 0; ch < K; ch++)
     for (int q = 0; q < G; q++) {
       PState &dq = ctxs[q]->p;
       hipStream_t st = ls;
-      const XChunk xq = xchunk(dq, ch);
+      const XChunk xq = xchunk(ctxs[q], ch);
       for (int g = 0; g < G; g++) {
         if (g == q || !xq.rc[g]) continue;
-        const XChunk xg = xchunk(ctxs[g]->p, ch);
+        const XChunk xg = xchunk(ctxs[g], ch);
         const PState &sg = ctxs[g]->p;
         if (xg.sc[q] != xq.rc[g]) return GM_ESTATE;
         HIPCHECK(hipMemcpyAsync(dq.recv_hdr + xq.rd[g] * 8, sg.pk_hdr + xg.sd[q] * 8, sizeof(int32_t) * 8 * xq.rc[g],

@@ -56,11 +56,12 @@ struct PState {
                          //   sent them; the next tick's kernels decode them in place
   // packed exchange blocks (gm_p_pack): chunk c's records to shard q compacted to the front of the
   // rows [q * nloc + r0_c, +cap) of these buffers; only the block's first cap rows travel (cap: the
-  // host's binomial bound, gm_host.hip xcap); rows past the records keep older stamps, so receivers
-  // need no count (gm_p_unpack takes the rows stamped t)
+  // host's binomial bound from the live nodes per shard, gm_host.hip xcap); rows past the records
+  // keep older stamps, so receivers need no count (gm_p_unpack takes the rows stamped t)
   int32_t *pk_hdr;       // [G][nloc][8]
   uint32_t *pk_list;     // [G][nloc][V]
   int32_t *pk_cnt;       // [K][G] records packed per (chunk, shard) this tick
+  int32_t *pk_cap;       // [K][G] capacity of the block (chunk, shard) (host-written when the crash set changes)
   float xcap_frac;       // diagnostics (GM_XCHG_CAP_FRAC): block capacity = this fraction of the slots
   int32_t *shard_n0;     // [G+1] first node of every row shard (shard_n0[G] = n)
   uint32_t *err;

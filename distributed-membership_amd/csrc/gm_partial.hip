@@ -672,11 +672,7 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
   const int owner = (s.G > 1 && lane < ng) ? p_owner(s, dst) : s.rank;
   if (lane < ng) {
     s.targets[(size_t)li * GM_FANOUT + lane] = dst;
-#ifdef GM_P_ROUTE  // the local appends are gm_p_route's, after the chunk's node kernels
-    if (false) {
-#else
     if (owner == s.rank) {
-#endif
       int32_t *row = s.inbox[par ^ 1] + (size_t)(dst - s.n0) * P_KMAX;  // count and slots share a line
       const int slot = atomicAdd(row, 1);
       if (slot < s.kcap) row[1 + slot] = li;
@@ -897,35 +893,14 @@ __global__ __launch_bounds__(256) void gm_p_unpack(PState s, int t, int base, in
   }
 }
 
-// Inbox appends of chunk c's local targets as a separate pass (GM_P_ROUTE): thread per node, its
-// <= 5 returning atomics issued back to back, no node work waiting on them
-__global__ __launch_bounds__(256) void gm_p_route(PState s, int t, int r0, int r1) {
-  const int li = r0 + blockIdx.x * blockDim.x + threadIdx.x;
-  if (li >= r1) return;
-  const int ng = s.rowstat[(size_t)li * 4 + 3];
-  int d[GM_FANOUT];
-#pragma unroll
-  for (int q = 0; q < GM_FANOUT; q++) d[q] = q < ng ? s.targets[(size_t)li * GM_FANOUT + q] - s.n0 : -1;
-  int32_t *ib = s.inbox[(t & 1) ^ 1];
-  int slot[GM_FANOUT];
-#pragma unroll
-  for (int q = 0; q < GM_FANOUT; q++)
-    slot[q] = d[q] >= 0 && d[q] < s.nloc ? atomicAdd(ib + (size_t)d[q] * P_KMAX, 1) : -1;
-#pragma unroll
-  for (int q = 0; q < GM_FANOUT; q++) {
-    if (slot[q] < 0) continue;
-    if (slot[q] < s.kcap) ib[(size_t)d[q] * P_KMAX + 1 + slot[q]] = li;
-    else atomicOr(s.err, GM_ERR_INBOX);
-  }
-}
-
 // Row shards: compact chunk c's records to shard q (slots (q, li), li in [r0, r1), stamped t) to the
 // front of the packed block (q, r0): one tile of 256 slots per workgroup and peer (blockIdx.y),
 // a workgroup scan of the stamp flags, one atomic per (tile, peer) for the block offset. The
 // records' order inside the block is the atomics' -- the receivers' merge is order-free. A block
 // that would exceed `cap` sets GM_ERR_XCHG (-> GM_ERANGE), never drops a record silently.
-__global__ __launch_bounds__(256) void gm_p_pack(PState s, int t, int c, int r0, int r1, int cap) {
+__global__ __launch_bounds__(256) void gm_p_pack(PState s, int t, int c, int r0, int r1) {
   const int q = (int)blockIdx.y + (blockIdx.y >= (unsigned)s.rank);  // the peer (own rank skipped)
+  const int cap = s.pk_cap[(size_t)c * s.G + q];
   const int li = r0 + blockIdx.x * 256 + threadIdx.x;
   const size_t rec = (size_t)q * s.nloc + li;
   const bool has = li < r1 && s.sp_hdr[rec * 8 + 7] == t;
@@ -966,10 +941,10 @@ __global__ __launch_bounds__(256) void gm_p_pack(PState s, int t, int c, int r0,
   }
 }
 
-hipError_t gm_launch_partial_pack(const PState &s, int t, int c, int cap, hipStream_t st) {
+hipError_t gm_launch_partial_pack(const PState &s, int t, int c, hipStream_t st) {
   const int r0 = (int)((int64_t)s.nloc * c / s.nchunk), r1 = (int)((int64_t)s.nloc * (c + 1) / s.nchunk);
   if (r1 > r0 && s.G > 1)
-    hipLaunchKernelGGL(gm_p_pack, dim3((r1 - r0 + 255) / 256, s.G - 1), dim3(256), 0, st, s, t, c, r0, r1, cap);
+    hipLaunchKernelGGL(gm_p_pack, dim3((r1 - r0 + 255) / 256, s.G - 1), dim3(256), 0, st, s, t, c, r0, r1);
   return hipGetLastError();
 }
 
@@ -1009,9 +984,6 @@ hipError_t gm_launch_partial_chunk(const PState &s, int t, const uint32_t *mtraw
                      4 * PLds<P_HB>::bytes, st, s, t, mtraw, c, r0);
   hipLaunchKernelGGL(mc ? gm_p_tick_huge<true> : gm_p_tick_huge<false>, dim3(P_HUGE_GRID), dim3(64),
                      PLds<P_HH>::bytes, st, s, t, mtraw, c, r0);
-#ifdef GM_P_ROUTE
-  if (r1 > r0) hipLaunchKernelGGL(gm_p_route, dim3((r1 - r0 + 255) / 256), dim3(256), 0, st, s, t, r0, r1);
-#endif
   return hipGetLastError();
 }
 
@@ -1038,10 +1010,11 @@ hipError_t gm_launch_partial_unpack(const PState &s, int t, int base, int nrecv,
 size_t gm_partial_lds_bytes() { return 4 * (size_t)PLds<P_HB>::bytes; }
 
 // measurement builds: the per-section clocks (0 elsewhere)
-void gm_partial_profile_dump() {
+void gm_partial_profile_dump(hipStream_t st) {
 #ifdef GM_P_PROFILE
   unsigned long long h[16];
-  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_pprof), sizeof h) == hipSuccess && h[15]) {
+  if (hipMemcpyFromSymbolAsync(h, HIP_SYMBOL(g_pprof), sizeof h, 0, hipMemcpyDeviceToHost, st) == hipSuccess &&
+      hipStreamSynchronize(st) == hipSuccess && h[15]) {
     const char *nm[9] = {"loads", "own-insert", "merge", "self", "sweep", "evict", "rank+store", "draw", "sends"};
     unsigned long long tot = 0;
     for (int q = 0; q < 9; q++) tot += h[q];

@@ -11,8 +11,8 @@
 #define S_SB 8                   // sender ids prefetched per row; payload loads in flight per lane
 #define S_MT_RAW 16              // mt19937 outputs precomputed per row and tick (gm_s_mtgen)
 #define S_SELFADD_CAP 65536      // join ramp: self appends verified per tick (gm_s_selfcheck)
-#define S_PLIST_CAP 4096
-#define S_FB_BLOCKS 2048         // workgroups (4 waves) of gm_s_band's pass over the fast path's handed-back units         // sharded tick: rows a second (bounded) draw round takes
+#define S_PLIST_CAP 4096         // sharded tick: rows a second (bounded) draw round takes
+#define S_FB_BLOCKS 2048         // workgroups (4 waves) of gm_s_band's pass over the fast path's handed-back units
 #define GM_D_MORE_ROUND 64       // S2 outputs of bounded round 1 (= one host-driven round)
 #define GM_D_LAST_ROUND 256      // S2 outputs of bounded round 2 (= host-driven rounds 2..5)
 
@@ -116,6 +116,7 @@ struct SState {
   // Allocation is STRIPED: (band, row) list u allocates in stripe (band * n + row) & (stripes - 1),
   // a region of `region` entries with its own counter -- one global counter would serialise
   // every (band, row) of a crash-window tick on one address (4 M atomics at S-A: 25 ms)
+  int esc_dense;           // the pools are dense-equivalent (no run can overflow them); gm_pool_info
   int esc_stripes;         // power of two
   unsigned long long *tesc_cnt;  // [2][esc_stripes] cells allocated per stripe this tick (zeroed a tick ahead)
   uint32_t tesc_region;    // entries per stripe

@@ -561,11 +561,7 @@ __device__ __forceinline__ void unit_records(const SState &s, int t, const UnitI
   if (live && li == 0 && tot)  // the tick's total (host staging), striped partial sums
     atomicAdd(s.ev_spill_cnt + 1 + ((slab + (size_t)r) & (S_EV_STRIPES - 1)), (uint32_t)tot);
   sbase = LPR == 64 ? __builtin_amdgcn_readfirstlane(sbase) : __shfl(sbase, sub * LPR, 64);
-#ifdef GM_ABL_NO_EVREC  // measurement builds only (scripts/r04 ablation): the event records not written
-  if (false) {
-#else
   if (live && nev) {
-#endif
     int slot = x - nev;
     uint32_t *slots = s.ev_band + ((size_t)r * s.nb + band) * E;
     for (uint32_t ek = evk; ek; ek &= ek - 1) {
@@ -1049,9 +1045,6 @@ __device__ __forceinline__ bool unit_fast(const SState &s, int t, const UnitIn<B
     spm |= 1u << esc_bit(selfc);
     hbself = s.hbctr[r] + 1;
   }
-#ifdef GM_ABL_SPECIAL_ALWAYS  // measurement builds only: every unit takes the per-cell pass (cell 0 of lane 0, exact anyway)
-  if (li == 0) spm |= 1u;
-#endif
   // 4. the marked cells, exactly (fast_cell). The lane's merged bytes and nibble bytes wait in LDS
   // (park: 32 B per lane), so that a cell is one byte read and two byte writes there, not register
   // selects. Escaped cells go entry-parallel: lane j takes entry j of the row slice's escape list (the

@@ -25,7 +25,7 @@ class GmConfig(ctypes.Structure):
                 ("device", ctypes.c_int32), ("shard_rank", ctypes.c_int32), ("shard_count", ctypes.c_int32),
                 ("init_mode", ctypes.c_int32), ("init_t0", ctypes.c_int32), ("init_seed", ctypes.c_uint64),
                 ("band", ctypes.c_int32), ("view", ctypes.c_int32), ("view_seed", ctypes.c_uint64),
-                ("reserved", ctypes.c_int32 * 2)]
+                ("device_share", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 class GmEvent(ctypes.Structure):
@@ -39,7 +39,7 @@ EXPORTS = ["gm_parse_conf", "gm_create", "gm_destroy", "gm_tick", "gm_sync", "gm
            "gm_comm_unique_id", "gm_comm_init", "gm_shard_layout", "gm_shard_merge", "gm_shard_draw",
            "gm_shard_accept", "gm_shard_end_tick", "gm_shard_loopback", "gm_partial_loopback_tick",
            "gm_shard_exchange_bytes", "gm_keep_events", "gm_event_totals", "gm_read_views", "gm_shard_stub",
-           "gm_msgcount_record", "gm_comm_info", "gm_shard_export", "gm_shard_import"]
+           "gm_msgcount_record", "gm_comm_info", "gm_shard_export", "gm_shard_import", "gm_pool_info"]
 
 _lib = None
 
@@ -76,7 +76,7 @@ def load_library():
         "gm_read_table": [ctypes.c_void_p, i32, i32, P(i32), P(i32)],
         "gm_read_nodes": [ctypes.c_void_p, P(i32)],
         "gm_dump_tables": [ctypes.c_void_p, ctypes.c_char_p, sz, P(sz)],
-        "gm_tick_stats": [ctypes.c_void_p, P(ctypes.c_int64)],
+        "gm_tick_stats": [ctypes.c_void_p, P(ctypes.c_int64)], "gm_pool_info": [ctypes.c_void_p, P(ctypes.c_int64)],
         "gm_set_timing": [ctypes.c_void_p, i32], "gm_last_kernel_ms": [ctypes.c_void_p, P(ctypes.c_float)],
         "gm_crash_set": [i32, i32, u64, P(i32)],
         "gm_comm_unique_id": [ctypes.c_char_p],
@@ -119,7 +119,7 @@ class Simulator:
 
     def __init__(self, n, mode=GM_MODE_FAITHFUL, single_failure=1, drop_msg=0, drop_prob=0.1, time_seed=0,
                  rd_seed=0, drop_pct=0, drop_from=0, drop_to=0, drop_seed=0, device=0, shard_rank=0, shard_count=1,
-                 init_mode=0, init_t0=0, init_seed=0, band=0, view=0, view_seed=0):
+                 init_mode=0, init_t0=0, init_seed=0, band=0, view=0, view_seed=0, device_share=0):
         self.lib = load_library()
         cfg = GmConfig()
         cfg.abi_version = GM_ABI_VERSION
@@ -131,6 +131,7 @@ class Simulator:
         cfg.init_mode, cfg.init_t0, cfg.init_seed = init_mode, init_t0, init_seed
         cfg.band = band
         cfg.view, cfg.view_seed = view, view_seed
+        cfg.device_share = device_share
         self.cfg = cfg
         self.n = n
         self.mode = mode
@@ -280,6 +281,13 @@ class Simulator:
         s = (ctypes.c_int64 * 4)()
         self._call("gm_tick_stats", self.h, s)
         return {"lists": int(s[0]), "live": int(s[1]), "max_inbox": int(s[2]), "err": int(s[3])}
+
+    def pool_info(self):
+        """SCALED escape storage as sized at create (gm_pool_info)"""
+        v = (ctypes.c_int64 * 4)()
+        self._call("gm_pool_info", self.h, v)
+        return {"dense": bool(v[0]), "table_pool_entries": int(v[1]), "payload_pool_slots": int(v[2]),
+                "event_spill_records": int(v[3])}
 
     def set_timing(self, on):
         self._call("gm_set_timing", self.h, 1 if on else 0)

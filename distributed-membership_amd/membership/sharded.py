@@ -100,7 +100,11 @@ def distributed_shard(n, rank, world, local_rank, **kw):
     """This rank's column shard of an n-node cluster, with RCCL attached.
 
     Expects torch.distributed initialised with the gloo backend (CPU only: the
-    GPU is driven by libgm alone, so torch never initialises HIP here)."""
+    GPU is driven by libgm alone, so torch never initialises HIP here). Every rank has a GPU of
+    its own (device_share = 1: the escape pools take a quarter of that device's free HBM), unless
+    the diagnostics env GM_DEVICE_OVERRIDE pins all ranks to one device."""
+    share = world if "GM_DEVICE_OVERRIDE" in os.environ else 1
+    kw.setdefault("device_share", share)
     sim = Simulator(n, GM_MODE_SCALED, shard_rank=rank, shard_count=world, device=local_rank, **kw)
     sim.comm_init(rendezvous_uid(rank, world), world, rank)
     return sim

@@ -100,10 +100,15 @@ typedef struct gm_config {
   int32_t init_mode;
   int32_t init_t0;
   uint64_t init_seed;
-  int32_t band;            /* SCALED columns per band of the tick kernel (64/128/256/512; 0 = auto) */
+  int32_t band;            /* SCALED columns per band of the tick kernel (64/128/256/512/1024; 0 = auto:
+                              1024, the band fast path, whenever the row width allows it) */
   int32_t view;            /* PARTIAL view capacity V (2..32; 0 = 32) */
   uint64_t view_seed;      /* PARTIAL initial views and eviction tie-break */
-  int32_t reserved[2];
+  int32_t device_share;    /* SCALED: contexts of this cluster that share this context's device and
+                              split its free HBM for the escape pools / event ring (0 = shard_count:
+                              every shard on one device, as the loopback tests run them; 1 = a device
+                              of its own, one RCCL rank per GPU) */
+  int32_t reserved;
 } gm_config;
 
 /* one log record; `order` sorts records of a drain into reference log order */
@@ -198,6 +203,10 @@ int gm_dump_tables(gm_ctx *ctx, char *buf, size_t cap, size_t *len);
 /* SCALED telemetry of the last tick: [0]=delivered gossip lists M, [1]=live nodes,
  * [2]=max inbox depth, [3]=error flags */
 int gm_tick_stats(gm_ctx *ctx, int64_t stats[4]);
+/* SCALED escape storage as sized at create: info = {1 if the pools are dense-equivalent (no run can
+ * overflow them) else 0, table escape-pool entries, payload escape-pool 16-byte slots, event spill
+ * ring records}; GM_EUNSUPPORTED for the other modes */
+int gm_pool_info(gm_ctx *ctx, int64_t info[4]);
 /* Mean per-tick duration (ms) of the tick kernel over the timing window, measured
  * with HIP events recorded on the context stream before the window's first
  * kernel and after its last. gm_set_timing(ctx, 1) opens a new window at the

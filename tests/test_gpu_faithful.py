@@ -67,3 +67,24 @@ def test_grader_unseeded(case, tmp_path):
                        capture_output=True, timeout=120)
     assert p.returncode == 0, p.stderr
     assert grade((tmp_path / "dbg.log").read_bytes(), case) == (30 if case != "msgdropsinglefailure" else 30)
+
+
+@pytest.mark.parametrize("case", ["singlefailure", "multifailure", "msgdropsinglefailure"])
+def test_reference_binding(case, tmp_path):
+    """The reference-side binding (tests/integration/Application_gm.cpp: the reference's own
+    Application class, Params, Log and Member code, with every tick handed to libgm) built by
+    oracle/Makefile.ref in the build container, run end to end: dbg.log (written by the
+    reference's own Log.cpp), msgcount.log and stdout equal the seeded reference's."""
+    exe = os.path.join(REPO, "oracle", "_ref", "Application_gm")
+    if not os.path.exists(exe):
+        pytest.skip("binding not built (oracle/Makefile.ref binding needs the reference sources)")
+    m = load_case(f"{case}_T42_R7")
+    conf = tmp_path / f"{case}.conf"
+    conf.write_text(m["conf"])
+    env = dict(os.environ, TIME_SEED="42", RD_SEED="7")
+    p = subprocess.run([exe, str(conf)], cwd=tmp_path, env=env, capture_output=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    assert (tmp_path / "dbg.log").read_bytes() == m["dbg"], "dbg.log differs: " + first_diff(
+        (tmp_path / "dbg.log").read_bytes(), m["dbg"])
+    assert (tmp_path / "msgcount.log").read_bytes() == m["msgcount"]
+    assert p.stdout == m["stdout"]

@@ -1,6 +1,7 @@
 """PARTIAL-view parity (scenario S-C semantics, oracle/ref_cpu.c "PARTIAL"): the HIP
 V-entry-view tick against the oracle, tick by tick -- every node's list (dump),
 node state and the join / remove event set -- with a crash set and keyed drops."""
+import numpy as np
 import pytest
 
 import oracle_py
@@ -141,12 +142,34 @@ def test_rccl_single_rank_row_shard_matches_oracle(monkeypatch):
     assert sim.tick_stats()["err"] == 0
 
 
+def block_caps(n, world, chunks, failed):
+    """Python mirror of gm_host.hip xcap: capacity of every (sender shard g, chunk c, receiver q)
+    block from the live nodes per shard -- f_q = max(n_q / n, live_q / live), address probability
+    p = 1 - (1 - f_q)^5, capacity min(rows, ceil(rows p + 8 sqrt(rows p (1 - p)) + 64))."""
+    import math
+    b = [n * g // world for g in range(world + 1)]
+    live = [int((~failed[b[g]:b[g + 1]]).sum()) for g in range(world)]
+    tot = sum(live)
+    pq = [1 - (1 - max((b[g + 1] - b[g]) / n, live[g] / tot)) ** 5 for g in range(world)]
+    caps = {}
+    for g in range(world):
+        nl = b[g + 1] - b[g]
+        for c in range(chunks):
+            rows = nl * (c + 1) // chunks - nl * c // chunks
+            for q in range(world):
+                if q != g:
+                    m = rows * pq[q] + 8 * math.sqrt(rows * pq[q] * (1 - pq[q])) + 64
+                    caps[g, c, q] = min(rows, math.ceil(m))
+    return caps
+
+
 def test_row_shards_packed_blocks_match_oracle(monkeypatch):
     """The exchange sends each (chunk, peer) block packed to its records (gm_p_pack) and only the
     block's capacity travels: a binomial bound, 49 % of the slots at S-C (G = 8). At N = 16,384,
     G = 4, one chunk, a block has 4,096 slots whose records are ~Binomial(4096, 0.763) (mean 3,124,
-    sigma 27): the capacity is mean + 8 sigma + 64 = 3,406 rows, 83 % of the slots. Views, events
-    and the oracle agree tick by tick, and each shard receives exactly the capacities' bytes."""
+    sigma 27): the capacity is mean + 8 sigma + 64 = 3,406 rows, 83 % of the slots, before the crash;
+    after it the capacities follow the live nodes per shard (block_caps). Views, events and the
+    oracle agree tick by tick, and each shard receives exactly the capacities' bytes."""
     from membership.abi import partial_loopback_tick
     n, v, world = 16384, 32, 4
     monkeypatch.setenv("GM_CHUNKS", "1")
@@ -169,9 +192,15 @@ def test_row_shards_packed_blocks_match_oracle(monkeypatch):
         assert ev == sorted(ora.events()), f"events differ at tick {t}"
         if t % 3 == 0:
             assert digest64(b"".join(s.dump_tables() for s in shards)) == digest64(ora.dump()), f"views differ at tick {t}"
-    for s in shards:
+        if t == 11:  # before the crash: 3 peers x one block of capacity 3,406 rows
+            for s in shards:
+                assert s.exchange_bytes() == 3 * 3406 * (32 + 4 * v)
+    failed = np.zeros(n, dtype=bool)
+    failed[crash] = True
+    caps = block_caps(n, world, 1, failed)
+    for q, s in enumerate(shards):
         assert s.tick_stats()["err"] == 0
-        assert s.exchange_bytes() == 3 * 3406 * (32 + 4 * v)  # 3 peers x one block of capacity 3,406 rows
+        assert s.exchange_bytes() == sum(caps[g, 0, q] for g in range(world) if g != q) * (32 + 4 * v)
 
 
 def test_packed_block_overflow_fails_loudly(monkeypatch):
@@ -187,3 +216,43 @@ def test_packed_block_overflow_fails_loudly(monkeypatch):
         for _ in range(3):
             partial_loopback_tick(sh)
     assert e.value.code == -4
+
+
+@pytest.mark.parametrize("chunks", [1, 4])
+def test_row_shards_contiguous_half_crash_match_single_context(chunks, monkeypatch):
+    """The reference's multifailure schedule crashes a contiguous half of the cluster
+    (Application.cpp:188-195: nodes [r, r + N/2)), which takes out whole row shards: after TFAIL
+    every survivor addresses each surviving shard with ~76 % at G = 8, far past the 49 % of evenly
+    spread targets. The block capacities follow the live nodes per shard, so G = 8
+    loopback row shards run the schedule without GM_ERANGE and equal the single context (itself
+    oracle-pinned by the tests above) tick by tick: views, events, node state."""
+    from membership.abi import partial_loopback_tick
+    n, v, world, r = 16384, 32, 8, 3000
+    monkeypatch.setenv("GM_CHUNKS", str(chunks))
+    monkeypatch.delenv("GM_XCHG_CAP_FRAC", raising=False)
+    kw = dict(rd_seed=7, view=v, view_seed=5, init_mode=1, init_t0=8, init_seed=11, drop_pct=5, drop_from=0,
+              drop_to=1000, drop_seed=42)
+    one = Simulator(n, GM_MODE_PARTIAL, **kw)
+    shards = [Simulator(n, GM_MODE_PARTIAL, shard_rank=g, shard_count=world, **kw) for g in range(world)]
+    crash = np.arange(r, r + n // 2, dtype=np.int32)
+    failed = np.zeros(n, dtype=bool)
+    failed[crash] = True
+    caps = block_caps(n, world, chunks, failed)
+    for _ in range(40):
+        t = one.time
+        one.tick()
+        partial_loopback_tick(shards)
+        if t == 10:
+            one.set_failed(crash)
+            for s in shards:
+                s.set_failed(crash)
+        ev1 = sorted(one.drain_events())
+        evs = sorted(e for s in shards for e in s.drain_events())
+        assert evs == ev1, f"events differ at tick {t}"
+        if t % 4 == 0 or t in (15, 16, 31):
+            assert b"".join(s.dump_tables() for s in shards) == one.dump_tables(), f"views differ at tick {t}"
+    assert np.array_equal(np.concatenate([s.read_nodes() for s in shards]), one.read_nodes())
+    for q, s in enumerate(shards):
+        assert s.tick_stats()["err"] == 0
+        want = sum(caps[g, c, q] for g in range(world) if g != q for c in range(chunks))
+        assert s.exchange_bytes() == want * (32 + 4 * v), q
