@@ -30,8 +30,11 @@ __global__ void gm_f_sendprep(FState s);
 __global__ void gm_f_s1expand(FState s);
 hipError_t gm_launch_tick(const SState &s, int t, int drop_pct, hipStream_t st, hipEvent_t k0, hipEvent_t k1,
                           bool pick);
-hipError_t gm_launch_draw(const SState &s, int t, int round, int D, int listed, hipStream_t st);
-hipError_t gm_launch_accept(const SState &s, int t, int D, int in_list, int out, hipStream_t st);
+hipError_t gm_launch_tick_prologue(const SState &s, int t, hipStream_t st);
+hipError_t gm_launch_band_rows(const SState &s, int t, int drop_pct, int r0, int r1, hipStream_t st);
+hipError_t gm_launch_draw(const SState &s, int t, int round, int D, int listed, hipStream_t st, int r0 = 0, int r1 = -1);
+hipError_t gm_launch_accept(const SState &s, int t, int D, int in_list, int out, hipStream_t st, int r0 = 0,
+                            int r1 = -1);
 hipError_t gm_launch_plist_sort(const SState &s, int l, hipStream_t st);
 hipError_t gm_launch_init(const SState &s, int warm, int t0, uint64_t seed, hipStream_t st);
 hipError_t gm_launch_partial_tick(const PState &s, int t, uint32_t *mtraw, hipStream_t st, hipEvent_t k0,
@@ -340,6 +343,14 @@ static int pick_band(const gm_ctx *c, int n, int wp) {
   return 64;
 }
 
+// the chunk-major exchange buffer of a column shard (SState.xcnt, S_XC)
+static size_t xcnt_bytes(const SState &s) {
+  return sizeof(int32_t) * 2 * (size_t)s.xk * s.shard_count * ((size_t)1 << s.xlog);
+}
+static int xchunk_rows(const SState &s, int ch) {  // real rows of exchange chunk ch
+  return (int)std::min<int64_t>((int64_t)1 << s.xlog, (int64_t)s.n - ((int64_t)ch << s.xlog));
+}
+
 static int create_scaled(gm_ctx *c) {
   const int n = c->n;
   const int G = c->cfg.shard_count > 0 ? c->cfg.shard_count : 1;
@@ -522,7 +533,17 @@ static int create_scaled(gm_ctx *c) {
     TRY(dalloc(c, &s.pending, n));
     TRY(dalloc(c, &s.npending, 1));
     c->dmax = 64;
-    TRY(dalloc(c, &s.xcnt, (size_t)G * n * 2));
+    // the exchange's row chunks (tick_sharded pipelines band -> all-gather -> draw -> MAX-allreduce ->
+    // acceptance chunk by chunk): 2^xlog rows each (>= 64: a multiple of every band width's rows per
+    // unit), K = GM_SCHUNKS chunks by default 4
+    {
+      int K = getenv("GM_SCHUNKS") ? atoi(getenv("GM_SCHUNKS")) : 4;
+      if (K < 1 || K > 64) return GM_EINVAL;
+      s.xlog = 6;
+      while (((int64_t)1 << s.xlog) * K < n) s.xlog++;
+      s.xk = (int)((n + (1 << s.xlog) - 1) >> s.xlog);
+    }
+    TRY(dalloc(c, &s.xcnt, (size_t)s.xk * G * ((size_t)1 << s.xlog) * 2));
     TRY(dalloc(c, &s.status, (size_t)n * c->dmax));
     // bounded rounds (tick_sharded): round 0 takes every row's first 16 S2 outputs, round 1
     // the next 64 for up to plist_cap rows left pending -- no host round trip per tick
@@ -539,7 +560,11 @@ static int create_scaled(gm_ctx *c) {
       TRY(dalloc(c, &s.statusl[l], (size_t)s.plist_cap[l] * (l == 1 ? GM_D_MORE : GM_D_LAST)));
     }
     HIPCHECK(ctx_memset(c, s.pending, 0, sizeof(int32_t) * n));
-    HIPCHECK(ctx_memset(c, s.xcnt, 0, sizeof(int32_t) * (size_t)G * n * 2));
+    HIPCHECK(ctx_memset(c, s.xcnt, 0, xcnt_bytes(s)));
+    HIPCHECK(hipStreamCreateWithFlags(&c->p_comm, hipStreamNonBlocking));  // the pipelined exchange
+    c->p_chev.assign(s.xk, nullptr);
+    for (hipEvent_t &e : c->p_chev) HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIPCHECK(hipEventCreateWithFlags(&c->p_done, hipEventDisableTiming));
   }
   c->t = t0 + 1;  // the converged table is the state "as of tick t0"
   return GM_OK;
@@ -1733,8 +1758,7 @@ extern "C" int gm_shard_merge(gm_ctx *c) {
   TRY(ramp_starters(c));
   const int t_send = c->t - 1;
   const bool drop = c->cfg.drop_pct > 0 && t_send >= c->cfg.drop_from && t_send < c->cfg.drop_to;
-  HIPCHECK(hipMemsetAsync(c->s.xcnt + (size_t)c->s.shard_rank * c->n * 2, 0, sizeof(int32_t) * 2 * (size_t)c->n,
-                          c->stream));
+  HIPCHECK(hipMemsetAsync(c->s.xcnt, 0, xcnt_bytes(c->s), c->stream));
   hipEvent_t k0 = nullptr, k1 = nullptr;
   if (c->timing) TRY(timing_slot(c, &k0, &k1));
   HIPCHECK(gm_launch_tick(c->s, c->t, drop ? c->cfg.drop_pct : -1, c->stream, k0, k1, false));
@@ -1798,11 +1822,16 @@ extern "C" int gm_shard_loopback(gm_ctx **ctxs, int32_t G, int32_t what, int32_t
   const size_t n = (size_t)ctxs[0]->n;
   hipStream_t st = ctxs[0]->stream;
   if (what == 0) {
+    const SState &s0 = ctxs[0]->s;
+    for (int g = 1; g < G; g++)
+      if (ctxs[g]->s.xlog != s0.xlog) return GM_EINVAL;
     for (int dst = 0; dst < G; dst++)
       for (int src = 0; src < G; src++)
-        if (src != dst)
-          HIPCHECK(hipMemcpyAsync(ctxs[dst]->s.xcnt + (size_t)src * n * 2, ctxs[src]->s.xcnt + (size_t)src * n * 2,
-                                  sizeof(int32_t) * n * 2, hipMemcpyDeviceToDevice, st));
+        for (int ch = 0; ch < s0.xk && src != dst; ch++) {
+          const size_t o = S_XC(s0, src, (size_t)ch << s0.xlog);
+          HIPCHECK(hipMemcpyAsync(ctxs[dst]->s.xcnt + o, ctxs[src]->s.xcnt + o, sizeof(int32_t) * 2 * xchunk_rows(s0, ch),
+                                  hipMemcpyDeviceToDevice, st));
+        }
   } else if (what == 2) {  // msgcount: SUM of the shards' fresh counts (and kept entries on loss ticks)
     const int t = ctxs[0]->t;
     if (!mc_on(ctxs[0], t)) return GM_ESTATE;
@@ -1825,6 +1854,85 @@ extern "C" int gm_shard_loopback(gm_ctx **ctxs, int32_t G, int32_t what, int32_t
   return GM_OK;
 }
 
+// One PIPELINED column-shard tick (tick_sharded's chunk order) of G shard contexts living on one
+// device, the collectives done by device copies / MAX kernels on one stream: per exchange chunk the
+// all-gather of the counts, every shard's round-0 draws of the chunk's rows, the MAX-reduce of their
+// statuses, every shard's acceptance; then the bounded rounds 1, 2 with their MAX-reduces. Tests
+// compare it with the fused kernel and with the phase-API loopback (gm_shard_loopback); tick_sharded
+// runs the same per-chunk steps with RCCL on the comm stream, overlapped with later chunks' merges.
+extern "C" int gm_shard_loopback_tick(gm_ctx **ctxs, int32_t G) {
+  if (!ctxs || G < 2) return GM_EINVAL;
+  for (int g = 0; g < G; g++) {
+    TRY(shard_ready(ctxs[g]));
+    const SState &sg = ctxs[g]->s;
+    if (sg.shard_count != G || sg.shard_rank != g || ctxs[g]->n != ctxs[0]->n || ctxs[g]->t != ctxs[0]->t ||
+        sg.xlog != ctxs[0]->s.xlog || sg.ramp || mc_on(ctxs[g], ctxs[g]->t))
+      return GM_EINVAL;
+    TRY(draw_settle(ctxs[g]));
+    TRY(before_tick_events(ctxs[g]));
+    HIPCHECK(hipStreamSynchronize(ctxs[g]->stream));
+  }
+  hipStream_t ls = ctxs[0]->stream;
+  const int t = ctxs[0]->t, t_send = t - 1;
+  const SState &s0 = ctxs[0]->s;
+  for (int g = 0; g < G; g++) {
+    gm_ctx *c = ctxs[g];
+    SState &s = c->s;
+    const bool drop = c->cfg.drop_pct > 0 && t_send >= c->cfg.drop_from && t_send < c->cfg.drop_to;
+    HIPCHECK(hipMemsetAsync(s.xcnt, 0, xcnt_bytes(s), ls));
+    for (int l = 1; l <= 2; l++) HIPCHECK(hipMemsetAsync(s.plist_cnt[l], 0, sizeof(uint32_t), ls));
+    HIPCHECK(hipMemsetAsync(s.npending, 0, sizeof(int32_t), ls));
+    HIPCHECK(gm_launch_tick_prologue(s, t, ls));
+    for (int ch = 0; ch < s.xk; ch++) {
+      const int r0 = ch << s.xlog;
+      HIPCHECK(gm_launch_band_rows(s, t, drop ? c->cfg.drop_pct : -1, r0, r0 + xchunk_rows(s, ch), ls));
+    }
+  }
+  auto max_reduce = [&](auto buf_of, size_t off, size_t cnt) -> int {  // MAX over the shards, into every shard
+    if (!cnt) return GM_OK;
+    for (int g = 1; g < G; g++)
+      hipLaunchKernelGGL(gm_max_into, dim3(256), dim3(256), 0, ls, buf_of(0) + off, buf_of(g) + off, cnt);
+    for (int g = 1; g < G; g++)
+      HIPCHECK(hipMemcpyAsync(buf_of(g) + off, buf_of(0) + off, sizeof(int32_t) * cnt, hipMemcpyDeviceToDevice, ls));
+    return GM_OK;
+  };
+  for (int ch = 0; ch < s0.xk; ch++) {
+    const int r0 = ch << s0.xlog, r1 = r0 + xchunk_rows(s0, ch);
+    for (int dst = 0; dst < G; dst++)  // the chunk's all-gather
+      for (int src = 0; src < G; src++)
+        if (src != dst) {
+          const size_t o = S_XC(s0, src, (size_t)r0);
+          HIPCHECK(hipMemcpyAsync(ctxs[dst]->s.xcnt + o, ctxs[src]->s.xcnt + o, sizeof(int32_t) * 2 * (r1 - r0),
+                                  hipMemcpyDeviceToDevice, ls));
+        }
+    for (int g = 0; g < G; g++) HIPCHECK(gm_launch_draw(ctxs[g]->s, t, 0, GM_D_FIRST, 0, ls, r0, r1));
+    TRY(max_reduce([&](int g) { return ctxs[g]->s.status; }, (size_t)r0 * GM_D_FIRST, (size_t)(r1 - r0) * GM_D_FIRST));
+    for (int g = 0; g < G; g++) HIPCHECK(gm_launch_accept(ctxs[g]->s, t, GM_D_FIRST, 0, 1, ls, r0, r1));
+  }
+  for (int l = 1; l <= 2; l++) {
+    const int D = l == 1 ? GM_D_MORE : GM_D_LAST;
+    for (int g = 0; g < G; g++) {
+      HIPCHECK(gm_launch_plist_sort(ctxs[g]->s, l, ls));
+      HIPCHECK(gm_launch_draw(ctxs[g]->s, t, l, D, l, ls));
+    }
+    TRY(max_reduce([&](int g) { return ctxs[g]->s.statusl[l]; }, 0, (size_t)s0.plist_cap[l] * D));
+    for (int g = 0; g < G; g++) HIPCHECK(gm_launch_accept(ctxs[g]->s, t, D, l, l == 1 ? 2 : -1, ls));
+  }
+  HIPCHECK(hipGetLastError());
+  for (int g = 0; g < G; g++) {
+    gm_ctx *c = ctxs[g];
+    HIPCHECK(hipMemcpyAsync(c->draw_left_h, c->s.npending, sizeof(int32_t), hipMemcpyDeviceToHost, ls));
+    HIPCHECK(hipStreamSynchronize(ls));
+    if (*c->draw_left_h) {  // rows the bounded rounds could not take: the phase API's host-driven rounds
+      snprintf(g_errbuf, sizeof g_errbuf, "pipelined loopback tick: %d rows left after the bounded rounds",
+               *c->draw_left_h);
+      return GM_ERANGE;
+    }
+    TRY(gm_shard_end_tick(c));
+  }
+  return GM_OK;
+}
+
 // Host-collective hook: the phase exchange buffers of ONE shard context as plain host arrays, so
 // that any host-side collective (gloo across processes: membership.sharded.host_tick) can stand
 // in for RCCL / gm_shard_loopback. Layouts (n = cluster size, G = shard count):
@@ -1837,9 +1945,11 @@ static int shard_buf(gm_ctx *c, int what, int D, std::vector<std::pair<void *, s
   const size_t n = (size_t)c->n;
   SState &s = c->s;
   parts.clear();
-  if (what == 0) {
-    if (import) parts.push_back({s.xcnt, sizeof(int32_t) * n * 2 * s.shard_count});
-    else parts.push_back({s.xcnt + (size_t)s.shard_rank * n * 2, sizeof(int32_t) * n * 2});
+  if (what == 0) {  // host layout [n][2] (export) / [G][n][2] (import); device chunk-major (S_XC)
+    for (int g = import ? 0 : s.shard_rank; g < (import ? s.shard_count : s.shard_rank + 1); g++)
+      for (int ch = 0; ch < s.xk; ch++)
+        parts.push_back({s.xcnt + S_XC(s, g, (size_t)ch << s.xlog), sizeof(int32_t) * 2 * xchunk_rows(s, ch)});
+    (void)n;
   } else if (what == 1) {
     if (D <= 0 || D > c->dmax) return GM_EINVAL;
     parts.push_back({s.status, sizeof(int32_t) * n * D});
@@ -1899,79 +2009,142 @@ extern "C" int gm_shard_stub(gm_ctx *c, int32_t on) {
   return GM_OK;
 }
 
+// the all-gather of this shard's per-row (present, numfailed) for exchange chunk ch (stub: mirrored
+// into every peer slot), on stream st
+static int xcnt_allgather(gm_ctx *c, int ch, hipStream_t st) {
+  SState &s = c->s;
+  const size_t R = (size_t)1 << s.xlog, r0 = (size_t)ch << s.xlog;
+  int32_t *own = s.xcnt + S_XC(s, s.shard_rank, r0);
+  if (s.stub) {
+    for (int g = 0; g < s.shard_count; g++)
+      if (g != s.shard_rank)
+        HIPCHECK(hipMemcpyAsync(s.xcnt + S_XC(s, g, r0), own, sizeof(int32_t) * 2 * xchunk_rows(s, ch),
+                                hipMemcpyDeviceToDevice, st));
+    return GM_OK;
+  }
+  // chunk-major: the chunk's G slots are contiguous, rank g's at g * R rows -- in place
+  NCCLCHECK(ncclAllGather(own, s.xcnt + S_XC(s, 0, r0), R * 2, ncclInt32, c->comm, st));
+  return GM_OK;
+}
+
+// Bounded rounds 1 and 2 (no host round trip) over the rows round 0 left pending: their sorted
+// list (identical on every rank) takes the next 64 S2 outputs, then up to 256 rows the next 256;
+// a row still short sets GM_ERR_DRAWS. Then the device count of rows the rounds could not take is
+// read back without a wait (draw_settle finishes them with host-driven rounds).
+static int bounded_rounds(gm_ctx *c) {
+  SState &s = c->s;
+  for (int l = 1; l <= 2; l++) {
+    const int D = l == 1 ? GM_D_MORE : GM_D_LAST;
+    HIPCHECK(gm_launch_plist_sort(s, l, c->stream));
+    HIPCHECK(gm_launch_draw(s, c->t, l, D, l, c->stream));
+    if (!s.stub)
+      NCCLCHECK(ncclAllReduce(s.statusl[l], s.statusl[l], (size_t)s.plist_cap[l] * D, ncclInt32, ncclMax, c->comm,
+                              c->stream));
+    HIPCHECK(gm_launch_accept(s, c->t, D, l, l == 1 ? 2 : -1, c->stream));
+  }
+  if (getenv("GM_DEBUG_ROUNDS")) {  // diagnostics: rows left after round 0, error flags
+    uint32_t pc1 = 0, pc2 = 0, e = 0;
+    HIPCHECK(hipMemcpyAsync(&pc1, s.plist_cnt[1], sizeof pc1, hipMemcpyDeviceToHost, c->stream));
+    HIPCHECK(hipMemcpyAsync(&pc2, s.plist_cnt[2], sizeof pc2, hipMemcpyDeviceToHost, c->stream));
+    HIPCHECK(hipMemcpyAsync(&e, s.err, sizeof e, hipMemcpyDeviceToHost, c->stream));
+    HIPCHECK(hipStreamSynchronize(c->stream));
+    fprintf(stderr, "[gm] t=%d rows pending after round 0: %u (cap %d), after round 1: %u (cap %d), err 0x%x\n", c->t,
+            pc1, s.plist_cap[1], pc2, s.plist_cap[2], e);
+  }
+  HIPCHECK(hipMemcpyAsync(c->draw_left_h, s.npending, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  HIPCHECK(hipEventRecord(c->draw_ev, c->stream));
+  c->t--;  // gm_tick advances globaltime
+  c->draw_check = true;  // before end_tick: the msgcount phase waits for draw_settle
+  TRY(gm_shard_end_tick(c));
+  c->ticks_done--;  // gm_tick counts it
+  return GM_OK;
+}
+
+// The column-shard tick, pipelined over the exchange's row chunks (north_star: the exchange
+// overlapped with the local merge on a second stream). The compute stream runs the band kernels
+// chunk after chunk; as soon as chunk ch's are done (event), the comm stream all-gathers the
+// chunk's per-row counts, draws round 0 of its rows (every rank replays every row's first 16 S2
+// outputs and resolves the draws landing in its columns), MAX-allreduces their statuses and runs
+// the acceptance -- while the band kernels of chunks ch+1.. still run. A row's draws need only
+// its own post-sweep row (in chunk ch) and the other ranks' counts of that row; the acceptance
+// appends to the inboxes of tick t+1 (the other parity), which no band kernel of tick t reads.
+// Then the bounded rounds 1, 2 on the compute stream. Ticks that record msgcount (their
+// fresh-count all-reduce precedes every draw), the join ramp and the host-driven draw loop (mass
+// failure, heavy loss) take the same steps unchunked.
 static int tick_sharded(gm_ctx *c) {
   if (!c->comm && !c->s.stub) return GM_EUNSUPPORTED;  // multi-GPU ticks need gm_comm_init (or the phase API + loopback)
+  SState &s = c->s;
   const size_t n = (size_t)c->n;
-  TRY(gm_shard_merge(c));
-  if (c->s.stub) {
-    for (int g = 0; g < c->s.shard_count; g++)
-      if (g != c->s.shard_rank)
-        HIPCHECK(hipMemcpyAsync(c->s.xcnt + (size_t)g * n * 2, c->s.xcnt + (size_t)c->s.shard_rank * n * 2,
-                                sizeof(int32_t) * n * 2, hipMemcpyDeviceToDevice, c->stream));
-  } else {
-    NCCLCHECK(ncclAllGather(c->s.xcnt + (size_t)c->s.shard_rank * n * 2, c->s.xcnt, n * 2, ncclInt32, c->comm,
-                            c->stream));
-    if (mc_on(c, c->t)) {  // msgcount: whole-row fresh counts (and kept entries on loss ticks)
-      NCCLCHECK(ncclAllReduce(c->s.mc_fresh + (size_t)(c->t & 1) * n, c->s.mc_fresh + (size_t)(c->t & 1) * n, n,
-                              ncclUint32, ncclSum, c->comm, c->stream));
-      if (drop_tick(c, c->t))
-        NCCLCHECK(ncclAllReduce(c->s.mc_rdrop, c->s.mc_rdrop, n, ncclUint32, ncclSum, c->comm, c->stream));
-    }
-  }
   const int64_t nfailed = c->nfailed;
   // mass failure or heavy loss leaves many entries stale, so rows need many draws: the
   // host-driven unbounded loop below (also GM_SHARD_SYNC=1)
   const bool sync = c->shard_sync == 1 || (c->shard_sync < 0 && (c->cfg.drop_pct >= 30 || 10 * nfailed > (int64_t)n));
+  const bool pipe = !sync && !mc_on(c, c->t) && !s.ramp && !(getenv("GM_SHARD_PIPE") && !atoi(getenv("GM_SHARD_PIPE")));
+  if (pipe) {
+    TRY(shard_ready(c));
+    TRY(before_tick_events(c));
+    const int t = c->t, t_send = t - 1;
+    const bool drop = c->cfg.drop_pct > 0 && t_send >= c->cfg.drop_from && t_send < c->cfg.drop_to;
+    HIPCHECK(hipMemsetAsync(s.xcnt, 0, xcnt_bytes(s), c->stream));
+    for (int l = 1; l <= 2; l++) HIPCHECK(hipMemsetAsync(s.plist_cnt[l], 0, sizeof(uint32_t), c->stream));
+    HIPCHECK(hipMemsetAsync(s.npending, 0, sizeof(int32_t), c->stream));
+    HIPCHECK(gm_launch_tick_prologue(s, t, c->stream));
+    hipEvent_t k0 = nullptr, k1 = nullptr;
+    if (c->timing) TRY(timing_slot(c, &k0, &k1));
+    if (k0) HIPCHECK(hipEventRecord(k0, c->stream));
+    for (int ch = 0; ch < s.xk; ch++) {
+      const int r0 = ch << s.xlog;
+      HIPCHECK(gm_launch_band_rows(s, t, drop ? c->cfg.drop_pct : -1, r0, r0 + xchunk_rows(s, ch), c->stream));
+      HIPCHECK(hipEventRecord(c->p_chev[ch], c->stream));
+    }
+    if (k1) HIPCHECK(hipEventRecord(k1, c->stream));
+    hipStream_t cs = c->p_comm;
+    for (int ch = 0; ch < s.xk; ch++) {
+      const int r0 = ch << s.xlog, r1 = r0 + xchunk_rows(s, ch);
+      HIPCHECK(hipStreamWaitEvent(cs, c->p_chev[ch], 0));
+      TRY(xcnt_allgather(c, ch, cs));
+      HIPCHECK(gm_launch_draw(s, t, 0, GM_D_FIRST, 0, cs, r0, r1));
+      if (!s.stub)
+        NCCLCHECK(ncclAllReduce(s.status + (size_t)r0 * GM_D_FIRST, s.status + (size_t)r0 * GM_D_FIRST,
+                                (size_t)(r1 - r0) * GM_D_FIRST, ncclInt32, ncclMax, c->comm, cs));
+      HIPCHECK(gm_launch_accept(s, t, GM_D_FIRST, 0, 1, cs, r0, r1));
+    }
+    HIPCHECK(hipEventRecord(c->p_done, cs));
+    HIPCHECK(hipStreamWaitEvent(c->stream, c->p_done, 0));
+    return bounded_rounds(c);
+  }
+  TRY(gm_shard_merge(c));
+  for (int ch = 0; ch < s.xk; ch++) TRY(xcnt_allgather(c, ch, c->stream));
+  if (!s.stub && mc_on(c, c->t)) {  // msgcount: whole-row fresh counts (and kept entries on loss ticks)
+    NCCLCHECK(ncclAllReduce(s.mc_fresh + (size_t)(c->t & 1) * n, s.mc_fresh + (size_t)(c->t & 1) * n, n, ncclUint32,
+                            ncclSum, c->comm, c->stream));
+    if (drop_tick(c, c->t))
+      NCCLCHECK(ncclAllReduce(s.mc_rdrop, s.mc_rdrop, n, ncclUint32, ncclSum, c->comm, c->stream));
+  }
   if (!sync) {
     // bounded rounds, stream-ordered (no host round trip): round 0 = every row's first 16
     // S2 outputs; rows left pending go to a list (sorted: identical on every rank) that
     // round 1 serves with the next 64; a row still short after that sets GM_ERR_DRAWS
-    SState &s = c->s;
     for (int l = 1; l <= 2; l++) HIPCHECK(hipMemsetAsync(s.plist_cnt[l], 0, sizeof(uint32_t), c->stream));
     HIPCHECK(hipMemsetAsync(s.npending, 0, sizeof(int32_t), c->stream));
     HIPCHECK(gm_launch_draw(s, c->t, 0, GM_D_FIRST, 0, c->stream));
     if (!s.stub)
       NCCLCHECK(ncclAllReduce(s.status, s.status, n * GM_D_FIRST, ncclInt32, ncclMax, c->comm, c->stream));
     HIPCHECK(gm_launch_accept(s, c->t, GM_D_FIRST, 0, 1, c->stream));
-    for (int l = 1; l <= 2; l++) {  // rounds 1, 2 over the sorted pending lists
-      const int D = l == 1 ? GM_D_MORE : GM_D_LAST;
-      HIPCHECK(gm_launch_plist_sort(s, l, c->stream));
-      HIPCHECK(gm_launch_draw(s, c->t, l, D, l, c->stream));
-      if (!s.stub)
-        NCCLCHECK(ncclAllReduce(s.statusl[l], s.statusl[l], (size_t)s.plist_cap[l] * D, ncclInt32, ncclMax, c->comm,
-                                c->stream));
-      HIPCHECK(gm_launch_accept(s, c->t, D, l, l == 1 ? 2 : -1, c->stream));
-    }
-    if (getenv("GM_DEBUG_ROUNDS")) {  // diagnostics: rows left after round 0, error flags
-      uint32_t pc1 = 0, pc2 = 0, e = 0;
-      HIPCHECK(hipMemcpyAsync(&pc1, s.plist_cnt[1], sizeof pc1, hipMemcpyDeviceToHost, c->stream));
-      HIPCHECK(hipMemcpyAsync(&pc2, s.plist_cnt[2], sizeof pc2, hipMemcpyDeviceToHost, c->stream));
-      HIPCHECK(hipMemcpyAsync(&e, s.err, sizeof e, hipMemcpyDeviceToHost, c->stream));
-      HIPCHECK(hipStreamSynchronize(c->stream));
-      fprintf(stderr, "[gm] t=%d rows pending after round 0: %u (cap %d), after round 1: %u (cap %d), err 0x%x\n", c->t,
-              pc1, s.plist_cap[1], pc2, s.plist_cap[2], e);
-    }
-    // rows the bounded rounds could not take: counted on the device, read back without a wait
-    HIPCHECK(hipMemcpyAsync(c->draw_left_h, s.npending, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
-    HIPCHECK(hipEventRecord(c->draw_ev, c->stream));
-    c->t--;  // gm_tick advances globaltime
-    c->draw_check = true;  // before end_tick: the msgcount phase waits for draw_settle
-    TRY(gm_shard_end_tick(c));
-    c->ticks_done--;  // gm_tick counts it
-    return GM_OK;
+    return bounded_rounds(c);
   }
   int round = 0, D = GM_D_FIRST;
   for (;;) {
     TRY(gm_shard_draw(c, round, D));
-    if (!c->s.stub)
-      NCCLCHECK(ncclAllReduce(c->s.status, c->s.status, n * D, ncclInt32, ncclMax, c->comm, c->stream));
+    if (!s.stub)
+      NCCLCHECK(ncclAllReduce(s.status, s.status, n * D, ncclInt32, ncclMax, c->comm, c->stream));
     int32_t pend = 0;
     TRY(gm_shard_accept(c, D, &pend));
     if (getenv("GM_DEBUG_ROUNDS")) fprintf(stderr, "[gm] t=%d round %d: %d rows still drawing\n", c->t, round, pend);
     if (pend == 0) break;
     if (++round > GM_MAX_ROUNDS) {  // a row that never finds its targets: same guard as gm_s_pick
       uint32_t e = GM_ERR_DRAWS;
-      HIPCHECK(ctx_memcpy(c, c->s.err, &e, sizeof e, hipMemcpyHostToDevice));
+      HIPCHECK(ctx_memcpy(c, s.err, &e, sizeof e, hipMemcpyHostToDevice));
       c->latched = GM_ERANGE;
       return c->latched;
     }

@@ -73,6 +73,9 @@ __host__ __device__ inline bool s_ingroup(int ramp, int intro_until, int r, int 
 }
 // column shards: xcnt's per-(rank, row) present word carries a flag for a self append
 #define S_XC_SELFAPP 0x40000000
+// int32 index of (rank g, row r)'s present word in the chunk-major xcnt (numfailed follows it)
+#define S_XC(s, g, r) \
+  ((((((size_t)(r) >> (s).xlog) * (size_t)(s).shard_count + (size_t)(g)) << (s).xlog) + ((size_t)(r) & ((1u << (s).xlog) - 1))) * 2)
 #define S_XC_COUNT 0x3FFFFFFF
 #define S_H(c) ((c) >> 5)
 #define S_AGE(c) ((c) & 31u)
@@ -164,7 +167,11 @@ struct SState {
   int32_t *mecol;            // [n] ramp: myPos's column this tick (self, or the updateMyPos quirk's target)
   int32_t *selfadd;          // [S_SELFADD_CAP] ramp: rows that appended their own entry this tick
   uint32_t *selfadd_cnt;
-  int32_t *xcnt;             // bound exchange buffer [shard_count][n][2]: (present, numfailed) per shard
+  int32_t *xcnt;             // bound exchange buffer, chunk-major: [chunk][shard_count][2^xlog][2] (present,
+                             //   numfailed) per shard and row (s_xc): a row chunk's slots of every rank are
+                             //   contiguous, so each chunk's all-gather is one in-place ncclAllGather
+  int xlog;                  // log2 of the rows per exchange chunk (chunk c = rows [c << xlog, (c + 1) << xlog))
+  int xk;                    // exchange chunks = ceil(n / 2^xlog)
   int32_t *status;           // bound exchange buffer [n][D]: resolved draws, MAX-allreduced
   int32_t *acc;              // [n][8]: targets so far, g[5], numpot, size
   int32_t *pending;          // [n] rows still drawing

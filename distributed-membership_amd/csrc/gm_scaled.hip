@@ -587,7 +587,7 @@ __device__ __forceinline__ void unit_records(const SState &s, int t, const UnitI
     // column shard: this shard's row totals (present, numfailed) for the all-gather,
     // accumulated as one packed 64-bit add per (row, band) into the zeroed slot
     if (s.sharded && live)
-      atomicAdd((unsigned long long *)(s.xcnt + ((size_t)s.shard_rank * s.n + r) * 2),
+      atomicAdd((unsigned long long *)(s.xcnt + S_XC(s, s.shard_rank, r)),
                 (unsigned long long)(pf & 0xFFFF) | ((unsigned long long)(pf >> 16) << 32));
   }
 }
@@ -762,7 +762,7 @@ __device__ __forceinline__ void unit_finish(const SState &s, int t, int drop_pct
             if (slot < S_SELFADD_CAP) s.selfadd[slot] = r;
             else atomicOr(s.err, GM_ERR_SELF);
             // column shards: the other ranks check their (higher) columns in gm_s_draw
-            if (s.sharded) atomicOr((uint32_t *)(s.xcnt + ((size_t)s.shard_rank * s.n + r) * 2), S_XC_SELFAPP);
+            if (s.sharded) atomicOr((uint32_t *)(s.xcnt + S_XC(s, s.shard_rank, r)), S_XC_SELFAPP);
           }
         }
       }
@@ -1237,11 +1237,11 @@ template <int B, bool DROP>
 #endif
 // grid (units of a band / 4, bands): blockIdx.y is the band, so workgroups still dispatch
 // band-major, and the wave-uniform unit index needs no division
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DROP ? GM_DROP_MINW : GM_BAND_MINW, 8))) void gm_s_band(SState s, int t, int drop_pct) {
+// units [u0, u1) of every band: a row chunk of the column-sharded pipeline, or all of them
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DROP ? GM_DROP_MINW : GM_BAND_MINW, 8))) void gm_s_band(SState s, int t, int drop_pct, int u0, int u1) {
   constexpr int RPW = 64 / (B / S_COLS_PER_LANE);
-  const int U = (s.n + RPW - 1) / RPW;
-  const int ub = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
-  if (ub >= U) return;  // whole wave
+  const int ub = __builtin_amdgcn_readfirstlane(u0 + (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6));
+  if (ub >= u1) return;  // whole wave
   UnitIn<B> in;
   unit_load<B, RPW == 1>(s, t, (int)blockIdx.y, ub, in);
   u32x2 m[S_SB];
@@ -1254,15 +1254,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DROP ? GM_D
 
 // The general path over the units gm_s_band_fast handed back this tick (s.fb_list): a fixed grid of
 // waves striding over the list (rows through vector registers: the units come from memory).
+// Only the units of rows [u0, u1) (one row per unit at B = 1024): the pipelined sharded tick runs it
+// after each row chunk's fast pass, over the list so far.
 template <int B>
-__global__ __launch_bounds__(256) void gm_s_band_listed(SState s, int t) {
+__global__ __launch_bounds__(256) void gm_s_band_listed(SState s, int t, int u0, int u1) {
   __shared__ uint32_t lds_all[4 * S_LDS_WAVE_WORDS];
   uint32_t *lds = lds_all + (threadIdx.x >> 6) * S_LDS_WAVE_WORDS;
   const uint32_t cnt = s.fb_cnt[t & 1];
   const uint32_t nw = gridDim.x * 4;
   for (uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6); i < cnt; i += nw) {
     const int2 u = s.fb_list[i];
-    band_unit<B, false, false>(s, t, -1, __builtin_amdgcn_readfirstlane(u.x), __builtin_amdgcn_readfirstlane(u.y), lds);
+    const int ub = __builtin_amdgcn_readfirstlane(u.y);
+    if (ub < u0 || ub >= u1) continue;
+    band_unit<B, false, false>(s, t, -1, __builtin_amdgcn_readfirstlane(u.x), ub, lds);
   }
 }
 
@@ -1270,9 +1274,9 @@ __global__ __launch_bounds__(256) void gm_s_band_listed(SState s, int t) {
 // unit it hands back (not merged, a delivered escape nibble, a payload for the wide plane) goes to
 // s.fb_list for gm_s_band's listed pass right after, untouched. The list of tick t+1 starts empty.
 template <int B>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GM_BAND_MINW, 8))) void gm_s_band_fast(SState s, int t) {
-  const int ub = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
-  if (ub >= s.n) return;  // whole wave (one row per wave)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GM_BAND_MINW, 8))) void gm_s_band_fast(SState s, int t, int u0, int u1) {
+  const int ub = __builtin_amdgcn_readfirstlane(u0 + (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6));
+  if (ub >= u1) return;  // whole wave (one row per wave)
   // per wave: escape cells by column, the park, the per-lane words of the escaped cells' outcomes
   constexpr int W = 2 * S_LDS_WAVE_WORDS + 192;
   __shared__ uint32_t lds_all[4 * W];
@@ -1659,16 +1663,17 @@ hipError_t gm_launch_msgcount(const SState &s, int t, bool dropped, int phase, h
 // status[r][d] = -2 for an output Lemire rejects (same on every rank),
 // (global column << 1) | fresh on the owning rank, -1 elsewhere (MAX-allreduced).
 template <int B>
-__global__ __launch_bounds__(256) void gm_s_draw(SState s, int t, int round, int D, int listed) {
+__global__ __launch_bounds__(256) void gm_s_draw(SState s, int t, int round, int D, int listed, int r0, int r1) {
   extern __shared__ __align__(16) uint32_t p_smem[];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   // listed: the rows still pending after round 0, in ascending order (gm_s_plist_sort);
-  // their statuses go to status1 by list position
-  const int i = blockIdx.x * 4 + wave;
+  // their statuses go to status1 by list position. Unlisted: rows [r0, r1) (a row chunk)
+  const int i = (listed ? 0 : r0) + (int)blockIdx.x * 4 + wave;
   if (listed && i >= (int)min(*s.plist_cnt[listed], (uint32_t)s.plist_cap[listed])) return;
   const int r = listed ? s.plist[listed][i] : i;
-  if (r >= s.n) return;
-  uint32_t *pre = p_smem + wave * gm_draw_lds_words(s.wp, B);
+  if (r >= (listed ? s.n : r1)) return;
+  // round 0 has no lazy generator state (gm_launch_draw sizes its LDS to the chunk prefix)
+  uint32_t *pre = p_smem + wave * (round == 0 ? (size_t)gm_draw_chunks(s.wp, B) + 1 : gm_draw_lds_words(s.wp, B));
   uint32_t *mts = pre + gm_draw_chunks(s.wp, B) + 1;
   const int G = s.shard_count;
   int32_t *acc = s.acc + (size_t)r * 8;
@@ -1682,10 +1687,10 @@ __global__ __launch_bounds__(256) void gm_s_draw(SState s, int t, int round, int
     int size = 0, nf = 0;
     bool selfapp = false;
     for (int g = 0; g < G; g++) {
-      const int pr = s.xcnt[((size_t)g * s.n + r) * 2];
+      const int pr = s.xcnt[S_XC(s, g, r)];
       size += pr & S_XC_COUNT;
       selfapp |= (pr & S_XC_SELFAPP) != 0;
-      nf += s.xcnt[((size_t)g * s.n + r) * 2 + 1];
+      nf += s.xcnt[S_XC(s, g, r) + 1];
     }
     if (selfapp && lane == 0) {
       // join ramp: row r appended its own entry (updateMyPos found no larger id in its start
@@ -1693,7 +1698,7 @@ __global__ __launch_bounds__(256) void gm_s_draw(SState s, int t, int round, int
       // the shards above the group must hold nothing of the row (present, or removed this tick)
       for (int g = 0; g < G; g++) {
         const int c0g = (int)((int64_t)s.n * g / G);
-        if (c0g > (r | 3) && ((s.xcnt[((size_t)g * s.n + r) * 2] & S_XC_COUNT) || s.xcnt[((size_t)g * s.n + r) * 2 + 1]))
+        if (c0g > (r | 3) && ((s.xcnt[S_XC(s, g, r)] & S_XC_COUNT) || s.xcnt[S_XC(s, g, r) + 1]))
           atomicOr(s.err, GM_ERR_SELF);
       }
     }
@@ -1732,8 +1737,8 @@ __global__ __launch_bounds__(256) void gm_s_draw(SState s, int t, int round, int
   const int rr = (round == 0 || listed) ? round : s.pending[r];
   const uint32_t size = (uint32_t)acc[7];
   uint32_t own_lo = 0;
-  for (int g = 0; g < s.shard_rank; g++) own_lo += (uint32_t)s.xcnt[((size_t)g * s.n + r) * 2] & S_XC_COUNT;
-  const uint32_t own_cnt = (uint32_t)s.xcnt[((size_t)s.shard_rank * s.n + r) * 2] & S_XC_COUNT;
+  for (int g = 0; g < s.shard_rank; g++) own_lo += (uint32_t)s.xcnt[S_XC(s, g, r)] & S_XC_COUNT;
+  const uint32_t own_cnt = (uint32_t)s.xcnt[S_XC(s, s.shard_rank, r)] & S_XC_COUNT;
   // "me" (myPos's id, MP1Node.cpp:459-460,470) is the row's own column, or in the join ramp
   // the quirk's target column; only the rank owning it knows it (mecol is -1 elsewhere), and
   // only that rank resolves a draw there: it reports "me" as not fresh, which the acceptance
@@ -1796,11 +1801,11 @@ __global__ __launch_bounds__(256) void gm_s_draw(SState s, int t, int round, int
 // in_list 0: every row, statuses by row; 1 / 2: the rows of pending list 1 / 2, statuses by
 // list position. Rows left pending go to: out -1 -> GM_ERR_DRAWS (bounded rounds exhausted),
 // 0 -> the npending count (host-driven loop), 1 / 2 -> pending list 1 / 2 (next bounded round).
-__global__ __launch_bounds__(256) void gm_s_accept(SState s, int t, int D, int in_list, int out) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(256) void gm_s_accept(SState s, int t, int D, int in_list, int out, int r0, int r1) {
+  const int i = (in_list ? 0 : r0) + (int)(blockIdx.x * blockDim.x + threadIdx.x);
   if (in_list && i >= (int)min(*s.plist_cnt[in_list], (uint32_t)s.plist_cap[in_list])) return;
   const int r = in_list ? s.plist[in_list][i] : i;
-  if (r >= s.n || !s.pending[r]) return;
+  if (r >= (in_list ? s.n : r1) || !s.pending[r]) return;
   int32_t *acc = s.acc + (size_t)r * 8;
   int n = acc[0];
   const int numpot = acc[6];
@@ -1925,23 +1930,49 @@ __global__ __launch_bounds__(256) void gm_s_init(SState s, int warm, int t0, uin
 
 // ------------------------------------------------------------ launch wrappers
 // (template dispatch over the band width; called by gm_host.hip)
+// the band kernels of rows [r0, r1) (r0, r1 multiples of the rows per unit, or r1 = n)
 template <int B>
-static hipError_t launch_tick_b(const SState &s, int t, int drop_pct, hipStream_t st, hipEvent_t k0,
-                                hipEvent_t k1, bool pick) {
+static void launch_band_b(const SState &s, int t, int drop_pct, int r0, int r1, hipStream_t st) {
   constexpr int RPW = 64 / (B / S_COLS_PER_LANE);
-  const dim3 nblk((((s.n + RPW - 1) / RPW) + 3) / 4, s.nb);  // (units of a band / 4, bands)
+  const int u0 = r0 / RPW, u1 = (r1 + RPW - 1) / RPW;
+  if (u1 <= u0) return;
+  const dim3 nblk((u1 - u0 + 3) / 4, s.nb);  // (units of the chunk in a band / 4, bands)
+  if (drop_pct >= 0) {
+    hipLaunchKernelGGL((gm_s_band<B, true>), dim3(nblk), dim3(256), 0, st, s, t, drop_pct, u0, u1);
+  } else if (B == 1024 && !s.ramp && s.fb_list) {  // the fast path, then the units it handed back
+    hipLaunchKernelGGL((gm_s_band_fast<B == 1024 ? B : 1024>), dim3(nblk), dim3(256), 0, st, s, t, u0, u1);
+    hipLaunchKernelGGL((gm_s_band_listed<B == 1024 ? B : 1024>), dim3(S_FB_BLOCKS), dim3(256), 0, st, s, t, u0, u1);
+  } else {
+    hipLaunchKernelGGL((gm_s_band<B, false>), dim3(nblk), dim3(256), 0, st, s, t, drop_pct, u0, u1);
+  }
+}
+
+// the per-tick work before the band kernels: event counters, the S2 precompute
+hipError_t gm_launch_tick_prologue(const SState &s, int t, hipStream_t st) {
   // the event records of a tick (per-(row, band) slots + spill ring) stay readable until the next tick
   (void)hipMemsetAsync(s.ev_spill_cnt, 0, (1 + S_EV_STRIPES) * sizeof(uint32_t), st);
   hipLaunchKernelGGL(gm_s_mtgen, dim3((s.n + 255) / 256), dim3(256), 0, st, s, t);
-  if (k0) (void)hipEventRecord(k0, st);
-  if (drop_pct >= 0) {
-    hipLaunchKernelGGL((gm_s_band<B, true>), dim3(nblk), dim3(256), 0, st, s, t, drop_pct);
-  } else if (B == 1024 && !s.ramp && s.fb_list) {  // the fast path, then the units it handed back
-    hipLaunchKernelGGL((gm_s_band_fast<B == 1024 ? B : 1024>), dim3(nblk), dim3(256), 0, st, s, t);
-    hipLaunchKernelGGL((gm_s_band_listed<B == 1024 ? B : 1024>), dim3(S_FB_BLOCKS), dim3(256), 0, st, s, t);
-  } else {
-    hipLaunchKernelGGL((gm_s_band<B, false>), dim3(nblk), dim3(256), 0, st, s, t, drop_pct);
+  return hipGetLastError();
+}
+
+hipError_t gm_launch_band_rows(const SState &s, int t, int drop_pct, int r0, int r1, hipStream_t st) {
+  switch (s.band) {
+    case 64: launch_band_b<64>(s, t, drop_pct, r0, r1, st); break;
+    case 128: launch_band_b<128>(s, t, drop_pct, r0, r1, st); break;
+    case 256: launch_band_b<256>(s, t, drop_pct, r0, r1, st); break;
+    case 512: launch_band_b<512>(s, t, drop_pct, r0, r1, st); break;
+    case 1024: launch_band_b<1024>(s, t, drop_pct, r0, r1, st); break;
+    default: return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+template <int B>
+static hipError_t launch_tick_b(const SState &s, int t, int drop_pct, hipStream_t st, hipEvent_t k0,
+                                hipEvent_t k1, bool pick) {
+  (void)gm_launch_tick_prologue(s, t, st);
+  if (k0) (void)hipEventRecord(k0, st);
+  launch_band_b<B>(s, t, drop_pct, 0, s.n, st);
   if (k1) (void)hipEventRecord(k1, st);
   if (s.ramp) {
     hipLaunchKernelGGL(gm_s_selfcheck, dim3(16), dim3(256), 0, st, s);
@@ -1964,23 +1995,31 @@ hipError_t gm_launch_tick(const SState &s, int t, int drop_pct, hipStream_t st, 
   }
 }
 
-hipError_t gm_launch_draw(const SState &s, int t, int round, int D, int listed, hipStream_t st) {
-  const size_t smem = sizeof(uint32_t) * 4 * gm_draw_lds_words(s.wp, s.band);
-  const dim3 grid(((listed ? s.plist_cap[listed] : s.n) + 3) / 4), blk(256);
+// rows [r0, r1) (unlisted) or the pending list `listed`. Round 0 draws only the 16 precomputed
+// outputs: no lazy generator, so its waves take the chunk prefix's LDS alone.
+hipError_t gm_launch_draw(const SState &s, int t, int round, int D, int listed, hipStream_t st, int r0, int r1) {
+  if (r1 < 0) r1 = s.n;
+  const size_t words = round == 0 ? (size_t)gm_draw_chunks(s.wp, s.band) + 1 : gm_draw_lds_words(s.wp, s.band);
+  const size_t smem = sizeof(uint32_t) * 4 * words;
+  const int rows = listed ? s.plist_cap[listed] : r1 - r0;
+  if (rows <= 0) return hipSuccess;
+  const dim3 grid((rows + 3) / 4), blk(256);
   switch (s.band) {
-    case 64: hipLaunchKernelGGL(gm_s_draw<64>, grid, blk, smem, st, s, t, round, D, listed); break;
-    case 128: hipLaunchKernelGGL(gm_s_draw<128>, grid, blk, smem, st, s, t, round, D, listed); break;
-    case 256: hipLaunchKernelGGL(gm_s_draw<256>, grid, blk, smem, st, s, t, round, D, listed); break;
-    case 512: hipLaunchKernelGGL(gm_s_draw<512>, grid, blk, smem, st, s, t, round, D, listed); break;
-    case 1024: hipLaunchKernelGGL(gm_s_draw<1024>, grid, blk, smem, st, s, t, round, D, listed); break;
+    case 64: hipLaunchKernelGGL(gm_s_draw<64>, grid, blk, smem, st, s, t, round, D, listed, r0, r1); break;
+    case 128: hipLaunchKernelGGL(gm_s_draw<128>, grid, blk, smem, st, s, t, round, D, listed, r0, r1); break;
+    case 256: hipLaunchKernelGGL(gm_s_draw<256>, grid, blk, smem, st, s, t, round, D, listed, r0, r1); break;
+    case 512: hipLaunchKernelGGL(gm_s_draw<512>, grid, blk, smem, st, s, t, round, D, listed, r0, r1); break;
+    case 1024: hipLaunchKernelGGL(gm_s_draw<1024>, grid, blk, smem, st, s, t, round, D, listed, r0, r1); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
 
-hipError_t gm_launch_accept(const SState &s, int t, int D, int in_list, int out, hipStream_t st) {
-  const int rows = in_list ? s.plist_cap[in_list] : s.n;
-  hipLaunchKernelGGL(gm_s_accept, dim3((rows + 255) / 256), dim3(256), 0, st, s, t, D, in_list, out);
+hipError_t gm_launch_accept(const SState &s, int t, int D, int in_list, int out, hipStream_t st, int r0, int r1) {
+  if (r1 < 0) r1 = s.n;
+  const int rows = in_list ? s.plist_cap[in_list] : r1 - r0;
+  if (rows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(gm_s_accept, dim3((rows + 255) / 256), dim3(256), 0, st, s, t, D, in_list, out, r0, r1);
   return hipGetLastError();
 }
 

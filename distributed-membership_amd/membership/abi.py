@@ -39,7 +39,7 @@ EXPORTS = ["gm_parse_conf", "gm_create", "gm_destroy", "gm_tick", "gm_sync", "gm
            "gm_comm_unique_id", "gm_comm_init", "gm_shard_layout", "gm_shard_merge", "gm_shard_draw",
            "gm_shard_accept", "gm_shard_end_tick", "gm_shard_loopback", "gm_partial_loopback_tick",
            "gm_shard_exchange_bytes", "gm_keep_events", "gm_event_totals", "gm_read_views", "gm_shard_stub",
-           "gm_msgcount_record", "gm_comm_info", "gm_shard_export", "gm_shard_import", "gm_pool_info"]
+           "gm_msgcount_record", "gm_comm_info", "gm_shard_export", "gm_shard_import", "gm_pool_info", "gm_shard_loopback_tick"]
 
 _lib = None
 
@@ -86,7 +86,7 @@ def load_library():
         "gm_shard_import": [ctypes.c_void_p, i32, i32, ctypes.c_void_p, sz],
         "gm_shard_layout": [ctypes.c_void_p, P(i32), P(i32)],
         "gm_shard_loopback": [P(ctypes.c_void_p), i32, i32, i32],
-        "gm_partial_loopback_tick": [P(ctypes.c_void_p), i32],
+        "gm_partial_loopback_tick": [P(ctypes.c_void_p), i32], "gm_shard_loopback_tick": [P(ctypes.c_void_p), i32],
         "gm_shard_exchange_bytes": [ctypes.c_void_p, P(ctypes.c_int64)],
         "gm_shard_merge": [ctypes.c_void_p], "gm_shard_draw": [ctypes.c_void_p, i32, i32],
         "gm_shard_accept": [ctypes.c_void_p, i32, P(i32)], "gm_shard_end_tick": [ctypes.c_void_p],
@@ -362,6 +362,14 @@ def shard_loopback(sims, what, d=0):
     rc = load_library().gm_shard_loopback(arr, len(sims), what, d)
     if rc:
         raise GmError(rc, "gm_shard_loopback")
+
+
+def shard_loopback_tick(sims):
+    """One column-shard tick of G contexts on one device in the pipelined tick's chunk order."""
+    arr = (ctypes.c_void_p * len(sims))(*[s.h for s in sims])
+    rc = load_library().gm_shard_loopback_tick(arr, len(sims))
+    if rc:
+        raise GmError(rc, "gm_shard_loopback_tick")
 
 
 def partial_loopback_tick(sims):

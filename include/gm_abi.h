@@ -239,6 +239,11 @@ int gm_shard_end_tick(gm_ctx *ctx);
 /* what = 0: all-gather the per-row counts; what = 1: MAX-allreduce the first n*D draws;
  * what = 2 (msgcount recording, after what = 0): SUM-allreduce this tick's fresh counts */
 int gm_shard_loopback(gm_ctx **ctxs, int32_t G, int32_t what, int32_t D);
+/* One whole tick of G column-shard contexts on one device in the chunk order of the pipelined
+ * RCCL tick (per exchange row chunk: all-gather of the counts, round-0 draws, MAX-reduce, acceptance;
+ * then the bounded rounds 1, 2), the collectives by device copies. Not for the join ramp or msgcount
+ * recording (GM_EINVAL); rows the bounded rounds cannot take return GM_ERANGE (use the phase API). */
+int gm_shard_loopback_tick(gm_ctx **ctxs, int32_t G);
 /* Host-collective hook: the exchange buffers of ONE column-shard context as host arrays, so a
  * host-side collective (e.g. gloo between processes) can stand in for RCCL or gm_shard_loopback
  * between the phase calls. what = 0: export this rank's per-row counts int32[n][2], import all

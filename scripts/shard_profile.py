@@ -80,7 +80,7 @@ def main():
     p.add_argument("--shards", type=int, default=8)
     p.add_argument("--rank", type=int, default=3)
     p.add_argument("--prologue", type=int, default=25)
-    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--steps", type=int, default=20)
     p.add_argument("--sb", action="store_true", help="one S-B shard alone on the device (gm_shard_stub)")
     a = p.parse_args()
     load_library()

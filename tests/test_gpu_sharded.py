@@ -76,6 +76,43 @@ def test_shards_match_fused_kernel(n, world, drop, warm):
         assert st["lists"] == ref.tick_stats()["lists"]
 
 
+@pytest.mark.parametrize("n,world,drop,chunks", [(2048, 8, 10, 4), (1100, 3, 20, 3), (600, 2, 0, 7), (4099, 4, 5, 2)])
+def test_pipelined_shards_match_fused_kernel(n, world, drop, chunks, monkeypatch):
+    """The chunk order of the pipelined RCCL tick (per exchange row chunk: all-gather of the
+    counts, round-0 draws, MAX-reduce of their statuses, acceptance -- on the comm stream while
+    later chunks merge; then the bounded rounds) with G shard contexts on one device
+    (gm_shard_loopback_tick, collectives by device copies): tick for tick equal to the fused
+    kernel, and to the phase-API loopback shards. GM_SCHUNKS sets the exchange chunks (R rows,
+    a power of two; the last chunk shorter)."""
+    from membership.abi import shard_loopback_tick
+    monkeypatch.setenv("GM_SCHUNKS", str(chunks))
+    kw = dict(rd_seed=7, drop_pct=drop, drop_from=3, drop_to=25, drop_seed=42, init_mode=1, init_t0=6, init_seed=5)
+    ref = Simulator(n, GM_MODE_SCALED, **kw)
+    shards = [Simulator(n, GM_MODE_SCALED, shard_rank=g, shard_count=world, **kw) for g in range(world)]
+    phase = [Simulator(n, GM_MODE_SCALED, shard_rank=g, shard_count=world, **kw) for g in range(world)]
+    monkeypatch.delenv("GM_SCHUNKS")
+    owners = np.zeros(n, dtype=int)
+    for g, s in enumerate(shards):
+        c0, w = s.shard_layout()
+        owners[c0:c0 + w] = g
+    crash = crash_set(n, max(2, n // 64), 42)
+    for _ in range(34):
+        t = ref.time
+        ref.tick()
+        shard_loopback_tick(shards)
+        loopback_tick(phase)
+        if t == 8:
+            for s in [ref] + shards + phase:
+                s.set_failed(crash)
+        ev = sorted(ref.drain_events())
+        assert sorted(e for s in shards for e in s.drain_events()) == ev, f"events differ at tick {t}"
+        assert sorted(e for s in phase for e in s.drain_events()) == ev, f"phase-API events differ at tick {t}"
+        assert_same_state(shards, owners, ref, f"at tick {t}")
+    assert_same_state(phase, owners, ref, "(phase API) at the end")
+    for s in shards:
+        assert s.tick_stats()["err"] == 0
+
+
 @pytest.mark.parametrize("n,drop,ncrash,rounds", [(777, 0, 12, "auto"), (2048, 20, 32, "auto"), (777, 0, 12, "sync"),
                                                   (777, 0, 388, "bounded"), (777, 0, 388, "overflow")])
 def test_rccl_single_rank_matches_fused_kernel(n, drop, ncrash, rounds, monkeypatch):
