@@ -32,6 +32,7 @@ hipError_t gm_launch_tick(const SState &s, int t, int drop_pct, hipStream_t st, 
                           bool pick);
 hipError_t gm_launch_tick_prologue(const SState &s, int t, hipStream_t st);
 hipError_t gm_launch_band_rows(const SState &s, int t, int drop_pct, int r0, int r1, hipStream_t st);
+hipError_t gm_launch_xrows(const SState &s, int r0, int r1, hipStream_t st);
 hipError_t gm_launch_draw(const SState &s, int t, int round, int D, int listed, hipStream_t st, int r0 = 0, int r1 = -1);
 hipError_t gm_launch_accept(const SState &s, int t, int D, int in_list, int out, hipStream_t st, int r0 = 0,
                             int r1 = -1);
@@ -1762,6 +1763,7 @@ extern "C" int gm_shard_merge(gm_ctx *c) {
   hipEvent_t k0 = nullptr, k1 = nullptr;
   if (c->timing) TRY(timing_slot(c, &k0, &k1));
   HIPCHECK(gm_launch_tick(c->s, c->t, drop ? c->cfg.drop_pct : -1, c->stream, k0, k1, false));
+  HIPCHECK(gm_launch_xrows(c->s, 0, c->n, c->stream));  // this shard's row totals for the all-gather
   // msgcount: this shard's fresh counts (its columns), SUM-allreduced before the draws
   if (mc_on(c, c->t)) HIPCHECK(gm_launch_msgcount(c->s, c->t, drop, 0, c->stream));
   return GM_OK;
@@ -1898,6 +1900,7 @@ extern "C" int gm_shard_loopback_tick(gm_ctx **ctxs, int32_t G) {
   };
   for (int ch = 0; ch < s0.xk; ch++) {
     const int r0 = ch << s0.xlog, r1 = r0 + xchunk_rows(s0, ch);
+    for (int g = 0; g < G; g++) HIPCHECK(gm_launch_xrows(ctxs[g]->s, r0, r1, ls));
     for (int dst = 0; dst < G; dst++)  // the chunk's all-gather
       for (int src = 0; src < G; src++)
         if (src != dst) {
@@ -2102,6 +2105,7 @@ static int tick_sharded(gm_ctx *c) {
     for (int ch = 0; ch < s.xk; ch++) {
       const int r0 = ch << s.xlog, r1 = r0 + xchunk_rows(s, ch);
       HIPCHECK(hipStreamWaitEvent(cs, c->p_chev[ch], 0));
+      HIPCHECK(gm_launch_xrows(s, r0, r1, cs));
       TRY(xcnt_allgather(c, ch, cs));
       HIPCHECK(gm_launch_draw(s, t, 0, GM_D_FIRST, 0, cs, r0, r1));
       if (!s.stub)

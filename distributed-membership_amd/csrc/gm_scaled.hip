@@ -584,11 +584,7 @@ __device__ __forceinline__ void unit_records(const SState &s, int t, const UnitI
     const uint32_t bc = (uint32_t)(pf & 0xFFFF) | ((uint32_t)(pf >> 16) << 11) | ((uint32_t)min(tot, 1023) << 22);
     s.brec[slab + r] = live ? make_uint4((uint32_t)piece, (uint32_t)(piece >> 32), bc, eb_out)
                             : make_uint4(0u, 0u, 0u, eb_out);
-    // column shard: this shard's row totals (present, numfailed) for the all-gather,
-    // accumulated as one packed 64-bit add per (row, band) into the zeroed slot
-    if (s.sharded && live)
-      atomicAdd((unsigned long long *)(s.xcnt + S_XC(s, s.shard_rank, r)),
-                (unsigned long long)(pf & 0xFFFF) | ((unsigned long long)(pf >> 16) << 32));
+    // (a column shard's row totals for the all-gather are summed from these records by gm_s_xrows)
   }
 }
 
@@ -1342,16 +1338,23 @@ __host__ __device__ __forceinline__ size_t gm_draw_lds_words(int wp, int band) {
 
 // Row r of this shard: numfailed (band counts), size and the chunk prefix
 // pre[c] = present cells in chunks [0, c) (pre[nc] = size), from the chunk counts.
+// the lane's first (band, row) record of row r (all of them when nb <= 64), as gm_row_totals reads it
+__device__ __forceinline__ uint4 gm_row_rec0(const SState &s, int r, int lane) {
+  const int perb = (s.nb + 63) >> 6, b0 = lane * perb;
+  return b0 < s.nb ? s.brec[(size_t)b0 * s.n + r] : make_uint4(0u, 0u, 0u, 0u);
+}
+
+// pre0: the lane's first record, when the caller loaded it already (gm_row_rec0)
 template <int B>
 __device__ __forceinline__ void gm_row_totals(const SState &s, int r, int lane, uint32_t *pre, uint32_t &size,
-                                              uint32_t &nfail) {
+                                              uint32_t &nfail, const uint4 *pre0 = nullptr) {
   constexpr int CPB = B / S_CHUNK(B);  // rank-select chunks per band
   const int nb = s.nb, perb = (nb + 63) >> 6;
   const int b0 = min(nb, lane * perb), b1 = min(nb, b0 + perb);
   uint32_t fs = 0, ps = 0;
   uint4 rec0 = make_uint4(0u, 0u, 0u, 0u);  // the lane's first (band, row) record (all of them when nb <= 64)
   for (int b = b0; b < b1; b++) {
-    const uint4 rc = s.brec[(size_t)b * s.n + r];
+    const uint4 rc = (b == b0 && pre0) ? *pre0 : s.brec[(size_t)b * s.n + r];
     if (b == b0) rec0 = rc;
     fs += S_BC_FAIL(rc.z);
     ps += S_BC_PRES(rc.z);
@@ -1657,6 +1660,29 @@ hipError_t gm_launch_msgcount(const SState &s, int t, bool dropped, int phase, h
 // Phase A (gm_s_band, sharded): merge / sweep of this shard's columns; each row's
 // shard totals (present, numfailed) accumulate into xcnt[rank] for the all-gather.
 
+// Phase A': this shard's per-row totals (present, numfailed) for the all-gather, summed over the
+// row's band records (thread per row of [r0, r1): a wave reads 1 KB per band, coalesced) -- not a
+// device-scope atomic per (row, band) inside the band kernel. The ramp's self-append flag, set by
+// the band kernel, is kept.
+__global__ __launch_bounds__(256) void gm_s_xrows(SState s, int r0, int r1) {
+  const int r = r0 + (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (r >= r1) return;
+  uint32_t p = 0, f = 0;
+  for (int b = 0; b < s.nb; b++) {
+    const uint32_t z = s.brec[(size_t)b * s.n + r].z;
+    p += S_BC_PRES(z);
+    f += S_BC_FAIL(z);
+  }
+  int32_t *x = s.xcnt + S_XC(s, s.shard_rank, r);
+  x[0] = (int32_t)((uint32_t)x[0] & S_XC_SELFAPP) | (int32_t)p;
+  x[1] = (int32_t)f;
+}
+
+hipError_t gm_launch_xrows(const SState &s, int r0, int r1, hipStream_t st) {
+  if (r1 > r0) hipLaunchKernelGGL(gm_s_xrows, dim3((r1 - r0 + 255) / 256), dim3(256), 0, st, s, r0, r1);
+  return hipGetLastError();
+}
+
 // Phase B: every rank replays every pending row's S2 stream (round 0: outputs
 // [0, 16) from gm_s_mtgen; round q >= 1: [16 + 64(q-1), 16 + 64q) from the lazy
 // generator) and resolves the draws whose rank lands in its own columns.
@@ -1677,20 +1703,29 @@ __global__ __launch_bounds__(256) void gm_s_draw(SState s, int t, int round, int
   uint32_t *mts = pre + gm_draw_chunks(s.wp, B) + 1;
   const int G = s.shard_count;
   int32_t *acc = s.acc + (size_t)r * 8;
+  // round 0: every load of the row issues at once -- crash flag, delivered-list count, the ranks'
+  // counts, the 16 S2 outputs and this shard's first band record (for the chunk prefix; ~88 % of the
+  // rows resolve a draw here) -- one memory round trip before the chunk search, not four
+  uint32_t raw0 = 0;
+  uint4 rec0 = make_uint4(0u, 0u, 0u, 0u);
   if (round == 0) {
-    const bool live = !s.failed[r] && s_ingroup(s.ramp, s.intro_until, r, t);  // else untouched
-    if (lane == 0) {  // lists delivered this tick; consumed by gm_s_band, the append target of tick t+2
-      const int par = t & 1;
-      s.rowstat[(size_t)r * 4] = live ? s.inbox_cnt[par][r] : 0;
-      s.inbox_cnt[par][r] = 0;
-    }
+    const int par = t & 1;
+    int failed = s.failed[r], kin = s.inbox_cnt[par][r];
     int size = 0, nf = 0;
     bool selfapp = false;
+    raw0 = lane < S_MT_RAW ? s.mtraw[(size_t)r * S_MT_RAW + lane] : 0u;
+    rec0 = gm_row_rec0(s, r, lane);
     for (int g = 0; g < G; g++) {
       const int pr = s.xcnt[S_XC(s, g, r)];
       size += pr & S_XC_COUNT;
       selfapp |= (pr & S_XC_SELFAPP) != 0;
       nf += s.xcnt[S_XC(s, g, r) + 1];
+    }
+    asm volatile("" : "+v"(raw0), "+v"(rec0.x), "+v"(rec0.y), "+v"(rec0.z), "+v"(rec0.w));
+    const bool live = !failed && s_ingroup(s.ramp, s.intro_until, r, t);  // else untouched
+    if (lane == 0) {  // lists delivered this tick; consumed by gm_s_band, the append target of tick t+2
+      s.rowstat[(size_t)r * 4] = live ? kin : 0;
+      s.inbox_cnt[par][r] = 0;
     }
     if (selfapp && lane == 0) {
       // join ramp: row r appended its own entry (updateMyPos found no larger id in its start
@@ -1752,7 +1787,7 @@ __global__ __launch_bounds__(256) void gm_s_draw(SState s, int t, int round, int
     const int cnt = min(64, D - d0);
     uint32_t raw = 0;
     if (round == 0) {
-      if (lane < cnt) raw = s.mtraw[(size_t)r * S_MT_RAW + d0 + lane];
+      raw = raw0;  // D = 16: the one batch
     } else {  // round q >= 1 continues after 16 + 64 (q - 1) outputs (round 2 of the bounded tick: after 80)
       raw = gm_mt_batch(mt, mts, gm_rd_seed(s.rd_seed, t, r + 1), d0 == 0, S_MT_RAW + 64 * (rr - 1) + d0, cnt,
                         lane);
@@ -1765,7 +1800,7 @@ __global__ __launch_bounds__(256) void gm_s_draw(SState s, int t, int round, int
     uint64_t m = __ballot(mine);
     if (m && !have_pre) {
       uint32_t osz, onf;
-      gm_row_totals<B>(s, r, lane, pre, osz, onf);
+      gm_row_totals<B>(s, r, lane, pre, osz, onf, round == 0 ? &rec0 : nullptr);
       have_pre = true;
     }
     while (m) {
