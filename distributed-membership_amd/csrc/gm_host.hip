@@ -1569,6 +1569,21 @@ extern "C" int gm_dump_tables(gm_ctx *c, char *buf, size_t cap, size_t *len) {
   return GM_OK;
 }
 
+extern "C" int gm_read_targets(gm_ctx *c, int32_t *targets, int32_t *counts) {
+  if (!c || !targets || !counts) return GM_EINVAL;
+  if (c->cfg.mode != GM_MODE_SCALED) return GM_EUNSUPPORTED;
+  TRY(draw_settle(c));
+  const size_t n = (size_t)c->n;
+  std::vector<int32_t> st(n * 4);
+  HIPCHECK(ctx_memcpy(c, targets, c->s.targets, sizeof(int32_t) * n * GM_FANOUT, hipMemcpyDeviceToHost));
+  HIPCHECK(ctx_memcpy(c, st.data(), c->s.rowstat, sizeof(int32_t) * n * 4, hipMemcpyDeviceToHost));
+  for (size_t r = 0; r < n; r++) {
+    counts[r] = st[r * 4 + 3];
+    for (int q = counts[r]; q < GM_FANOUT; q++) targets[r * GM_FANOUT + q] = 0;
+  }
+  return check_err(c);
+}
+
 extern "C" int gm_tick_stats(gm_ctx *c, int64_t stats[4]) {
   if (!c || !stats) return GM_EINVAL;
   if (c->cfg.mode == GM_MODE_FAITHFUL) return GM_EUNSUPPORTED;

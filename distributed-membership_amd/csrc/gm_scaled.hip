@@ -1683,6 +1683,162 @@ hipError_t gm_launch_xrows(const SState &s, int r0, int r1, hipStream_t st) {
   return hipGetLastError();
 }
 
+// Phase B, round 0, four rows per wave (16 lanes per row: lane q of a row holds S2 output q, the
+// counts of rank q, this shard's bands [q * perb, +perb)). Same results as gm_s_draw's round 0 with
+// a fraction of its instructions: per row the 16 Lemire draws, the rank range of this shard's
+// entries, a band prefix in LDS, and for each draw landing in this shard's columns a 16-ary search
+// of the bands, the band record's 8 chunk counts and one 128-cell chunk read by the row's 16 lanes
+// (8 bytes each, SWAR counts, a DPP prefix). Not for the join ramp (gm_s_draw handles it); needs
+// G <= 16 ranks and B = 1024 (8 rank-select chunks per band).
+__device__ __forceinline__ int row16_scan(int v) {  // inclusive scan within each 16-lane DPP row
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);  // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);  // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);  // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);  // row_shr:8
+  return v;
+}
+__device__ __forceinline__ int row16_bcast(int v, int g, int q) { return __shfl(v, 16 * g + q, 64); }
+__device__ __forceinline__ uint32_t row16_bits(uint64_t bal, int g) { return (uint32_t)(bal >> (16 * g)) & 0xFFFFu; }
+
+template <int B>
+__global__ __launch_bounds__(256) void gm_s_draw0(SState s, int t, int r0, int r1) {
+  static_assert(B == 1024, "8 rank-select chunks of 128 columns per band");
+  extern __shared__ __align__(16) uint32_t p_smem[];
+  const int lane = threadIdx.x & 63, g = lane >> 4, q = lane & 15;
+  const int slot = (int)(threadIdx.x >> 4);  // row slot of the workgroup (0..15)
+  const int r = r0 + (int)blockIdx.x * 16 + slot;
+  const bool valid = r < r1;
+  const int rc = valid ? r : r1 - 1;
+  const int G = s.shard_count, nb = s.nb, perb = (nb + 15) >> 4, par = t & 1;
+  uint32_t *bpre = p_smem + (size_t)slot * (nb + 1);  // band prefix of this shard's present cells
+  // every load of the row at once
+  const int failed = s.failed[rc], kin = s.inbox_cnt[par][rc];
+  const uint32_t raw = s.mtraw[(size_t)rc * S_MT_RAW + q];
+  const int xp = q < G ? s.xcnt[S_XC(s, q, rc)] & S_XC_COUNT : 0;
+  const int xf = q < G ? s.xcnt[S_XC(s, q, rc) + 1] : 0;
+  uint32_t bsum = 0;
+  for (int k = 0; k < perb; k++) {
+    const int b = q * perb + k;
+    if (b < nb) bsum += S_BC_PRES(s.brec[(size_t)b * s.n + rc].z);
+  }
+  // row sums over the 16 lanes: size, numfailed, this shard's rank range [own_lo, own_lo + own_cnt)
+  const int xpi = row16_scan(xp), xfi = row16_scan(xf), bi = row16_scan((int)bsum);
+  const uint32_t size = (uint32_t)row16_bcast(xpi, g, 15);
+  const int nf = row16_bcast(xfi, g, 15);
+  const uint32_t own_lo = s.shard_rank > 0 ? (uint32_t)row16_bcast(xpi, g, s.shard_rank - 1) : 0u;
+  const uint32_t own_cnt = (uint32_t)row16_bcast(xp, g, s.shard_rank);
+  const int numpot = (int)size - 1 - nf;
+  const bool live = valid && !failed;
+  const bool pend = live && numpot > 0;
+  if (valid && q == 0) {
+    int32_t *acc = s.acc + (size_t)r * 8;
+    acc[0] = 0;
+    acc[6] = numpot;
+    acc[7] = (int)size;
+    s.pending[r] = pend;
+    int32_t *stat = s.rowstat + (size_t)r * 4;
+    stat[0] = live ? kin : 0;  // lists delivered this tick; consumed by gm_s_band, the append target of tick t+2
+    stat[1] = live ? (int)size : 0;
+    stat[2] = live ? nf : 0;
+    stat[3] = 0;
+    s.inbox_cnt[par][r] = 0;
+  }
+  // band prefix (exclusive) of this shard's row, in LDS
+  {
+    uint32_t a = (uint32_t)bi - bsum;
+    for (int k = 0; k < perb; k++) {
+      const int b = q * perb + k;
+      if (b < nb) {
+        bpre[b] = a;
+        a += S_BC_PRES(s.brec[(size_t)b * s.n + rc].z);
+      }
+    }
+    if (q == 15) bpre[nb] = (uint32_t)bi;
+  }
+  // Lemire on output q (uniform_int_distribution, MP1Node.cpp:466): rejection threshold 2^32 mod size
+  const uint32_t sz = pend ? size : 1u;
+  const uint32_t thr = (0u - sz) % sz;
+  const uint64_t prod = (uint64_t)raw * sz;
+  const bool ok = pend && (uint32_t)prod >= thr;
+  const uint32_t ix = (uint32_t)(prod >> 32);
+  const bool mine = ok && ix >= own_lo && ix < own_lo + own_cnt;
+  int32_t *st = s.status + (size_t)rc * S_MT_RAW;  // round 0: D = the 16 precomputed outputs
+  if (pend && !mine) st[q] = ok ? (s.stub ? (int32_t)((ix % (uint32_t)s.n) << 1) | 1 : -1) : -2;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  uint32_t mm = row16_bits(__ballot(mine), g);  // this row's draws to resolve here
+  const uint64_t any = __ballot(mm != 0);
+  if (!any) return;
+  const int me = r;
+  while (__ballot(mm != 0)) {
+    const bool act = mm != 0;
+    const int d = act ? __builtin_ctz(mm) : 0;
+    mm &= mm - 1;
+    const uint32_t x = (uint32_t)row16_bcast((int)ix, g, d) - own_lo;  // rank among this shard's entries
+    // 16-ary search: the band b with bpre[b] <= x < bpre[b + 1]
+    int lo = 0, span = nb;
+    while (__ballot(act && span > 1)) {
+      const int step = (span + 15) >> 4;
+      const int idx = lo + q * step;
+      const bool le = act && q * step < span && bpre[idx] <= x;
+      const int c = __builtin_popcount(row16_bits(__ballot(le), g));
+      if (act && span > 1) {
+        lo += (max(c, 1) - 1) * step;
+        span = min(step, span - (max(c, 1) - 1) * step);
+      }
+    }
+    const int band = lo;
+    uint32_t rem = act ? x - bpre[band] : 0u;  // rank inside the band
+    // the band record's 8 chunk counts, then the chunk (128 cells: 8 bytes per lane of the row)
+    const uint4 rec = act ? s.brec[(size_t)band * s.n + rc] : make_uint4(0u, 0u, 0u, 0u);
+    const uint64_t cc = (uint64_t)rec.x | ((uint64_t)rec.y << 32);
+    int ch = 0;
+#pragma unroll
+    for (int k = 0; k < 7; k++) {
+      const uint32_t c8 = (uint32_t)(cc >> (8 * ch)) & 0xFFu;
+      if (rem >= c8 && ch == k) {
+        rem -= c8;
+        ch++;
+      }
+    }
+    uint2 w = make_uint2(0u, 0u);
+    if (act) w = *(const uint2 *)(s.table + ((size_t)band * s.n + rc) * B + ch * 128 + q * 8);
+    // present (non-zero) bytes of the lane's 8 cells
+    auto nzb = [](uint32_t v) { return (v | (v >> 1) | (v >> 2) | (v >> 3) | (v >> 4) | (v >> 5) | (v >> 6) | (v >> 7)) & 0x01010101u; };
+    const uint32_t m0 = nzb(w.x), m1 = nzb(w.y);
+    const int cnt = __builtin_popcount(m0) + __builtin_popcount(m1);
+    const int incl = row16_scan(cnt);
+    const int excl = incl - cnt;
+    if (act && (int)rem >= excl && (int)rem < incl) {  // the holder: the (rem - excl)-th present cell of its 8
+      int need = (int)rem - excl, pos = 0;
+      uint32_t byte = 0;
+#pragma unroll
+      for (int v = 0; v < 8; v++) {
+        const uint32_t bv = ((v < 4 ? w.x : w.y) >> (8 * (v & 3))) & 0xFFu;
+        if (bv != 0) {
+          if (need == 0) { pos = v; byte = bv; }
+          need--;
+        }
+      }
+      const int col = band * B + ch * 128 + q * 8 + pos;  // shard-local column
+      const bool fresh = s_is_esc(byte) ? esc_fresh(s, rc, col) : S_AGE(s_widen(byte)) < GM_TFAIL;
+      st[d] = ((s.c0 + col) << 1) | (int32_t)(fresh && s.c0 + col != me);
+    }
+  }
+}
+
+hipError_t gm_launch_draw0(const SState &s, int t, int r0, int r1, hipStream_t st) {
+  if (r1 <= r0) return hipSuccess;
+  const size_t smem = sizeof(uint32_t) * 16 * (size_t)(s.nb + 1);
+  hipLaunchKernelGGL(gm_s_draw0<1024>, dim3((r1 - r0 + 15) / 16), dim3(256), smem, st, s, t, r0, r1);
+  return hipGetLastError();
+}
+// true when gm_s_draw0 applies: B = 1024, no join ramp, <= 16 ranks, the band prefix fits LDS
+bool gm_draw0_ok(const SState &s) {
+  return s.band == 1024 && !s.ramp && s.shard_count <= 16 && sizeof(uint32_t) * 16 * (size_t)(s.nb + 1) <= 65536;
+}
+
 // Phase B: every rank replays every pending row's S2 stream (round 0: outputs
 // [0, 16) from gm_s_mtgen; round q >= 1: [16 + 64(q-1), 16 + 64q) from the lazy
 // generator) and resolves the draws whose rank lands in its own columns.
@@ -2034,6 +2190,8 @@ hipError_t gm_launch_tick(const SState &s, int t, int drop_pct, hipStream_t st, 
 // outputs: no lazy generator, so its waves take the chunk prefix's LDS alone.
 hipError_t gm_launch_draw(const SState &s, int t, int round, int D, int listed, hipStream_t st, int r0, int r1) {
   if (r1 < 0) r1 = s.n;
+  if (round == 0 && !listed && D == S_MT_RAW && gm_draw0_ok(s) && !(getenv("GM_DRAW0") && !atoi(getenv("GM_DRAW0"))))
+    return gm_launch_draw0(s, t, r0, r1, st);  // four rows per wave
   const size_t words = round == 0 ? (size_t)gm_draw_chunks(s.wp, s.band) + 1 : gm_draw_lds_words(s.wp, s.band);
   const size_t smem = sizeof(uint32_t) * 4 * words;
   const int rows = listed ? s.plist_cap[listed] : r1 - r0;

@@ -39,7 +39,7 @@ EXPORTS = ["gm_parse_conf", "gm_create", "gm_destroy", "gm_tick", "gm_sync", "gm
            "gm_comm_unique_id", "gm_comm_init", "gm_shard_layout", "gm_shard_merge", "gm_shard_draw",
            "gm_shard_accept", "gm_shard_end_tick", "gm_shard_loopback", "gm_partial_loopback_tick",
            "gm_shard_exchange_bytes", "gm_keep_events", "gm_event_totals", "gm_read_views", "gm_shard_stub",
-           "gm_msgcount_record", "gm_comm_info", "gm_shard_export", "gm_shard_import", "gm_pool_info", "gm_shard_loopback_tick"]
+           "gm_msgcount_record", "gm_comm_info", "gm_shard_export", "gm_shard_import", "gm_pool_info", "gm_shard_loopback_tick", "gm_read_targets"]
 
 _lib = None
 
@@ -74,7 +74,7 @@ def load_library():
         "gm_msgcount_record": [ctypes.c_void_p, i32],
         "gm_read_row": [ctypes.c_void_p, i32, i32, i32, P(i32), P(i32)],
         "gm_read_table": [ctypes.c_void_p, i32, i32, P(i32), P(i32)],
-        "gm_read_nodes": [ctypes.c_void_p, P(i32)],
+        "gm_read_nodes": [ctypes.c_void_p, P(i32)], "gm_read_targets": [ctypes.c_void_p, P(i32), P(i32)],
         "gm_dump_tables": [ctypes.c_void_p, ctypes.c_char_p, sz, P(sz)],
         "gm_tick_stats": [ctypes.c_void_p, P(ctypes.c_int64)], "gm_pool_info": [ctypes.c_void_p, P(ctypes.c_int64)],
         "gm_set_timing": [ctypes.c_void_p, i32], "gm_last_kernel_ms": [ctypes.c_void_p, P(ctypes.c_float)],
@@ -267,6 +267,13 @@ class Simulator:
         st = np.zeros((rows, 4), dtype=np.int32)
         self._call("gm_read_nodes", self.h, _ptr(st))
         return st
+
+    def read_targets(self):
+        """SCALED: (targets int32 [n][5], counts int32 [n]) of the last tick (gm_read_targets)"""
+        tg = np.zeros((self.n, 5), dtype=np.int32)
+        cnt = np.zeros(self.n, dtype=np.int32)
+        self._call("gm_read_targets", self.h, _ptr(tg), _ptr(cnt))
+        return tg, cnt
 
     def dump_tables(self):
         n = ctypes.c_size_t()

@@ -196,6 +196,10 @@ int gm_read_table(gm_ctx *ctx, int32_t r0, int32_t count, int32_t *hb, int32_t *
 int gm_read_views(gm_ctx *ctx, int32_t r0, int32_t count, uint64_t *out);
 /* node state: inited, inGroup, bFailed, heartbeat counter (4 int32 per node) */
 int gm_read_nodes(gm_ctx *ctx, int32_t *state4);
+/* SCALED: the gossip targets every node drew in the last tick (the gossipnodes of nodeLoopOps,
+ * MP1Node.cpp:449-489, as node indices; [n][5], unused slots 0) and their counts [n] -- with the
+ * tables and node state, the whole state between two ticks */
+int gm_read_targets(gm_ctx *ctx, int32_t *targets, int32_t *counts);
 /* Render the membership lists of every node in the parity dump format
  * ("t i inited inGroup bFailed heartbeat n id:hb:ts ...\n" per node). */
 int gm_dump_tables(gm_ctx *ctx, char *buf, size_t cap, size_t *len);

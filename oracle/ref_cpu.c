@@ -791,6 +791,57 @@ int oc_row(oc_ctx *c, int r, int32_t *hb, int32_t *ts) {
   return 0;
 }
 
+/* SCALED: the gossip targets every node drew in the last tick (row-major [n][FANOUT], node indices)
+ * and their counts -- the sends the next tick delivers */
+int oc_targets(const oc_ctx *c, int32_t *tgt, int32_t *ntgt) {
+  if (!is_scaled(c)) return -1;
+  memcpy(tgt, c->tgt, sizeof(int32_t) * (size_t)c->n * FANOUT);
+  memcpy(ntgt, c->ntgt, sizeof(int32_t) * (size_t)c->n);
+  return 0;
+}
+
+/* SCALED (converged start, no join ramp): replace the whole state between two ticks by one read
+ * from elsewhere -- the oracle's own oc_row / oc_node / oc_targets, or the HIP path's
+ * gm_read_table / gm_read_nodes / gm_read_targets, which are bit-exact to them: every row's
+ * members (hb / ts per column, -1 = absent; sorted by id as every tick leaves them), heartbeat
+ * counters and crash flags, and the last tick's gossip targets. The payload each target receives
+ * next (the sender's fresh entries at t - 1, node_loop_ops' snapshot) follows from the rows. `t`
+ * is the next tick to run. Measurement infrastructure (scripts/cpu_hour.py): a long CPU run
+ * continues from a state the GPU reached in seconds. */
+int oc_load_scaled(oc_ctx *c, int t, const int32_t *hb, const int32_t *ts, const int32_t *heartbeat,
+                   const int32_t *failed, const int32_t *tgt, const int32_t *ntgt) {
+  if (!is_scaled(c) || c->cfg.init_mode == 2 || t < 1) return -1;
+  const size_t n = (size_t)c->n;
+  for (size_t i = 0; i < n; i++) {
+    node *nd = &c->nodes[i];
+    nd->list.n = 0;
+    for (size_t j = 0; j < n; j++) {
+      if (hb[i * n + j] < 0) continue;
+      entry e = {(int32_t)j + 1, 0, hb[i * n + j], ts[i * n + j]};
+      el_push(&nd->list, e);
+    }
+    nd->heartbeat = heartbeat[i];
+    nd->failed = failed[i] != 0;
+    nd->inited = nd->in_group = 1;
+    nd->q.n = 0;
+    snap *s = &c->snaps[i];  /* the sends of tick t - 1 (node_loop_ops) */
+    s->n = 0;
+    for (int k = 0; k < nd->list.n; k++) {
+      const entry *e = &nd->list.v[k];
+      if ((t - 1) - e->ts >= TFAIL) continue;
+      s->ids[s->n] = e->id;
+      s->hbs[s->n] = (int32_t)e->hb;
+      s->n++;
+    }
+    if (ntgt[i] < 0 || ntgt[i] > FANOUT) return -1;
+    c->ntgt[i] = ntgt[i];  /* a node failed at the end of t - 1 still sent in t - 1 */
+    for (int k = 0; k < FANOUT; k++) c->tgt[i * FANOUT + k] = k < ntgt[i] ? tgt[i * FANOUT + k] : 0;
+  }
+  memset(c->ntgt_next, 0, sizeof(int32_t) * n);
+  c->t = t;
+  return 0;
+}
+
 /* SCALED: fail these nodes now, i.e. at the end of the tick just run (the host side of
  * Application::fail, Application.cpp:184-196, with the victims chosen by the caller) */
 int oc_set_failed(oc_ctx *c, const int32_t *idx, int k) {

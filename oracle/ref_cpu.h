@@ -81,6 +81,12 @@ int oc_last_msgcount(const oc_ctx *c, int32_t *sent, int32_t *recv);
 int oc_node(oc_ctx *c, int r, int32_t *state4);
 /* SCALED: fail nodes idx[0..k) at the end of the tick just run (host fail() with caller-chosen victims) */
 int oc_set_failed(oc_ctx *c, const int32_t *idx, int k);
+/* SCALED: the last tick's gossip targets [n][5] (node indices) and their counts [n] */
+int oc_targets(const oc_ctx *c, int32_t *tgt, int32_t *ntgt);
+/* SCALED (not the join ramp): load the state between ticks -- hb / ts [n][n] (-1 absent), heartbeat
+ * counters, crash flags, the last tick's targets -- then tick t runs next (ref_cpu.c) */
+int oc_load_scaled(oc_ctx *c, int t, const int32_t *hb, const int32_t *ts, const int32_t *heartbeat,
+                   const int32_t *failed, const int32_t *tgt, const int32_t *ntgt);
 /* test telemetry: [0] = updateMyPos quirk firings, [1] = largest start-tick gap self -> target */
 void oc_quirks(const oc_ctx *c, int64_t out[2]);
 /* the crash set the SCALED driver uses (host fault injection) */

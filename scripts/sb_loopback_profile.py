@@ -16,6 +16,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "distributed-membership_amd"))
 
 from membership import GM_MODE_SCALED, Simulator, crash_set, load_library  # noqa: E402
+from membership.abi import shard_loopback_tick  # noqa: E402
 from membership.sharded import loopback_tick  # noqa: E402
 
 
@@ -25,6 +26,9 @@ def main():
     ap.add_argument("--shards", type=int, default=8)
     ap.add_argument("--ticks", type=int, default=20)
     ap.add_argument("--prologue", type=int, default=28)
+    ap.add_argument("--pipelined", action="store_true",
+                    help="time gm_shard_loopback_tick (the pipelined RCCL tick's chunk order, one stream) "
+                         "instead of the phase-API loopback")
     a = ap.parse_args()
     load_library()
     n, G = a.cluster, a.shards
@@ -46,14 +50,18 @@ def main():
     t0 = time.perf_counter()
     for _ in range(a.ticks):
         w = time.perf_counter()
-        rounds.append(loopback_tick(sims))
+        if a.pipelined:
+            shard_loopback_tick(sims)
+            rounds.append(1)
+        else:
+            rounds.append(loopback_tick(sims))
         print(f"tick {sims[0].time - 1}: {(time.perf_counter() - w) * 1e3:.1f} ms", file=sys.stderr, flush=True)
     for s in sims:
         s.sync()
     el = (time.perf_counter() - t0) / a.ticks
     errs = [s.tick_stats()["err"] for s in sims]
     removed = sum(s.event_totals()["removed"] for s in sims)
-    print(json.dumps({"n": n, "shards": G, "ticks": a.ticks, "ms_per_tick_all_shards_serialised": el * 1e3,
+    print(json.dumps({"n": n, "shards": G, "ticks": a.ticks, "mode": "pipelined" if a.pipelined else "phase API", "ms_per_tick_all_shards_serialised": el * 1e3,
                       "ms_per_shard_tick": el * 1e3 / G, "draw_rounds": rounds, "err": errs,
                       "removed_total": removed}), flush=True)
 

@@ -62,6 +62,8 @@ def lib():
         L.oc_node.argtypes = [ctypes.c_void_p, ctypes.c_int, P(ctypes.c_int32)]
         L.oc_quirks.argtypes = [ctypes.c_void_p, P(ctypes.c_int64)]
         L.oc_set_failed.argtypes = [ctypes.c_void_p, P(ctypes.c_int32), ctypes.c_int]
+        L.oc_targets.argtypes = [ctypes.c_void_p, P(ctypes.c_int32), P(ctypes.c_int32)]
+        L.oc_load_scaled.argtypes = [ctypes.c_void_p, ctypes.c_int] + [P(ctypes.c_int32)] * 6
         L.oc_last_msgcount.argtypes = [ctypes.c_void_p, P(ctypes.c_int32), P(ctypes.c_int32)]
         L.op_last_msgcount.argtypes = [ctypes.c_void_p, P(ctypes.c_int32), P(ctypes.c_int32)]
         L.op_last_msgcount.restype = None
@@ -173,6 +175,21 @@ class Oracle:
         a = np.ascontiguousarray(idx, dtype=np.int32)
         if self.L.oc_set_failed(self.h, _i32p(a), len(a)):
             raise ValueError("oc_set_failed")
+
+    def targets(self):
+        """SCALED: (targets int32 [n][5], counts [n]) drawn in the last tick"""
+        tg = np.zeros((self.n, 5), dtype=np.int32)
+        cnt = np.zeros(self.n, dtype=np.int32)
+        if self.L.oc_targets(self.h, _i32p(tg), _i32p(cnt)):
+            raise RuntimeError("oc_targets: SCALED only")
+        return tg, cnt
+
+    def load_state(self, t, hb, ts, heartbeat, failed, targets, counts):
+        """SCALED (no join ramp): replace the state between ticks (oc_load_scaled); tick t runs next.
+        hb / ts [n][n] (-1 absent), heartbeat / failed [n], targets [n][5], counts [n]."""
+        arrs = [np.ascontiguousarray(a, dtype=np.int32) for a in (hb, ts, heartbeat, failed, targets, counts)]
+        if self.L.oc_load_scaled(self.h, t, *[_i32p(a) for a in arrs]):
+            raise ValueError("oc_load_scaled")
 
     def last_msgcount(self):
         """SCALED: per-node gossip entries sent (before loss) / received (after loss) last tick"""
