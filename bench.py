@@ -284,6 +284,17 @@ def scaled_run(a, n, rank, world, local, dist, rtx, profiled):
                 removed_ok=removed_ok, W=W, t0=t0, t1=t1)
 
 
+def collective_bytes(n, world):
+    """RCCL payload one rank contributes per column-shard tick (gm_host.hip tick_sharded): the
+    all-gather of its per-row (present, numfailed) int32 pairs, the MAX-allreduce of the round-0
+    draw statuses int32[n][16], and the bounded rounds' MAX-allreduces int32[cap1][64] +
+    int32[256][256] (cap1 = min(4096, max(min(n, 1024), n / 16))). 0 on one GPU (no exchange)."""
+    if world <= 1:
+        return {"allgather_counts": 0, "allreduce_draws": 0, "allreduce_rounds": 0}
+    cap1 = min(4096, max(min(n, 1024), n // 16))
+    return {"allgather_counts": 8 * n, "allreduce_draws": 4 * 16 * n, "allreduce_rounds": 4 * (64 * cap1 + 256 * 256)}
+
+
 def companion_sb(a, rank, world, local, dist, rtx):
     """The north_star scaling cluster measured beside the headline: the same schedule at
     N = 262,144 (S-B, BASELINE.json configs[3]) on the same G ranks, so that every
@@ -294,10 +305,16 @@ def companion_sb(a, rank, world, local, dist, rtx):
     except (AssertionError, RuntimeError, OSError) as e:  # reported, not fatal to the headline line
         return {"scenario": "S-B", "error": f"{type(e).__name__}: {e}"}
     n = r["n"]
+    st, W, kms = r["st"], r["W"], r["kernel_ms"]
+    b_alg = (5 * st["live"] + st["lists"]) * W // 2  # rank 0's band kernels, as for S-A
+    ach = b_alg / (kms * 1e-3) / 1e9 if kms > 0 else None
     out = {"scenario": "S-B", "metric": "simulated node-ticks/sec (S-B N=262,144 full membership)",
            "value": n * a.steps / r["elapsed"], "unit": "node-ticks/s", "n_gpus": world,
-           "ms_per_step": r["elapsed"] / a.steps * 1e3, "kernel_ms_rank0": r["kernel_ms"],
-           "n": n, "crashed": r["ncrash"], "columns_per_gpu": r["W"], "scaling": "strong",
+           "ms_per_step": r["elapsed"] / a.steps * 1e3, "kernel_ms_rank0": kms,
+           "n": n, "crashed": r["ncrash"], "columns_per_gpu": W, "scaling": "strong",
+           "roofline_rank0": {"bound": "hbm", "alg_bytes_per_launch": b_alg, "achieved": ach, "peak": PEAK_HBM_GBPS,
+                              "unit": "GB/s", "frac": ach / PEAK_HBM_GBPS if ach else None},
+           "collective_bytes_per_rank_tick": collective_bytes(n, world),
            "check": {"removed_rank0": r["tot"]["removed"], "joined_rank0": r["tot"]["joined"]}}
     r["sim"].close()
     return out
@@ -394,6 +411,7 @@ def main():
                      "alg_bytes_per_launch": b_alg, "survey_int32_bytes_per_launch": b_survey,
                      "dram_bytes_est": dram_est, "frac_dram": frac_dram,
                      "columns_per_gpu": W},
+        "collective_bytes_per_rank_tick": collective_bytes(n, world),
         "check": {"removed_rank0": tot["removed"], "joined_rank0": tot["joined"], "removed_all_expected":
                   (n - ncrash) * ncrash if removed_ok else None},
     }

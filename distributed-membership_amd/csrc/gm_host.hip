@@ -2027,17 +2027,24 @@ extern "C" int gm_shard_stub(gm_ctx *c, int32_t on) {
   return GM_OK;
 }
 
+__global__ void gm_xc_mirror(int32_t *chunk, int rank, int G, size_t words) {  // stub all-gather
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < words; i += (size_t)gridDim.x * blockDim.x) {
+    const int32_t v = chunk[(size_t)rank * words + i];
+    for (int g = 0; g < G; g++)
+      if (g != rank) chunk[(size_t)g * words + i] = v;
+  }
+}
+
 // the all-gather of this shard's per-row (present, numfailed) for exchange chunk ch (stub: mirrored
 // into every peer slot), on stream st
 static int xcnt_allgather(gm_ctx *c, int ch, hipStream_t st) {
   SState &s = c->s;
   const size_t R = (size_t)1 << s.xlog, r0 = (size_t)ch << s.xlog;
   int32_t *own = s.xcnt + S_XC(s, s.shard_rank, r0);
-  if (s.stub) {
-    for (int g = 0; g < s.shard_count; g++)
-      if (g != s.shard_rank)
-        HIPCHECK(hipMemcpyAsync(s.xcnt + S_XC(s, g, r0), own, sizeof(int32_t) * 2 * xchunk_rows(s, ch),
-                                hipMemcpyDeviceToDevice, st));
+  if (s.stub) {  // one kernel mirrors the chunk's slot into every peer slot (the all-gather's local cost)
+    hipLaunchKernelGGL(gm_xc_mirror, dim3(256), dim3(256), 0, st, s.xcnt + S_XC(s, 0, r0), s.shard_rank,
+                       s.shard_count, (size_t)2 << s.xlog);
+    HIPCHECK(hipGetLastError());
     return GM_OK;
   }
   // chunk-major: the chunk's G slots are contiguous, rank g's at g * R rows -- in place

@@ -138,3 +138,33 @@ def test_scaled_escaped_payloads_match_oracle():
             esc_after_window += _escaped_sends(d, t)
     assert esc_after_window > 0  # the escape plane really carried loss-free deliveries
     assert sim.tick_stats()["err"] == 0
+
+
+@pytest.mark.parametrize("drop", [0, 20])
+def test_oracle_continues_from_gpu_state(drop):
+    """The whole SCALED state between two ticks, read from the HIP path (gm_read_table,
+    gm_read_nodes, gm_read_targets), loaded into the oracle (oc_load_scaled): the oracle's next
+    ticks equal the HIP path's, events and tables. This is the hand-over scripts/cpu_hour.py uses
+    to time a long CPU run in segments that start where the GPU got in seconds."""
+    n = 300
+    kw = dict(rd_seed=7, init_mode=1, init_t0=8, init_seed=11, drop_pct=drop, drop_from=0, drop_to=1000, drop_seed=5)
+    sim = Simulator(n, GM_MODE_SCALED, **kw)
+    crash = crash_set(n, 9, 42)
+    while sim.time <= 24:
+        t = sim.time
+        sim.tick()
+        if t == 10:
+            sim.set_failed(crash)
+    sim.drain_events()
+    hb, ts = sim.read_table()
+    st = sim.read_nodes()
+    tg, cnt = sim.read_targets()
+    ora = oracle_py.Oracle(n, oracle_py.OC_SCALED, crash_tick=10, crash_count=9, crash_seed=42, **kw)
+    ora.load_state(sim.time, hb, ts, st[:, 3], st[:, 2], tg, cnt)
+    assert digest64(ora.dump()) == digest64(sim.dump_tables())
+    for _ in range(14):
+        t = sim.time
+        sim.tick()
+        ora.tick()
+        assert [(e[0], e[1], e[2], e[3]) for e in sim.drain_events()] == ora.events(), f"events t={t}"
+        assert digest64(sim.dump_tables()) == digest64(ora.dump()), f"tables t={t}"
