@@ -612,6 +612,7 @@ static int create_partial(gm_ctx *c) {
   TRY(dalloc(c, &p.failed, nl));
   TRY(dalloc(c, &p.ev, (size_t)nl * 2 * p.V));
   TRY(dalloc(c, &p.ev_cnt, nl));
+  TRY(dalloc(c, &p.ev_jm, nl));
   TRY(dalloc(c, &p.rowstat, (size_t)nl * 4));
   TRY(dalloc(c, &p.targets, (size_t)nl * GM_FANOUT));
   TRY(dalloc(c, &p.big, nl));
@@ -662,6 +663,7 @@ static int create_partial(gm_ctx *c) {
   HIPCHECK(ctx_memset(c, p.lists, 0, sizeof(uint64_t) * 2 * p.rows * p.V));
   HIPCHECK(ctx_memset(c, p.failed, 0, sizeof(int32_t) * nl));
   HIPCHECK(ctx_memset(c, p.ev_cnt, 0, sizeof(int32_t) * nl));
+  HIPCHECK(ctx_memset(c, p.ev_jm, 0, sizeof(uint32_t) * nl));
   HIPCHECK(ctx_memset(c, p.rowstat, 0, sizeof(int32_t) * nl * 4));
   HIPCHECK(ctx_memset(c, p.err, 0, sizeof(uint32_t)));
   HIPCHECK(gm_launch_partial_init(p, t0, c->cfg.init_seed, c->stream));
@@ -1125,18 +1127,30 @@ static int drain_partial(gm_ctx *c, std::vector<gm_event> &out) {
   size_t tot = 0;
   for (int32_t v : cnt) tot += (size_t)(v & 0xFFFF) + (size_t)(v >> 16);
   if (!tot) return GM_OK;
-  const size_t row = 2 * (size_t)p.V;  // joins from the front, removals from the back
-  std::vector<uint32_t> ev((size_t)p.nloc * row);
-  HIPCHECK(ctx_memcpy(c, ev.data(), p.ev, sizeof(uint32_t) * ev.size(), hipMemcpyDeviceToHost));
+  // joins: the set bits of each node's join mask over its final list of the tick (lists of parity t & 1,
+  // intact until tick t + 2); removals: the records at the back of the node's event row
+  const size_t row = 2 * (size_t)p.V;
   const int t = c->t - 1;
+  std::vector<uint32_t> jm(p.nloc);
+  HIPCHECK(ctx_memcpy(c, jm.data(), p.ev_jm, sizeof(uint32_t) * jm.size(), hipMemcpyDeviceToHost));
+  std::vector<uint64_t> lst((size_t)p.nloc * p.V);
+  HIPCHECK(ctx_memcpy(c, lst.data(), p.lists + (size_t)(t & 1) * p.rows * p.V, sizeof(uint64_t) * lst.size(),
+                      hipMemcpyDeviceToHost));
+  bool any_rem = false;
+  for (int32_t v : cnt) any_rem |= (v >> 16) != 0;
+  std::vector<uint32_t> ev;
+  if (any_rem) {
+    ev.resize((size_t)p.nloc * row);
+    HIPCHECK(ctx_memcpy(c, ev.data(), p.ev, sizeof(uint32_t) * ev.size(), hipMemcpyDeviceToHost));
+  }
   out.reserve(out.size() + tot);
   for (int r = 0; r < p.nloc; r++) {
     const int nj = cnt[r] & 0xFFFF, nr = cnt[r] >> 16;
-    for (int q = 0; q < nj + nr; q++) {
-      const uint32_t rec = ev[(size_t)r * row + (q < nj ? q : row - 1 - (q - nj))];
-      out.push_back(gm_event{t, p.n0 + r, (rec >> 30) == P_EV_ADD ? GM_EV_JOINED : GM_EV_REMOVED,
-                             (int32_t)(rec & 0x3FFFFFFFu)});
-    }
+    if (__builtin_popcount(jm[r]) != nj) return GM_ESTATE;
+    for (uint32_t b = jm[r]; b; b &= b - 1)
+      out.push_back(gm_event{t, p.n0 + r, GM_EV_JOINED, (int32_t)(lst[(size_t)r * p.V + __builtin_ctz(b)] >> 32)});
+    for (int q = 0; q < nr; q++)
+      out.push_back(gm_event{t, p.n0 + r, GM_EV_REMOVED, (int32_t)(ev[(size_t)r * row + row - 1 - q] & 0x3FFFFFFFu)});
   }
   return GM_OK;
 }

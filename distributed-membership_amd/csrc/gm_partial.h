@@ -36,8 +36,10 @@ struct PState {
   int32_t *rsrc[2];      // [n - nloc] global sender index of each received list row, by parity
   int32_t *hbctr;        // [nloc] heartbeat counter
   int32_t *failed;       // [nloc]
-  uint32_t *ev;          // [nloc][2V] kind<<30 | subject id: joins from the front (ascending id), removals from the back
+  uint32_t *ev;          // [nloc][2V] kind<<30 | subject id of the removals, from the back of the row
   int32_t *ev_cnt;       // [nloc] joins | removals << 16
+  uint32_t *ev_jm;       // [nloc] joins as a mask over the node's final list of the tick (bit e: entry e is new;
+                         //   the list is id-sorted, so the joins in ascending id order are its set bits)
   int32_t *rowstat;      // [nloc][4]: lists merged, view size, numfailed, targets chosen
   int32_t *targets;      // [nloc][GM_FANOUT] (global node indices)
   int32_t *big;          // [nloc] worklists of nodes with > P_KSMALL lists (big-table kernel), chunk c at rows r0_c..

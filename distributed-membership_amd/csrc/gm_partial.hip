@@ -17,16 +17,19 @@
 //      its inbox (sender indices), its 16 precomputed S2 outputs, then every
 //      delivered list (V lanes per list, several lists per wave step);
 //   2. merge into an open-addressing LDS table keyed by id (32-bit CAS claim +
-//      ds_max of the heartbeat word), own entries first so they carry the
-//      "own" bit, delivered entries filtered to fresh + not dropped;
-//   3. self bump, then one sweep compacts the table in place into a dense
-//      array (TREMOVE removals counted and logged on the way);
+//      ds_max of the heartbeat word), the own list in the same step as the first
+//      delivered list (own entries set an "own" bit), delivered entries filtered
+//      to fresh + not dropped. The lane that CLAIMS an id's slot holds that id
+//      from then on: the union is the set of claimers, in registers (round 5: no
+//      sweep of the 512-slot table, no compaction, no dense re-read);
+//   3. self bump; every claimer reads its slot's merged entry back (TREMOVE
+//      removals counted and logged on the way);
 //   4. eviction to V only when the union exceeds V: an LDS histogram of the
 //      heartbeat distance from the top finds the cut heartbeat; inside the cut
 //      bucket a 6-bit radix histogram of the eviction keys and (rarely) an
 //      exact min-selection pick the smallest keys -- no full sort;
 //   5. the <= V kept entries are ranked by id (broadcast LDS compare) = the
-//      id-sorted list, stored as one coalesced row;
+//      id-sorted list, stored as one coalesced row; joins as a bit mask over it;
 //   6. the gossip draw: the 16 precomputed S2 outputs resolved in parallel across
 //      the wave (duplicates by shuffle-compares), the rare rest on scalars.
 // Nodes with more than P_KSMALL delivered lists (Poisson tail, ~0.2 % at 12) do not fit
@@ -132,22 +135,6 @@ __device__ __forceinline__ uint64_t p_readlane64(uint64_t v, int l) {
   return ((uint64_t)hi << 32) | lo;
 }
 
-// claim or find the slot of `id` (idw = id | flags on claim), raise its heartbeat word
-template <int H>
-__device__ __forceinline__ int p_insert(uint32_t *tid, uint32_t *thb, uint32_t id, uint32_t idw, uint32_t hb) {
-  // slot = low bits of id ^ id >> 9: view ids are uniform node indices, so this spreads them like a
-  // multiplicative hash without its quarter-rate 32-bit multiply (the slot never shows in a result:
-  // the table is compacted and ranked by id)
-  uint32_t h = (id ^ (id >> 9)) & (H - 1);
-  for (;;) {  // claim-or-compare in one LDS op
-    const uint32_t cur = atomicCAS(&tid[h], 0u, idw);
-    if (cur == 0 || (cur & P_IDMASK) == id) break;
-    h = (h + 1) & (H - 1);
-  }
-  atomicMax(&thb[h], hb);
-  return (int)h;
-}
-
 // owning row shard of node d: contiguous balanced ranges [n*g/G, n*(g+1)/G), boundaries
 // in shard_n0[0..G]; a float estimate is off by at most one, two compares fix it
 __device__ __forceinline__ int p_owner(const PState &s, int d) {
@@ -232,11 +219,9 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
                                        int chunk, int r0) {
   int k = pre.k;
   const int i = s.n0 + li;  // global node index (ids, keys, seeds, targets)
-  constexpr int TS = H / 64;                          // table slots per lane
   constexpr int KK = H == P_HH ? P_KMAX : BIG ? P_KP : P_KSMALL;  // lists merged at most
-  constexpr int DS = ((1 + KK) * P_VMAX + 63) / 64;   // dense entries per lane
-  constexpr int NSTEP = (KK + 1) / 2;                 // list-load steps (>= 2 lists per step)
-  using mask_t = typename std::conditional<(DS > 32), uint64_t, uint32_t>::type;  // one bit per dense slot
+  constexpr int NS = (KK + 2) / 2;  // merge steps: the own list + KK lists, >= 2 list slots per step
+  using mask_t = typename std::conditional<(NS > 32), uint64_t, uint32_t>::type;  // one bit per step
 #ifdef GM_P_PROFILE
   uint64_t pp_[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, pt_ = __builtin_amdgcn_s_memtime();
 #endif
@@ -257,7 +242,9 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
     if (lane == 0) atomicOr(s.err, GM_ERR_INBOX);
     k = kmax;  // never read sender slots that were not written
   }
-  // ---- 1. loads (the independent ones arrived with `pre`)
+  // ---- 1. loads (the independent ones arrived with `pre`). List slots: slot 0 = the node's own
+  // list, slot j + 1 = delivered list j; one merge step covers `per` consecutive slots (a half-wave
+  // each at V = 32), so the own list shares the first step with delivered list 0
   const uint64_t own = pre.own;
   int sv = lane < k ? pre.sv : 0x7FFFFFFF;  // list rows
   const uint32_t raw0 = pre.raw0;
@@ -268,7 +255,7 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
     for (int q = 0; q < H / 128; q++) z[lane + 64 * q] = make_uint4(0, 0, 0, 0);
   }
   const int kk = min(k, KK);
-  // lists per load step (per), entry (l) and list slot (jo) of this lane; V = 32 (S-C) takes the
+  // lists per step (per), entry (l) and slot in the step (jo) of this lane; V = 32 (S-C) takes the
   // shifts instead of three integer divisions. The step's per-list values come by ds_bpermute
   // (the LDS port) rather than two readlanes + a select: VALU issue is what bounds this kernel
   const bool v32 = V == P_VMAX;
@@ -282,14 +269,16 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
     l = lane % V;
     jo = lane / V;
   }
-  auto step_val = [&](int v, int st) -> int { return __shfl(v, min(st * per + jo, 63), 64); };  // v of lane st * per + jo
-  uint64_t dv[NSTEP];
+  const int nst = (kk + per) / per;  // active steps: ceil((1 + kk) / per), wave-uniform
+  // the value v holds on the lane of delivered list slot - 1
+  auto step_val = [&](int v, int st) -> int { return __shfl(v, min(max(st * per + jo - 1, 0), 63), 64); };
+  uint64_t dv[NS];
 #pragma unroll
-  for (int st = 0; st < NSTEP; st++) {
-    const int j = st * per + jo;
-    const bool ok = jo < per && j < kk;
+  for (int st = 0; st < NS; st++) {
+    const int j = st * per + jo - 1;  // delivered list of this lane's slot (-1: the own list)
+    const bool ok = jo < per && j >= 0 && j < kk;
     const int sn = step_val(sv, st);
-    uint64_t e = 0;
+    uint64_t e = (st == 0 && jo == 0) ? own : 0ull;
     if (ok && (!RM || sn < s.nloc)) {
       e = prev[(size_t)sn * V + l];
     } else if (RM && ok) {  // a list another shard sent at t-1: wire entry id | (2(t-1)-1 - hb) << 25
@@ -311,144 +300,112 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
   const uint32_t dthr = gm_drop_thresh(s.drop_pct);
   PPROF(0);
   p_wsync();
-  // ---- 2. merge: own entries first (they carry P_OWN), then the delivered lists
-  int hslot = -1;
+  // ---- 2. merge: every entry into the table by id (32-bit CAS claim, ds_max of the heartbeat
+  // word); own entries set the "own" bit (after the claim when a delivered copy of the id in the
+  // same step claimed it first). The lane that claims an id's slot holds the id from then on: the
+  // union is the set of claimers, so the table is never swept or compacted
   const uint32_t self_id = (uint32_t)(i + 1);
-  if (own != 0) {
-    const uint32_t id = (uint32_t)(own >> 32);
-    hslot = p_insert<H>(tid, thb, id, id | P_OWN, (uint32_t)own);
-  }
-  PPROF(1);
-  p_wsync();
+  int csl[NS];    // this lane's claimed slot per step (-1: none)
+  int hself = -1;  // the slot of the node's own entry (on its own-list lane)
   {
     const uint32_t tfresh = (uint32_t)max(0, 2 * t - 11);  // hb >= 2t-11 <=> (t-1) - (hb+1)/2 < TFAIL
 #pragma unroll
-    for (int st = 0; st < NSTEP; st++) {
+    for (int st = 0; st < NS; st++) {
+      csl[st] = -1;
+      if (st >= nst) continue;
       const uint64_t e = dv[st];
-      bool take = e != 0 && (uint32_t)e >= tfresh;
+      const bool isown = st == 0 && jo == 0;
       const uint32_t id = (uint32_t)(e >> 32);
-      if (dropping && __ballot(take)) {  // per-entry drops keyed by (t_send, src, dst, id-1): lost iff the
-        // top 16 bits of fmix32(pair ^ (id-1)) are below the threshold
+      bool take = e != 0 && (isown || (uint32_t)e >= tfresh);
+      if (dropping && __ballot(take && !isown)) {  // per-entry drops keyed by (t_send, src, dst, id-1): lost
+        // iff the top 16 bits of fmix32(pair ^ (id-1)) are below the threshold
         const uint32_t pair = (uint32_t)step_val((int)pairv, st);
-        take = take && (gm_fmix32(pair ^ (id - 1)) >> 16) >= dthr;
+        take = take && (isown || (gm_fmix32(pair ^ (id - 1)) >> 16) >= dthr);
       }
-      if (take) (void)p_insert<H>(tid, thb, id, id, (uint32_t)e);
-      if (mc) nrecv += __builtin_popcountll(__ballot(take));
+      if (take) {
+        // slot = low bits of id ^ id >> 9: view ids are uniform node indices, so this spreads them like a
+        // multiplicative hash without its quarter-rate multiply (the slot never shows in a result)
+        uint32_t h = (id ^ (id >> 9)) & (H - 1);
+        uint32_t cur;
+        for (;;) {  // claim-or-compare in one LDS op
+          cur = atomicCAS(&tid[h], 0u, isown ? (id | P_OWN) : id);
+          if (cur == 0 || (cur & P_IDMASK) == id) break;
+          h = (h + 1) & (H - 1);
+        }
+        atomicMax(&thb[h], (uint32_t)e);
+        if (cur == 0) csl[st] = (int)h;
+        else if (isown) atomicOr(&tid[h], P_OWN);
+        if (isown && id == self_id) hself = (int)h;
+      }
+      if (mc) nrecv += __builtin_popcountll(__ballot(take && !isown));
     }
   }
   PPROF(2);
   p_wsync();
-  // ---- 3. self bump (heartbeat++; myPos->setheartbeat(heartbeat++)), then sweep + compaction
+  // ---- 3. self bump (heartbeat++; myPos->setheartbeat(heartbeat++))
   {
-    const uint64_t sb = __ballot(own != 0 && (uint32_t)(own >> 32) == self_id);
-    int hs;
+    const uint64_t sb = __ballot(hself >= 0);
     if (sb) {
-      hs = __builtin_amdgcn_readlane(hslot, __builtin_ctzll(sb));
-    } else {  // cannot happen for a live node (the oracle aborts): flag, and re-insert self
-      hs = 0;
+      const int hs = __builtin_amdgcn_readlane(hself, __builtin_ctzll(sb));
       if (lane == 0) {
-        atomicOr(s.err, GM_ERR_SELF);
-        hs = p_insert<H>(tid, thb, self_id, self_id | P_OWN, 1u);
+        thb[hs] = (uint32_t)hbnew;
+        tid[hs] |= P_SELF | P_OWN;
       }
-      hs = __builtin_amdgcn_readfirstlane(hs);
+    } else if (lane == 0) {  // cannot happen for a live node (the oracle aborts): the tick is void
+      atomicOr(s.err, GM_ERR_SELF);
     }
-    if (lane == 0) {
-      thb[hs] = (uint32_t)hbnew;
-      tid[hs] |= P_SELF | P_OWN;
-      s.hbctr[li] = hbnew + 1;
-    }
+    if (lane == 0) s.hbctr[li] = hbnew + 1;
   }
   PPROF(3);
   p_wsync();
+  // ---- 4. the union: each claimer reads its slot's merged entry back. alive <=> not aged past
+  // TREMOVE <=> hb >= xa (heartbeats are odd, >= 1); the aged ones are own entries (delivered
+  // entries are fresh) and are removed with a REMOVE event (rare: one ballot per step)
   uint32_t *evr = s.ev + (size_t)li * 2 * V;
-  int m, removed, nrem;
+  int m = 0, removed = 0, nrem = 0;
+  uint32_t cw[NS], ch[NS];  // the union's entries held by this lane: id word (0: none), heartbeat
   {
-    uint32_t w[TS], hh[TS];
-#pragma unroll
-    for (int q = 0; q < TS / 4; q++) {
-      const uint4 a = ((const uint4 *)tid)[lane * (TS / 4) + q];
-      const uint4 b = ((const uint4 *)thb)[lane * (TS / 4) + q];
-      w[4 * q] = a.x; w[4 * q + 1] = a.y; w[4 * q + 2] = a.z; w[4 * q + 3] = a.w;
-      hh[4 * q] = b.x; hh[4 * q + 1] = b.y; hh[4 * q + 2] = b.z; hh[4 * q + 3] = b.w;
-    }
-    using tmask_t = typename std::conditional<(TS > 32), uint64_t, uint32_t>::type;  // one bit per table slot
-    constexpr int CB = TS <= 8 ? 4 : TS <= 16 ? 5 : TS <= 32 ? 6 : 7;               // bits of a per-lane slot count
-    // alive <=> present and not aged past TREMOVE <=> hb >= xa: every present entry has hb >= 1
-    // (heartbeats start at 2t-1 >= 1; hb < 2^31) and an empty slot holds hb 0, so one compare per
-    // slot gives the alive bit; removals = present - alive (rare: tested once per row)
     const uint32_t xa = (uint32_t)max(2 * (t - GM_TREMOVE) + 1, 1);
-    tmask_t alive = 0, rown = 0;
-    int rcount = 0;
 #pragma unroll
-    for (int u = 0; u < TS; u++) {  // branch-free: exec-mask traffic is what this kernel spends SALU on
-      alive |= (tmask_t)((xa - 1u - hh[u]) >> 31) << u;
-      rcount += (int)min(w[u], 1u);
-    }
-    rcount -= __builtin_popcountll(alive);
-    int tot;
-    removed = nrem = 0;
-    if (__ballot(rcount != 0)) {  // rare: TREMOVE removals in this row
-#pragma unroll
-      for (int u = 0; u < TS; u++) rown |= (tmask_t)((w[u] >> 31) & (uint32_t)!((alive >> u) & 1)) << u;
-      (void)p_excl<CB>(rcount, &removed);
-      const int ro = __builtin_popcountll(rown);
-      int rpos = p_excl<CB>(ro, &nrem);
-      if (nrem) {  // REMOVE events of the node's own entries, from the back of its event row
-#pragma unroll
-        for (int u = 0; u < TS; u++)
-          if ((rown >> u) & 1) evr[2 * V - 1 - rpos++] = (P_EV_REMOVE << 30) | (w[u] & P_IDMASK);
+    for (int st = 0; st < NS; st++) {
+      cw[st] = ch[st] = 0u;
+      if (st >= nst) continue;
+      uint32_t w = 0u, hh = 0u;
+      if (csl[st] >= 0) {
+        w = tid[csl[st]];
+        hh = thb[csl[st]];
       }
-    }
-    // the alive slots' dense positions: an inclusive DPP scan of the per-lane counts (A/B on one box
-    // against p_excl's ballot per count bit: -0.3 %, profiles/r04/sc_sweep/)
-    const int na = __builtin_popcountll(alive);
-    const int incl = p_scan(na, lane);
-    tot = __builtin_amdgcn_readlane(incl, 63);
-    int pos = incl - na;
-    m = tot;
-    // every slot is stored: dead ones to a per-lane slot of [H-64, H), past the dense
-    // range (m <= (1+KK)V+1 < H-64) and free of bank conflicts
-#pragma unroll
-    for (int u = 0; u < TS; u++) {
-      const bool a = (alive >> u) & 1;
-      const int at = a ? pos : H - 64 + lane;
-      tid[at] = w[u];
-      thb[at] = hh[u];
-      pos += a;
+      const bool dead = w != 0u && hh < xa;
+      const uint64_t db = __ballot(dead);
+      if (db) {  // rare: TREMOVE removals (own entries) -- REMOVE events from the back of the event row
+        const uint64_t ob = __ballot(dead && (w & P_OWN));
+        if (dead && (w & P_OWN)) evr[2 * V - 1 - nrem - p_below(ob)] = (P_EV_REMOVE << 30) | (w & P_IDMASK);
+        nrem += __builtin_popcountll(ob);
+        removed += __builtin_popcountll(db);
+      }
+      cw[st] = dead ? 0u : w;
+      ch[st] = hh;
+      m += __builtin_popcountll(__ballot(cw[st] != 0u));
     }
   }
   PPROF(4);
-  p_wsync();
-  // ---- 4. dense entries e = s*64 + lane; eviction to V
-  // only the first dm = ceil(m / 64) of the DS per-lane slots hold entries (m is wave-uniform):
-  // every per-slot loop below skips the rest with a scalar branch
-  const int dm = (m + 63) >> 6;
-  uint32_t dw[DS], dh[DS];
-#pragma unroll
-  for (int q = 0; q < DS; q++) {  // DS*64 < H: the reads stay inside the table
-    dw[q] = dh[q] = 0u;
-    if (q < dm) {
-      const int e = q * 64 + lane;
-      const uint32_t a = tid[e], b = thb[e];
-      dw[q] = e < m ? a : 0u;
-      dh[q] = e < m ? b : 0u;
-    }
-  }
+  // ---- 5. eviction to V (self always kept): keep bit st = this lane's step-st entry stays
   mask_t keep = 0;
   if (m <= V) {
 #pragma unroll
-    for (int q = 0; q < DS; q++)
-      if (q < dm && dw[q]) keep |= (mask_t)1 << q;
+    for (int st = 0; st < NS; st++)
+      if (st < nst && cw[st]) keep |= (mask_t)1 << st;
   } else {
     // heartbeat distance from the top (2t-1 = this tick's self heartbeat); alive
-    // entries have age < TREMOVE, i.e. distance <= 40 < 64
+    // entries have age < TREMOVE, i.e. distance <= 40 < 64. The table is dead now: its last
+    // 64 words take the histogram adds of the entries that do not count
     const int top = 2 * t - 1;
     hist[lane] = 0;
     p_wsync();
 #pragma unroll
-    for (int q = 0; q < DS; q++)  // entries that do not count go to a private trash word
-      if (q < dm)
-        atomicAdd((dw[q] && !(dw[q] & P_SELF)) ? &hist[min(max(top - (int)dh[q], 0), 63)] : &tid[H - 64 + lane], 1u);
+    for (int st = 0; st < NS; st++)
+      if (st < nst)
+        atomicAdd((cw[st] && !(cw[st] & P_SELF)) ? &hist[min(max(top - (int)ch[st], 0), 63)] : &tid[H - 64 + lane], 1u);
     p_wsync();
     const int need = V - 1;  // self is always kept
     int c = (int)hist[lane];
@@ -460,12 +417,12 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
     const int needb = need - before;  // 1 <= needb <= bsz
     mask_t bucket = 0;
 #pragma unroll
-    for (int q = 0; q < DS; q++) {
-      if (q >= dm) continue;
-      const int d = min(max(top - (int)dh[q], 0), 63);
-      const mask_t v = dw[q] != 0;
-      keep |= (v & (mask_t)(((dw[q] & P_SELF) != 0) | (d < dcut))) << q;
-      bucket |= (v & (mask_t)(!(dw[q] & P_SELF) && d == dcut)) << q;
+    for (int st = 0; st < NS; st++) {
+      if (st >= nst) continue;
+      const int d = min(max(top - (int)ch[st], 0), 63);
+      const mask_t v = cw[st] != 0;
+      keep |= (v & (mask_t)(((cw[st] & P_SELF) != 0) | (d < dcut))) << st;
+      bucket |= (v & (mask_t)(!(cw[st] & P_SELF) && d == dcut)) << st;
     }
 #ifdef GM_P_PROFILE
     pp_[10] += 1;  // evictions
@@ -478,18 +435,19 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
       // the needb smallest eviction keys of the bucket: 6-bit radix on the top bits,
       // then exact min-selection inside the cut bin
       const uint32_t oseed = (uint32_t)gm_mix64(gm_mix64(s.view_seed ^ (uint64_t)(uint32_t)t) ^ (uint64_t)(uint32_t)i);
-      uint32_t key[DS];
+      uint32_t key[NS];
 #pragma unroll
-      for (int q = 0; q < DS; q++) {
-        key[q] = ~0u;
-        if (q < dm && __ballot((bucket >> q) & 1)) key[q] = ((bucket >> q) & 1) ? p_evict_key(oseed, dw[q] & P_IDMASK) : ~0u;
+      for (int st = 0; st < NS; st++) {
+        key[st] = ~0u;
+        if (st < nst && __ballot((bucket >> st) & 1))
+          key[st] = ((bucket >> st) & 1) ? p_evict_key(oseed, cw[st] & P_IDMASK) : ~0u;
       }
       p_wsync();
       hist[lane] = 0;
       p_wsync();
 #pragma unroll
-      for (int q = 0; q < DS; q++)
-        if (q < dm) atomicAdd(((bucket >> q) & 1) ? &hist[key[q] >> 26] : &tid[H - 64 + lane], 1u);
+      for (int st = 0; st < NS; st++)
+        if (st < nst) atomicAdd(((bucket >> st) & 1) ? &hist[key[st] >> 26] : &tid[H - 64 + lane], 1u);
       p_wsync();
       c = (int)hist[lane];
       inc = p_scan(c, lane);
@@ -500,12 +458,12 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
       int needc = needb - before2;  // 1 <= needc <= bsz2
       mask_t cand = 0;
 #pragma unroll
-      for (int q = 0; q < DS; q++) {
-        if (q >= dm) continue;
-        const mask_t b = (bucket >> q) & 1;
-        const int bin = (int)(key[q] >> 26);
-        keep |= (b & (mask_t)(bin < bcut)) << q;
-        cand |= (b & (mask_t)(bin == bcut)) << q;
+      for (int st = 0; st < NS; st++) {
+        if (st >= nst) continue;
+        const mask_t b = (bucket >> st) & 1;
+        const int bin = (int)(key[st] >> 26);
+        keep |= (b & (mask_t)(bin < bcut)) << st;
+        cand |= (b & (mask_t)(bin == bcut)) << st;
       }
       if (needc == bsz2) {
         keep |= cand;
@@ -516,34 +474,34 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
         for (; needc > 0; needc--) {  // take the smallest remaining candidate key (keys are distinct)
           uint32_t mn = ~0u;
 #pragma unroll
-          for (int q = 0; q < DS; q++)
-            if (q < dm && ((cand >> q) & 1)) mn = min(mn, key[q]);
+          for (int st = 0; st < NS; st++)
+            if (st < nst && ((cand >> st) & 1)) mn = min(mn, key[st]);
 #pragma unroll
           for (int o = 32; o >= 1; o >>= 1) mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, 64));
 #pragma unroll
-          for (int q = 0; q < DS; q++)
-            if (q < dm && ((cand >> q) & 1) && key[q] == mn) {
-              keep |= (mask_t)1 << q;
-              cand &= ~((mask_t)1 << q);
+          for (int st = 0; st < NS; st++)
+            if (st < nst && ((cand >> st) & 1) && key[st] == mn) {
+              keep |= (mask_t)1 << st;
+              cand &= ~((mask_t)1 << st);
             }
         }
       }
     }
   }
   PPROF(5);
-  // ---- 5. compact the kept entries (<= V), rank them by id
+  // ---- 6. compact the kept entries (<= V), rank them by id
   int cnt = 0;
   p_wsync();  // the eviction histogram is dead: it takes the stores of the entries not kept
 #pragma unroll
-  for (int q = 0; q < DS; q++) {
-    if (q >= dm) break;
-    const bool kq = (keep >> q) & 1;
+  for (int st = 0; st < NS; st++) {
+    if (st >= nst) break;
+    const bool kq = (keep >> st) & 1;
     const uint64_t bal = __ballot(kq);
     const int p = cnt + p_below(bal);
     // id word rotated left by 2: id << 2 | own << 1 | self (ids < 2^25, bits 25..29 clear),
     // so the rank below compares whole words
-    *(kq ? kid + p : hist + lane) = __builtin_amdgcn_alignbit(dw[q], dw[q], 30);
-    *(kq ? khb + p : hist + lane) = dh[q];
+    *(kq ? kid + p : hist + lane) = __builtin_amdgcn_alignbit(cw[st], cw[st], 30);
+    *(kq ? khb + p : hist + lane) = ch[st];
     cnt += __builtin_popcountll(bal);
   }
   if (lane >= cnt && lane < P_VMAX) kid[lane] = ~0u;  // sentinels rank after every real entry
@@ -576,7 +534,8 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
   // joins (ascending id) from the front of the event row
   const uint64_t jb = __ballot(lane < cnt && !(f & 2u));  // rotated P_OWN
   const int nj = __builtin_popcountll(jb);
-  if (lane < cnt && !(f & 2u)) evr[p_below(jb)] = (P_EV_ADD << 30) | (uint32_t)(x >> 32);
+  // joins (ascending id): a mask over the final list (ev_jm, with the counts below) -- the drain
+  // reads the ids from the list itself, so no record is written per join
   const int numfailed = removed + __builtin_popcountll(__ballot(lane < cnt && p_aged(t, (uint32_t)x, GM_TFAIL)));
   PPROF(6);
   // ---- 6. gossip draw over the final list (MP1Node.cpp:449-489)
@@ -714,6 +673,7 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
   }
   if (lane < 4) s.rowstat[(size_t)li * 4 + lane] = lane == 0 ? kk : lane == 1 ? cnt : lane == 2 ? numfailed : ng;
   if (lane == 0) s.ev_cnt[li] = nj | (nrem << 16);
+  if (lane == 1) s.ev_jm[li] = (uint32_t)jb;  // lanes < cnt <= 32
   if (mc && lane == 0) {  // entries sent = fresh entries of the final list x targets (MP1Node.cpp:372-375)
     s.mc_sent[(size_t)t * s.nloc + li] = (uint32_t)(ng * (cnt - (numfailed - removed)));
     s.mc_recv[(size_t)t * s.nloc + li] = (uint32_t)nrecv;
@@ -736,6 +696,7 @@ __device__ __forceinline__ void p_frozen(const PState &s, int t, int li, int lan
   if (lane == 0) {
     s.inbox[par][(size_t)li * P_KMAX] = 0;
     s.ev_cnt[li] = 0;
+    s.ev_jm[li] = 0;
   }
 }
 

@@ -91,7 +91,10 @@ def load_library():
         "gm_shard_merge": [ctypes.c_void_p], "gm_shard_draw": [ctypes.c_void_p, i32, i32],
         "gm_shard_accept": [ctypes.c_void_p, i32, P(i32)], "gm_shard_end_tick": [ctypes.c_void_p],
     }
+    ab_build = "GM_LIBRARY" in os.environ  # an older measurement build (A/B) may lack newer entry points
     for name, args in sig.items():
+        if ab_build and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = ctypes.c_int
