@@ -479,6 +479,14 @@ static int create_scaled(gm_ctx *c) {
     HIPCHECK(ctx_memset(c, s.fb_cnt, 0, 2 * sizeof(uint32_t)));
     TRY(dalloc(c, &s.fb_list, (size_t)n * s.nb));
   }
+  // gm_s_pick0 (single context, B = 1024) and the list of rows it leaves to gm_s_pick
+  s.pk_list = nullptr;
+  s.pk_cnt = nullptr;
+  if (s.band == 1024 && !s.sharded && sizeof(uint32_t) * 16 * (size_t)(s.nb + 1) <= 65536 &&
+      !(getenv("GM_PICK0") && atoi(getenv("GM_PICK0")) == 0)) {
+    TRY(dalloc(c, &s.pk_list, n));
+    TRY(dalloc(c, &s.pk_cnt, 1));
+  }
   TRY(dalloc(c, &s.ev_band, (size_t)n * s.nb * s.evs));
   {  // event spill ring (records past a (row, band)'s E slots): up to every cell of the shard, within a
      // 1/32 share of the free HBM (the loopback shards of one device split it); at least 2^24 records.

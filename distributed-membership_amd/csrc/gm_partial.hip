@@ -366,26 +366,34 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
   uint32_t cw[NS], ch[NS];  // the union's entries held by this lane: id word (0: none), heartbeat
   {
     const uint32_t xa = (uint32_t)max(2 * (t - GM_TREMOVE) + 1, 1);
+    uint32_t deadm = 0;  // steps whose claimed entry this lane drops (aged past TREMOVE)
+    int mloc = 0;
 #pragma unroll
-    for (int st = 0; st < NS; st++) {
+    for (int st = 0; st < NS; st++) {  // branch-free per step: a non-claimer reads slot 0 and drops it
       cw[st] = ch[st] = 0u;
       if (st >= nst) continue;
-      uint32_t w = 0u, hh = 0u;
-      if (csl[st] >= 0) {
-        w = tid[csl[st]];
-        hh = thb[csl[st]];
-      }
+      const int sl = max(csl[st], 0);
+      const uint32_t w = csl[st] >= 0 ? tid[sl] : 0u;
+      const uint32_t hh = thb[sl];
       const bool dead = w != 0u && hh < xa;
-      const uint64_t db = __ballot(dead);
-      if (db) {  // rare: TREMOVE removals (own entries) -- REMOVE events from the back of the event row
+      deadm |= (uint32_t)dead << st;
+      cw[st] = dead ? 0u : w;
+      ch[st] = hh;
+      mloc += cw[st] != 0u;
+    }
+    m = __builtin_amdgcn_readlane(p_scan(mloc, lane), 63);
+    if (__ballot(deadm != 0)) {  // rare: TREMOVE removals (own entries) -- REMOVE events from the back
+#pragma unroll
+      for (int st = 0; st < NS; st++) {
+        if (st >= nst) continue;
+        const bool dead = (deadm >> st) & 1;
+        const uint32_t w = dead ? tid[max(csl[st], 0)] : 0u;
+        const uint64_t db = __ballot(dead);
         const uint64_t ob = __ballot(dead && (w & P_OWN));
         if (dead && (w & P_OWN)) evr[2 * V - 1 - nrem - p_below(ob)] = (P_EV_REMOVE << 30) | (w & P_IDMASK);
         nrem += __builtin_popcountll(ob);
         removed += __builtin_popcountll(db);
       }
-      cw[st] = dead ? 0u : w;
-      ch[st] = hh;
-      m += __builtin_popcountll(__ballot(cw[st] != 0u));
     }
   }
   PPROF(4);

@@ -195,6 +195,10 @@ struct SState {
   // by tick parity (the count of tick t+1 is zeroed during tick t); nullptr: fast path off
   uint32_t *fb_cnt;             // [2]
   int2 *fb_list;                // [nb * n]: (band, row)
+  // gm_s_pick0 (single context, B = 1024): rows whose first 16 S2 outputs do not finish their draw go
+  // to this list, which gm_s_pick then takes from output 0 (nullptr: gm_s_pick takes every row)
+  int32_t *pk_list;             // [n]
+  uint32_t *pk_cnt;
   int lag_hmin;                 // a present cell with h < lag_hmin sets GM_ERR_LAG: 3 (lag > 125 ticks, the
                                 // encoding's limit); the diagnostics env GM_LAG_CAP=L (L >= 15) lowers it to lag > L
 };

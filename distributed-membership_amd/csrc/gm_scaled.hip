@@ -1485,13 +1485,24 @@ __device__ __forceinline__ uint32_t gm_mt_batch(GmLazyMT &mt, uint32_t *mts, uin
 // ------------------------------------------------------------------- gm_s_pick
 // Single-context tick, phase 2: one wave per observer row.
 template <int B>
+__device__ __forceinline__ void pick_row(const SState &s, int t, int r, int wave, int lane);
+template <int B>
 // 6 waves per SIMD (80 VGPRs, no spills) rather than the compiler's 5 (89): the kernel waits on
 // dependent loads, 141 -> 125 us per S-A tick (profiles/r04/pick_occupancy/)
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) void gm_s_pick(SState s, int t) {
-  extern __shared__ __align__(16) uint32_t p_smem[];
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) void gm_s_pick(SState s, int t, int listed) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int r = blockIdx.x * 4 + wave;
-  if (r >= s.n) return;  // whole wave; no workgroup barrier follows
+  if (!listed) {
+    const int r = blockIdx.x * 4 + wave;
+    if (r < s.n) pick_row<B>(s, t, r, wave, lane);  // whole wave; no workgroup barrier follows
+    return;
+  }
+  // listed: the rows gm_s_pick0 left (its list, any order: each row's draw is its own), grid-stride
+  const int cnt = (int)*s.pk_cnt;
+  for (int i = blockIdx.x * 4 + wave; i < cnt; i += gridDim.x * 4) pick_row<B>(s, t, s.pk_list[i], wave, lane);
+}
+template <int B>
+__device__ __forceinline__ void pick_row(const SState &s, int t, int r, int wave, int lane) {
+  extern __shared__ __align__(16) uint32_t p_smem[];
   uint32_t *pre = p_smem + wave * gm_draw_lds_words(s.wp, B);
   uint32_t *mts = pre + gm_draw_chunks(s.wp, B) + 1;
   const int par = t & 1;
@@ -1588,6 +1599,170 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
     stat[0] = k;
     stat[1] = (int)size;
     stat[2] = (int)numfailed;
+    stat[3] = n;
+  }
+}
+
+__device__ __forceinline__ int row16_scan(int v) {  // inclusive scan within each 16-lane DPP row
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);  // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);  // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);  // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);  // row_shr:8
+  return v;
+}
+__device__ __forceinline__ int row16_bcast(int v, int g, int q) { return __shfl(v, 16 * g + q, 64); }
+__device__ __forceinline__ uint32_t row16_bits(uint64_t bal, int g) { return (uint32_t)(bal >> (16 * g)) & 0xFFFFu; }
+
+// Single-context tick, phase 2, four rows per wave (16 lanes per row), B = 1024, no join ramp: the
+// draw of MP1Node.cpp:449-489 over the row's first 16 S2 outputs (lane q: output q), each ok draw
+// resolved in draw order by a 16-ary search of a band prefix in LDS, the band record's 8 chunk
+// counts and one 128-cell chunk read by the row's 16 lanes, and accepted unless it is "me", stale or
+// a repeat. Rows the 16 outputs do not finish go to s.pk_list for gm_s_pick (from output 0). Same
+// results as gm_s_pick at a fraction of its instructions.
+template <int B>
+__global__ __launch_bounds__(256) void gm_s_pick0(SState s, int t) {
+  static_assert(B == 1024, "8 rank-select chunks of 128 columns per band");
+  extern __shared__ __align__(16) uint32_t p_smem[];
+  const int lane = threadIdx.x & 63, g = lane >> 4, q = lane & 15;
+  const int slot = (int)(threadIdx.x >> 4);  // row slot of the workgroup (0..15)
+  const int r = (int)blockIdx.x * 16 + slot;
+  const bool valid = r < s.n;
+  const int rc = valid ? r : s.n - 1;
+  const int nb = s.nb, perb = (nb + 15) >> 4, par = t & 1;
+  uint32_t *bpre = p_smem + (size_t)slot * (nb + 1);
+  const int k = s.inbox_cnt[par][rc], failed = s.failed[rc];
+  const uint32_t raw = s.mtraw[(size_t)rc * S_MT_RAW + q];
+  uint32_t bp = 0, bf = 0;
+  for (int kb = 0; kb < perb; kb++) {
+    const int b = q * perb + kb;
+    if (b < nb) {
+      const uint32_t z = s.brec[(size_t)b * s.n + rc].z;
+      bp += S_BC_PRES(z);
+      bf += S_BC_FAIL(z);
+    }
+  }
+  const int bi = row16_scan((int)bp), fi = row16_scan((int)bf);
+  const uint32_t size = (uint32_t)row16_bcast(bi, g, 15);
+  const int numfailed = row16_bcast(fi, g, 15);  // counts removed entries too (MP1Node.cpp:463)
+  {
+    uint32_t a = (uint32_t)bi - bp;
+    for (int kb = 0; kb < perb; kb++) {
+      const int b = q * perb + kb;
+      if (b < nb) {
+        bpre[b] = a;
+        a += S_BC_PRES(s.brec[(size_t)b * s.n + rc].z);
+      }
+    }
+    if (q == 15) bpre[nb] = (uint32_t)bi;
+  }
+  const bool live = valid && !failed;
+  const int numpot = (int)size - 1 - numfailed;
+  const int target = min(GM_FANOUT, numpot);
+  const bool pend = live && numpot > 0;
+  const uint32_t sz = pend ? size : 1u;
+  const uint32_t thr = (0u - sz) % sz;  // Lemire rejection threshold (uniform_int_dist.h)
+  const uint64_t prod = (uint64_t)raw * sz;
+  const uint32_t ix = (uint32_t)(prod >> 32);
+  uint32_t okm = row16_bits(__ballot(pend && (uint32_t)prod >= thr), g);  // the row's draws, in order
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  int n = 0, g0 = -1, g1 = -1, g2 = -1, g3 = -1, g4 = -1;  // row-uniform (every lane of the row)
+  bool done = !pend;
+  while (__ballot(!done && okm != 0)) {
+    const bool act = !done && okm != 0;
+    const int d = act ? __builtin_ctz(okm) : 0;
+    okm &= okm - 1;
+    const uint32_t x = (uint32_t)row16_bcast((int)ix, g, d);
+    int lo = 0, span = nb;
+    while (__ballot(act && span > 1)) {  // 16-ary search: the band b with bpre[b] <= x < bpre[b + 1]
+      const int step = (span + 15) >> 4;
+      const bool le = act && q * step < span && bpre[lo + q * step] <= x;
+      const int c = __builtin_popcount(row16_bits(__ballot(le), g));
+      if (act && span > 1) {
+        lo += (max(c, 1) - 1) * step;
+        span = min(step, span - (max(c, 1) - 1) * step);
+      }
+    }
+    const int band = lo;
+    uint32_t rem = act ? x - bpre[band] : 0u;
+    const uint4 rec = act ? s.brec[(size_t)band * s.n + rc] : make_uint4(0u, 0u, 0u, 0u);
+    const uint64_t cc = (uint64_t)rec.x | ((uint64_t)rec.y << 32);
+    int ch = 0;
+#pragma unroll
+    for (int kc = 0; kc < 7; kc++) {
+      const uint32_t c8 = (uint32_t)(cc >> (8 * ch)) & 0xFFu;
+      if (rem >= c8 && ch == kc) {
+        rem -= c8;
+        ch++;
+      }
+    }
+    uint2 w = make_uint2(0u, 0u);
+    if (act) w = *(const uint2 *)(s.table + ((size_t)band * s.n + rc) * B + ch * 128 + q * 8);
+    auto nzb = [](uint32_t v) { return (v | (v >> 1) | (v >> 2) | (v >> 3) | (v >> 4) | (v >> 5) | (v >> 6) | (v >> 7)) & 0x01010101u; };
+    const int cnt = __builtin_popcount(nzb(w.x)) + __builtin_popcount(nzb(w.y));
+    const int incl = row16_scan(cnt);
+    const int excl = incl - cnt;
+    const bool holder = act && (int)rem >= excl && (int)rem < incl;
+    int col = -1, fr = 0;
+    if (holder) {  // the (rem - excl)-th present cell of the lane's 8
+      int need = (int)rem - excl, pos = 0;
+      uint32_t byte = 0;
+#pragma unroll
+      for (int v = 0; v < 8; v++) {
+        const uint32_t bv = ((v < 4 ? w.x : w.y) >> (8 * (v & 3))) & 0xFFu;
+        if (bv != 0) {
+          if (need == 0) { pos = v; byte = bv; }
+          need--;
+        }
+      }
+      col = band * B + ch * 128 + q * 8 + pos;
+      fr = s_is_esc(byte) ? esc_fresh(s, rc, col) : S_AGE(s_widen(byte)) < GM_TFAIL;
+    }
+    const uint32_t hm = row16_bits(__ballot(holder), g);
+    const int src = hm ? __builtin_ctz(hm) : 0;
+    const int c = row16_bcast(col, g, src);
+    const int f = row16_bcast(fr, g, src);
+    if (act) {
+      if (!hm) {  // a draw no chunk resolved: counts and cells disagree
+        if (q == 0) atomicOr(s.err, GM_ERR_DRAWS);
+        done = true;
+      } else if (c != r && f && !((n > 0 && g0 == c) || (n > 1 && g1 == c) || (n > 2 && g2 == c) || (n > 3 && g3 == c))) {
+        if (n == 0) g0 = c;  // "me" (MP1Node.cpp:459-460,470), age >= TFAIL (:471), repeats skipped
+        else if (n == 1) g1 = c;
+        else if (n == 2) g2 = c;
+        else if (n == 3) g3 = c;
+        else g4 = c;
+        n++;
+        if (n >= target) done = true;
+      }
+    }
+  }
+  if (!valid) return;
+  int32_t *stat = s.rowstat + (size_t)r * 4;
+  if (!live) {
+    if (q == 0) {
+      s.inbox_cnt[par][r] = 0;
+      stat[0] = stat[1] = stat[2] = stat[3] = 0;
+    }
+    return;
+  }
+  if (pend && n < target) {  // more than 16 outputs needed: gm_s_pick takes the row (it resets the inbox count)
+    if (q == 0) s.pk_list[atomicAdd(s.pk_cnt, 1u)] = r;
+    return;
+  }
+  if (q == 0) s.inbox_cnt[par][r] = 0;  // consumed by gm_s_band; the append target of tick t+2
+  if (q < n) {  // delivery: one target per lane (an inbox's order is free: the merge is a max)
+    const int dst = q == 0 ? g0 : q == 1 ? g1 : q == 2 ? g2 : q == 3 ? g3 : g4;
+    s.targets[(size_t)r * GM_FANOUT + q] = dst;
+    const int sl = atomicAdd(&s.inbox_cnt[par ^ 1][dst], 1);
+    if (sl < s.kcap) s.inbox[par ^ 1][(size_t)dst * S_KMAX + sl] = r;
+    else atomicOr(s.err, GM_ERR_INBOX);
+  }
+  if (q == 0) {
+    stat[0] = k;
+    stat[1] = (int)size;
+    stat[2] = numfailed;
     stat[3] = n;
   }
 }
@@ -1690,16 +1865,6 @@ hipError_t gm_launch_xrows(const SState &s, int r0, int r1, hipStream_t st) {
 // of the bands, the band record's 8 chunk counts and one 128-cell chunk read by the row's 16 lanes
 // (8 bytes each, SWAR counts, a DPP prefix). Not for the join ramp (gm_s_draw handles it); needs
 // G <= 16 ranks and B = 1024 (8 rank-select chunks per band).
-__device__ __forceinline__ int row16_scan(int v) {  // inclusive scan within each 16-lane DPP row
-  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);  // row_shr:1
-  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);  // row_shr:2
-  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);  // row_shr:4
-  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);  // row_shr:8
-  return v;
-}
-__device__ __forceinline__ int row16_bcast(int v, int g, int q) { return __shfl(v, 16 * g + q, 64); }
-__device__ __forceinline__ uint32_t row16_bits(uint64_t bal, int g) { return (uint32_t)(bal >> (16 * g)) & 0xFFFFu; }
-
 template <int B>
 __global__ __launch_bounds__(256) void gm_s_draw0(SState s, int t, int r0, int r1) {
   static_assert(B == 1024, "8 rank-select chunks of 128 columns per band");
@@ -2170,7 +2335,14 @@ static hipError_t launch_tick_b(const SState &s, int t, int drop_pct, hipStream_
     (void)hipMemsetAsync(s.selfadd_cnt, 0, sizeof(uint32_t), st);
   }
   const size_t smem = sizeof(uint32_t) * 4 * gm_draw_lds_words(s.wp, s.band);
-  if (pick) hipLaunchKernelGGL((gm_s_pick<B>), dim3((s.n + 3) / 4), dim3(256), smem, st, s, t);
+  if (pick && B == 1024 && s.pk_list && !s.ramp) {  // four rows per wave, then the rows it left
+    (void)hipMemsetAsync(s.pk_cnt, 0, sizeof(uint32_t), st);
+    hipLaunchKernelGGL((gm_s_pick0<B == 1024 ? B : 1024>), dim3((s.n + 15) / 16), dim3(256),
+                       sizeof(uint32_t) * 16 * (size_t)(s.nb + 1), st, s, t);
+    hipLaunchKernelGGL((gm_s_pick<B>), dim3(256), dim3(256), smem, st, s, t, 1);
+  } else if (pick) {
+    hipLaunchKernelGGL((gm_s_pick<B>), dim3((s.n + 3) / 4), dim3(256), smem, st, s, t, 0);
+  }
   return hipGetLastError();
 }
 
