@@ -650,9 +650,6 @@ static int create_partial(gm_ctx *c) {
     c->p_chev.assign(p.nchunk, nullptr);
     for (hipEvent_t &e : c->p_chev) HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIPCHECK(hipEventCreateWithFlags(&c->p_done, hipEventDisableTiming));
-    TRY(dalloc(c, &p.sp_hdr, (size_t)G * nl * 8));
-    TRY(dalloc(c, &p.sp_list, (size_t)G * nl * p.V));
-    HIPCHECK(ctx_memset(c, p.sp_hdr, 0xFF, sizeof(int32_t) * G * nl * 8));  // stamp -1: no record yet
     TRY(dalloc(c, &p.pk_hdr, (size_t)G * nl * 8));
     TRY(dalloc(c, &p.pk_list, (size_t)G * nl * p.V));
     HIPCHECK(ctx_memset(c, p.pk_hdr, 0xFF, sizeof(int32_t) * G * nl * 8));
@@ -2236,14 +2233,13 @@ static int draw_settle(gm_ctx *c) {
 }
 
 // ------------------------------------------------------------ PARTIAL row shards
-// After chunk c's local kernels of tick t every shard holds, at the fixed slots (q, li) of
-// sp_hdr / sp_list, the records its nodes of rows [r0_c, r1_c) address to shard q. The exchange
-// sends each such block whole (no counts, no packing, no host round trip: every size is fixed by
-// the shard layout) with two all-to-allv -- headers, then lists (wire format) into recv_list[t&1],
-// where tick t+1 reads its senders' lists -- and gm_p_unpack appends each received record whose
-// stamp is t to its targets' inboxes (a slot without a record of this tick is skipped). A shard
-// thus moves its whole slot range per tick, ~2x the records it has (a sender addresses a given
-// peer with probability 1 - (1 - 1/G)^5: 0.49 at G = 8), over xGMI, while later chunks compute.
+// After chunk c's local kernels of tick t, gm_p_pack (on the comm stream) builds the records the
+// chunk's nodes address to each other shard q -- from their targets and their final lists of the
+// tick, no record written by the node kernels -- packed to the front of block (q, r0_c), whose
+// capacity every rank knows (xcap). The exchange sends the blocks with two all-to-allv -- headers,
+// then lists (wire format) into recv_list[t&1], where tick t+1 reads its senders' lists -- and
+// gm_p_unpack appends each received record whose stamp is t to its targets' inboxes (rows of a block
+// past its records keep older stamps), while later chunks compute. No host round trip.
 // Capacity of a packed block (gm_p_pack): the records one chunk of `rows` senders addresses to
 // shard q. A sender's five targets are drawn from its view; with a fraction f_q of the view's
 // entries on shard q it addresses q with probability 1 - (1 - f_q)^5, so the block's record count is

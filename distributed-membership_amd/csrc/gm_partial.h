@@ -46,13 +46,10 @@ struct PState {
   int32_t *big_cnt;      // [K]
   int32_t *huge;         // [nloc] worklists of nodes with > P_KP lists (huge-table kernel), chunk c at rows r0_c..
   int32_t *huge_cnt;     // [K]
-  // outgoing lists to the other row shards (sharded only): one record per (sender, remote rank)
-  // at the fixed slot (q, li) of these buffers -- no contended counters, no packing: chunk c's
-  // slots to shard q, rows [r0_c, r1_c), go out as one fixed-size block of the all-to-allv (every
-  // size and offset is known on the host from the shard layout: no host round trip), and the
-  // header's stamp (word 7 = the tick) tells the receiver which slots hold a record of this tick
-  int32_t *sp_hdr;       // [G][nloc][8]: sender global index, #targets on that rank, targets (global), stamp t
-  uint32_t *sp_list;     // [G][nloc][V]: the sender's fresh entries of the tick, wire format
+  // outgoing lists to the other row shards (sharded only): after chunk c's node kernels, gm_p_pack
+  // builds one record per (sender, remote shard) from the sender's targets and its final list of the
+  // tick, packed per peer (below); the header's stamp (word 7 = the tick) tells the receiver which
+  // rows of a block hold a record of this tick
   int32_t *recv_hdr;     // [n - nloc][8] received headers: chunk-major, source shard ascending
   uint32_t *recv_list[2]; // [n - nloc][V] received lists (wire format), by the parity of the tick that
                          //   sent them; the next tick's kernels decode them in place

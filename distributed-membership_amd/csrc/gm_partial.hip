@@ -17,13 +17,10 @@
 //      its inbox (sender indices), its 16 precomputed S2 outputs, then every
 //      delivered list (V lanes per list, several lists per wave step);
 //   2. merge into an open-addressing LDS table keyed by id (32-bit CAS claim +
-//      ds_max of the heartbeat word), the own list in the same step as the first
-//      delivered list (own entries set an "own" bit), delivered entries filtered
-//      to fresh + not dropped. The lane that CLAIMS an id's slot holds that id
-//      from then on: the union is the set of claimers, in registers (round 5: no
-//      sweep of the 512-slot table, no compaction, no dense re-read);
-//   3. self bump; every claimer reads its slot's merged entry back (TREMOVE
-//      removals counted and logged on the way);
+//      ds_max of the heartbeat word), own entries first so they carry the
+//      "own" bit, delivered entries filtered to fresh + not dropped;
+//   3. self bump, then one sweep compacts the table in place into a dense
+//      array (TREMOVE removals counted and logged on the way);
 //   4. eviction to V only when the union exceeds V: an LDS histogram of the
 //      heartbeat distance from the top finds the cut heartbeat; inside the cut
 //      bucket a 6-bit radix histogram of the eviction keys and (rarely) an
@@ -135,6 +132,22 @@ __device__ __forceinline__ uint64_t p_readlane64(uint64_t v, int l) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+// claim or find the slot of `id` (idw = id | flags on claim), raise its heartbeat word
+template <int H>
+__device__ __forceinline__ int p_insert(uint32_t *tid, uint32_t *thb, uint32_t id, uint32_t idw, uint32_t hb) {
+  // slot = low bits of id ^ id >> 9: view ids are uniform node indices, so this spreads them like a
+  // multiplicative hash without its quarter-rate 32-bit multiply (the slot never shows in a result:
+  // the table is compacted and ranked by id)
+  uint32_t h = (id ^ (id >> 9)) & (H - 1);
+  for (;;) {  // claim-or-compare in one LDS op
+    const uint32_t cur = atomicCAS(&tid[h], 0u, idw);
+    if (cur == 0 || (cur & P_IDMASK) == id) break;
+    h = (h + 1) & (H - 1);
+  }
+  atomicMax(&thb[h], hb);
+  return (int)h;
+}
+
 // owning row shard of node d: contiguous balanced ranges [n*g/G, n*(g+1)/G), boundaries
 // in shard_n0[0..G]; a float estimate is off by at most one, two compares fix it
 __device__ __forceinline__ int p_owner(const PState &s, int d) {
@@ -219,9 +232,11 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
                                        int chunk, int r0) {
   int k = pre.k;
   const int i = s.n0 + li;  // global node index (ids, keys, seeds, targets)
+  constexpr int TS = H / 64;                          // table slots per lane
   constexpr int KK = H == P_HH ? P_KMAX : BIG ? P_KP : P_KSMALL;  // lists merged at most
-  constexpr int NS = (KK + 2) / 2;  // merge steps: the own list + KK lists, >= 2 list slots per step
-  using mask_t = typename std::conditional<(NS > 32), uint64_t, uint32_t>::type;  // one bit per step
+  constexpr int DS = ((1 + KK) * P_VMAX + 63) / 64;   // dense entries per lane
+  constexpr int NSTEP = (KK + 1) / 2;                 // list-load steps (>= 2 lists per step)
+  using mask_t = typename std::conditional<(DS > 32), uint64_t, uint32_t>::type;  // one bit per dense slot
 #ifdef GM_P_PROFILE
   uint64_t pp_[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, pt_ = __builtin_amdgcn_s_memtime();
 #endif
@@ -242,9 +257,7 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
     if (lane == 0) atomicOr(s.err, GM_ERR_INBOX);
     k = kmax;  // never read sender slots that were not written
   }
-  // ---- 1. loads (the independent ones arrived with `pre`). List slots: slot 0 = the node's own
-  // list, slot j + 1 = delivered list j; one merge step covers `per` consecutive slots (a half-wave
-  // each at V = 32), so the own list shares the first step with delivered list 0
+  // ---- 1. loads (the independent ones arrived with `pre`)
   const uint64_t own = pre.own;
   int sv = lane < k ? pre.sv : 0x7FFFFFFF;  // list rows
   const uint32_t raw0 = pre.raw0;
@@ -255,7 +268,7 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
     for (int q = 0; q < H / 128; q++) z[lane + 64 * q] = make_uint4(0, 0, 0, 0);
   }
   const int kk = min(k, KK);
-  // lists per step (per), entry (l) and slot in the step (jo) of this lane; V = 32 (S-C) takes the
+  // lists per load step (per), entry (l) and list slot (jo) of this lane; V = 32 (S-C) takes the
   // shifts instead of three integer divisions. The step's per-list values come by ds_bpermute
   // (the LDS port) rather than two readlanes + a select: VALU issue is what bounds this kernel
   const bool v32 = V == P_VMAX;
@@ -269,16 +282,14 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
     l = lane % V;
     jo = lane / V;
   }
-  const int nst = (kk + per) / per;  // active steps: ceil((1 + kk) / per), wave-uniform
-  // the value v holds on the lane of delivered list slot - 1
-  auto step_val = [&](int v, int st) -> int { return __shfl(v, min(max(st * per + jo - 1, 0), 63), 64); };
-  uint64_t dv[NS];
+  auto step_val = [&](int v, int st) -> int { return __shfl(v, min(st * per + jo, 63), 64); };  // v of lane st * per + jo
+  uint64_t dv[NSTEP];
 #pragma unroll
-  for (int st = 0; st < NS; st++) {
-    const int j = st * per + jo - 1;  // delivered list of this lane's slot (-1: the own list)
-    const bool ok = jo < per && j >= 0 && j < kk;
+  for (int st = 0; st < NSTEP; st++) {
+    const int j = st * per + jo;
+    const bool ok = jo < per && j < kk;
     const int sn = step_val(sv, st);
-    uint64_t e = (st == 0 && jo == 0) ? own : 0ull;
+    uint64_t e = 0;
     if (ok && (!RM || sn < s.nloc)) {
       e = prev[(size_t)sn * V + l];
     } else if (RM && ok) {  // a list another shard sent at t-1: wire entry id | (2(t-1)-1 - hb) << 25
@@ -300,120 +311,144 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
   const uint32_t dthr = gm_drop_thresh(s.drop_pct);
   PPROF(0);
   p_wsync();
-  // ---- 2. merge: every entry into the table by id (32-bit CAS claim, ds_max of the heartbeat
-  // word); own entries set the "own" bit (after the claim when a delivered copy of the id in the
-  // same step claimed it first). The lane that claims an id's slot holds the id from then on: the
-  // union is the set of claimers, so the table is never swept or compacted
+  // ---- 2. merge: own entries first (they carry P_OWN), then the delivered lists
+  int hslot = -1;
   const uint32_t self_id = (uint32_t)(i + 1);
-  int csl[NS];    // this lane's claimed slot per step (-1: none)
-  int hself = -1;  // the slot of the node's own entry (on its own-list lane)
+  if (own != 0) {
+    const uint32_t id = (uint32_t)(own >> 32);
+    hslot = p_insert<H>(tid, thb, id, id | P_OWN, (uint32_t)own);
+  }
+  PPROF(1);
+  p_wsync();
   {
     const uint32_t tfresh = (uint32_t)max(0, 2 * t - 11);  // hb >= 2t-11 <=> (t-1) - (hb+1)/2 < TFAIL
 #pragma unroll
-    for (int st = 0; st < NS; st++) {
-      csl[st] = -1;
-      if (st >= nst) continue;
+    for (int st = 0; st < NSTEP; st++) {
       const uint64_t e = dv[st];
-      const bool isown = st == 0 && jo == 0;
+      bool take = e != 0 && (uint32_t)e >= tfresh;
       const uint32_t id = (uint32_t)(e >> 32);
-      bool take = e != 0 && (isown || (uint32_t)e >= tfresh);
-      if (dropping && __ballot(take && !isown)) {  // per-entry drops keyed by (t_send, src, dst, id-1): lost
-        // iff the top 16 bits of fmix32(pair ^ (id-1)) are below the threshold
+      if (dropping && __ballot(take)) {  // per-entry drops keyed by (t_send, src, dst, id-1): lost iff the
+        // top 16 bits of fmix32(pair ^ (id-1)) are below the threshold
         const uint32_t pair = (uint32_t)step_val((int)pairv, st);
-        take = take && (isown || (gm_fmix32(pair ^ (id - 1)) >> 16) >= dthr);
+        take = take && (gm_fmix32(pair ^ (id - 1)) >> 16) >= dthr;
       }
-      if (take) {
-        // slot = low bits of id ^ id >> 9: view ids are uniform node indices, so this spreads them like a
-        // multiplicative hash without its quarter-rate multiply (the slot never shows in a result)
-        uint32_t h = (id ^ (id >> 9)) & (H - 1);
-        uint32_t cur;
-        for (;;) {  // claim-or-compare in one LDS op
-          cur = atomicCAS(&tid[h], 0u, isown ? (id | P_OWN) : id);
-          if (cur == 0 || (cur & P_IDMASK) == id) break;
-          h = (h + 1) & (H - 1);
-        }
-        atomicMax(&thb[h], (uint32_t)e);
-        if (cur == 0) csl[st] = (int)h;
-        else if (isown) atomicOr(&tid[h], P_OWN);
-        if (isown && id == self_id) hself = (int)h;
-      }
-      if (mc) nrecv += __builtin_popcountll(__ballot(take && !isown));
+      if (take) (void)p_insert<H>(tid, thb, id, id, (uint32_t)e);
+      if (mc) nrecv += __builtin_popcountll(__ballot(take));
     }
   }
   PPROF(2);
   p_wsync();
-  // ---- 3. self bump (heartbeat++; myPos->setheartbeat(heartbeat++))
+  // ---- 3. self bump (heartbeat++; myPos->setheartbeat(heartbeat++)), then sweep + compaction
   {
-    const uint64_t sb = __ballot(hself >= 0);
+    const uint64_t sb = __ballot(own != 0 && (uint32_t)(own >> 32) == self_id);
+    int hs;
     if (sb) {
-      const int hs = __builtin_amdgcn_readlane(hself, __builtin_ctzll(sb));
+      hs = __builtin_amdgcn_readlane(hslot, __builtin_ctzll(sb));
+    } else {  // cannot happen for a live node (the oracle aborts): flag, and re-insert self
+      hs = 0;
       if (lane == 0) {
-        thb[hs] = (uint32_t)hbnew;
-        tid[hs] |= P_SELF | P_OWN;
+        atomicOr(s.err, GM_ERR_SELF);
+        hs = p_insert<H>(tid, thb, self_id, self_id | P_OWN, 1u);
       }
-    } else if (lane == 0) {  // cannot happen for a live node (the oracle aborts): the tick is void
-      atomicOr(s.err, GM_ERR_SELF);
+      hs = __builtin_amdgcn_readfirstlane(hs);
     }
-    if (lane == 0) s.hbctr[li] = hbnew + 1;
+    if (lane == 0) {
+      thb[hs] = (uint32_t)hbnew;
+      tid[hs] |= P_SELF | P_OWN;
+      s.hbctr[li] = hbnew + 1;
+    }
   }
   PPROF(3);
   p_wsync();
-  // ---- 4. the union: each claimer reads its slot's merged entry back. alive <=> not aged past
-  // TREMOVE <=> hb >= xa (heartbeats are odd, >= 1); the aged ones are own entries (delivered
-  // entries are fresh) and are removed with a REMOVE event (rare: one ballot per step)
   uint32_t *evr = s.ev + (size_t)li * 2 * V;
-  int m = 0, removed = 0, nrem = 0;
-  uint32_t cw[NS], ch[NS];  // the union's entries held by this lane: id word (0: none), heartbeat
+  int m, removed, nrem;
   {
-    const uint32_t xa = (uint32_t)max(2 * (t - GM_TREMOVE) + 1, 1);
-    uint32_t deadm = 0;  // steps whose claimed entry this lane drops (aged past TREMOVE)
-    int mloc = 0;
+    uint32_t w[TS], hh[TS];
 #pragma unroll
-    for (int st = 0; st < NS; st++) {  // branch-free per step: a non-claimer reads slot 0 and drops it
-      cw[st] = ch[st] = 0u;
-      if (st >= nst) continue;
-      const int sl = max(csl[st], 0);
-      const uint32_t w = csl[st] >= 0 ? tid[sl] : 0u;
-      const uint32_t hh = thb[sl];
-      const bool dead = w != 0u && hh < xa;
-      deadm |= (uint32_t)dead << st;
-      cw[st] = dead ? 0u : w;
-      ch[st] = hh;
-      mloc += cw[st] != 0u;
+    for (int q = 0; q < TS / 4; q++) {
+      const uint4 a = ((const uint4 *)tid)[lane * (TS / 4) + q];
+      const uint4 b = ((const uint4 *)thb)[lane * (TS / 4) + q];
+      w[4 * q] = a.x; w[4 * q + 1] = a.y; w[4 * q + 2] = a.z; w[4 * q + 3] = a.w;
+      hh[4 * q] = b.x; hh[4 * q + 1] = b.y; hh[4 * q + 2] = b.z; hh[4 * q + 3] = b.w;
     }
-    m = __builtin_amdgcn_readlane(p_scan(mloc, lane), 63);
-    if (__ballot(deadm != 0)) {  // rare: TREMOVE removals (own entries) -- REMOVE events from the back
+    using tmask_t = typename std::conditional<(TS > 32), uint64_t, uint32_t>::type;  // one bit per table slot
+    constexpr int CB = TS <= 8 ? 4 : TS <= 16 ? 5 : TS <= 32 ? 6 : 7;               // bits of a per-lane slot count
+    // alive <=> present and not aged past TREMOVE <=> hb >= xa: every present entry has hb >= 1
+    // (heartbeats start at 2t-1 >= 1; hb < 2^31) and an empty slot holds hb 0, so one compare per
+    // slot gives the alive bit; removals = present - alive (rare: tested once per row)
+    const uint32_t xa = (uint32_t)max(2 * (t - GM_TREMOVE) + 1, 1);
+    tmask_t alive = 0, rown = 0;
+    int rcount = 0;
 #pragma unroll
-      for (int st = 0; st < NS; st++) {
-        if (st >= nst) continue;
-        const bool dead = (deadm >> st) & 1;
-        const uint32_t w = dead ? tid[max(csl[st], 0)] : 0u;
-        const uint64_t db = __ballot(dead);
-        const uint64_t ob = __ballot(dead && (w & P_OWN));
-        if (dead && (w & P_OWN)) evr[2 * V - 1 - nrem - p_below(ob)] = (P_EV_REMOVE << 30) | (w & P_IDMASK);
-        nrem += __builtin_popcountll(ob);
-        removed += __builtin_popcountll(db);
+    for (int u = 0; u < TS; u++) {  // branch-free: exec-mask traffic is what this kernel spends SALU on
+      alive |= (tmask_t)((xa - 1u - hh[u]) >> 31) << u;
+      rcount += (int)min(w[u], 1u);
+    }
+    rcount -= __builtin_popcountll(alive);
+    int tot;
+    removed = nrem = 0;
+    if (__ballot(rcount != 0)) {  // rare: TREMOVE removals in this row
+#pragma unroll
+      for (int u = 0; u < TS; u++) rown |= (tmask_t)((w[u] >> 31) & (uint32_t)!((alive >> u) & 1)) << u;
+      (void)p_excl<CB>(rcount, &removed);
+      const int ro = __builtin_popcountll(rown);
+      int rpos = p_excl<CB>(ro, &nrem);
+      if (nrem) {  // REMOVE events of the node's own entries, from the back of its event row
+#pragma unroll
+        for (int u = 0; u < TS; u++)
+          if ((rown >> u) & 1) evr[2 * V - 1 - rpos++] = (P_EV_REMOVE << 30) | (w[u] & P_IDMASK);
       }
+    }
+    // the alive slots' dense positions: an inclusive DPP scan of the per-lane counts (A/B on one box
+    // against p_excl's ballot per count bit: -0.3 %, profiles/r04/sc_sweep/)
+    const int na = __builtin_popcountll(alive);
+    const int incl = p_scan(na, lane);
+    tot = __builtin_amdgcn_readlane(incl, 63);
+    int pos = incl - na;
+    m = tot;
+    // every slot is stored: dead ones to a per-lane slot of [H-64, H), past the dense
+    // range (m <= (1+KK)V+1 < H-64) and free of bank conflicts
+#pragma unroll
+    for (int u = 0; u < TS; u++) {
+      const bool a = (alive >> u) & 1;
+      const int at = a ? pos : H - 64 + lane;
+      tid[at] = w[u];
+      thb[at] = hh[u];
+      pos += a;
     }
   }
   PPROF(4);
-  // ---- 5. eviction to V (self always kept): keep bit st = this lane's step-st entry stays
+  p_wsync();
+  // ---- 4. dense entries e = s*64 + lane; eviction to V
+  // only the first dm = ceil(m / 64) of the DS per-lane slots hold entries (m is wave-uniform):
+  // every per-slot loop below skips the rest with a scalar branch
+  const int dm = (m + 63) >> 6;
+  uint32_t dw[DS], dh[DS];
+#pragma unroll
+  for (int q = 0; q < DS; q++) {  // DS*64 < H: the reads stay inside the table
+    dw[q] = dh[q] = 0u;
+    if (q < dm) {
+      const int e = q * 64 + lane;
+      const uint32_t a = tid[e], b = thb[e];
+      dw[q] = e < m ? a : 0u;
+      dh[q] = e < m ? b : 0u;
+    }
+  }
   mask_t keep = 0;
   if (m <= V) {
 #pragma unroll
-    for (int st = 0; st < NS; st++)
-      if (st < nst && cw[st]) keep |= (mask_t)1 << st;
+    for (int q = 0; q < DS; q++)
+      if (q < dm && dw[q]) keep |= (mask_t)1 << q;
   } else {
     // heartbeat distance from the top (2t-1 = this tick's self heartbeat); alive
-    // entries have age < TREMOVE, i.e. distance <= 40 < 64. The table is dead now: its last
-    // 64 words take the histogram adds of the entries that do not count
+    // entries have age < TREMOVE, i.e. distance <= 40 < 64
     const int top = 2 * t - 1;
     hist[lane] = 0;
     p_wsync();
 #pragma unroll
-    for (int st = 0; st < NS; st++)
-      if (st < nst)
-        atomicAdd((cw[st] && !(cw[st] & P_SELF)) ? &hist[min(max(top - (int)ch[st], 0), 63)] : &tid[H - 64 + lane], 1u);
+    for (int q = 0; q < DS; q++)  // entries that do not count go to a private trash word
+      if (q < dm)
+        atomicAdd((dw[q] && !(dw[q] & P_SELF)) ? &hist[min(max(top - (int)dh[q], 0), 63)] : &tid[H - 64 + lane], 1u);
     p_wsync();
     const int need = V - 1;  // self is always kept
     int c = (int)hist[lane];
@@ -425,12 +460,12 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
     const int needb = need - before;  // 1 <= needb <= bsz
     mask_t bucket = 0;
 #pragma unroll
-    for (int st = 0; st < NS; st++) {
-      if (st >= nst) continue;
-      const int d = min(max(top - (int)ch[st], 0), 63);
-      const mask_t v = cw[st] != 0;
-      keep |= (v & (mask_t)(((cw[st] & P_SELF) != 0) | (d < dcut))) << st;
-      bucket |= (v & (mask_t)(!(cw[st] & P_SELF) && d == dcut)) << st;
+    for (int q = 0; q < DS; q++) {
+      if (q >= dm) continue;
+      const int d = min(max(top - (int)dh[q], 0), 63);
+      const mask_t v = dw[q] != 0;
+      keep |= (v & (mask_t)(((dw[q] & P_SELF) != 0) | (d < dcut))) << q;
+      bucket |= (v & (mask_t)(!(dw[q] & P_SELF) && d == dcut)) << q;
     }
 #ifdef GM_P_PROFILE
     pp_[10] += 1;  // evictions
@@ -443,19 +478,18 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
       // the needb smallest eviction keys of the bucket: 6-bit radix on the top bits,
       // then exact min-selection inside the cut bin
       const uint32_t oseed = (uint32_t)gm_mix64(gm_mix64(s.view_seed ^ (uint64_t)(uint32_t)t) ^ (uint64_t)(uint32_t)i);
-      uint32_t key[NS];
+      uint32_t key[DS];
 #pragma unroll
-      for (int st = 0; st < NS; st++) {
-        key[st] = ~0u;
-        if (st < nst && __ballot((bucket >> st) & 1))
-          key[st] = ((bucket >> st) & 1) ? p_evict_key(oseed, cw[st] & P_IDMASK) : ~0u;
+      for (int q = 0; q < DS; q++) {
+        key[q] = ~0u;
+        if (q < dm && __ballot((bucket >> q) & 1)) key[q] = ((bucket >> q) & 1) ? p_evict_key(oseed, dw[q] & P_IDMASK) : ~0u;
       }
       p_wsync();
       hist[lane] = 0;
       p_wsync();
 #pragma unroll
-      for (int st = 0; st < NS; st++)
-        if (st < nst) atomicAdd(((bucket >> st) & 1) ? &hist[key[st] >> 26] : &tid[H - 64 + lane], 1u);
+      for (int q = 0; q < DS; q++)
+        if (q < dm) atomicAdd(((bucket >> q) & 1) ? &hist[key[q] >> 26] : &tid[H - 64 + lane], 1u);
       p_wsync();
       c = (int)hist[lane];
       inc = p_scan(c, lane);
@@ -466,12 +500,12 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
       int needc = needb - before2;  // 1 <= needc <= bsz2
       mask_t cand = 0;
 #pragma unroll
-      for (int st = 0; st < NS; st++) {
-        if (st >= nst) continue;
-        const mask_t b = (bucket >> st) & 1;
-        const int bin = (int)(key[st] >> 26);
-        keep |= (b & (mask_t)(bin < bcut)) << st;
-        cand |= (b & (mask_t)(bin == bcut)) << st;
+      for (int q = 0; q < DS; q++) {
+        if (q >= dm) continue;
+        const mask_t b = (bucket >> q) & 1;
+        const int bin = (int)(key[q] >> 26);
+        keep |= (b & (mask_t)(bin < bcut)) << q;
+        cand |= (b & (mask_t)(bin == bcut)) << q;
       }
       if (needc == bsz2) {
         keep |= cand;
@@ -482,34 +516,34 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
         for (; needc > 0; needc--) {  // take the smallest remaining candidate key (keys are distinct)
           uint32_t mn = ~0u;
 #pragma unroll
-          for (int st = 0; st < NS; st++)
-            if (st < nst && ((cand >> st) & 1)) mn = min(mn, key[st]);
+          for (int q = 0; q < DS; q++)
+            if (q < dm && ((cand >> q) & 1)) mn = min(mn, key[q]);
 #pragma unroll
           for (int o = 32; o >= 1; o >>= 1) mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, 64));
 #pragma unroll
-          for (int st = 0; st < NS; st++)
-            if (st < nst && ((cand >> st) & 1) && key[st] == mn) {
-              keep |= (mask_t)1 << st;
-              cand &= ~((mask_t)1 << st);
+          for (int q = 0; q < DS; q++)
+            if (q < dm && ((cand >> q) & 1) && key[q] == mn) {
+              keep |= (mask_t)1 << q;
+              cand &= ~((mask_t)1 << q);
             }
         }
       }
     }
   }
   PPROF(5);
-  // ---- 6. compact the kept entries (<= V), rank them by id
+  // ---- 5. compact the kept entries (<= V), rank them by id
   int cnt = 0;
   p_wsync();  // the eviction histogram is dead: it takes the stores of the entries not kept
 #pragma unroll
-  for (int st = 0; st < NS; st++) {
-    if (st >= nst) break;
-    const bool kq = (keep >> st) & 1;
+  for (int q = 0; q < DS; q++) {
+    if (q >= dm) break;
+    const bool kq = (keep >> q) & 1;
     const uint64_t bal = __ballot(kq);
     const int p = cnt + p_below(bal);
     // id word rotated left by 2: id << 2 | own << 1 | self (ids < 2^25, bits 25..29 clear),
     // so the rank below compares whole words
-    *(kq ? kid + p : hist + lane) = __builtin_amdgcn_alignbit(cw[st], cw[st], 30);
-    *(kq ? khb + p : hist + lane) = ch[st];
+    *(kq ? kid + p : hist + lane) = __builtin_amdgcn_alignbit(dw[q], dw[q], 30);
+    *(kq ? khb + p : hist + lane) = dh[q];
     cnt += __builtin_popcountll(bal);
   }
   if (lane >= cnt && lane < P_VMAX) kid[lane] = ~0u;  // sentinels rank after every real entry
@@ -542,8 +576,7 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
   // joins (ascending id) from the front of the event row
   const uint64_t jb = __ballot(lane < cnt && !(f & 2u));  // rotated P_OWN
   const int nj = __builtin_popcountll(jb);
-  // joins (ascending id): a mask over the final list (ev_jm, with the counts below) -- the drain
-  // reads the ids from the list itself, so no record is written per join
+  // joins (ascending id): a mask over the final list (ev_jm)
   const int numfailed = removed + __builtin_popcountll(__ballot(lane < cnt && p_aged(t, (uint32_t)x, GM_TFAIL)));
   PPROF(6);
   // ---- 6. gossip draw over the final list (MP1Node.cpp:449-489)
@@ -633,8 +666,9 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
   }
   PPROF(7);
   p_wsync();
-  // ---- sends: one parallel round of inbox appends, one lane per target; targets owned by
-  // another row shard get one record per (sender, shard): header + this tick's list
+  // ---- sends: one parallel round of inbox appends, one lane per local target. A target owned by
+  // another row shard is only recorded (targets / rowstat): gm_p_pack builds the exchange records from
+  // them and this tick's list after the chunk (no record written per (sender, shard) here)
   const int dst = lane < ng ? (int)gl[lane] : 0;
   const int owner = (s.G > 1 && lane < ng) ? p_owner(s, dst) : s.rank;
   if (lane < ng) {
@@ -644,39 +678,6 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
       const int slot = atomicAdd(row, 1);
       if (slot < s.kcap) row[1 + slot] = li;
       else atomicOr(s.err, GM_ERR_INBOX);
-    }
-  }
-  if (s.G > 1 && __ballot(lane < ng && owner != s.rank)) {
-    bool first = lane < ng && owner != s.rank;
-#pragma unroll
-    for (int q = 0; q < GM_FANOUT - 1; q++)
-      if (q < lane && __builtin_amdgcn_readlane(owner, q) == owner) first = false;
-    uint64_t fm = __ballot(first);
-    while (fm) {  // one record per (sender, shard) at its fixed sparse slot (rr, li)
-      const int fl = __builtin_ctzll(fm);
-      fm &= fm - 1;
-      const int rr = __builtin_amdgcn_readlane(owner, fl);
-      const size_t rec = (size_t)rr * s.nloc + li;
-      uint64_t tm = __ballot(lane < ng && owner == rr);
-      const int nt = __builtin_popcountll(tm);
-      int tv0 = -1, tv1 = -1, tv2 = -1, tv3 = -1, tv4 = -1;
-      for (int q = 0; tm; q++) {
-        const int d = __builtin_amdgcn_readlane(dst, __builtin_ctzll(tm));
-        tm &= tm - 1;
-        if (q == 0) tv0 = d;
-        else if (q == 1) tv1 = d;
-        else if (q == 2) tv2 = d;
-        else if (q == 3) tv3 = d;
-        else tv4 = d;
-      }
-      if (lane < 8)
-        s.sp_hdr[rec * 8 + lane] = lane == 0 ? i : lane == 1 ? nt : lane == 2 ? tv0 : lane == 3 ? tv1
-                                 : lane == 4 ? tv2 : lane == 5 ? tv3 : lane == 6 ? tv4 : t;  // stamp: this tick's record
-      if (lane < V) {  // wire entry: fresh entries only, heartbeat as distance from this tick's 2t-1
-        const uint32_t hb = (uint32_t)x;
-        const bool fresh = lane < cnt && !p_aged(t, hb, GM_TFAIL);
-        s.sp_list[rec * V + lane] = fresh ? ((uint32_t)(x >> 32) | ((uint32_t)(2 * t - 1) - hb) << P_WIRE_IDBITS) : 0u;
-      }
     }
   }
   if (lane < 4) s.rowstat[(size_t)li * 4 + lane] = lane == 0 ? kk : lane == 1 ? cnt : lane == 2 ? numfailed : ng;
@@ -862,17 +863,29 @@ __global__ __launch_bounds__(256) void gm_p_unpack(PState s, int t, int base, in
   }
 }
 
-// Row shards: compact chunk c's records to shard q (slots (q, li), li in [r0, r1), stamped t) to the
-// front of the packed block (q, r0): one tile of 256 slots per workgroup and peer (blockIdx.y),
-// a workgroup scan of the stamp flags, one atomic per (tile, peer) for the block offset. The
-// records' order inside the block is the atomics' -- the receivers' merge is order-free. A block
-// that would exceed `cap` sets GM_ERR_XCHG (-> GM_ERANGE), never drops a record silently.
+// Row shards: the exchange records of chunk c (rows [r0, r1)) for peer q, packed to the front of the
+// block (q, r0): one tile of 256 nodes per workgroup and peer (blockIdx.y). A node with a target on q
+// (its targets / rowstat of this tick) has one record: the header (sender, #targets on q, those
+// targets, the tick as a stamp) and its final list of the tick (lists[t & 1]) in wire format -- the
+// entries fresh at t, id | (2t-1 - hb) << 25. A wave ballot + an LDS scan rank the tile's records,
+// ONE atomic per (tile, peer) reserves their run (the receivers' merge is order-free). A block that
+// would exceed its capacity (pk_cap, gm_host.hip xcap) sets GM_ERR_XCHG, never drops a record silently.
 __global__ __launch_bounds__(256) void gm_p_pack(PState s, int t, int c, int r0, int r1) {
   const int q = (int)blockIdx.y + (blockIdx.y >= (unsigned)s.rank);  // the peer (own rank skipped)
   const int cap = s.pk_cap[(size_t)c * s.G + q];
   const int li = r0 + blockIdx.x * 256 + threadIdx.x;
-  const size_t rec = (size_t)q * s.nloc + li;
-  const bool has = li < r1 && s.sp_hdr[rec * 8 + 7] == t;
+  const int lo = s.shard_n0[q], hi = s.shard_n0[q + 1];
+  int tv[GM_FANOUT], nt = 0;
+  if (li < r1) {
+    const int ng = min(s.rowstat[(size_t)li * 4 + 3], GM_FANOUT);
+#pragma unroll
+    for (int k = 0; k < GM_FANOUT; k++) {
+      const int d = k < ng ? s.targets[(size_t)li * GM_FANOUT + k] : -1;
+      tv[k] = -1;
+      if (d >= lo && d < hi) tv[nt++] = d;
+    }
+  }
+  const bool has = nt > 0;
   __shared__ int wsum[4];
   __shared__ int base;
   __shared__ int srcs[256];
@@ -893,20 +906,25 @@ __global__ __launch_bounds__(256) void gm_p_pack(PState s, int t, int c, int r0,
     const int d = b + off;
     srcs[off] = li;
     if (d < cap) {
-      const int4 *h = (const int4 *)(s.sp_hdr + rec * 8);
       int4 *o = (int4 *)(s.pk_hdr + ((size_t)q * s.nloc + r0 + d) * 8);
-      o[0] = h[0];
-      o[1] = h[1];
+      // (tv holds the targets on q in draw order, -1 past nt; the stamp marks this tick's record)
+      o[0] = make_int4(s.n0 + li, nt, tv[0], tv[1]);
+      o[1] = make_int4(tv[2], tv[3], tv[4], t);
     } else {
       atomicOr(s.err, GM_ERR_XCHG);
     }
   }
   __syncthreads();
   const int V = s.V, nw = tot * V;
+  const uint64_t *cur = s.lists + (size_t)(t & 1) * s.rows * V;
+  const uint32_t tf = (uint32_t)(2 * t - 1);
   for (int k = threadIdx.x; k < nw; k += 256) {  // the lists, V threads per record (coalesced rows)
     const int j = k / V, e = k - j * V;
-    if (b + j < cap)
-      s.pk_list[((size_t)q * s.nloc + r0 + b + j) * V + e] = s.sp_list[((size_t)q * s.nloc + srcs[j]) * V + e];
+    if (b + j >= cap) continue;
+    const uint64_t x = cur[(size_t)srcs[j] * V + e];
+    const uint32_t hb = (uint32_t)x;
+    const bool fresh = x != 0 && !p_aged(t, hb, GM_TFAIL);
+    s.pk_list[((size_t)q * s.nloc + r0 + b + j) * V + e] = fresh ? ((uint32_t)(x >> 32) | (tf - hb) << P_WIRE_IDBITS) : 0u;
   }
 }
 

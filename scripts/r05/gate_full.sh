@@ -12,7 +12,7 @@ O=gpurun_out/$TAG
 mkdir -p $O
 CPU_PID=
 if [ -n "$2" ]; then
-  timeout -k 10 ${CPU_LIMIT:-1100} taskset -c 3 python3 -u scripts/cpu_hour.py --cluster 13722 --start $2 --ticks ${3:-25} \
+  timeout -k 10 ${CPU_LIMIT:-1100} python3 -u scripts/cpu_hour.py --cluster 13722 --start $2 --ticks ${3:-25} \
     --out $O/cpu_hour_seg$2.jsonl > $O/cpu_hour_seg$2.log 2>&1 &
   CPU_PID=$!
 fi
