@@ -22,6 +22,14 @@ timeout -k 10 300 python3 scripts/shard_profile.py --sb --cluster 65536 > $O/sa_
 timeout -k 10 600 python3 scripts/sb_loopback_profile.py --pipelined > $O/sb_loopback_pipe.json 2> $O/sb_loopback_pipe.err &&
 bash scripts/gpu.sh $TAG prof_sa ticks
 rc=$?
+# bisect of the S-A band-kernel time over round-5 commits (var_ab/libgm_<commit>.so), when present
+if [ $rc -eq 0 ] && ls var_ab/libgm_*.so > /dev/null 2>&1; then
+  for L in var_ab/libgm_*.so; do
+    v=$(basename $L .so)
+    GM_LIBRARY=$L timeout -k 10 300 python3 bench.py --no-cpu --no-pmc --no-companion > $O/bisect_$v.json 2> $O/bisect_$v.err || break
+    python3 -c "import json;d=json.load(open('$O/bisect_$v.json'));print('$v', round(d['roofline']['kernel_ms'],3), round(d['ms_per_step'],3))"
+  done
+fi
 if [ -n "$CPU_PID" ]; then wait $CPU_PID; echo "cpu segment rc=$?"; tail -2 $O/cpu_hour_seg$2.jsonl; fi
 for f in $O/sb_stub.json $O/sa_stub.json $O/sb_loopback_pipe.json; do [ -f $f ] && cut -c1-300 $f; done
 exit $rc
