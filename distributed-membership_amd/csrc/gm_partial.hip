@@ -733,13 +733,13 @@ __device__ __forceinline__ void p_small_node(const PState &s, int t, const PPre 
 // VGPR lanes: ~40 more VALU per node, still faster than one node per wave: 26.1 vs 27.5 ms)
 template <bool MC, bool RM, int VF>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void gm_p_tick_small_pf(
-    PState s, int t, const uint32_t *mtraw, int chunk, int r0, int r1) {
+    PState s, int t, const uint32_t *mtraw, int chunk, int r0, int r1, int npw) {
   extern __shared__ __align__(16) unsigned char p_smem[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int l0 = r0 + (blockIdx.x * 4 + wave) * P_NPW;
+  const int l0 = r0 + (blockIdx.x * 4 + wave) * npw;
   if (l0 >= r1) return;  // whole wave; no workgroup barrier in this kernel
   unsigned char *base = p_smem + (size_t)wave * PLds<P_HS>::bytes;
-  const int l1 = min(r1, l0 + P_NPW);
+  const int l1 = min(r1, l0 + npw);
   uint32_t *pf = (uint32_t *)(p_smem + 4 * (size_t)PLds<P_HS>::bytes + (size_t)wave * P_PF_BYTES);
   const uint32_t pfa =
       __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(__attribute__((address_space(3))) uint32_t *)pf);
@@ -864,16 +864,18 @@ __global__ __launch_bounds__(256) void gm_p_unpack(PState s, int t, int base, in
 }
 
 // Row shards: the exchange records of chunk c (rows [r0, r1)) for peer q, packed to the front of the
-// block (q, r0): one tile of 256 nodes per workgroup and peer (blockIdx.y). A node with a target on q
+// block (q, r0): one tile of 256 nodes per workgroup and peer (blockIdx.x). A node with a target on q
 // (its targets / rowstat of this tick) has one record: the header (sender, #targets on q, those
 // targets, the tick as a stamp) and its final list of the tick (lists[t & 1]) in wire format -- the
 // entries fresh at t, id | (2t-1 - hb) << 25. A wave ballot + an LDS scan rank the tile's records,
 // ONE atomic per (tile, peer) reserves their run (the receivers' merge is order-free). A block that
 // would exceed its capacity (pk_cap, gm_host.hip xcap) sets GM_ERR_XCHG, never drops a record silently.
+// Grid (peers, tiles): the G - 1 workgroups of a tile are adjacent in dispatch order, so the tile's
+// targets and lists are read from L2 by all but the first.
 __global__ __launch_bounds__(256) void gm_p_pack(PState s, int t, int c, int r0, int r1) {
-  const int q = (int)blockIdx.y + (blockIdx.y >= (unsigned)s.rank);  // the peer (own rank skipped)
+  const int q = (int)blockIdx.x + (blockIdx.x >= (unsigned)s.rank);  // the peer (own rank skipped)
   const int cap = s.pk_cap[(size_t)c * s.G + q];
-  const int li = r0 + blockIdx.x * 256 + threadIdx.x;
+  const int li = r0 + blockIdx.y * 256 + threadIdx.x;
   const int lo = s.shard_n0[q], hi = s.shard_n0[q + 1];
   int tv[GM_FANOUT], nt = 0;
   if (li < r1) {
@@ -931,7 +933,7 @@ __global__ __launch_bounds__(256) void gm_p_pack(PState s, int t, int c, int r0,
 hipError_t gm_launch_partial_pack(const PState &s, int t, int c, hipStream_t st) {
   const int r0 = (int)((int64_t)s.nloc * c / s.nchunk), r1 = (int)((int64_t)s.nloc * (c + 1) / s.nchunk);
   if (r1 > r0 && s.G > 1)
-    hipLaunchKernelGGL(gm_p_pack, dim3((r1 - r0 + 255) / 256, s.G - 1), dim3(256), 0, st, s, t, c, r0, r1);
+    hipLaunchKernelGGL(gm_p_pack, dim3(s.G - 1, (r1 - r0 + 255) / 256), dim3(256), 0, st, s, t, c, r0, r1);
   return hipGetLastError();
 }
 
@@ -964,8 +966,11 @@ hipError_t gm_launch_partial_chunk(const PState &s, int t, const uint32_t *mtraw
                             : (mc ? gm_p_tick_small_pf<true, false, P_VMAX> : gm_p_tick_small_pf<false, false, P_VMAX>))
                       : (rm ? (mc ? gm_p_tick_small_pf<true, true, 0> : gm_p_tick_small_pf<false, true, 0>)
                             : (mc ? gm_p_tick_small_pf<true, false, 0> : gm_p_tick_small_pf<false, false, 0>));
-    hipLaunchKernelGGL(small, dim3((r1 - r0 + 4 * P_NPW - 1) / (4 * P_NPW)), dim3(256),
-                       4 * (PLds<P_HS>::bytes + P_PF_BYTES), st, s, t, mtraw, c, r0, r1);
+    // nodes per wave: P_NPW; a row shard's chunk (a few hundred thousand nodes per launch) takes
+    // P_NPW_CHUNK, so the launch's last round of waves is a smaller share of it
+    const int npw = s.nchunk > 1 ? P_NPW_CHUNK : P_NPW;
+    hipLaunchKernelGGL(small, dim3((r1 - r0 + 4 * npw - 1) / (4 * npw)), dim3(256),
+                       4 * (PLds<P_HS>::bytes + P_PF_BYTES), st, s, t, mtraw, c, r0, r1, npw);
   }
   hipLaunchKernelGGL(mc ? gm_p_tick_big<true> : gm_p_tick_big<false>, dim3(P_BIG_GRID), dim3(256),
                      4 * PLds<P_HB>::bytes, st, s, t, mtraw, c, r0);

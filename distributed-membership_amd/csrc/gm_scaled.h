@@ -119,7 +119,6 @@ struct SState {
   // Allocation is STRIPED: (band, row) list u allocates in stripe (band * n + row) & (stripes - 1),
   // a region of `region` entries with its own counter -- one global counter would serialise
   // every (band, row) of a crash-window tick on one address (4 M atomics at S-A: 25 ms)
-  int esc_dense;           // the pools are dense-equivalent (no run can overflow them); gm_pool_info
   int esc_stripes;         // power of two
   unsigned long long *tesc_cnt;  // [2][esc_stripes] cells allocated per stripe this tick (zeroed a tick ahead)
   uint32_t tesc_region;    // entries per stripe
@@ -170,8 +169,6 @@ struct SState {
   int32_t *xcnt;             // bound exchange buffer, chunk-major: [chunk][shard_count][2^xlog][2] (present,
                              //   numfailed) per shard and row (s_xc): a row chunk's slots of every rank are
                              //   contiguous, so each chunk's all-gather is one in-place ncclAllGather
-  int xlog;                  // log2 of the rows per exchange chunk (chunk c = rows [c << xlog, (c + 1) << xlog))
-  int xk;                    // exchange chunks = ceil(n / 2^xlog)
   int32_t *status;           // bound exchange buffer [n][D]: resolved draws, MAX-allreduced
   int32_t *acc;              // [n][8]: targets so far, g[5], numpot, size
   int32_t *pending;          // [n] rows still drawing
@@ -195,10 +192,16 @@ struct SState {
   // by tick parity (the count of tick t+1 is zeroed during tick t); nullptr: fast path off
   uint32_t *fb_cnt;             // [2]
   int2 *fb_list;                // [nb * n]: (band, row)
+  int lag_hmin;                 // a present cell with h < lag_hmin sets GM_ERR_LAG: 3 (lag > 125 ticks, the
+                                // encoding's limit); the diagnostics env GM_LAG_CAP=L (L >= 15) lowers it to lag > L
+  // ---- round-5 fields, kept at the end: the band kernels are short-lived waves whose first scalar
+  // loads come from this struct in the kernel arguments, and fields inserted above shifted their
+  // offsets and the compiler's load grouping (S-A band kernels +7 %, profiles/r05/sa_regression/)
+  int esc_dense;                // the pools are dense-equivalent (no run can overflow them); gm_pool_info
+  int xlog;                     // column shards: log2 of the rows per exchange chunk (rows [c << xlog, (c + 1) << xlog))
+  int xk;                       // exchange chunks = ceil(n / 2^xlog)
   // gm_s_pick0 (single context, B = 1024): rows whose first 16 S2 outputs do not finish their draw go
   // to this list, which gm_s_pick then takes from output 0 (nullptr: gm_s_pick takes every row)
   int32_t *pk_list;             // [n]
   uint32_t *pk_cnt;
-  int lag_hmin;                 // a present cell with h < lag_hmin sets GM_ERR_LAG: 3 (lag > 125 ticks, the
-                                // encoding's limit); the diagnostics env GM_LAG_CAP=L (L >= 15) lowers it to lag > L
 };

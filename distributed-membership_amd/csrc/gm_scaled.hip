@@ -1269,8 +1269,14 @@ __global__ __launch_bounds__(256) void gm_s_band_listed(SState s, int t, int u0,
 // The fast path's kernel (B = 1024, no keyed loss, no join ramp): every unit takes unit_fast; a
 // unit it hands back (not merged, a delivered escape nibble, a payload for the wide plane) goes to
 // s.fb_list for gm_s_band's listed pass right after, untouched. The list of tick t+1 starts empty.
-template <int B>
+// CH: a row chunk [u0, u1) of the pipelined column-shard tick; otherwise every row (no unit bounds
+// among the kernel arguments: the wave's first loads issue as in round 4's codegen)
+template <int B, bool CH>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GM_BAND_MINW, 8))) void gm_s_band_fast(SState s, int t, int u0, int u1) {
+  if (!CH) {
+    u0 = 0;
+    u1 = s.n;
+  }
   const int ub = __builtin_amdgcn_readfirstlane(u0 + (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6));
   if (ub >= u1) return;  // whole wave (one row per wave)
   // per wave: escape cells by column, the park, the per-lane words of the escaped cells' outcomes
@@ -2296,7 +2302,10 @@ static void launch_band_b(const SState &s, int t, int drop_pct, int r0, int r1, 
   if (drop_pct >= 0) {
     hipLaunchKernelGGL((gm_s_band<B, true>), dim3(nblk), dim3(256), 0, st, s, t, drop_pct, u0, u1);
   } else if (B == 1024 && !s.ramp && s.fb_list) {  // the fast path, then the units it handed back
-    hipLaunchKernelGGL((gm_s_band_fast<B == 1024 ? B : 1024>), dim3(nblk), dim3(256), 0, st, s, t, u0, u1);
+    if (u0 == 0 && r1 == s.n)
+      hipLaunchKernelGGL((gm_s_band_fast<B == 1024 ? B : 1024, false>), dim3(nblk), dim3(256), 0, st, s, t, u0, u1);
+    else
+      hipLaunchKernelGGL((gm_s_band_fast<B == 1024 ? B : 1024, true>), dim3(nblk), dim3(256), 0, st, s, t, u0, u1);
     hipLaunchKernelGGL((gm_s_band_listed<B == 1024 ? B : 1024>), dim3(S_FB_BLOCKS), dim3(256), 0, st, s, t, u0, u1);
   } else {
     hipLaunchKernelGGL((gm_s_band<B, false>), dim3(nblk), dim3(256), 0, st, s, t, drop_pct, u0, u1);
