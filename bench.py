@@ -434,10 +434,41 @@ def main():
                                "sample": f"{nodes} node-ticks of the N={n} SCALED workload on one host core "
                                          f"({secs:.1f} s): per node-tick 5 gossip lists x {n} entries merged via "
                                          "updatelistCallBack + nodeLoopOps sweep/sort/draw (oracle/ref_cpu.c)"}
+        hr = hour_run()
+        if hr:
+            out["cpu_baseline"]["hour_run"] = hr
     if rank == 0:
         emit(out)
     if dist is not None:
         dist.destroy_process_group()
+
+
+HOUR_DIR = os.path.join(REPO, "profiles", "cpu_hour")  # (travels to the GPU box: not gpurun-ignored)
+
+
+def hour_run():
+    """The hour-sized CPU run, read from its committed segments
+    (scripts/cpu_hour.py: the SCALED restatement at N = 13,722 on one host core of the GPU box,
+    ticks 9..108 of the S-A schedule in 25-tick segments, each started from the GPU-reached state of
+    its first tick, which gm_read_* hands to oc_load_scaled). Summed per tick, not re-run here:
+    an hour of CPU is not a bench step. None when the segments are absent."""
+    import glob
+    ticks, host = {}, None
+    for f in sorted(glob.glob(os.path.join(HOUR_DIR, "cpu_hour_seg*.jsonl"))):
+        with open(f) as fh:
+            for line in fh:
+                r = json.loads(line)
+                if "tick" in r:
+                    ticks[r["tick"]] = r["s"]
+                elif r.get("summary"):
+                    host = r.get("cpu")
+                    n = r["n"]
+    if not ticks:
+        return None
+    secs = sum(ticks.values())
+    return {"value": n * len(ticks) / secs, "unit": "node-ticks/s", "cores": 1, "kind": "port", "n": n,
+            "ticks": f"{min(ticks)}..{max(ticks)} ({len(ticks)} ticks)", "seconds": round(secs, 1),
+            "host": host, "source": "profiles/cpu_hour/cpu_hour_seg*.jsonl (scripts/cpu_hour.py)"}
 
 
 def main_partial(a):

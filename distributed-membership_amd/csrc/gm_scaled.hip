@@ -35,6 +35,7 @@
 #include <algorithm>
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
 typedef uint8_t u8x16 __attribute__((ext_vector_type(16)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
@@ -59,6 +60,12 @@ __global__ __launch_bounds__(256) void gm_s_mtgen(SState s, int t) {
 // inbox count, first S_SB sender ids) together with its table slice, then the
 // payload slices, merges, sweeps, stores and exits (short-lived waves keep more
 // bytes in flight than a persistent loop; measured with scripts/ubench).
+#ifndef GM_KP
+#define GM_KP 1  // A/B: the row's kernel-argument words in one batch (row_meta)
+#endif
+#ifndef GM_FAST_HOOK
+#define GM_FAST_HOOK 3  // A/B: where the fast kernel's second unit issues its loads (0: after the first unit)
+#endif
 template <int B>
 struct RowMeta {
   int k;           // lists delivered to the row (-1: no such row, or a crashed node)
@@ -66,26 +73,62 @@ struct RowMeta {
   uint32_t ebase;  // the (band, row) record's escape-list word of the last tick (S_EW_*, 0: no escaped cells)
   uint32_t bz;     // the record's count word of the last tick (S_BC_*: the slice's present cells as stored)
   uint64_t evc;    // EVC: the (row, band)'s cumulative events (evcum), read with the metadata
+  uint32_t ebase2, bz2;  // band2 >= 0: the same words of the (band2, row) record
+  uint64_t evc2;         // and its evcum cell (EVC)
 };
 
 // Every load of the row's metadata issues at once, none behind a branch on another (one
 // memory round trip before the payload gathers can issue, not a chain of three).
+// a load through a pointer known to be global memory (a pointer out of an asm statement is no
+// longer known to be one, and a generic pointer's loads are never scalar)
+template <typename T>
+__device__ __forceinline__ T gld(const T *p) {
+#if __HIP_DEVICE_COMPILE__
+  return *(const __attribute__((address_space(1))) T *)p;
+#else
+  return *p;  // (host pass: never executed)
+#endif
+}
+// band2 >= 0 (one row per wave): also the record and evcum cell of the row in band2 -- loaded here,
+// before the empty asm statements below, which the compiler takes for memory writes (a load after
+// them is not known unclobbered and becomes a vector load)
 template <int B, bool UNI, bool EVC = false>
-__device__ __forceinline__ RowMeta<B> row_meta(const SState &s, int r, int par, int t, size_t slab, int band) {
+__device__ __forceinline__ RowMeta<B> row_meta(const SState &s, int r, int par, int t, size_t slab, int band,
+                                               int band2 = -1) {
   RowMeta<B> m;
   const int rc = min(r, s.n - 1);  // r >= n (a partial unit): loads stay in bounds, k = -1
-  const int32_t *ib = s.inbox[par] + (size_t)rc * S_KMAX;
-  int4 a = *(const int4 *)ib;
-  int4 b = *(const int4 *)(ib + 4);
-  int k = s.inbox_cnt[par][rc];
-  int failed = s.failed[rc];
-  const uint4 rec = s.brec[slab + rc];
+  const int32_t *ibase = par ? s.inbox[1] : s.inbox[0], *cbase = par ? s.inbox_cnt[1] : s.inbox_cnt[0];
+  const int32_t *fbase = s.failed;
+  const uint4 *rbase = s.brec;
+  const uint64_t *ecbase = s.evcum;
+  int ramp = s.ramp;
+#if GM_KP
+  // every kernel-argument word the row's loads need, in one batch: without this the compiler
+  // interleaves these (scalar-cache) loads with the row's memory loads, and a wait for one of them
+  // waits for all -- the evcum cell then issued only after the inbox had arrived (a second round trip
+  // before the gathers). A plain asm statement (not volatile: no memory effect assumed).
+  if (UNI) asm("" : "+s"(ibase), "+s"(cbase), "+s"(fbase), "+s"(rbase), "+s"(ecbase), "+s"(ramp));
+#endif
+  const int32_t *ib = ibase + (size_t)rc * S_KMAX;
+  const i32x4 av = gld((const i32x4 *)ib), bv = gld((const i32x4 *)(ib + 4));
+  int4 a = make_int4(av.x, av.y, av.z, av.w);
+  int4 b = make_int4(bv.x, bv.y, bv.z, bv.w);
+  int k = gld(cbase + rc);
+  int failed = gld(fbase + rc);
+  const u32x4 rv = gld((const u32x4 *)(rbase + slab + rc));
+  const uint4 rec = make_uint4(rv.x, rv.y, rv.z, rv.w);
   m.ebase = rec.w;
   m.bz = rec.z;
   // the fast path (one row per wave): the unit is the only writer of its evcum cell this tick, so it is read
   // here (in flight with the rest) and written back plainly -- no device-scope atomic per unit with
   // events (at the TREMOVE peak ~4 M of them held the fast path's waves: +2 ms per tick)
-  m.evc = EVC ? s.evcum[(size_t)rc * s.nb + band] : 0ull;
+  m.evc = EVC ? gld(ecbase + (size_t)rc * s.nb + band) : 0ull;
+  if (band2 >= 0) {
+    const u32x4 rec2 = gld((const u32x4 *)(rbase + (size_t)band2 * s.n + rc));
+    m.ebase2 = rec2.w;
+    m.bz2 = rec2.z;
+    m.evc2 = EVC ? gld(ecbase + (size_t)rc * s.nb + band2) : 0ull;
+  }
   // empty asm statements that read the values here: without them the compiler sinks the
   // inbox-count load into a branch on `failed` and the sender ids behind that, two more
   // round trips before the gathers (one row per wave: scalar registers)
@@ -98,8 +141,8 @@ __device__ __forceinline__ RowMeta<B> row_meta(const SState &s, int r, int par, 
   m.snd[0] = a.x; m.snd[1] = a.y; m.snd[2] = a.z; m.snd[3] = a.w;
   m.snd[4] = b.x; m.snd[5] = b.y; m.snd[6] = b.z; m.snd[7] = b.w;
   // not in the group (join ramp) or crashed: untouched
-  m.k = (r >= s.n || failed || !s_ingroup(s.ramp, s.intro_until, r, t)) ? -1 : k;
-  if (r >= s.n) m.ebase = 0;
+  m.k = (r >= s.n || failed || !s_ingroup(ramp, s.intro_until, r, t)) ? -1 : k;
+  if (r >= s.n) m.ebase = m.ebase2 = 0;
   return m;
 }
 
@@ -406,22 +449,38 @@ struct UnitIn {
   uint32_t bz;     // the (band, row) record's count word of tick t-1 (S_BC_PRES: present cells as loaded)
   uint64_t evc;    // evcum of the (row, band) as of tick t-1 (uni: read by unit_load)
   bool uni;        // the fast path's unit: its evcum cell is written back plainly, not by an atomic
+  const uint8_t *msg;     // s.msg and the inline escape entries of tick t-1, read with the row's
+  const uint32_t *tesc;   // kernel-argument words (unit_load)
 };
 
+// the unit's table slice (this lane's 16 cell bytes); r >= n: out of range -> zeros
+template <int B>
+__device__ __forceinline__ void unit_table(const SState &s, UnitIn<B> &in) {
+  constexpr int LPR = B / S_COLS_PER_LANE, Q = S_COLS_PER_LANE;
+  const int li = (threadIdx.x & 63) % LPR;
+  const __amdgpu_buffer_rsrc_t trs = gm_rsrc(s.table + (size_t)in.band * s.n * B, (uint32_t)(s.n * B));
+  in.ta = __builtin_amdgcn_raw_buffer_load_b128(trs, (uint32_t)(in.r * B + li * Q), 0, GM_AUX_NT);
+}
+
 // UNI: the row is wave-uniform and known to be (one row per wave, a grid-derived unit)
-template <int B, bool UNI = false, bool EVC = false>
-__device__ __forceinline__ void unit_load(const SState &s, int t, int band, int ub, UnitIn<B> &in) {
-  constexpr int LPR = B / S_COLS_PER_LANE, RPW = 64 / LPR, Q = S_COLS_PER_LANE;
-  const int lane = threadIdx.x & 63;
-  const int sub = lane / LPR, li = lane % LPR;
+// in2 (one row per wave): the same row's unit in band2 -- the row's inbox, count and state are shared,
+// its record words and evcum cell load with this unit's; its table slice issues later (unit_table)
+template <int B, bool UNI = false, bool EVC = false, bool TWO = false>
+__device__ __forceinline__ void unit_load(const SState &s, int t, int band, int ub, UnitIn<B> &in,
+                                          UnitIn<B> &in2, int band2) {
+  constexpr int LPR = B / S_COLS_PER_LANE, RPW = 64 / LPR;
+  const int sub = (threadIdx.x & 63) / LPR;
   in.band = band;
   in.r = ub * RPW + sub;
+  in.msg = s.msg;
+  in.tesc = (t & 1) ? s.tesc_in[0] : s.tesc_in[1];
+#if GM_KP
+  if (UNI) asm("" : "+s"(in.msg), "+s"(in.tesc));
+#endif
   const size_t slab = (size_t)in.band * s.n;
-  const __amdgpu_buffer_rsrc_t trs = gm_rsrc(s.table + slab * B, (uint32_t)(s.n * B));
-  const uint32_t toff = (uint32_t)(in.r * B + li * Q);  // r >= n: out of range -> zeros, dropped
   // the table slice first: it is independent of the metadata, both in flight together
-  in.ta = __builtin_amdgcn_raw_buffer_load_b128(trs, toff, 0, GM_AUX_NT);
-  const RowMeta<B> meta = row_meta<B, UNI, EVC>(s, in.r, t & 1, t, slab, band);
+  unit_table<B>(s, in);
+  const RowMeta<B> meta = row_meta<B, UNI, EVC>(s, in.r, t & 1, t, slab, band, TWO ? band2 : -1);
 #pragma unroll
   for (int j = 0; j < S_SB; j++) in.snd[j] = meta.snd[j];
   in.k = meta.k;
@@ -429,7 +488,25 @@ __device__ __forceinline__ void unit_load(const SState &s, int t, int band, int 
   in.bz = meta.bz;
   in.evc = meta.evc;
   in.uni = EVC;
+  if (TWO) {
+    in2.band = band2;
+    in2.r = in.r;
+#pragma unroll
+    for (int j = 0; j < S_SB; j++) in2.snd[j] = meta.snd[j];
+    in2.k = meta.k;
+    in2.ebase = meta.ebase2;
+    in2.bz = meta.bz2;
+    in2.evc = meta.evc2;
+    in2.uni = EVC;
+    in2.msg = in.msg;
+    in2.tesc = in.tesc;
+  }
 }
+template <int B, bool UNI = false, bool EVC = false>
+__device__ __forceinline__ void unit_load(const SState &s, int t, int band, int ub, UnitIn<B> &in) {
+  unit_load<B, UNI, EVC, false>(s, t, band, ub, in, in, -1);
+}
+
 
 // every payload slice at once; slots j >= k read out of range (zeros = "not sent"); with them,
 // lane li < 16 of a row whose slice held escaped cells fetches entry li of its list (ent)
@@ -439,8 +516,8 @@ __device__ __forceinline__ void unit_gather(const SState &s, int t, const UnitIn
   const int li = (threadIdx.x & 63) % LPR;
   ent = 0;
   if (li < (int)min(S_EW_TOT(in.ebase), (uint32_t)S_ESC_IN))
-    ent = s.tesc_in[(t & 1) ^ 1][((size_t)in.band * s.n + in.r) * S_ESC_IN + li];
-  const __amdgpu_buffer_rsrc_t prs = gm_rsrc(s.msg + (size_t)in.band * s.n * B, (uint32_t)(s.n * B));
+    ent = gld(in.tesc + ((size_t)in.band * s.n + in.r) * S_ESC_IN + li);
+  const __amdgpu_buffer_rsrc_t prs = gm_rsrc(in.msg + (size_t)in.band * s.n * B, (uint32_t)(s.n * B));
   const uint32_t poff = (uint32_t)(((t & 1) ^ 1) * (B / 2) + li * 8);  // + sender * B
   const int k = min(in.k, S_KMAX);
 #pragma unroll
@@ -952,9 +1029,12 @@ __device__ __forceinline__ FastCell fast_cell(const SState &s, int t, uint32_t y
 // the row's own cell (heartbeat bump). A delivered escape nibble, or a fresh cell whose payload needs
 // the wide plane, sends the whole wave to the general path: the function then returns false before
 // any global store. Returns true when the unit is done.
-template <int B>
+// nxt: called at most once, as soon as the payload words m are consumed (or not needed): the wave's
+// next unit issues its table slice and payload gathers into m there, in flight under this unit's sweep
+// (a unit handed to the general path may return before it: the caller then issues them).
+template <int B, typename F>
 __device__ __forceinline__ bool unit_fast(const SState &s, int t, const UnitIn<B> &in, const u32x2 m[S_SB],
-                                          uint32_t ent, uint32_t *lds, uint32_t *park) {
+                                          uint32_t ent, uint32_t *lds, uint32_t *park, F &&nxt) {
   static_assert(B / S_COLS_PER_LANE == 64, "the fast path takes one row per wave");
   constexpr int Q = S_COLS_PER_LANE;
   const int lane = threadIdx.x & 63, li = lane;
@@ -963,9 +1043,10 @@ __device__ __forceinline__ bool unit_fast(const SState &s, int t, const UnitIn<B
   const int colb = band * B + li * Q;  // shard-local column of this lane's first cell
   const size_t slab = (size_t)band * s.n;
   const int k = in.k;  // wave-uniform
-  if (k > S_KMAX || s.ramp) return false;  // inbox error / join ramp: general path
+  if (k > S_KMAX || s.ramp) return false;  // inbox error / join ramp: general path (nxt: as for a bail)
   if (k < 0) {  // a row not merged this tick (crashed): its cells stay as they are, its escape list moves
-    uint32_t eb_out = 0;  // to this tick's storage (entries carry their columns), its record is written
+    nxt();        // to this tick's storage (entries carry their columns), its record is written
+    uint32_t eb_out = 0;
     if (in.ebase != 0) {
       const int etot = (int)S_EW_TOT(in.ebase);
       eb_out = row_alloc<64>(s, par, slab, r, etot, li, lane);
@@ -995,6 +1076,9 @@ __device__ __forceinline__ bool unit_fast(const SState &s, int t, const UnitIn<B
       nib_max(acc, mv.x, mv.y);
     }
   }
+#if GM_FAST_HOOK == 1
+  nxt();
+#endif
   {
     u16x2 amx = acc[0];
 #pragma unroll
@@ -1055,7 +1139,11 @@ __device__ __forceinline__ bool unit_fast(const SState &s, int t, const UnitIn<B
   uint32_t gmask = 0, em = 0, sent = 0;
   bool sv = false, epar = true;
   const bool eslice = in.ebase != 0;  // row-uniform
-  if (eslice || __builtin_amdgcn_ballot_w64(spm != 0)) {
+  const bool slow = eslice || __builtin_amdgcn_ballot_w64(spm != 0);
+#if GM_FAST_HOOK == 2
+  if (!slow) nxt();
+#endif
+  if (slow) {
     uint16_t *row16 = (uint16_t *)lds;  // the wave's LDS: a 16-bit cell per column (lane li: [16 li, +16))
     u32x4 *pk4 = (u32x4 *)(park + li * 8);
     pk4[0] = (u32x4){bw[0], bw[1], bw[2], bw[3]};
@@ -1121,7 +1209,7 @@ __device__ __forceinline__ bool unit_fast(const SState &s, int t, const UnitIn<B
       pb[q] = (uint8_t)o.nbyte;
       pb[16 + q] = (uint8_t)o.nib;
     }
-    if (__builtin_amdgcn_ballot_w64(bail)) return false;
+    if (__builtin_amdgcn_ballot_w64(bail)) return false;  // (nxt not called: the caller issues it)
     lds_wave_sync();  // other lanes' entries wrote into this lane's park and words
     if (eslice) {
       const uint32_t ge = cor[64 + li], cd = cor[128 + li];
@@ -1135,6 +1223,9 @@ __device__ __forceinline__ bool unit_fast(const SState &s, int t, const UnitIn<B
     bw[0] = b0.x; bw[1] = b0.y; bw[2] = b0.z; bw[3] = b0.w;
     nb[0] = b1.x; nb[1] = b1.y; nb[2] = b1.z; nb[3] = b1.w;
     if (!epar) em = esc_mask16(bw[0], bw[1], bw[2], bw[3]);  // every escape byte: row16 holds its cell
+#if GM_FAST_HOOK == 2
+    nxt();
+#endif
   }
   // payload words in nib_max's order: the high nibbles of cells [4, 0, 5, 1] | those of [6, 2, 7, 3]
   // shifted down, for cells 0..7 and likewise 8..15
@@ -1173,6 +1264,9 @@ __device__ __forceinline__ bool unit_fast(const SState &s, int t, const UnitIn<B
   }
   // 6. commit: the table and payload stores (the general path's), then this tick's escape list --
   // the entry lanes' survivors first (ballot rank), the lanes' escape bytes after them (esc_emit)
+#if GM_FAST_HOOK >= 3
+  nxt();
+#endif
   if (selflane) s.hbctr[r] = hbself + 1;
   uint32_t eb_out = unit_stores<B>(s, t, in, bw, ov0, ov1, false, 0u, lds);
   const uint64_t svb = __builtin_amdgcn_ballot_w64(sv);
@@ -1271,7 +1365,12 @@ __global__ __launch_bounds__(256) void gm_s_band_listed(SState s, int t, int u0,
 // s.fb_list for gm_s_band's listed pass right after, untouched. The list of tick t+1 starts empty.
 // CH: a row chunk [u0, u1) of the pipelined column-shard tick; otherwise every row (no unit bounds
 // among the kernel arguments: the wave's first loads issue as in round 4's codegen)
-template <int B, bool CH>
+// BPW: bands per wave (blockIdx.y = a group of BPW bands). With 2, the wave's second unit is the same
+// row in the next band: it shares the row's metadata (one round trip, not two), and its table slice
+// and payload gathers issue as soon as the first unit's payload words are merged (nxt), so they are
+// in flight under the first unit's sweep and stores -- one dependent round trip per unit instead of
+// two (inbox, then gathers).
+template <int B, bool CH, int BPW>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GM_BAND_MINW, 8))) void gm_s_band_fast(SState s, int t, int u0, int u1) {
   if (!CH) {
     u0 = 0;
@@ -1283,14 +1382,37 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GM_BAND_MIN
   constexpr int W = 2 * S_LDS_WAVE_WORDS + 192;
   __shared__ uint32_t lds_all[4 * W];
   uint32_t *lds = lds_all + (threadIdx.x >> 6) * W;
-  UnitIn<B> in;
-  unit_load<B, true, true>(s, t, (int)blockIdx.y, ub, in);
+  const int b0 = (int)blockIdx.y * BPW;
+  const bool two = BPW == 2 && b0 + 1 < s.nb;  // wave-uniform
+  UnitIn<B> in, in2;
+  unit_load<B, true, true, BPW == 2>(s, t, b0, ub, in, in2, two ? b0 + 1 : b0);
   u32x2 m[S_SB];
-  uint32_t ent;
+  uint32_t ent, ent2 = 0;
   unit_gather<B, false>(s, t, in, m, ent);
-  if (!unit_fast<B>(s, t, in, m, ent, lds, lds + S_LDS_WAVE_WORDS) && (threadIdx.x & 63) == 0) {
+  bool issued = false;  // wave-uniform
+  const bool ok = unit_fast<B>(s, t, in, m, ent, lds, lds + S_LDS_WAVE_WORDS, [&]() {
+    if (two) {
+      if (GM_FAST_HOOK != 4) unit_table<B>(s, in2);
+      unit_gather<B, false>(s, t, in2, m, ent2);
+    }
+    issued = true;
+  });
+  if (!ok && (threadIdx.x & 63) == 0) {
     const uint32_t slot = atomicAdd(&s.fb_cnt[t & 1], 1u);  // < the units of a tick: the list's size
-    s.fb_list[slot] = make_int2((int)blockIdx.y, ub);
+    s.fb_list[slot] = make_int2(b0, ub);
+  }
+  if (two) {
+    if (!issued) {  // the first unit went to the general path before its payload words were consumed
+      unit_table<B>(s, in2);
+      unit_gather<B, false>(s, t, in2, m, ent2);
+    } else if (GM_FAST_HOOK == 4) {
+      unit_table<B>(s, in2);
+    }
+    lds_wave_sync();  // the first unit's LDS reads are done before the second one's writes
+    if (!unit_fast<B>(s, t, in2, m, ent2, lds, lds + S_LDS_WAVE_WORDS, []() {}) && (threadIdx.x & 63) == 0) {
+      const uint32_t slot = atomicAdd(&s.fb_cnt[t & 1], 1u);
+      s.fb_list[slot] = make_int2(b0 + 1, ub);
+    }
   }
   if (ub == 0 && blockIdx.y == 0) band_reset_pools(s, t);
 }
@@ -2293,6 +2415,9 @@ __global__ __launch_bounds__(256) void gm_s_init(SState s, int warm, int t0, uin
 // ------------------------------------------------------------ launch wrappers
 // (template dispatch over the band width; called by gm_host.hip)
 // the band kernels of rows [r0, r1) (r0, r1 multiples of the rows per unit, or r1 = n)
+#ifndef GM_FAST_BPW
+#define GM_FAST_BPW 2  // bands per wave of gm_s_band_fast
+#endif
 template <int B>
 static void launch_band_b(const SState &s, int t, int drop_pct, int r0, int r1, hipStream_t st) {
   constexpr int RPW = 64 / (B / S_COLS_PER_LANE);
@@ -2302,10 +2427,11 @@ static void launch_band_b(const SState &s, int t, int drop_pct, int r0, int r1, 
   if (drop_pct >= 0) {
     hipLaunchKernelGGL((gm_s_band<B, true>), dim3(nblk), dim3(256), 0, st, s, t, drop_pct, u0, u1);
   } else if (B == 1024 && !s.ramp && s.fb_list) {  // the fast path, then the units it handed back
+    const dim3 nblk2(nblk.x, (s.nb + GM_FAST_BPW - 1) / GM_FAST_BPW);
     if (u0 == 0 && r1 == s.n)
-      hipLaunchKernelGGL((gm_s_band_fast<B == 1024 ? B : 1024, false>), dim3(nblk), dim3(256), 0, st, s, t, u0, u1);
+      hipLaunchKernelGGL((gm_s_band_fast<B == 1024 ? B : 1024, false, GM_FAST_BPW>), nblk2, dim3(256), 0, st, s, t, u0, u1);
     else
-      hipLaunchKernelGGL((gm_s_band_fast<B == 1024 ? B : 1024, true>), dim3(nblk), dim3(256), 0, st, s, t, u0, u1);
+      hipLaunchKernelGGL((gm_s_band_fast<B == 1024 ? B : 1024, true, GM_FAST_BPW>), nblk2, dim3(256), 0, st, s, t, u0, u1);
     hipLaunchKernelGGL((gm_s_band_listed<B == 1024 ? B : 1024>), dim3(S_FB_BLOCKS), dim3(256), 0, st, s, t, u0, u1);
   } else {
     hipLaunchKernelGGL((gm_s_band<B, false>), dim3(nblk), dim3(256), 0, st, s, t, drop_pct, u0, u1);

@@ -15,3 +15,16 @@ def test_partial_cpu_leg_runs():
         ora.tick()
     sent, recv = ora.last_msgcount()
     assert sent.sum() > 0 and recv.sum() > 0
+
+
+def test_hour_run_reads_committed_segments():
+    """bench.py's cpu_baseline.hour_run: the committed CPU-hour segments summed per tick (no re-run)."""
+    import importlib.util
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(root, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    hr = bench.hour_run()
+    assert hr is not None and hr["n"] == 13722 and hr["cores"] == 1
+    assert hr["seconds"] > 0 and hr["value"] > 0 and "cpu_hour_seg" in hr["source"]
