@@ -544,9 +544,10 @@ static int create_scaled(gm_ctx *c) {
     c->dmax = 64;
     // the exchange's row chunks (tick_sharded pipelines band -> all-gather -> draw -> MAX-allreduce ->
     // acceptance chunk by chunk): 2^xlog rows each (>= 64: a multiple of every band width's rows per
-    // unit), K = GM_SCHUNKS chunks by default 4
+    // unit), K = GM_SCHUNKS chunks, by default 2 (one-box A/B, profiles/r05/ab5: stub shard 7.64 vs 7.76 ms
+    // at 4, G = 8 loopback 7.58 vs 7.79 ms per shard-tick)
     {
-      int K = getenv("GM_SCHUNKS") ? atoi(getenv("GM_SCHUNKS")) : 4;
+      int K = getenv("GM_SCHUNKS") ? atoi(getenv("GM_SCHUNKS")) : 2;
       if (K < 1 || K > 64) return GM_EINVAL;
       s.xlog = 6;
       while (((int64_t)1 << s.xlog) * K < n) s.xlog++;

@@ -863,77 +863,102 @@ __global__ __launch_bounds__(256) void gm_p_unpack(PState s, int t, int base, in
   }
 }
 
-// Row shards: the exchange records of chunk c (rows [r0, r1)) for peer q, packed to the front of the
-// block (q, r0): one tile of 256 nodes per workgroup and peer (blockIdx.x). A node with a target on q
-// (its targets / rowstat of this tick) has one record: the header (sender, #targets on q, those
-// targets, the tick as a stamp) and its final list of the tick (lists[t & 1]) in wire format -- the
-// entries fresh at t, id | (2t-1 - hb) << 25. A wave ballot + an LDS scan rank the tile's records,
-// ONE atomic per (tile, peer) reserves their run (the receivers' merge is order-free). A block that
-// would exceed its capacity (pk_cap, gm_host.hip xcap) sets GM_ERR_XCHG, never drops a record silently.
-// Grid (peers, tiles): the G - 1 workgroups of a tile are adjacent in dispatch order, so the tile's
-// targets and lists are read from L2 by all but the first.
+// Row shards: the exchange records of chunk c (rows [r0, r1)), packed per peer q to the front of
+// block (q, r0). A node with targets on q (its targets / rowstat of this tick) has one record for q:
+// the header (sender, #targets on q, those targets in draw order, the tick as a stamp) and its final
+// list of the tick (lists[t & 1]) in wire format -- the entries fresh at t, id | (2t-1 - hb) << 25.
+// One workgroup per tile of 256 nodes and every peer: a node's distinct remote peers take their
+// record slots in the tile by LDS atomics, ONE global atomic per (tile, peer) reserves each peer's
+// run (the receivers' merge is order-free), and each node's list is read and converted once, by a
+// half-wave, then written to each of its records. A block that would exceed its capacity (pk_cap,
+// gm_host.hip xcap) sets GM_ERR_XCHG, never drops a record silently.
+template <int VF>
 __global__ __launch_bounds__(256) void gm_p_pack(PState s, int t, int c, int r0, int r1) {
-  const int q = (int)blockIdx.x + (blockIdx.x >= (unsigned)s.rank);  // the peer (own rank skipped)
-  const int cap = s.pk_cap[(size_t)c * s.G + q];
-  const int li = r0 + blockIdx.y * 256 + threadIdx.x;
-  const int lo = s.shard_n0[q], hi = s.shard_n0[q + 1];
-  int tv[GM_FANOUT], nt = 0;
-  if (li < r1) {
-    const int ng = min(s.rowstat[(size_t)li * 4 + 3], GM_FANOUT);
+  extern __shared__ int pk_sm[];  // [G] records per peer in this tile, then [G] the tile's run in each block
+  const int G = s.G, V = VF ? VF : s.V;
+  int *tcnt = pk_sm, *tbase = pk_sm + G;
+  for (int q = threadIdx.x; q < G; q += 256) tcnt[q] = 0;
+  __syncthreads();
+  const int li = r0 + (int)blockIdx.x * 256 + (int)threadIdx.x;
+  int tv[GM_FANOUT], tq[GM_FANOUT];
+  const int ng = li < r1 ? min(s.rowstat[(size_t)li * 4 + 3], GM_FANOUT) : 0;
 #pragma unroll
-    for (int k = 0; k < GM_FANOUT; k++) {
-      const int d = k < ng ? s.targets[(size_t)li * GM_FANOUT + k] : -1;
-      tv[k] = -1;
-      if (d >= lo && d < hi) tv[nt++] = d;
-    }
+  for (int k = 0; k < GM_FANOUT; k++) {
+    tv[k] = k < ng ? s.targets[(size_t)li * GM_FANOUT + k] : -1;
+    tq[k] = k < ng ? p_owner(s, tv[k]) : -1;
   }
-  const bool has = nt > 0;
-  __shared__ int wsum[4];
-  __shared__ int base;
-  __shared__ int srcs[256];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint64_t bal = __ballot(has);
-  const int below = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-  if (lane == 0) wsum[wave] = __builtin_popcountll(bal);
-  __syncthreads();
-  int off = below, tot = 0;
-  for (int w = 0; w < 4; w++) {
-    off += w < wave ? wsum[w] : 0;
-    tot += wsum[w];
-  }
-  if (threadIdx.x == 0) base = tot ? atomicAdd(s.pk_cnt + (size_t)c * s.G + q, tot) : 0;
-  __syncthreads();
-  const int b = base;
-  if (has) {
-    const int d = b + off;
-    srcs[off] = li;
-    if (d < cap) {
-      int4 *o = (int4 *)(s.pk_hdr + ((size_t)q * s.nloc + r0 + d) * 8);
-      // (tv holds the targets on q in draw order, -1 past nt; the stamp marks this tick's record)
-      o[0] = make_int4(s.n0 + li, nt, tv[0], tv[1]);
-      o[1] = make_int4(tv[2], tv[3], tv[4], t);
-    } else {
-      atomicOr(s.err, GM_ERR_XCHG);
+  // distinct remote peers in first-appearance order, each with its slot in the tile's run for that peer
+  int pq[GM_FANOUT], ps[GM_FANOUT], np = 0;
+#pragma unroll
+  for (int k = 0; k < GM_FANOUT; k++) {
+    bool fresh = tq[k] >= 0 && tq[k] != s.rank;
+#pragma unroll
+    for (int j = 0; j < k; j++) fresh = fresh && tq[j] != tq[k];
+    if (fresh) {
+      pq[np] = tq[k];
+      ps[np] = atomicAdd(&tcnt[tq[k]], 1);
+      np++;
     }
   }
   __syncthreads();
-  const int V = s.V, nw = tot * V;
+  for (int q = threadIdx.x; q < G; q += 256) tbase[q] = tcnt[q] ? atomicAdd(s.pk_cnt + (size_t)c * G + q, tcnt[q]) : 0;
+  __syncthreads();
+  // headers (the targets on q in draw order, -1 past nt); rec[j] = the record's row in block (pq[j], r0), -1 if over
+  int rec[GM_FANOUT];
+#pragma unroll
+  for (int j = 0; j < GM_FANOUT; j++) {
+    rec[j] = -1;
+    if (j < np) {
+      const int q = pq[j], d = tbase[q] + ps[j];
+      if (d < s.pk_cap[(size_t)c * G + q]) {
+        int h[GM_FANOUT], nt = 0;
+#pragma unroll
+        for (int k = 0; k < GM_FANOUT; k++) {
+          h[k] = -1;
+          if (tq[k] == q) h[nt++] = tv[k];
+        }
+        rec[j] = d;
+        int4 *o = (int4 *)(s.pk_hdr + ((size_t)q * s.nloc + r0 + d) * 8);
+        o[0] = make_int4(s.n0 + li, nt, h[0], h[1]);
+        o[1] = make_int4(h[2], h[3], h[4], t);
+      } else {
+        atomicOr(s.err, GM_ERR_XCHG);
+      }
+    }
+  }
+  // lists: half-wave per node (entry e = lane & 31), two nodes of the wave per step; the node's
+  // record rows and peers come from its own lane by shuffles
+  const int lane = threadIdx.x & 63, e = lane & 31;
+  const int wbase = r0 + (int)blockIdx.x * 256 + (int)(threadIdx.x & ~63u);
   const uint64_t *cur = s.lists + (size_t)(t & 1) * s.rows * V;
   const uint32_t tf = (uint32_t)(2 * t - 1);
-  for (int k = threadIdx.x; k < nw; k += 256) {  // the lists, V threads per record (coalesced rows)
-    const int j = k / V, e = k - j * V;
-    if (b + j >= cap) continue;
-    const uint64_t x = cur[(size_t)srcs[j] * V + e];
-    const uint32_t hb = (uint32_t)x;
-    const bool fresh = x != 0 && !p_aged(t, hb, GM_TFAIL);
-    s.pk_list[((size_t)q * s.nloc + r0 + b + j) * V + e] = fresh ? ((uint32_t)(x >> 32) | (tf - hb) << P_WIRE_IDBITS) : 0u;
+  for (int it = 0; it < 32; it++) {
+    const int src = 2 * it + (lane >> 5);  // the node's lane in this wave
+    const int nnp = __shfl(np, src, 64);
+    if (!__ballot(nnp > 0)) continue;
+    const int node = wbase + src;
+    uint32_t w = 0;
+    if (nnp > 0 && e < V) {
+      const uint64_t x = cur[(size_t)node * V + e];
+      const uint32_t hb = (uint32_t)x;
+      w = (x != 0 && !p_aged(t, hb, GM_TFAIL)) ? ((uint32_t)(x >> 32) | (tf - hb) << P_WIRE_IDBITS) : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < GM_FANOUT; j++) {
+      const int q = __shfl(pq[j], src, 64), d = __shfl(rec[j], src, 64);
+      if (j < nnp && d >= 0 && e < V) s.pk_list[((size_t)q * s.nloc + r0 + d) * V + e] = w;
+    }
   }
 }
 
 hipError_t gm_launch_partial_pack(const PState &s, int t, int c, hipStream_t st) {
   const int r0 = (int)((int64_t)s.nloc * c / s.nchunk), r1 = (int)((int64_t)s.nloc * (c + 1) / s.nchunk);
-  if (r1 > r0 && s.G > 1)
-    hipLaunchKernelGGL(gm_p_pack, dim3(s.G - 1, (r1 - r0 + 255) / 256), dim3(256), 0, st, s, t, c, r0, r1);
+  if (r1 > r0 && s.G > 1) {
+    const dim3 grid((r1 - r0 + 255) / 256);
+    const size_t sm = sizeof(int) * 2 * (size_t)s.G;
+    if (s.V == 32) hipLaunchKernelGGL(gm_p_pack<32>, grid, dim3(256), sm, st, s, t, c, r0, r1);
+    else hipLaunchKernelGGL(gm_p_pack<0>, grid, dim3(256), sm, st, s, t, c, r0, r1);
+  }
   return hipGetLastError();
 }
 
