@@ -60,12 +60,6 @@ __global__ __launch_bounds__(256) void gm_s_mtgen(SState s, int t) {
 // inbox count, first S_SB sender ids) together with its table slice, then the
 // payload slices, merges, sweeps, stores and exits (short-lived waves keep more
 // bytes in flight than a persistent loop; measured with scripts/ubench).
-#ifndef GM_KP
-#define GM_KP 1  // A/B: the row's kernel-argument words in one batch (row_meta)
-#endif
-#ifndef GM_FAST_HOOK
-#define GM_FAST_HOOK 3  // A/B: where the fast kernel's second unit issues its loads (0: after the first unit)
-#endif
 template <int B>
 struct RowMeta {
   int k;           // lists delivered to the row (-1: no such row, or a crashed node)
@@ -102,13 +96,11 @@ __device__ __forceinline__ RowMeta<B> row_meta(const SState &s, int r, int par, 
   const uint4 *rbase = s.brec;
   const uint64_t *ecbase = s.evcum;
   int ramp = s.ramp;
-#if GM_KP
   // every kernel-argument word the row's loads need, in one batch: without this the compiler
   // interleaves these (scalar-cache) loads with the row's memory loads, and a wait for one of them
   // waits for all -- the evcum cell then issued only after the inbox had arrived (a second round trip
   // before the gathers). A plain asm statement (not volatile: no memory effect assumed).
   if (UNI) asm("" : "+s"(ibase), "+s"(cbase), "+s"(fbase), "+s"(rbase), "+s"(ecbase), "+s"(ramp));
-#endif
   const int32_t *ib = ibase + (size_t)rc * S_KMAX;
   const i32x4 av = gld((const i32x4 *)ib), bv = gld((const i32x4 *)(ib + 4));
   int4 a = make_int4(av.x, av.y, av.z, av.w);
@@ -474,9 +466,7 @@ __device__ __forceinline__ void unit_load(const SState &s, int t, int band, int 
   in.r = ub * RPW + sub;
   in.msg = s.msg;
   in.tesc = (t & 1) ? s.tesc_in[0] : s.tesc_in[1];
-#if GM_KP
   if (UNI) asm("" : "+s"(in.msg), "+s"(in.tesc));
-#endif
   const size_t slab = (size_t)in.band * s.n;
   // the table slice first: it is independent of the metadata, both in flight together
   unit_table<B>(s, in);
@@ -1076,9 +1066,6 @@ __device__ __forceinline__ bool unit_fast(const SState &s, int t, const UnitIn<B
       nib_max(acc, mv.x, mv.y);
     }
   }
-#if GM_FAST_HOOK == 1
-  nxt();
-#endif
   {
     u16x2 amx = acc[0];
 #pragma unroll
@@ -1140,9 +1127,6 @@ __device__ __forceinline__ bool unit_fast(const SState &s, int t, const UnitIn<B
   bool sv = false, epar = true;
   const bool eslice = in.ebase != 0;  // row-uniform
   const bool slow = eslice || __builtin_amdgcn_ballot_w64(spm != 0);
-#if GM_FAST_HOOK == 2
-  if (!slow) nxt();
-#endif
   if (slow) {
     uint16_t *row16 = (uint16_t *)lds;  // the wave's LDS: a 16-bit cell per column (lane li: [16 li, +16))
     u32x4 *pk4 = (u32x4 *)(park + li * 8);
@@ -1223,9 +1207,6 @@ __device__ __forceinline__ bool unit_fast(const SState &s, int t, const UnitIn<B
     bw[0] = b0.x; bw[1] = b0.y; bw[2] = b0.z; bw[3] = b0.w;
     nb[0] = b1.x; nb[1] = b1.y; nb[2] = b1.z; nb[3] = b1.w;
     if (!epar) em = esc_mask16(bw[0], bw[1], bw[2], bw[3]);  // every escape byte: row16 holds its cell
-#if GM_FAST_HOOK == 2
-    nxt();
-#endif
   }
   // payload words in nib_max's order: the high nibbles of cells [4, 0, 5, 1] | those of [6, 2, 7, 3]
   // shifted down, for cells 0..7 and likewise 8..15
@@ -1264,9 +1245,7 @@ __device__ __forceinline__ bool unit_fast(const SState &s, int t, const UnitIn<B
   }
   // 6. commit: the table and payload stores (the general path's), then this tick's escape list --
   // the entry lanes' survivors first (ballot rank), the lanes' escape bytes after them (esc_emit)
-#if GM_FAST_HOOK >= 3
-  nxt();
-#endif
+  nxt();  // the next unit's loads: in flight under this unit's stores
   if (selflane) s.hbctr[r] = hbself + 1;
   uint32_t eb_out = unit_stores<B>(s, t, in, bw, ov0, ov1, false, 0u, lds);
   const uint64_t svb = __builtin_amdgcn_ballot_w64(sv);
@@ -1392,7 +1371,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GM_BAND_MIN
   bool issued = false;  // wave-uniform
   const bool ok = unit_fast<B>(s, t, in, m, ent, lds, lds + S_LDS_WAVE_WORDS, [&]() {
     if (two) {
-      if (GM_FAST_HOOK != 4) unit_table<B>(s, in2);
+      unit_table<B>(s, in2);
       unit_gather<B, false>(s, t, in2, m, ent2);
     }
     issued = true;
@@ -1405,8 +1384,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GM_BAND_MIN
     if (!issued) {  // the first unit went to the general path before its payload words were consumed
       unit_table<B>(s, in2);
       unit_gather<B, false>(s, t, in2, m, ent2);
-    } else if (GM_FAST_HOOK == 4) {
-      unit_table<B>(s, in2);
     }
     lds_wave_sync();  // the first unit's LDS reads are done before the second one's writes
     if (!unit_fast<B>(s, t, in2, m, ent2, lds, lds + S_LDS_WAVE_WORDS, []() {}) && (threadIdx.x & 63) == 0) {
@@ -2415,9 +2392,7 @@ __global__ __launch_bounds__(256) void gm_s_init(SState s, int warm, int t0, uin
 // ------------------------------------------------------------ launch wrappers
 // (template dispatch over the band width; called by gm_host.hip)
 // the band kernels of rows [r0, r1) (r0, r1 multiples of the rows per unit, or r1 = n)
-#ifndef GM_FAST_BPW
-#define GM_FAST_BPW 2  // bands per wave of gm_s_band_fast
-#endif
+#define GM_FAST_BPW 2  // bands per wave of gm_s_band_fast (profiles/r05/ab4, ab5: 3.38 vs 3.48 ms at one)
 template <int B>
 static void launch_band_b(const SState &s, int t, int drop_pct, int r0, int r1, hipStream_t st) {
   constexpr int RPW = 64 / (B / S_COLS_PER_LANE);
