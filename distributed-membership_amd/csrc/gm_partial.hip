@@ -56,9 +56,6 @@ __device__ unsigned long long g_pprof[16];
   } while (0)
 #endif
 
-#ifndef GM_P_SKIP
-#define GM_P_SKIP 1  // A/B: list-load / merge steps past the node's lists skipped by a scalar branch
-#endif
 #define P_IDMASK 0x01FFFFFFu  // ids <= 2^25
 #define P_OWN 0x80000000u     // table id-word flag: the id was in the node's own list
 #define P_SELF 0x40000000u    // table id-word flag: the node's own entry
@@ -290,9 +287,8 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
 #pragma unroll
   for (int st = 0; st < NSTEP; st++) {
     dv[st] = 0;
-#if GM_P_SKIP
-    if (st * per >= kk) continue;  // wave-uniform: no list in this step (k ~ 5 of up to 12 at S-C)
-#endif
+    if (st * per >= kk) continue;  // wave-uniform: no list in this step (k ~ 5 of up to 12 at S-C; -1.1 %,
+                                   // profiles/r05/ab7/)
     const int j = st * per + jo;
     const bool ok = jo < per && j < kk;
     const int sn = step_val(sv, st);
@@ -331,9 +327,7 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
     const uint32_t tfresh = (uint32_t)max(0, 2 * t - 11);  // hb >= 2t-11 <=> (t-1) - (hb+1)/2 < TFAIL
 #pragma unroll
     for (int st = 0; st < NSTEP; st++) {
-#if GM_P_SKIP
       if (st * per >= kk) continue;  // wave-uniform
-#endif
       const uint64_t e = dv[st];
       bool take = e != 0 && (uint32_t)e >= tfresh;
       const uint32_t id = (uint32_t)(e >> 32);
