@@ -1126,7 +1126,62 @@ __device__ __forceinline__ bool unit_fast(const SState &s, int t, const UnitIn<B
   uint32_t gmask = 0, em = 0, sent = 0;
   bool sv = false, epar = true;
   const bool eslice = in.ebase != 0;  // row-uniform
-  const bool slow = eslice || __builtin_amdgcn_ballot_w64(spm != 0);
+  // 4a. the crash window's common case, without the park: no other cell is marked, the list fits its
+  // inline slot, every escaped cell is stale and no delivered list has a fresh entry at its column
+  // (its merged byte is 0). Then an escaped cell is only re-based (c - 63): it stays escaped -- its
+  // entry lane writes it to this tick's list -- or reaches TREMOVE (a removal: the uniform loop over
+  // the gone entries), and its holding lane restores the escape byte and counts the cell present
+  // and stale, as fast_cell would (y = 0: dpres = dfail = 1; removed: dpres = 0, dfail = 1).
+  bool quick = false;
+  if (eslice && S_EW_TOT(in.ebase) <= S_ESC_IN && !__builtin_amdgcn_ballot_w64(spm != 0)) {
+    const int etot = (int)S_EW_TOT(in.ebase);
+    // 0x01 in the bytes whose stored cell is escaped (byte == S_B_ESC), exact per byte (recomputed
+    // below rather than held across the ballot: registers are what sets this kernel's occupancy)
+    auto esc_bytes = [&](int w) {
+      const uint32_t z = tb4[w] ^ (0x01010101u * S_B_ESC);
+      return (~(((z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | z) & 0x80808080u) >> 7;
+    };
+    bool loud = false;
+#pragma unroll
+    for (int w = 0; w < 4; w++) loud |= (bw[w] & (esc_bytes(w) * 0xFFu)) != 0u;
+    const bool ent_lane = li < etot;
+    const uint32_t ev = ent_lane ? ent >> 16 : 0u;
+    const uint32_t c = ev ? ev - 63u : 0u;  // the re-based cell (y = 0 delivers nothing)
+    const bool gone = ent_lane && (c & 31u) >= GM_TREMOVE;
+    const bool fresh = ent_lane && (c & 31u) < GM_TFAIL;
+    if (!__builtin_amdgcn_ballot_w64(loud || fresh)) {
+      quick = true;
+      int ne = 0;
+#pragma unroll
+      for (int w = 0; w < 4; w++) {
+        const uint32_t eb = esc_bytes(w);
+        bw[w] |= eb;
+        ne += __builtin_popcount(eb);
+      }
+      npres += ne;
+      nfail += ne;
+      const uint32_t col = ent & 0xFFFFu;
+      uint64_t gb = __builtin_amdgcn_ballot_w64(gone);
+      if (gb) {  // TREMOVE ticks: the holding lanes' removal bits, one gone entry per (uniform) step
+        for (; gb; gb &= gb - 1) {
+          const int cg = __builtin_amdgcn_readlane((int)col, __builtin_ctzll(gb));
+          gmask |= li == cg / Q ? 1u << (cg % Q) : 0u;
+        }
+        ngone = __builtin_popcount(gmask);
+        npres -= ngone;
+#pragma unroll
+        for (int w = 0; w < 4; w++) {  // the removed cells' bytes to 0 (absent): cell 4w + b is byte b of word w
+          uint32_t x = (gmask >> (4 * w)) & 0xFu;
+          x = (x | (x << 14)) & 0x00030003u;  // bits 2, 3 -> 16, 17
+          x = (x | (x << 7)) & 0x01010101u;   // bits 1, 17 -> 8, 24
+          bw[w] &= ~(x * 0xFFu);
+        }
+      }
+      sv = ent_lane && !gone;
+      sent = col | (c << 16);
+    }
+  }
+  const bool slow = !quick && (eslice || __builtin_amdgcn_ballot_w64(spm != 0));
   if (slow) {
     uint16_t *row16 = (uint16_t *)lds;  // the wave's LDS: a 16-bit cell per column (lane li: [16 li, +16))
     u32x4 *pk4 = (u32x4 *)(park + li * 8);
@@ -1344,13 +1399,14 @@ __global__ __launch_bounds__(256) void gm_s_band_listed(SState s, int t, int u0,
 // s.fb_list for gm_s_band's listed pass right after, untouched. The list of tick t+1 starts empty.
 // CH: a row chunk [u0, u1) of the pipelined column-shard tick; otherwise every row (no unit bounds
 // among the kernel arguments: the wave's first loads issue as in round 4's codegen)
+// Held to 7 waves per SIMD (72 VGPRs; the crash-window quick path alone would take 75, occupancy 6).
 // BPW: bands per wave (blockIdx.y = a group of BPW bands). With 2, the wave's second unit is the same
 // row in the next band: it shares the row's metadata (one round trip, not two), and its table slice
 // and payload gathers issue as soon as the first unit's payload words are merged (nxt), so they are
 // in flight under the first unit's sweep and stores -- one dependent round trip per unit instead of
 // two (inbox, then gathers).
 template <int B, bool CH, int BPW>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GM_BAND_MINW, 8))) void gm_s_band_fast(SState s, int t, int u0, int u1) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) void gm_s_band_fast(SState s, int t, int u0, int u1) {
   if (!CH) {
     u0 = 0;
     u1 = s.n;
