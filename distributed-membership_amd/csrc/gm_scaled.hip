@@ -40,8 +40,13 @@ typedef uint8_t u8x16 __attribute__((ext_vector_type(16)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 // ------------------------------------------------------------------ gm_s_mtgen
+// Also zeroes the tick's counters (no fill launch of their own each tick): the event spill ring's
+// count and the striped event totals (the last tick's records stay readable until here), and the
+// fused draw's fallback-row count (gm_s_pick0 runs after the band kernels). Grid: max(n, 1 + S_EV_STRIPES).
 __global__ __launch_bounds__(256) void gm_s_mtgen(SState s, int t) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < 1 + S_EV_STRIPES) s.ev_spill_cnt[r] = 0;
+  if (r == 0 && s.pk_cnt) *s.pk_cnt = 0;
   if (r >= s.n) return;
   uint32_t out[S_MT_RAW];
   gm_mt_first16(gm_rd_seed(s.rd_seed, t, r + 1), out);
@@ -548,9 +553,34 @@ __device__ __forceinline__ uint32_t unit_stores(const SState &s, int t, const Un
 // unit_records (every lane): the (band, row) record (rank-select chunk counts, the row's present /
 // numfailed / event counts, the escape-list word eb_out), the events, a column shard's exchange
 // slot. live: the row was merged and swept (else only its record is written).
+// pre (one row per wave, the fast path): the chunk counts and row totals were reduced by the caller
+// (row_counts), which needed the totals first -- piece_in / pf_in, not reduced again here
+struct RowCounts {
+  uint64_t piece;  // present cells per 128-column chunk, one byte each
+  int pf;          // the row slice's present | numfailed << 16
+};
+// one row per wave: the present | numfailed counts per 8-lane chunk on DPP (xor 1, xor 2 by quad_perm,
+// then + the mirrored lane of the other quad), the 8 chunk words by readlane on the scalar side
+__device__ __forceinline__ RowCounts row_counts(int npres, int nfail) {
+  int pf = npres | (nfail << 16);
+  pf += __builtin_amdgcn_update_dpp(0, pf, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+  pf += __builtin_amdgcn_update_dpp(0, pf, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+  pf += __builtin_amdgcn_update_dpp(0, pf, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  RowCounts rc;
+  rc.piece = 0;
+  rc.pf = 0;
+#pragma unroll
+  for (int c = 0; c < 8; c++) {
+    const int v = __builtin_amdgcn_readlane(pf, 8 * c);
+    rc.piece |= (uint64_t)(v & 0xFF) << (8 * c);
+    rc.pf += v;
+  }
+  return rc;
+}
 template <int B, bool DROP>
 __device__ __forceinline__ void unit_records(const SState &s, int t, const UnitIn<B> &in, bool live, uint32_t eb_out,
-                                             int npres, int nfail, int nev, uint32_t evk, int nkept) {
+                                             int npres, int nfail, int nev, uint32_t evk, int nkept,
+                                             const RowCounts *pre = nullptr) {
   constexpr int LPR = B / S_COLS_PER_LANE;  // lanes per row
   constexpr int Q = S_COLS_PER_LANE;        // cells per lane
   const int lane = threadIdx.x & 63;
@@ -571,20 +601,13 @@ __device__ __forceinline__ void unit_records(const SState &s, int t, const UnitI
   // as present | numfailed << 16 (each <= B)
   int pf = npres | (nfail << 16);
   uint64_t piece = 0;
-  if (LPR == 64 && LPC == 8) {
-    // one row per wave: 8-lane chunk sums on DPP (xor 1, xor 2 by quad_perm, then + the
-    // mirrored lane of the other quad), then the 8 chunk words by readlane on the scalar side
-    pf += __builtin_amdgcn_update_dpp(0, pf, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
-    pf += __builtin_amdgcn_update_dpp(0, pf, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
-    pf += __builtin_amdgcn_update_dpp(0, pf, 0x141, 0xF, 0xF, false);  // row_half_mirror
-    int tsum = 0;
-#pragma unroll
-    for (int c = 0; c < 8; c++) {
-      const int v = __builtin_amdgcn_readlane(pf, 8 * c);
-      piece |= (uint64_t)(v & 0xFF) << (8 * c);
-      tsum += v;
-    }
-    pf = tsum;
+  if (LPR == 64 && LPC == 8 && pre) {
+    piece = pre->piece;
+    pf = pre->pf;
+  } else if (LPR == 64 && LPC == 8) {
+    const RowCounts rc = row_counts(npres, nfail);
+    piece = rc.piece;
+    pf = rc.pf;
   } else {
     int cc = npres;
 #pragma unroll
@@ -1273,13 +1296,19 @@ __device__ __forceinline__ bool unit_fast(const SState &s, int t, const UnitIn<B
   // compared; they are always compared where any differ)
   int nev = 0;
   uint32_t evk = 0;
-  int tot = npres + ngone;
-  tot += __builtin_amdgcn_update_dpp(0, tot, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
-  tot += __builtin_amdgcn_update_dpp(0, tot, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
-  tot += __builtin_amdgcn_update_dpp(0, tot, 0x141, 0xF, 0xF, false);  // row_half_mirror
-  tot += __builtin_amdgcn_update_dpp(0, tot, 0x140, 0xF, 0xF, false);  // row_mirror
-  tot = __builtin_amdgcn_readlane(tot, 0) + __builtin_amdgcn_readlane(tot, 16) + __builtin_amdgcn_readlane(tot, 32) +
-        __builtin_amdgcn_readlane(tot, 48);
+  // (the record's chunk counts and totals, reduced once here: their present total is the sweep's, and
+  // the removals are added only where there are some)
+  const RowCounts rcnt = row_counts(npres, nfail);
+  int tot = rcnt.pf & 0xFFFF;
+  if (__builtin_amdgcn_ballot_w64(ngone != 0)) {
+    int g = ngone;
+    g += __builtin_amdgcn_update_dpp(0, g, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    g += __builtin_amdgcn_update_dpp(0, g, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+    g += __builtin_amdgcn_update_dpp(0, g, 0x141, 0xF, 0xF, false);  // row_half_mirror
+    g += __builtin_amdgcn_update_dpp(0, g, 0x140, 0xF, 0xF, false);  // row_mirror
+    tot += __builtin_amdgcn_readlane(g, 0) + __builtin_amdgcn_readlane(g, 16) + __builtin_amdgcn_readlane(g, 32) +
+           __builtin_amdgcn_readlane(g, 48);
+  }
   if (tot != (int)S_BC_PRES(in.bz)) {
 #pragma unroll
     for (int q = 0; q < Q; q++) {
@@ -1322,7 +1351,7 @@ __device__ __forceinline__ bool unit_fast(const SState &s, int t, const UnitIn<B
       if (emany) esc_emit(lds, lane, l, ns + eoff, em, li * Q, etot <= S_ESC_IN, s.err, s.lag_hmin);
     }
   }
-  unit_records<B, false>(s, t, in, true, eb_out, npres, nfail, nev, evk, 0);
+  unit_records<B, false>(s, t, in, true, eb_out, npres, nfail, nev, evk, 0, &rcnt);
   return true;
 }
 
@@ -2471,9 +2500,9 @@ static void launch_band_b(const SState &s, int t, int drop_pct, int r0, int r1, 
 
 // the per-tick work before the band kernels: event counters, the S2 precompute
 hipError_t gm_launch_tick_prologue(const SState &s, int t, hipStream_t st) {
-  // the event records of a tick (per-(row, band) slots + spill ring) stay readable until the next tick
-  (void)hipMemsetAsync(s.ev_spill_cnt, 0, (1 + S_EV_STRIPES) * sizeof(uint32_t), st);
-  hipLaunchKernelGGL(gm_s_mtgen, dim3((s.n + 255) / 256), dim3(256), 0, st, s, t);
+  // the event records of a tick (per-(row, band) slots + spill ring) stay readable until the next
+  // tick: gm_s_mtgen zeroes their counters
+  hipLaunchKernelGGL(gm_s_mtgen, dim3((std::max(s.n, 1 + S_EV_STRIPES) + 255) / 256), dim3(256), 0, st, s, t);
   return hipGetLastError();
 }
 
@@ -2501,8 +2530,7 @@ static hipError_t launch_tick_b(const SState &s, int t, int drop_pct, hipStream_
     (void)hipMemsetAsync(s.selfadd_cnt, 0, sizeof(uint32_t), st);
   }
   const size_t smem = sizeof(uint32_t) * 4 * gm_draw_lds_words(s.wp, s.band);
-  if (pick && B == 1024 && s.pk_list && !s.ramp) {  // four rows per wave, then the rows it left
-    (void)hipMemsetAsync(s.pk_cnt, 0, sizeof(uint32_t), st);
+  if (pick && B == 1024 && s.pk_list && !s.ramp) {  // four rows per wave, then the rows it left (pk_cnt: 0 by gm_s_mtgen)
     hipLaunchKernelGGL((gm_s_pick0<B == 1024 ? B : 1024>), dim3((s.n + 15) / 16), dim3(256),
                        sizeof(uint32_t) * 16 * (size_t)(s.nb + 1), st, s, t);
     hipLaunchKernelGGL((gm_s_pick<B>), dim3(256), dim3(256), smem, st, s, t, 1);
