@@ -9,6 +9,8 @@ export TMPDIR=/tmp
 TAG=${1:-r05q}
 O=gpurun_out/$TAG
 mkdir -p $O
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_band_fast.py -m gpu > $O/band_fast_tests.txt 2>&1 || { tail -30 $O/band_fast_tests.txt; exit 1; }
+tail -2 $O/band_fast_tests.txt
 bash scripts/gpu.sh $TAG sc || exit 1
 timeout -k 10 300 python3 scripts/shard_profile.py --sb > $O/sb_stub.json 2> $O/sb_stub.err || exit 1
 timeout -k 10 300 python3 scripts/shard_profile.py --sb --cluster 65536 > $O/sa_stub.json 2> $O/sa_stub.err || exit 1

@@ -2,7 +2,7 @@
 cells redone one by one; gm_scaled.hip unit_fast) against the general path (GM_BAND_FAST=0),
 tick by tick: events in order, tick statistics, membership tables, msgcount. The schedules drive
 every branch of the fast path: the crash window (cells aging to 15 escape, then TREMOVE removes
-them: the per-cell pass and the removal events), cold start (every cell escaped: escape lists read
+them: the per-cell pass, the quick case of a slice whose escapes only age, and the removal events), cold start (every cell escaped: escape lists read
 back), a loss window (DROP ticks take the general kernel; the ticks after it deliver stale and
 lagging entries, so units are handed back to the general path), and column shards. The oracle
 parity of both paths is test_gpu_scaled.py's (bands 1024 included). Reference: the merge
@@ -31,8 +31,11 @@ def _same_tables(a, b, n, t):
     assert np.array_equal(ha, hb) and np.array_equal(ta, tb), f"tables differ at tick {t}"
 
 
-@pytest.mark.parametrize("init_mode,loss", [(1, 0), (0, 0), (1, 1), (0, 2)])
-def test_fast_path_matches_general_path(monkeypatch, init_mode, loss):
+@pytest.mark.parametrize("init_mode,loss,ncrash", [(1, 0, 41), (1, 0, 20), (0, 0, 41), (1, 1, 41), (0, 2, 41)])
+def test_fast_path_matches_general_path(monkeypatch, init_mode, loss, ncrash):
+    # ncrash 20 (1 %, S-A's share): ~10 escaped cells per 1024-column slice, so most units of the
+    # crash window take the fast path's quick case (inline list, stale, undelivered; removals by the
+    # gone-entry loop); 41 (2 %): ~20 per slice, past the inline slot, the park path
     n = 2048
     kw = dict(rd_seed=7, init_mode=init_mode, init_t0=8 if init_mode else 0, init_seed=11, band=1024)
     if loss == 1:  # 40 % loss for ticks 12..19: stale and lagging entries afterwards
@@ -43,7 +46,7 @@ def test_fast_path_matches_general_path(monkeypatch, init_mode, loss):
     gen, fast = _pair(monkeypatch, n, **kw)
     for s in (gen, fast):
         s.msgcount_record(64)
-    crash = crash_set(n, 41, 42)  # 2 %
+    crash = crash_set(n, ncrash, 42)
     for _ in range(56):
         t = fast.time
         gen.tick()
