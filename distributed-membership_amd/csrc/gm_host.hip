@@ -482,7 +482,9 @@ static int create_scaled(gm_ctx *c) {
   // gm_s_pick0 (single context, B = 1024) and the list of rows it leaves to gm_s_pick
   s.pk_list = nullptr;
   s.pk_cnt = nullptr;
-  if (s.band == 1024 && !s.sharded && sizeof(uint32_t) * 16 * (size_t)(s.nb + 1) <= 65536 &&
+  // gm_s_pick0's LDS: per row of the workgroup's 16, the band prefix (nb + 1 words) and the bands'
+  // chunk counts (nb x 8 bytes)
+  if (s.band == 1024 && !s.sharded && 16 * (sizeof(uint32_t) * (size_t)(s.nb + 1) + sizeof(uint2) * (size_t)s.nb) <= 65536 &&
       !(getenv("GM_PICK0") && atoi(getenv("GM_PICK0")) == 0)) {
     TRY(dalloc(c, &s.pk_list, n));
     TRY(dalloc(c, &s.pk_cnt, 1));

@@ -1158,15 +1158,17 @@ __device__ __forceinline__ bool unit_fast(const SState &s, int t, const UnitIn<B
   bool quick = false;
   if (eslice && S_EW_TOT(in.ebase) <= S_ESC_IN && !__builtin_amdgcn_ballot_w64(spm != 0)) {
     const int etot = (int)S_EW_TOT(in.ebase);
-    // 0x01 in the bytes whose stored cell is escaped (byte == S_B_ESC), exact per byte (recomputed
-    // below rather than held across the ballot: registers are what sets this kernel's occupancy)
+    // 0x80 in the bytes whose stored cell is escaped (byte == S_B_ESC), exact per byte (recomputed
+    // below rather than held across the ballot: registers are what sets this kernel's occupancy);
+    // an escaped column is loud when its merged byte (the delivered nibble << 4) has a nonzero high
+    // nibble -- the SWAR pass's present test on bw, no multiply
     auto esc_bytes = [&](int w) {
       const uint32_t z = tb4[w] ^ (0x01010101u * S_B_ESC);
-      return (~(((z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | z) & 0x80808080u) >> 7;
+      return ~(((z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | z) & 0x80808080u;
     };
     bool loud = false;
 #pragma unroll
-    for (int w = 0; w < 4; w++) loud |= (bw[w] & (esc_bytes(w) * 0xFFu)) != 0u;
+    for (int w = 0; w < 4; w++) loud |= ((((bw[w] >> 1) & 0x78787878u) + 0x78787878u) & esc_bytes(w)) != 0u;
     const bool ent_lane = li < etot;
     const uint32_t ev = ent_lane ? ent >> 16 : 0u;
     const uint32_t c = ev ? ev - 63u : 0u;  // the re-based cell (y = 0 delivers nothing)
@@ -1178,7 +1180,7 @@ __device__ __forceinline__ bool unit_fast(const SState &s, int t, const UnitIn<B
 #pragma unroll
       for (int w = 0; w < 4; w++) {
         const uint32_t eb = esc_bytes(w);
-        bw[w] |= eb;
+        bw[w] |= eb >> 7;  // the escape byte S_B_ESC = 1 back (the merged byte there was 0)
         ne += __builtin_popcount(eb);
       }
       npres += ne;
@@ -1820,15 +1822,19 @@ __global__ __launch_bounds__(256) void gm_s_pick0(SState s, int t) {
   const int rc = valid ? r : s.n - 1;
   const int nb = s.nb, perb = (nb + 15) >> 4, par = t & 1;
   uint32_t *bpre = p_smem + (size_t)slot * (nb + 1);
+  // the band records' chunk counts in LDS too (read with the prefix's words, same lines): a draw then
+  // waits for one load (its table chunk), not two
+  uint2 *bcc = (uint2 *)(p_smem + 16 * (size_t)(nb + 1)) + (size_t)slot * nb;
   const int k = s.inbox_cnt[par][rc], failed = s.failed[rc];
   const uint32_t raw = s.mtraw[(size_t)rc * S_MT_RAW + q];
   uint32_t bp = 0, bf = 0;
   for (int kb = 0; kb < perb; kb++) {
     const int b = q * perb + kb;
     if (b < nb) {
-      const uint32_t z = s.brec[(size_t)b * s.n + rc].z;
-      bp += S_BC_PRES(z);
-      bf += S_BC_FAIL(z);
+      const uint4 rec = s.brec[(size_t)b * s.n + rc];
+      bp += S_BC_PRES(rec.z);
+      bf += S_BC_FAIL(rec.z);
+      bcc[b] = make_uint2(rec.x, rec.y);
     }
   }
   const int bi = row16_scan((int)bp), fi = row16_scan((int)bf);
@@ -1876,8 +1882,8 @@ __global__ __launch_bounds__(256) void gm_s_pick0(SState s, int t) {
     }
     const int band = lo;
     uint32_t rem = act ? x - bpre[band] : 0u;
-    const uint4 rec = act ? s.brec[(size_t)band * s.n + rc] : make_uint4(0u, 0u, 0u, 0u);
-    const uint64_t cc = (uint64_t)rec.x | ((uint64_t)rec.y << 32);
+    const uint2 rcc = act ? bcc[band] : make_uint2(0u, 0u);
+    const uint64_t cc = (uint64_t)rcc.x | ((uint64_t)rcc.y << 32);
     int ch = 0;
 #pragma unroll
     for (int kc = 0; kc < 7; kc++) {
@@ -2532,7 +2538,7 @@ static hipError_t launch_tick_b(const SState &s, int t, int drop_pct, hipStream_
   const size_t smem = sizeof(uint32_t) * 4 * gm_draw_lds_words(s.wp, s.band);
   if (pick && B == 1024 && s.pk_list && !s.ramp) {  // four rows per wave, then the rows it left (pk_cnt: 0 by gm_s_mtgen)
     hipLaunchKernelGGL((gm_s_pick0<B == 1024 ? B : 1024>), dim3((s.n + 15) / 16), dim3(256),
-                       sizeof(uint32_t) * 16 * (size_t)(s.nb + 1), st, s, t);
+                       sizeof(uint32_t) * 16 * (size_t)(s.nb + 1) + sizeof(uint2) * 16 * (size_t)s.nb, st, s, t);
     hipLaunchKernelGGL((gm_s_pick<B>), dim3(256), dim3(256), smem, st, s, t, 1);
   } else if (pick) {
     hipLaunchKernelGGL((gm_s_pick<B>), dim3((s.n + 3) / 4), dim3(256), smem, st, s, t, 0);
