@@ -1180,6 +1180,7 @@ __device__ __forceinline__ bool unit_fast(const SState &s, int t, const UnitIn<B
 #pragma unroll
       for (int w = 0; w < 4; w++) {
         const uint32_t eb = esc_bytes(w);
+        static_assert(S_B_ESC == 1u, "the escape byte is restored as the detection mask's low bit");
         bw[w] |= eb >> 7;  // the escape byte S_B_ESC = 1 back (the merged byte there was 0)
         ne += __builtin_popcount(eb);
       }
