@@ -292,7 +292,15 @@ def collective_bytes(n, world):
     if world <= 1:
         return {"allgather_counts": 0, "allreduce_draws": 0, "allreduce_rounds": 0}
     cap1 = min(4096, max(min(n, 1024), n // 16))
-    return {"allgather_counts": 8 * n, "allreduce_draws": 4 * 16 * n, "allreduce_rounds": 4 * (64 * cap1 + 256 * 256)}
+    # the pipelined all-gather sends whole exchange chunks: xk chunks of R = 2^xlog rows (gm_host.hip:
+    # xlog >= 6 is the least with R * K >= n, K = GM_SCHUNKS, default 2), padding included
+    k = int(os.environ.get("GM_SCHUNKS", "2") or 2)
+    xlog = 6
+    while (1 << xlog) * k < n:
+        xlog += 1
+    R = 1 << xlog
+    xk = (n + R - 1) // R
+    return {"allgather_counts": 8 * xk * R, "allreduce_draws": 4 * 16 * n, "allreduce_rounds": 4 * (64 * cap1 + 256 * 256)}
 
 
 def companion_sb(a, rank, world, local, dist, rtx):
@@ -405,6 +413,11 @@ def main():
         "ranks": ranks,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                      "frac": (achieved / PEAK_HBM_GBPS) if achieved else None, "traffic": traffic,
+                     "achieved_basis": "algorithmic bytes per launch / kernel time (contract field); NOT DRAM "
+                                       "bandwidth: ~5 of every 6 payload reads are Infinity-Cache hits, see "
+                                       "achieved_dram_est / frac_dram",
+                     "achieved_algorithmic": achieved,
+                     "achieved_dram_est": (dram_est / (kernel_ms * 1e-3) / 1e9) if kernel_ms > 0 else None,
                      "traffic_source": traffic_src,
                      "kernel": "gm_s_band" if a.drop_pct else "gm_s_band_fast + gm_s_band_listed",
                      "kernel_ms": kernel_ms,
@@ -453,22 +466,33 @@ def hour_run():
     its first tick, which gm_read_* hands to oc_load_scaled). Summed per tick, not re-run here:
     an hour of CPU is not a bench step. None when the segments are absent."""
     import glob
-    ticks, host = {}, None
+    ticks, host, n = {}, None, None
     for f in sorted(glob.glob(os.path.join(HOUR_DIR, "cpu_hour_seg*.jsonl"))):
+        seg, fn = {}, None
         with open(f) as fh:
             for line in fh:
-                r = json.loads(line)
+                try:
+                    r = json.loads(line)
+                except ValueError:  # a line cut off by an interrupted run
+                    continue
                 if "tick" in r:
-                    ticks[r["tick"]] = r["s"]
-                elif r.get("summary"):
-                    host = r.get("cpu")
-                    n = r["n"]
-    if not ticks:
+                    seg[r["tick"]] = r["s"]
+                elif r.get("segment") or r.get("summary"):
+                    fn = r.get("n", fn)  # the segment header names n; the summary repeats it
+                    host = r.get("cpu", host)
+        if fn is None or (n is not None and fn != n):
+            continue  # no header (or another cluster size): not part of the run
+        n = fn
+        ticks.update(seg)
+    if not ticks or n is None:
         return None
     secs = sum(ticks.values())
     return {"value": n * len(ticks) / secs, "unit": "node-ticks/s", "cores": 1, "kind": "port", "n": n,
             "ticks": f"{min(ticks)}..{max(ticks)} ({len(ticks)} ticks)", "seconds": round(secs, 1),
-            "host": host, "source": "profiles/cpu_hour/cpu_hour_seg*.jsonl (scripts/cpu_hour.py)"}
+            "host": host, "source": "profiles/cpu_hour/cpu_hour_seg*.jsonl (scripts/cpu_hour.py)",
+            "stitched": "25-tick segments run in separate calls; each segment after the first starts from "
+                        "the GPU-reached state of its first tick (gm_read_* -> oc_load_scaled), so the "
+                        "100 ticks are not one CPU process: read the value as seconds per tick"}
 
 
 def main_partial(a):
@@ -578,8 +602,9 @@ def main_partial(a):
                      "frac": (achieved / PEAK_HBM_GBPS) if achieved else None, "traffic": traffic,
                      "traffic_source": traffic_src,
                      "kernel": "gm_p_tick", "kernel_ms": kernel_ms, "alg_bytes_per_launch": b_alg,
-                     "note": "instruction-issue bound, not HBM bound: ~800 VALU + ~580 SALU instructions per "
-                             "node (PMC, profiles/r03/sc_hash32/mix_sc.txt; DESIGN.md PARTIAL); the "
+                     "achieved_basis": "algorithmic bytes per launch / kernel time",
+                     "note": "instruction-issue bound, not HBM bound (PMC SQ mix per node, "
+                             "profiles/r05/gate_close/mix_sc_small_per_dispatch.txt; DESIGN.md PARTIAL); the "
                              "contract's bound field only offers hbm|mfma"},
     }
     if world > 1:

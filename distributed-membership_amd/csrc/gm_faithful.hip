@@ -97,11 +97,6 @@ __global__ __launch_bounds__(F_RECV_THREADS) void gm_f_recv(FState s, int t) {
   uint16_t *scr = (uint16_t *)(act + ((n + 3) & ~3));   // [2][cap]: hole ranks, hit positions
   const int cap = (int)((F_RECV_LDS - ((uint8_t *)scr - (uint8_t *)s_lds)) / 4);
   int B = *s.bufsize;
-#ifdef GM_F_PROFILE
-  const uint64_t c0 = wall_clock64();
-  const int B00 = B;
-  uint64_t c1 = 0;
-#endif
   for (int j = threadIdx.x; j < (n + 1) * nsw; j += F_RECV_THREADS) cw[j] = 0;
   for (int i = threadIdx.x; i < n; i += F_RECV_THREADS)
     act[i] = t > s.start[i] && !s.failed[i];  // Application.cpp:130
@@ -124,9 +119,6 @@ __global__ __launch_bounds__(F_RECV_THREADS) void gm_f_recv(FState s, int t) {
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#ifdef GM_F_PROFILE
-  c1 = wall_clock64();
-#endif
   int qbase = 0;
   for (int i = 0; i < n; i++) {
     if (threadIdx.x == 0) { s.q_off[i] = qbase; s.q_cnt[i] = 0; }
@@ -207,11 +199,6 @@ __global__ __launch_bounds__(F_RECV_THREADS) void gm_f_recv(FState s, int t) {
     s.rmeta[0] = qbase;
     s.rmeta[1] = B;
   }
-#ifdef GM_F_PROFILE
-  if (threadIdx.x == 0 && t % 100 == 50)
-    printf("recv t=%d B0=%d q=%d prolog=%llu loop=%llu (x10ns)\n", t, B00, qbase, (unsigned long long)(c1 - c0),
-           (unsigned long long)(wall_clock64() - c1));
-#endif
 }
 
 // queues and survivors (grid-stride over both), recv_msgs counters

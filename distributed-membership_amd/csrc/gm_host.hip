@@ -48,7 +48,6 @@ hipError_t gm_launch_partial_reset(const PState &s, hipStream_t st);
 hipError_t gm_launch_partial_chunk(const PState &s, int t, const uint32_t *mtraw, int c, hipStream_t st);
 hipError_t gm_launch_msgcount(const SState &s, int t, bool dropped, int phase, hipStream_t st);
 size_t gm_partial_lds_bytes();
-void gm_partial_profile_dump(hipStream_t st);
 
 #define GM_T_LIMIT 32766  // packed 16-bit hb/ts stay exact: hb <= 2t+1 < 0xFFFF
 #define GM_F_MAILBOX 4096  // FAITHFUL events copied back with the count and error flags
@@ -67,6 +66,9 @@ struct gm_ctx {
   std::vector<hipEvent_t> tev;            // per-tick band-kernel event pairs (single context)
   double kernel_ms_sum = 0;
   int shard_sync = -1;               // sharded tick draw rounds: 1 host-driven unbounded loop, 0 bounded
+  int diag_zero_row = -1;            // diagnostics (GM_DIAG_ZERO_ROW, tests): the pipelined column-shard tick
+                                     //   clears this row's cells after its band kernels, so its records'
+                                     //   counts disagree with the cells and a draw finds no holder
                                      // stream-ordered, -1 auto (env GM_SHARD_SYNC)
   int64_t nfailed = 0;               // nodes with failed_h set (gm_set_failed; nodeStart clears it)
   // sharded bounded draw rounds: rows they could not finish (npending) copied back without a
@@ -112,6 +114,9 @@ struct gm_ctx {
   std::vector<hipEvent_t> p_chev;      // per chunk: its node ticks are done (compute stream)
   hipEvent_t p_done = nullptr;         // the tick's exchange + unpacks are done (comm stream)
   std::vector<double> p_xq;            // per row shard q: probability that a sender addresses q (xcap)
+  uint64_t p_crash_hash = 0;           // hash of the whole crash set the block capacities were derived from
+  bool p_crash_check = false;          // agree it across the ranks at the next RCCL tick
+  uint64_t *p_crash_dev = nullptr;     // [2] device words of that check
 };
 
 // Every copy and fill of a context goes through its own stream. That stream is non-blocking, so the
@@ -140,6 +145,14 @@ static thread_local char g_errbuf[256];
       snprintf(g_errbuf, sizeof g_errbuf, "%s:%d %s", __FILE__, __LINE__, hipGetErrorString(e_)); \
       return GM_EDEVICE;                                                              \
     }                                                                                 \
+  } while (0)
+#define NCCLCHECK(x)                                                                 \
+  do {                                                                               \
+    ncclResult_t r_ = (x);                                                           \
+    if (r_ != ncclSuccess) {                                                         \
+      snprintf(g_errbuf, sizeof g_errbuf, "%s:%d RCCL %s", __FILE__, __LINE__, ncclGetErrorString(r_)); \
+      return GM_ECOMM;                                                               \
+    }                                                                                \
   } while (0)
 
 // inbox slots per receiver: the compiled capacity; GM_INBOX_CAP (diagnostics, tests) lowers it
@@ -392,6 +405,7 @@ static int create_scaled(gm_ctx *c) {
     s.lag_hmin = 254 - 2 * L;
   }
   c->shard_sync = getenv("GM_SHARD_SYNC") ? (atoi(getenv("GM_SHARD_SYNC")) ? 1 : 0) : -1;
+  if (getenv("GM_DIAG_ZERO_ROW")) c->diag_zero_row = atoi(getenv("GM_DIAG_ZERO_ROW"));
   TRY(dalloc(c, &s.msg, cells));        // nibbles: 2 parities x band/2 bytes per (band, row)
   // Escape storage (gm_scaled.h), one set per tick parity: a 16-cell inline slot per (band, row)
   // list (1/32 B per cell at B = 1024) and the pools. The pools are DENSE-equivalent (every
@@ -742,7 +756,6 @@ extern "C" int gm_destroy(gm_ctx *c) {
   for (hipEvent_t e : c->p_chev) (void)hipEventDestroy(e);
   if (c->p_done) (void)hipEventDestroy(c->p_done);
   if (c->p_comm) (void)hipStreamDestroy(c->p_comm);
-  if (c->cfg.mode == GM_MODE_PARTIAL) gm_partial_profile_dump(c->stream);
   if (c->p_side) {
     (void)hipStreamSynchronize(c->p_side);
     (void)hipStreamDestroy(c->p_side);
@@ -941,6 +954,26 @@ static int tick_partial(gm_ctx *c) {
     HIPCHECK(gm_launch_partial_chunk(st, t, mt, 0, c->stream));
     if (k1) HIPCHECK(hipEventRecord(k1, c->stream));
   } else {
+    if (c->p_crash_check) {
+      // the block capacities (send counts of this rank, receive counts of its peers) derive from the
+      // crash set each rank was given (gm_set_failed): a rank holding another set would size its
+      // ncclAllToAllv differently and hang or corrupt it. One MAX-allreduce of (h, ~h) after each
+      // change shows any disagreement, and the context latches GM_ESTATE instead.
+      c->p_crash_check = false;
+      if (!c->p_crash_dev) {
+        HIPCHECK(hipMalloc(&c->p_crash_dev, 2 * sizeof(uint64_t)));
+        c->allocs.push_back(c->p_crash_dev);
+      }
+      uint64_t hv[2] = {c->p_crash_hash, ~c->p_crash_hash}, mx[2] = {0, 0};
+      HIPCHECK(hipMemcpyAsync(c->p_crash_dev, hv, sizeof hv, hipMemcpyHostToDevice, c->stream));
+      NCCLCHECK(ncclAllReduce(c->p_crash_dev, c->p_crash_dev, 2, ncclUint64, ncclMax, c->comm, c->stream));
+      HIPCHECK(hipMemcpyAsync(mx, c->p_crash_dev, sizeof mx, hipMemcpyDeviceToHost, c->stream));
+      HIPCHECK(hipStreamSynchronize(c->stream));
+      if (mx[0] != hv[0] || mx[1] != hv[1]) {
+        c->latched = GM_ESTATE;
+        return c->latched;
+      }
+    }
     // chunk pipeline: every chunk's node ticks queue on the compute stream; the exchange of
     // chunk q runs on the comm stream once q's kernels are done, while q+1.. still compute
     for (int q = 0; q < st.nchunk; q++) {
@@ -1141,16 +1174,45 @@ static int drain_partial(gm_ctx *c, std::vector<gm_event> &out) {
   const int t = c->t - 1;
   std::vector<uint32_t> jm(p.nloc);
   HIPCHECK(ctx_memcpy(c, jm.data(), p.ev_jm, sizeof(uint32_t) * jm.size(), hipMemcpyDeviceToHost));
-  std::vector<uint64_t> lst((size_t)p.nloc * p.V);
-  HIPCHECK(ctx_memcpy(c, lst.data(), p.lists + (size_t)(t & 1) * p.rows * p.V, sizeof(uint64_t) * lst.size(),
-                      hipMemcpyDeviceToHost));
-  bool any_rem = false;
-  for (int32_t v : cnt) any_rem |= (v >> 16) != 0;
+  // only the rows that hold events are copied: runs of such rows as async copies on the context
+  // stream, one wait at the end -- not the whole list / event buffers (~4.3 GB of lists
+  // per S-C context for a tick with any join). Gaps up to `gap` rows are bridged, so there are at
+  // most ~4096 copies however the rows are spread.
+  const int gap = std::max(64, p.nloc / 4096);
+  auto copy_rows = [&](void *dst, const void *src, size_t rowb, int sel) -> hipError_t {
+    int r = 0;
+    while (r < p.nloc) {
+      auto has = [&](int q) { return sel == 0 ? (cnt[q] & 0xFFFF) != 0 : (cnt[q] >> 16) != 0; };
+      while (r < p.nloc && !has(r)) r++;
+      if (r >= p.nloc) break;
+      int e = r + 1, last = r;
+      while (e < p.nloc && e - last <= gap) {
+        if (has(e)) last = e;
+        e++;
+      }
+      const hipError_t err = hipMemcpyAsync((uint8_t *)dst + (size_t)r * rowb, (const uint8_t *)src + (size_t)r * rowb,
+                                            (size_t)(last + 1 - r) * rowb, hipMemcpyDeviceToHost, c->stream);
+      if (err != hipSuccess) return err;
+      r = last + 1;
+    }
+    return hipSuccess;
+  };
+  bool any_join = false, any_rem = false;
+  for (int32_t v : cnt) {
+    any_join |= (v & 0xFFFF) != 0;
+    any_rem |= (v >> 16) != 0;
+  }
+  std::vector<uint64_t> lst;
+  if (any_join) {
+    lst.resize((size_t)p.nloc * p.V);
+    HIPCHECK(copy_rows(lst.data(), p.lists + (size_t)(t & 1) * p.rows * p.V, sizeof(uint64_t) * p.V, 0));
+  }
   std::vector<uint32_t> ev;
   if (any_rem) {
     ev.resize((size_t)p.nloc * row);
-    HIPCHECK(ctx_memcpy(c, ev.data(), p.ev, sizeof(uint32_t) * ev.size(), hipMemcpyDeviceToHost));
+    HIPCHECK(copy_rows(ev.data(), p.ev, sizeof(uint32_t) * row, 1));
   }
+  HIPCHECK(hipStreamSynchronize(c->stream));
   out.reserve(out.size() + tot);
   for (int r = 0; r < p.nloc; r++) {
     const int nj = cnt[r] & 0xFFFF, nr = cnt[r] >> 16;
@@ -1687,15 +1749,6 @@ extern "C" int gm_crash_set(int32_t n, int32_t count, uint64_t seed, int32_t *ou
 // has its targets. Collectives are RCCL on the context stream (gm_comm_init),
 // or in-process between contexts of one device (gm_shard_loopback, tests).
 
-#define NCCLCHECK(x)                                                                 \
-  do {                                                                               \
-    ncclResult_t r_ = (x);                                                           \
-    if (r_ != ncclSuccess) {                                                         \
-      snprintf(g_errbuf, sizeof g_errbuf, "%s:%d RCCL %s", __FILE__, __LINE__, ncclGetErrorString(r_)); \
-      return GM_ECOMM;                                                               \
-    }                                                                                \
-  } while (0)
-
 
 extern "C" int gm_comm_unique_id(uint8_t *out128) {
   if (!out128) return GM_EINVAL;
@@ -2142,6 +2195,10 @@ static int tick_sharded(gm_ctx *c) {
     for (int ch = 0; ch < s.xk; ch++) {
       const int r0 = ch << s.xlog;
       HIPCHECK(gm_launch_band_rows(s, t, drop ? c->cfg.drop_pct : -1, r0, r0 + xchunk_rows(s, ch), c->stream));
+      const int zr = c->diag_zero_row;
+      if (zr >= r0 && zr < r0 + xchunk_rows(s, ch) && zr < c->n)
+        for (int b = 0; b < s.nb; b++)
+          HIPCHECK(hipMemsetAsync(s.table + ((size_t)b * n + zr) * s.band, 0, s.band, c->stream));
       HIPCHECK(hipEventRecord(c->p_chev[ch], c->stream));
     }
     if (k1) HIPCHECK(hipEventRecord(k1, c->stream));
@@ -2301,6 +2358,11 @@ static int partial_caps(gm_ctx *c) {
     for (int i = a; i < b; i++) live[g] += c->failed_h[i] ? 0 : 1;
     tot += live[g];
   }
+  uint64_t h = 0x9E3779B97F4A7C15ull;  // the crash set every rank must hold (the capacities follow from it)
+  for (int i = 0; i < p.n; i++)
+    if (c->failed_h[i]) h = (h ^ (uint64_t)(uint32_t)i) * 0x100000001B3ull + 0x632BE59BD9B4E019ull;
+  c->p_crash_hash = h;
+  c->p_crash_check = true;
   c->p_xq.assign(G, 0.0);
   for (int g = 0; g < G; g++) {
     const double fs = (double)((int64_t)p.n * (g + 1) / G - (int64_t)p.n * g / G) / p.n;

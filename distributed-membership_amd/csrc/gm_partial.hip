@@ -42,20 +42,6 @@
 #include "gm_device.h"
 #include "gm_partial.h"
 
-#ifdef GM_P_PROFILE  // measurement builds only: per-section shader clocks of every 64th node
-__device__ unsigned long long g_pprof[16];
-#define PPROF(k)                                      \
-  do {                                                \
-    const uint64_t pnow_ = __builtin_amdgcn_s_memtime(); \
-    pp_[k] += pnow_ - pt_;                            \
-    pt_ = pnow_;                                      \
-  } while (0)
-#else
-#define PPROF(k) \
-  do {           \
-  } while (0)
-#endif
-
 #define P_IDMASK 0x01FFFFFFu  // ids <= 2^25
 #define P_OWN 0x80000000u     // table id-word flag: the id was in the node's own list
 #define P_SELF 0x40000000u    // table id-word flag: the node's own entry
@@ -237,9 +223,6 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
   constexpr int DS = ((1 + KK) * P_VMAX + 63) / 64;   // dense entries per lane
   constexpr int NSTEP = (KK + 1) / 2;                 // list-load steps (>= 2 lists per step)
   using mask_t = typename std::conditional<(DS > 32), uint64_t, uint32_t>::type;  // one bit per dense slot
-#ifdef GM_P_PROFILE
-  uint64_t pp_[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, pt_ = __builtin_amdgcn_s_memtime();
-#endif
   uint32_t *tid = (uint32_t *)base;
   uint32_t *thb = tid + H;
   uint32_t *hist = thb + H;
@@ -312,7 +295,6 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
     pairv = (uint32_t)gm_mix64(s.drop_seed ^ ((uint64_t)(uint32_t)(t - 1) << 48) ^ ((uint64_t)(uint32_t)sg << 24) ^
                                (uint64_t)(uint32_t)i);
   const uint32_t dthr = gm_drop_thresh(s.drop_pct);
-  PPROF(0);
   p_wsync();
   // ---- 2. merge: own entries first (they carry P_OWN), then the delivered lists
   int hslot = -1;
@@ -321,7 +303,6 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
     const uint32_t id = (uint32_t)(own >> 32);
     hslot = p_insert<H>(tid, thb, id, id | P_OWN, (uint32_t)own);
   }
-  PPROF(1);
   p_wsync();
   {
     const uint32_t tfresh = (uint32_t)max(0, 2 * t - 11);  // hb >= 2t-11 <=> (t-1) - (hb+1)/2 < TFAIL
@@ -340,7 +321,6 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
       if (mc) nrecv += __builtin_popcountll(__ballot(take));
     }
   }
-  PPROF(2);
   p_wsync();
   // ---- 3. self bump (heartbeat++; myPos->setheartbeat(heartbeat++)), then sweep + compaction
   {
@@ -362,7 +342,6 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
       s.hbctr[li] = hbnew + 1;
     }
   }
-  PPROF(3);
   p_wsync();
   uint32_t *evr = s.ev + (size_t)li * 2 * V;
   int m, removed, nrem;
@@ -421,7 +400,6 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
       pos += a;
     }
   }
-  PPROF(4);
   p_wsync();
   // ---- 4. dense entries e = s*64 + lane; eviction to V
   // only the first dm = ceil(m / 64) of the DS per-lane slots hold entries (m is wave-uniform):
@@ -471,11 +449,6 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
       keep |= (v & (mask_t)(((dw[q] & P_SELF) != 0) | (d < dcut))) << q;
       bucket |= (v & (mask_t)(!(dw[q] & P_SELF) && d == dcut)) << q;
     }
-#ifdef GM_P_PROFILE
-    pp_[10] += 1;  // evictions
-    pp_[11] += needb != bsz;  // key radix path
-    pp_[13] += bsz;
-#endif
     if (needb == bsz) {
       keep |= bucket;
     } else {
@@ -514,9 +487,6 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
       if (needc == bsz2) {
         keep |= cand;
       } else {
-#ifdef GM_P_PROFILE
-        pp_[12] += needc;  // min-selection rounds
-#endif
         for (; needc > 0; needc--) {  // take the smallest remaining candidate key (keys are distinct)
           uint32_t mn = ~0u;
 #pragma unroll
@@ -534,7 +504,6 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
       }
     }
   }
-  PPROF(5);
   // ---- 5. compact the kept entries (<= V), rank them by id
   int cnt = 0;
   p_wsync();  // the eviction histogram is dead: it takes the stores of the entries not kept
@@ -582,7 +551,6 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
   const int nj = __builtin_popcountll(jb);
   // joins (ascending id): a mask over the final list (ev_jm)
   const int numfailed = removed + __builtin_popcountll(__ballot(lane < cnt && p_aged(t, (uint32_t)x, GM_TFAIL)));
-  PPROF(6);
   // ---- 6. gossip draw over the final list (MP1Node.cpp:449-489)
   const int numpot = cnt - 1 - numfailed;
   const int target = min(GM_FANOUT, numpot);
@@ -668,7 +636,6 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
       if (lane < ng) gl[lane] = (uint32_t)(lane == 0 ? g0 : lane == 1 ? g1 : lane == 2 ? g2 : lane == 3 ? g3 : g4);
     }
   }
-  PPROF(7);
   p_wsync();
   // ---- sends: one parallel round of inbox appends, one lane per local target. A target owned by
   // another row shard is only recorded (targets / rowstat): gm_p_pack builds the exchange records from
@@ -691,14 +658,6 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
     s.mc_sent[(size_t)t * s.nloc + li] = (uint32_t)(ng * (cnt - (numfailed - removed)));
     s.mc_recv[(size_t)t * s.nloc + li] = (uint32_t)nrecv;
   }
-#ifdef GM_P_PROFILE
-  PPROF(8);
-  if (lane == 0 && (li & 63) == 0) {
-    pp_[14] = (uint64_t)m;
-    for (int q = 0; q < 15; q++) atomicAdd(&g_pprof[q], (unsigned long long)pp_[q]);
-    atomicAdd(&g_pprof[15], 1ull);
-  }
-#endif
 }
 
 // crashed node: frozen (its list carried to this tick's buffer unchanged), inbox dropped
@@ -1030,19 +989,3 @@ hipError_t gm_launch_partial_unpack(const PState &s, int t, int base, int nrecv,
 
 size_t gm_partial_lds_bytes() { return 4 * (size_t)PLds<P_HB>::bytes; }
 
-// measurement builds: the per-section clocks (0 elsewhere)
-void gm_partial_profile_dump(hipStream_t st) {
-#ifdef GM_P_PROFILE
-  unsigned long long h[16];
-  if (hipMemcpyFromSymbolAsync(h, HIP_SYMBOL(g_pprof), sizeof h, 0, hipMemcpyDeviceToHost, st) == hipSuccess &&
-      hipStreamSynchronize(st) == hipSuccess && h[15]) {
-    const char *nm[9] = {"loads", "own-insert", "merge", "self", "sweep", "evict", "rank+store", "draw", "sends"};
-    unsigned long long tot = 0;
-    for (int q = 0; q < 9; q++) tot += h[q];
-    for (int q = 0; q < 9; q++)
-      fprintf(stderr, "pprof %-10s %8.0f clk/node %5.1f%%\n", nm[q], (double)h[q] / h[15], 100.0 * h[q] / tot);
-    fprintf(stderr, "pprof per node: evictions %.3f, key-radix path %.3f, min-selection rounds %.3f, cut bucket %.1f, union m %.1f\n",
-            (double)h[10] / h[15], (double)h[11] / h[15], (double)h[12] / h[15], (double)h[13] / h[15], (double)h[14] / h[15]);
-  }
-#endif
-}

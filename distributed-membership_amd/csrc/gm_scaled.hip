@@ -2172,7 +2172,12 @@ __global__ __launch_bounds__(256) void gm_s_draw0(SState s, int t, int r0, int r
     const int cnt = __builtin_popcount(m0) + __builtin_popcount(m1);
     const int incl = row16_scan(cnt);
     const int excl = incl - cnt;
-    if (act && (int)rem >= excl && (int)rem < incl) {  // the holder: the (rem - excl)-th present cell of its 8
+    const bool holder = act && (int)rem >= excl && (int)rem < incl;
+    // a draw landing here that no lane holds (the record's counts and the cells disagree) would
+    // leave status[r][d] at an older tick's value, which the MAX-allreduce could pick: fail loudly
+    // instead, as gm_s_draw (status -1) and gm_s_pick0 do
+    if (act && q == 0 && !row16_bits(__ballot(holder), g)) atomicOr(s.err, GM_ERR_DRAWS);
+    if (holder) {  // the (rem - excl)-th present cell of its 8
       int need = (int)rem - excl, pos = 0;
       uint32_t byte = 0;
 #pragma unroll

@@ -91,7 +91,10 @@ def load_library():
         "gm_shard_merge": [ctypes.c_void_p], "gm_shard_draw": [ctypes.c_void_p, i32, i32],
         "gm_shard_accept": [ctypes.c_void_p, i32, P(i32)], "gm_shard_end_tick": [ctypes.c_void_p],
     }
-    ab_build = "GM_LIBRARY" in os.environ  # an older measurement build (A/B) may lack newer entry points
+    # GM_AB_BUILD=1 (A/B scripts only): an older measurement build may lack newer entry points, which
+    # are then left unbound. Otherwise every entry point must be present, whatever library GM_LIBRARY
+    # names, so a stale libgm fails here and not at its first call of a missing symbol
+    ab_build = os.environ.get("GM_AB_BUILD") == "1"
     for name, args in sig.items():
         if ab_build and not hasattr(lib, name):
             continue

@@ -111,7 +111,8 @@ typedef struct gm_config {
   int32_t reserved;
 } gm_config;
 
-/* one log record; `order` sorts records of a drain into reference log order */
+/* one log record; gm_drain_events returns them already in reference log order (Log.cpp lines of a
+ * tick: loggers descending, joins in dequeue / ascending id order, removals descending id) */
 typedef struct gm_event {
   int32_t t;
   int32_t logger;          /* node index (id = logger + 1) whose LOG call it is */
@@ -141,6 +142,10 @@ int gm_time(gm_ctx *ctx, int32_t *t);
 
 /* Application::fail hooks (called between ticks, host order preserved) */
 int gm_rand(gm_ctx *ctx, int32_t *out);
+/* gm_set_failed: sharded contexts (column or row shards of one cluster) must all be given the
+ * SAME crash set, as every rank of the reference run sees one Application::fail. Row shards derive
+ * their exchange block sizes from it; they all-reduce a hash of the set at the next tick and return
+ * GM_ESTATE when a rank disagrees. */
 int gm_set_failed(gm_ctx *ctx, const int32_t *idx, int32_t n);
 int gm_set_dropmsg(gm_ctx *ctx, int32_t on);
 

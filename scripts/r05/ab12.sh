@@ -13,12 +13,12 @@ timeout -k 10 900 $PT tests/test_gpu_band_fast.py tests/test_gpu_scaled.py tests
 tail -2 $O/gpu_tests.txt
 for k in 1 2 3; do
   timeout -k 10 300 python3 bench.py --no-cpu --no-pmc --no-companion > $O/sa_tree_$k.json 2> $O/sa_tree_$k.err || exit 1
-  GM_LIBRARY=var_q/libgm_nomul.so timeout -k 10 300 python3 bench.py --no-cpu --no-pmc --no-companion > $O/sa_base_$k.json 2> $O/sa_base_$k.err || exit 1
+  GM_AB_BUILD=1 GM_LIBRARY=var_q/libgm_nomul.so timeout -k 10 300 python3 bench.py --no-cpu --no-pmc --no-companion > $O/sa_base_$k.json 2> $O/sa_base_$k.err || exit 1
 done
 for f in $O/sa_*.json; do python3 -c "import json;d=json.load(open('$f'));print('$f', round(d['roofline']['kernel_ms'],3), round(d['ms_per_step'],3), round(d['value']/1e6,2))"; done
 for k in 1 2; do
   timeout -k 10 300 python -u scripts/tick_times.py 65536 > $O/ticks_tree_$k.txt 2>&1 || exit 1
-  GM_LIBRARY=var_q/libgm_nomul.so timeout -k 10 300 python -u scripts/tick_times.py 65536 > $O/ticks_base_$k.txt 2>&1 || exit 1
+  GM_AB_BUILD=1 GM_LIBRARY=var_q/libgm_nomul.so timeout -k 10 300 python -u scripts/tick_times.py 65536 > $O/ticks_base_$k.txt 2>&1 || exit 1
 done
 for f in $O/ticks_*.txt; do python3 -c "
 import re

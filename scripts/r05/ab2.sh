@@ -12,7 +12,7 @@ timeout -k 10 900 $PT tests/test_gpu_scaled.py tests/test_gpu_band_fast.py tests
 tail -3 $O/gpu_tests.txt
 for k in 1 2; do
   for v in base sweep_jm claim1 claim2; do
-    GM_LIBRARY=var_ab/libgm_$v.so timeout -k 10 300 python3 bench.py --scenario S-C --no-cpu --no-pmc --steps 10 --warmup 2 \
+    GM_AB_BUILD=1 GM_LIBRARY=var_ab/libgm_$v.so timeout -k 10 300 python3 bench.py --scenario S-C --no-cpu --no-pmc --steps 10 --warmup 2 \
       > $O/sc_${v}_$k.json 2> $O/sc_${v}_$k.err || exit 1
   done
   timeout -k 10 300 python3 bench.py --no-cpu --no-pmc --no-companion > $O/sa_pick0_$k.json 2> $O/sa_pick0_$k.err || exit 1

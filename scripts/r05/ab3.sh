@@ -13,11 +13,11 @@ timeout -k 10 900 $PT tests/test_gpu_scaled.py tests/test_gpu_band_fast.py tests
 tail -3 $O/gpu_tests.txt
 for k in 1 2 3; do
   timeout -k 10 300 python3 bench.py --no-cpu --no-pmc --no-companion > $O/sa_cur_$k.json 2> $O/sa_cur_$k.err || exit 1
-  GM_LIBRARY=var_ab/libgm_r04.so timeout -k 10 300 python3 bench.py --no-cpu --no-pmc --no-companion > $O/sa_r04_$k.json 2> $O/sa_r04_$k.err || exit 1
+  GM_AB_BUILD=1 GM_LIBRARY=var_ab/libgm_r04.so timeout -k 10 300 python3 bench.py --no-cpu --no-pmc --no-companion > $O/sa_r04_$k.json 2> $O/sa_r04_$k.err || exit 1
 done
 for f in $O/sa_*.json; do python3 -c "import json;d=json.load(open('$f'));print('$f', round(d['roofline']['kernel_ms'],3), round(d['ms_per_step'],3), round(d['value']/1e6,2))"; done
 timeout -k 10 300 python3 scripts/partial_shard_profile.py > $O/pshard_npw4.json 2> $O/pshard_npw4.err || exit 1
 for v in 8 16; do
-  GM_LIBRARY=var_pshard/libgm_npw$v.so timeout -k 10 300 python3 scripts/partial_shard_profile.py > $O/pshard_npw$v.json 2> $O/pshard_npw$v.err || exit 1
+  GM_AB_BUILD=1 GM_LIBRARY=var_pshard/libgm_npw$v.so timeout -k 10 300 python3 scripts/partial_shard_profile.py > $O/pshard_npw$v.json 2> $O/pshard_npw$v.err || exit 1
 done
 for f in $O/pshard_*.json; do python3 -c "import json;d=json.load(open('$f'));print('$f', round(d['ms_per_tick_all_shards_serialised']/d['shards'],3), d['recv_mb_mean'])"; done

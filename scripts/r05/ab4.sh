@@ -23,12 +23,12 @@ tail -2 $O/gpu_tests.txt
 for k in 1 2; do
   timeout -k 10 300 python3 bench.py --no-cpu --no-pmc --no-companion > $O/sa_h3_$k.json 2> $O/sa_h3_$k.err || fail "bench tree"
   for v in b1 b1kp0 b2h0 h1 h38 head; do
-    GM_LIBRARY=var_fast/libgm_$v.so timeout -k 10 300 python3 bench.py --no-cpu --no-pmc --no-companion > $O/sa_${v}_$k.json 2> $O/sa_${v}_$k.err || fail "bench $v"
+    GM_AB_BUILD=1 GM_LIBRARY=var_fast/libgm_$v.so timeout -k 10 300 python3 bench.py --no-cpu --no-pmc --no-companion > $O/sa_${v}_$k.json 2> $O/sa_${v}_$k.err || fail "bench $v"
   done
 done
 for f in $O/sa_*.json; do python3 -c "import json;d=json.load(open('$f'));print('$f', round(d['roofline']['kernel_ms'],3), round(d['ms_per_step'],3), round(d['value']/1e6,2))"; done
 timeout -k 10 300 python -u scripts/tick_times.py 65536 > $O/tick_times_h3.txt 2>&1 || fail "ticks"
-GM_LIBRARY=var_fast/libgm_head.so timeout -k 10 300 python -u scripts/tick_times.py 65536 > $O/tick_times_head.txt 2>&1 || fail "ticks head"
+GM_AB_BUILD=1 GM_LIBRARY=var_fast/libgm_head.so timeout -k 10 300 python -u scripts/tick_times.py 65536 > $O/tick_times_head.txt 2>&1 || fail "ticks head"
 timeout -k 10 300 python3 scripts/shard_profile.py --sb > $O/sb_stub.json 2> $O/sb_stub.err || fail "sb stub"
 timeout -k 10 300 python3 scripts/shard_profile.py --sb --cluster 65536 > $O/sa_stub.json 2> $O/sa_stub.err || fail "sa stub"
 GM_SCHUNKS=2 timeout -k 10 300 python3 scripts/shard_profile.py --sb > $O/sb_stub_k2.json 2> $O/sb_stub_k2.err || fail "sb stub k2"

@@ -18,13 +18,13 @@ fail() { echo "$1"; [ -n "$CPU_PID" ] && kill $CPU_PID; exit 1; }
 for k in 1 2 3; do
   timeout -k 10 300 python3 bench.py --no-cpu --no-pmc --no-companion > $O/sa_tree_$k.json 2> $O/sa_tree_$k.err || fail "bench tree"
   for v in head b2h0 b1; do
-    GM_LIBRARY=var_fast/libgm_$v.so timeout -k 10 300 python3 bench.py --no-cpu --no-pmc --no-companion > $O/sa_${v}_$k.json 2> $O/sa_${v}_$k.err || fail "bench $v"
+    GM_AB_BUILD=1 GM_LIBRARY=var_fast/libgm_$v.so timeout -k 10 300 python3 bench.py --no-cpu --no-pmc --no-companion > $O/sa_${v}_$k.json 2> $O/sa_${v}_$k.err || fail "bench $v"
   done
 done
 for f in $O/sa_*.json; do python3 -c "import json;d=json.load(open('$f'));print('$f', round(d['roofline']['kernel_ms'],3), round(d['ms_per_step'],3), round(d['value']/1e6,2))"; done
 for k in 1 2; do
   timeout -k 10 300 python -u scripts/tick_times.py 65536 > $O/ticks_tree_$k.txt 2>&1 || fail "ticks"
-  GM_LIBRARY=var_fast/libgm_head.so timeout -k 10 300 python -u scripts/tick_times.py 65536 > $O/ticks_head_$k.txt 2>&1 || fail "ticks head"
+  GM_AB_BUILD=1 GM_LIBRARY=var_fast/libgm_head.so timeout -k 10 300 python -u scripts/tick_times.py 65536 > $O/ticks_head_$k.txt 2>&1 || fail "ticks head"
 done
 for f in $O/ticks_*.txt; do python3 -c "
 import re,sys

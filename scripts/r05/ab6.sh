@@ -12,7 +12,7 @@ timeout -k 10 900 $PT tests/test_gpu_partial.py tests/test_gpu_fullsize_shards.p
 tail -2 $O/gpu_tests.txt
 for k in 1 2; do
   timeout -k 10 300 python3 scripts/partial_shard_profile.py > $O/pshard_tree_$k.json 2> $O/pshard_tree_$k.err || exit 1
-  GM_LIBRARY=var_fast/libgm_pack0.so timeout -k 10 300 python3 scripts/partial_shard_profile.py > $O/pshard_pack0_$k.json 2> $O/pshard_pack0_$k.err || exit 1
+  GM_AB_BUILD=1 GM_LIBRARY=var_fast/libgm_pack0.so timeout -k 10 300 python3 scripts/partial_shard_profile.py > $O/pshard_pack0_$k.json 2> $O/pshard_pack0_$k.err || exit 1
 done
 for f in $O/pshard_*.json; do python3 -c "import json;d=json.load(open('$f'));print('$f', round(d['ms_per_tick_all_shards_serialised']/d['shards'],3), d['recv_mb_mean'])"; done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_pshard -o ps -- python3 scripts/partial_shard_profile.py --ticks 6 > $O/prof_pshard.log 2>&1 || exit 1

@@ -12,6 +12,6 @@ timeout -k 10 900 $PT tests/test_gpu_partial.py -m gpu > $O/gpu_tests.txt 2>&1 |
 tail -2 $O/gpu_tests.txt
 for k in 1 2 3; do
   timeout -k 10 300 python3 bench.py --scenario S-C --no-cpu --no-pmc --steps 10 --warmup 2 > $O/sc_tree_$k.json 2> $O/sc_tree_$k.err || exit 1
-  GM_LIBRARY=var_sc/libgm_skip0.so timeout -k 10 300 python3 bench.py --scenario S-C --no-cpu --no-pmc --steps 10 --warmup 2 > $O/sc_skip0_$k.json 2> $O/sc_skip0_$k.err || exit 1
+  GM_AB_BUILD=1 GM_LIBRARY=var_sc/libgm_skip0.so timeout -k 10 300 python3 bench.py --scenario S-C --no-cpu --no-pmc --steps 10 --warmup 2 > $O/sc_skip0_$k.json 2> $O/sc_skip0_$k.err || exit 1
 done
 for f in $O/sc_*.json; do python3 -c "import json;d=json.load(open('$f'));print('$f', round(d['roofline']['kernel_ms'],3), round(d['ms_per_step'],3), round(d['value']/1e6,1))"; done

@@ -26,7 +26,7 @@ rc=$?
 if [ $rc -eq 0 ] && ls var_ab/libgm_*.so > /dev/null 2>&1; then
   for L in var_ab/libgm_*.so; do
     v=$(basename $L .so)
-    GM_LIBRARY=$L timeout -k 10 300 python3 bench.py --no-cpu --no-pmc --no-companion > $O/bisect_$v.json 2> $O/bisect_$v.err || break
+    GM_AB_BUILD=1 GM_LIBRARY=$L timeout -k 10 300 python3 bench.py --no-cpu --no-pmc --no-companion > $O/bisect_$v.json 2> $O/bisect_$v.err || break
     python3 -c "import json;d=json.load(open('$O/bisect_$v.json'));print('$v', round(d['roofline']['kernel_ms'],3), round(d['ms_per_step'],3))"
   done
 fi

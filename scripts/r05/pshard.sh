@@ -24,6 +24,6 @@ PY
 # the S-A headline: this tree's library against round 4's final one (var_ab/libgm_r04.so), interleaved
 for k in 1 2; do
   timeout -k 10 300 python3 bench.py --no-cpu --no-pmc --no-companion > $O/sa_cur_$k.json 2> $O/sa_cur_$k.err || exit 1
-  GM_LIBRARY=var_ab/libgm_r04.so timeout -k 10 300 python3 bench.py --no-cpu --no-pmc --no-companion > $O/sa_r04_$k.json 2> $O/sa_r04_$k.err || exit 1
+  GM_AB_BUILD=1 GM_LIBRARY=var_ab/libgm_r04.so timeout -k 10 300 python3 bench.py --no-cpu --no-pmc --no-companion > $O/sa_r04_$k.json 2> $O/sa_r04_$k.err || exit 1
 done
 for f in $O/sa_*.json; do python3 -c "import json;d=json.load(open('$f'));print('$f', round(d['roofline']['kernel_ms'],3), round(d['ms_per_step'],3), round(d['value']/1e6,2))"; done

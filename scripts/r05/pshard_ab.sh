@@ -12,7 +12,7 @@ timeout -k 10 600 $PT tests/test_gpu_partial.py tests/test_gpu_fullsize_shards.p
 tail -3 $O/gpu_tests.txt
 timeout -k 10 300 python3 scripts/partial_shard_profile.py > $O/pshard_npw4.json 2> $O/pshard_npw4.err || exit 1
 for v in 8 16; do
-  GM_LIBRARY=var_pshard/libgm_npw$v.so timeout -k 10 300 python3 scripts/partial_shard_profile.py > $O/pshard_npw$v.json 2> $O/pshard_npw$v.err || exit 1
+  GM_AB_BUILD=1 GM_LIBRARY=var_pshard/libgm_npw$v.so timeout -k 10 300 python3 scripts/partial_shard_profile.py > $O/pshard_npw$v.json 2> $O/pshard_npw$v.err || exit 1
 done
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_pshard -o p -- \
   python3 scripts/partial_shard_profile.py > $O/pshard_prof.json 2> $O/pshard_prof.err

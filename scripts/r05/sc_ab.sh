@@ -13,7 +13,7 @@ tail -3 $O/gpu_tests.txt
 timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 || { cat $O/smoke.txt; exit 1; }
 for k in 1 2; do
   timeout -k 10 300 python3 bench.py --scenario S-C --no-cpu --no-pmc --steps 10 --warmup 2 > $O/sc_new_$k.json 2> $O/sc_new_$k.err || exit 1
-  GM_LIBRARY=var_ab/libgm_base.so timeout -k 10 300 python3 bench.py --scenario S-C --no-cpu --no-pmc --steps 10 --warmup 2 > $O/sc_base_$k.json 2> $O/sc_base_$k.err || exit 1
+  GM_AB_BUILD=1 GM_LIBRARY=var_ab/libgm_base.so timeout -k 10 300 python3 bench.py --scenario S-C --no-cpu --no-pmc --steps 10 --warmup 2 > $O/sc_base_$k.json 2> $O/sc_base_$k.err || exit 1
 done
 bash scripts/gpu.sh ${1:-r05g} mix_sc
 rc=$?

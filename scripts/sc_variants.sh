@@ -1,7 +1,8 @@
 #!/bin/bash
-# Measurement builds of libgm (e.g. the per-section clock build -DGM_P_PROFILE, or a candidate
+# Measurement builds of libgm (e.g. the per-section clock build: apply
+# profiles/r06/profile_patches/gm_p_profile.patch, then -DGM_P_PROFILE; or a candidate
 # kernel change kept beside the in-tree library for an A/B timing) into
-# build_var/<name>/libgm.so; run with GM_LIBRARY=build_var/<name>/libgm.so python bench.py ...
+# build_var/<name>/libgm.so; run with GM_AB_BUILD=1 GM_LIBRARY=build_var/<name>/libgm.so python bench.py ...
 # Usage: scripts/sc_variants.sh name:FLAGS ...   e.g. prof:-DGM_P_PROFILE
 set -e
 cd "$(dirname "$0")/.."

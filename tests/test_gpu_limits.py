@@ -114,3 +114,31 @@ def test_heavy_loss_long_run_stays_inside_the_ceilings():
     assert tot["removed"] > 0 and tot["joined"] > 0, tot
     assert worst_inbox < 32, worst_inbox
     sim.close()
+
+
+GM_ERR_DRAWS = 8
+
+
+@pytest.mark.parametrize("diag", [True, False])
+def test_shard_draw_without_holder_fails_loudly(diag, monkeypatch):
+    """gm_s_draw0 (round 0 of the column-shard draws) resolves a draw that lands in its columns
+    from the row's band records and cells. If they disagree, no lane holds the drawn rank, and the
+    status slot would keep an older tick's value for the MAX-allreduce: the kernel sets
+    GM_ERR_DRAWS instead. GM_DIAG_ZERO_ROW clears one row's cells after its band kernels (the
+    records keep their counts) on a one-rank RCCL shard; without it the same run stays clean."""
+    from membership.abi import comm_unique_id
+    n = 2048
+    monkeypatch.setenv("GM_FORCE_SHARD", "1")
+    if diag:
+        monkeypatch.setenv("GM_DIAG_ZERO_ROW", "700")
+    sh = Simulator(n, GM_MODE_SCALED, shard_rank=0, shard_count=1, rd_seed=7, init_mode=1, init_t0=6, init_seed=5)
+    monkeypatch.delenv("GM_FORCE_SHARD")
+    monkeypatch.delenv("GM_DIAG_ZERO_ROW", raising=False)
+    sh.comm_init(comm_unique_id(), 1, 0)
+    code = first_error(sh, 3)
+    if diag:
+        assert code == GM_ERANGE
+        assert sh.tick_stats()["err"] & GM_ERR_DRAWS
+    else:
+        assert code == 0 and sh.tick_stats()["err"] == 0
+    sh.close()

@@ -7,8 +7,9 @@ context's kernels. One such fill at creation raced `gm_p_init` and zeroed S-C ro
 (intermittent GM_ERR_SELF in rounds r04u / r04z, profiles/r04/sc_self_flake/README.md).
 `hipDeviceSynchronize` would also wait for every other context's work on the device.
 
-Measurement-only variants (ablations, dropped routes) live as patches under profiles/,
-not as #ifdef blocks in the product kernels.
+Measurement-only variants (ablations, dropped routes, the per-section clock builds
+GM_P_PROFILE / GM_F_PROFILE) live as patches under profiles/ (e.g.
+profiles/r06/profile_patches/), not as #ifdef blocks in the product kernels.
 """
 import os
 import re
@@ -23,7 +24,7 @@ FORBIDDEN = re.compile(
     r"hipDeviceSynchronize)\s*\(")
 # an async copy / fill enqueued on the null stream by a literal 0 / nullptr stream argument
 NULL_STREAM = re.compile(r"\bhip(Memset|Memcpy\w*)Async\s*\([^;]*,\s*(0|nullptr|NULL)\s*\)\s*[;)]")
-ABLATION = re.compile(r"GM_ABL_\w+|GM_P_ROUTE")
+ABLATION = re.compile(r"GM_ABL_\w+|GM_P_ROUTE|GM_\w+_PROFILE")
 
 
 def _sources():
@@ -67,3 +68,9 @@ def test_lint_catches_the_r04_race_pattern():
     assert NULL_STREAM.search("  HIPCHECK(hipMemsetAsync(p.lists, 0, bytes, 0));")
     assert not FORBIDDEN.search("  HIPCHECK(hipMemsetAsync(p.lists, 0, bytes, c->stream));")
     assert not NULL_STREAM.search("  HIPCHECK(hipMemsetAsync(p.lists, 0, bytes, c->stream));")
+
+
+def test_lint_catches_profile_blocks():
+    assert ABLATION.search("#ifdef GM_P_PROFILE")
+    assert ABLATION.search("#ifdef GM_F_PROFILE")
+    assert ABLATION.search("#if defined(GM_S_PROFILE)")
