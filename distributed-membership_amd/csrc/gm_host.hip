@@ -2012,17 +2012,30 @@ extern "C" int gm_shard_loopback_tick(gm_ctx **ctxs, int32_t G) {
     for (int g = 0; g < G; g++) HIPCHECK(gm_launch_accept(ctxs[g]->s, t, D, l, l == 1 ? 2 : -1, ls));
   }
   HIPCHECK(hipGetLastError());
-  for (int g = 0; g < G; g++) {
-    gm_ctx *c = ctxs[g];
-    HIPCHECK(hipMemcpyAsync(c->draw_left_h, c->s.npending, sizeof(int32_t), hipMemcpyDeviceToHost, ls));
+  // rows the bounded rounds could not take (a pending list overflowed, or a row still short after
+  // round 2): the host-driven rounds of draw_settle, each row from its own next round, with the
+  // MAX-reduce by device kernels -- every shard must count the same rows
+  for (int round = 0;; round++) {
+    std::vector<int32_t> left(G, 0);
+    for (int g = 0; g < G; g++)
+      HIPCHECK(hipMemcpyAsync(&left[g], ctxs[g]->s.npending, sizeof(int32_t), hipMemcpyDeviceToHost, ls));
     HIPCHECK(hipStreamSynchronize(ls));
-    if (*c->draw_left_h) {  // rows the bounded rounds could not take: the phase API's host-driven rounds
-      snprintf(g_errbuf, sizeof g_errbuf, "pipelined loopback tick: %d rows left after the bounded rounds",
-               *c->draw_left_h);
-      return GM_ERANGE;
+    for (int g = 1; g < G; g++)
+      if (left[g] != left[0]) {
+        snprintf(g_errbuf, sizeof g_errbuf, "pipelined loopback tick: shards disagree on pending rows (%d vs %d)",
+                 left[g], left[0]);
+        return GM_ESTATE;
+      }
+    if (!left[0]) break;
+    if (round >= GM_MAX_ROUNDS) return GM_ERANGE;
+    for (int g = 0; g < G; g++) HIPCHECK(gm_launch_draw(ctxs[g]->s, t, 1, GM_D_MORE, 0, ls));
+    TRY(max_reduce([&](int g) { return ctxs[g]->s.status; }, 0, (size_t)ctxs[0]->n * GM_D_MORE));
+    for (int g = 0; g < G; g++) {
+      HIPCHECK(hipMemsetAsync(ctxs[g]->s.npending, 0, sizeof(int32_t), ls));
+      HIPCHECK(gm_launch_accept(ctxs[g]->s, t, GM_D_MORE, 0, 0, ls));
     }
-    TRY(gm_shard_end_tick(c));
   }
+  for (int g = 0; g < G; g++) TRY(gm_shard_end_tick(ctxs[g]));
   return GM_OK;
 }
 

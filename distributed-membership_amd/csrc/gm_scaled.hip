@@ -1803,6 +1803,12 @@ __device__ __forceinline__ int row16_scan(int v) {  // inclusive scan within eac
   v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);  // row_shr:8
   return v;
 }
+// rows in pending list l this tick: its append count, or 0 when the appends overflowed its
+// capacity (gm_s_plist_sort: such a list is void on every rank)
+__device__ __forceinline__ int plist_len(const SState &s, int l) {
+  const uint32_t c = *s.plist_cnt[l];
+  return c > (uint32_t)s.plist_cap[l] ? 0 : (int)c;
+}
 __device__ __forceinline__ int row16_bcast(int v, int g, int q) { return __shfl(v, 16 * g + q, 64); }
 __device__ __forceinline__ uint32_t row16_bits(uint64_t bal, int g) { return (uint32_t)(bal >> (16 * g)) & 0xFFFFu; }
 
@@ -2133,6 +2139,7 @@ __global__ __launch_bounds__(256) void gm_s_draw0(SState s, int t, int r0, int r
   const uint64_t any = __ballot(mm != 0);
   if (!any) return;
   const int me = r;
+  int32_t myst = -1;  // status of this lane's draw (output q), when it lands in this shard's columns
   while (__ballot(mm != 0)) {
     const bool act = mm != 0;
     const int d = act ? __builtin_ctz(mm) : 0;
@@ -2173,10 +2180,7 @@ __global__ __launch_bounds__(256) void gm_s_draw0(SState s, int t, int r0, int r
     const int incl = row16_scan(cnt);
     const int excl = incl - cnt;
     const bool holder = act && (int)rem >= excl && (int)rem < incl;
-    // a draw landing here that no lane holds (the record's counts and the cells disagree) would
-    // leave status[r][d] at an older tick's value, which the MAX-allreduce could pick: fail loudly
-    // instead, as gm_s_draw (status -1) and gm_s_pick0 do
-    if (act && q == 0 && !row16_bits(__ballot(holder), g)) atomicOr(s.err, GM_ERR_DRAWS);
+    int32_t val = -1;
     if (holder) {  // the (rem - excl)-th present cell of its 8
       int need = (int)rem - excl, pos = 0;
       uint32_t byte = 0;
@@ -2190,9 +2194,16 @@ __global__ __launch_bounds__(256) void gm_s_draw0(SState s, int t, int r0, int r
       }
       const int col = band * B + ch * 128 + q * 8 + pos;  // shard-local column
       const bool fresh = s_is_esc(byte) ? esc_fresh(s, rc, col) : S_AGE(s_widen(byte)) < GM_TFAIL;
-      st[d] = ((s.c0 + col) << 1) | (int32_t)(fresh && s.c0 + col != me);
+      val = ((s.c0 + col) << 1) | (int32_t)(fresh && s.c0 + col != me);
     }
+    // lane d of the row takes draw d's status from its holder; a draw no lane holds (the record's
+    // counts and the cells disagree) keeps -1, which the acceptance reports as GM_ERR_DRAWS if it
+    // reaches it -- never an older tick's value left in the reused status buffer
+    const uint32_t hm = row16_bits(__ballot(holder), g);
+    const int32_t v = row16_bcast(val, g, hm ? __builtin_ctz(hm) : 0);
+    if (act && q == d) myst = hm ? v : -1;
   }
+  if (mine) st[q] = myst;
 }
 
 hipError_t gm_launch_draw0(const SState &s, int t, int r0, int r1, hipStream_t st) {
@@ -2218,7 +2229,7 @@ __global__ __launch_bounds__(256) void gm_s_draw(SState s, int t, int round, int
   // listed: the rows still pending after round 0, in ascending order (gm_s_plist_sort);
   // their statuses go to status1 by list position. Unlisted: rows [r0, r1) (a row chunk)
   const int i = (listed ? 0 : r0) + (int)blockIdx.x * 4 + wave;
-  if (listed && i >= (int)min(*s.plist_cnt[listed], (uint32_t)s.plist_cap[listed])) return;
+  if (listed && i >= plist_len(s, listed)) return;
   const int r = listed ? s.plist[listed][i] : i;
   if (r >= (listed ? s.n : r1)) return;
   // round 0 has no lazy generator state (gm_launch_draw sizes its LDS to the chunk prefix)
@@ -2361,7 +2372,7 @@ __global__ __launch_bounds__(256) void gm_s_draw(SState s, int t, int round, int
 // 0 -> the npending count (host-driven loop), 1 / 2 -> pending list 1 / 2 (next bounded round).
 __global__ __launch_bounds__(256) void gm_s_accept(SState s, int t, int D, int in_list, int out, int r0, int r1) {
   const int i = (in_list ? 0 : r0) + (int)(blockIdx.x * blockDim.x + threadIdx.x);
-  if (in_list && i >= (int)min(*s.plist_cnt[in_list], (uint32_t)s.plist_cap[in_list])) return;
+  if (in_list && i >= plist_len(s, in_list)) return;
   const int r = in_list ? s.plist[in_list][i] : i;
   if (r >= (in_list ? s.n : r1) || !s.pending[r]) return;
   int32_t *acc = s.acc + (size_t)r * 8;
@@ -2595,11 +2606,17 @@ hipError_t gm_launch_accept(const SState &s, int t, int D, int in_list, int out,
 }
 
 // The pending rows of round 0 in ascending order: the list order (= status1 rows) must be
-// the same on every rank, whatever order the atomics appended them in.
+// the same on every rank, whatever order the atomics appended them in. A list that overflowed
+// holds a subset that depends on that order, so it is void (plist_len 0) and all of its rows go
+// to the host-driven rounds (every rank counts the same total, acceptance being identical).
 __global__ __launch_bounds__(1024) void gm_s_plist_sort(SState s, int l) {
   __shared__ int32_t v[S_PLIST_CAP];
   int32_t *list = s.plist[l];
-  const int cnt = (int)min(*s.plist_cnt[l], (uint32_t)s.plist_cap[l]);
+  if (*s.plist_cnt[l] > (uint32_t)s.plist_cap[l]) {  // the appends past cap were counted already
+    if (threadIdx.x == 0) atomicAdd(s.npending, s.plist_cap[l]);
+    return;
+  }
+  const int cnt = (int)*s.plist_cnt[l];
   if (cnt <= 1) return;
   int m = 1;
   while (m < cnt) m <<= 1;

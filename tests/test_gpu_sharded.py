@@ -76,21 +76,29 @@ def test_shards_match_fused_kernel(n, world, drop, warm):
         assert st["lists"] == ref.tick_stats()["lists"]
 
 
-@pytest.mark.parametrize("n,world,drop,chunks", [(2048, 8, 10, 4), (1100, 3, 20, 3), (600, 2, 0, 7), (4099, 4, 5, 2)])
-def test_pipelined_shards_match_fused_kernel(n, world, drop, chunks, monkeypatch):
+@pytest.mark.parametrize("n,world,drop,chunks,pcap", [(2048, 8, 10, 4, 0), (1100, 3, 20, 3, 0), (600, 2, 0, 7, 0),
+                                                      (4099, 4, 5, 2, 0), (2048, 8, 10, 4, 4), (4099, 4, 5, 2, 16)])
+def test_pipelined_shards_match_fused_kernel(n, world, drop, chunks, pcap, monkeypatch):
     """The chunk order of the pipelined RCCL tick (per exchange row chunk: all-gather of the
     counts, round-0 draws, MAX-reduce of their statuses, acceptance -- on the comm stream while
     later chunks merge; then the bounded rounds) with G shard contexts on one device
     (gm_shard_loopback_tick, collectives by device copies): tick for tick equal to the fused
     kernel, and to the phase-API loopback shards. GM_SCHUNKS sets the exchange chunks (R rows,
-    a power of two; the last chunk shorter)."""
+    a power of two; the last chunk shorter). pcap > 0 shrinks the pending lists (GM_PLIST_CAP):
+    in the warm-start transient and after the crash more rows stay pending than a list holds,
+    and the rows each rank's atomics had put in an overflowing list would differ -- such a list
+    is void on every rank and its rows take the host-driven rounds (the full-size S-B run at
+    tick 15 found it: ranks MAX-reduced statuses of different rows)."""
     from membership.abi import shard_loopback_tick
     monkeypatch.setenv("GM_SCHUNKS", str(chunks))
+    if pcap:
+        monkeypatch.setenv("GM_PLIST_CAP", str(pcap))
     kw = dict(rd_seed=7, drop_pct=drop, drop_from=3, drop_to=25, drop_seed=42, init_mode=1, init_t0=6, init_seed=5)
     ref = Simulator(n, GM_MODE_SCALED, **kw)
     shards = [Simulator(n, GM_MODE_SCALED, shard_rank=g, shard_count=world, **kw) for g in range(world)]
     phase = [Simulator(n, GM_MODE_SCALED, shard_rank=g, shard_count=world, **kw) for g in range(world)]
     monkeypatch.delenv("GM_SCHUNKS")
+    monkeypatch.delenv("GM_PLIST_CAP", raising=False)
     owners = np.zeros(n, dtype=int)
     for g, s in enumerate(shards):
         c0, w = s.shard_layout()
