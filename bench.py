@@ -273,7 +273,9 @@ def scaled_run(a, n, rank, world, local, dist, rtx, profiled):
     # TREMOVE sweep of the crashed nodes (MP1Node.cpp:429-444) -- every live observer removed
     # every crashed node exactly once, nothing else was removed or joined (device counters)
     tot = sim.event_totals()
-    removed_ok = (a.prologue + a.warmup + a.steps >= a.crash_tick + 38 and a.t0 > 0  # last removals ~tick 42
+    # (a cold start too: its transient converges without false removals by t0 + 10,
+    # test_sa_cold_start_converges_without_false_removals; profiles/r06/cold_start/)
+    removed_ok = (a.prologue + a.warmup + a.steps >= a.crash_tick + 38
                   and not a.drop_pct)  # loss can remove live nodes too
     if removed_ok:
         c0, wl = sim.shard_layout() if world > 1 else (0, n)  # a column shard counts its own columns
