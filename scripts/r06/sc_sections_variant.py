@@ -2,14 +2,15 @@
 """Measurement build (not product code): a copy of gm_partial.hip whose node ticks stop after one
 section on chosen ticks, so the SQ instruction mix per dispatch attributes the per-node VALU / SALU /
 LDS instructions to the sections (the ablated tick minus the same tick's cumulative predecessor).
-Tick -> last section kept:
-  29: loads + table clear + own insert + delivered-list inserts
-  32: + self bump + sweep / compaction
-  35: + dense read + eviction
-  38: + compaction of the kept entries + id rank + list store + joins / numfailed
-  41: + gossip draw (everything but the inbox appends and the row records)
-Two normal ticks separate the ablated ones (an ablated tick sends nothing, so the next tick's inboxes
-are empty). Writes build_dbg/sc_sections/gm_partial.hip.
+Only the LAST tick of the bench run (tick 42 of `bench.py --scenario S-C --steps 16 --warmup 1`)
+is cut, so the state it runs on is the normal one (an ablated tick sends nothing and writes no list:
+the ticks after it are not representative). Level -> last section kept:
+  1: loads + table clear + own insert + delivered-list inserts
+  2: + self bump + sweep / compaction
+  3: + dense read + eviction
+  4: + compaction of the kept entries + id rank + list store + joins / numfailed
+  5: + gossip draw (everything but the inbox appends and the row records)
+Writes build_dbg/sc_l<level>/gm_partial.hip for levels 1..5.
 usage: scripts/r06/sc_sections_variant.py"""
 import os
 
@@ -24,13 +25,14 @@ def ins(s, anchor, text, before=True, nth=0):
     return s[:i] + text + s[i:] if before else s[:i + len(anchor)] + text + s[i + len(anchor):]
 
 
-s = src
-s = ins(s, "  // ---- 3. self bump", '  if (t == 29) { asm volatile("" :: "v"(hslot)); return; }\n')
-s = ins(s, "  // ---- 4. dense entries", '  if (t == 32) { asm volatile("" :: "v"(m), "v"(removed), "v"(nrem)); return; }\n')
-s = ins(s, "  // ---- 5. compact the kept entries", '  if (t == 35) { asm volatile("" :: "v"(keep)); return; }\n')
-s = ins(s, "  // ---- 6. gossip draw", '  if (t == 38) { asm volatile("" :: "v"(numfailed), "v"(nj), "v"(jb)); return; }\n')
-s = ins(s, "  // ---- sends: one parallel round", '  if (t == 41) { asm volatile("" :: "v"(ng)); return; }\n')
-out = os.path.join(REPO, "build_dbg", "sc_sections")
-os.makedirs(out, exist_ok=True)
-open(os.path.join(out, "gm_partial.hip"), "w").write(s)
-print("wrote", os.path.join(out, "gm_partial.hip"))
+CUTS = [("  // ---- 3. self bump", 'asm volatile("" :: "v"(hslot))'),
+        ("  // ---- 4. dense entries", 'asm volatile("" :: "v"(m), "v"(removed), "v"(nrem))'),
+        ("  // ---- 5. compact the kept entries", 'asm volatile("" :: "v"(keep))'),
+        ("  // ---- 6. gossip draw", 'asm volatile("" :: "v"(numfailed), "v"(nj), "v"(jb))'),
+        ("  // ---- sends: one parallel round", 'asm volatile("" :: "v"(ng))')]
+for level, (anchor, use) in enumerate(CUTS, 1):
+    s = ins(src, anchor, f"  if (t == 42) {{ {use}; return; }}\n")
+    out = os.path.join(REPO, "build_dbg", f"sc_l{level}")
+    os.makedirs(out, exist_ok=True)
+    open(os.path.join(out, "gm_partial.hip"), "w").write(s)
+    print("wrote", os.path.join(out, "gm_partial.hip"))
