@@ -30,7 +30,7 @@ __global__ void gm_f_sendprep(FState s);
 __global__ void gm_f_s1expand(FState s);
 hipError_t gm_launch_tick(const SState &s, int t, int drop_pct, hipStream_t st, hipEvent_t k0, hipEvent_t k1,
                           bool pick);
-hipError_t gm_launch_tick_prologue(const SState &s, int t, hipStream_t st);
+hipError_t gm_launch_tick_prologue(const SState &s, int t, hipStream_t st, bool zero_draw = false);
 hipError_t gm_launch_band_rows(const SState &s, int t, int drop_pct, int r0, int r1, hipStream_t st);
 hipError_t gm_launch_xrows(const SState &s, int r0, int r1, hipStream_t st);
 hipError_t gm_launch_draw(const SState &s, int t, int round, int D, int listed, hipStream_t st, int r0 = 0, int r1 = -1);
@@ -73,7 +73,8 @@ struct gm_ctx {
   int64_t nfailed = 0;               // nodes with failed_h set (gm_set_failed; nodeStart clears it)
   // sharded bounded draw rounds: rows they could not finish (npending) copied back without a
   // wait; the next call that needs the tick finishes them with host-driven rounds (draw_settle)
-  int32_t *draw_left_h = nullptr;    // pinned
+  int32_t *draw_left_h = nullptr;    // pinned [2]: rows left to the host-driven rounds, rows pending after round 0
+  bool draw_rounds = false;          // the pipelined tick deferred bounded rounds 1, 2 to draw_settle
   hipEvent_t draw_ev = nullptr;
   bool draw_check = false;
   int t = 0;
@@ -556,7 +557,11 @@ static int create_scaled(gm_ctx *c) {
   if (s.sharded) {
     TRY(dalloc(c, &s.acc, (size_t)n * 8));
     TRY(dalloc(c, &s.pending, n));
-    TRY(dalloc(c, &s.npending, 1));
+    // npending, then the pending lists' append counts (plist_cnt[1], [2]): one word block, so the tick's
+    // end reads the first two back in one copy
+    TRY(dalloc(c, &s.npending, 4));
+    s.plist_cnt[1] = (uint32_t *)(s.npending + 1);
+    s.plist_cnt[2] = (uint32_t *)(s.npending + 2);
     c->dmax = 64;
     // the exchange's row chunks (tick_sharded pipelines band -> all-gather -> draw -> MAX-allreduce ->
     // acceptance chunk by chunk): 2^xlog rows each (>= 64: a multiple of every band width's rows per
@@ -577,12 +582,11 @@ static int create_scaled(gm_ctx *c) {
     s.plist_cap[2] = 256;                                             // round 2: 256 more outputs
     if (getenv("GM_PLIST_CAP"))  // diagnostics (tests): smaller lists, so rows overflow to the host-driven rounds
       for (int l = 1; l <= 2; l++) s.plist_cap[l] = std::max(1, std::min(s.plist_cap[l], atoi(getenv("GM_PLIST_CAP"))));
-    if (hipHostMalloc(&c->draw_left_h, sizeof(int32_t), hipHostMallocDefault) != hipSuccess) return GM_ENOMEM;
-    *c->draw_left_h = 0;
+    if (hipHostMalloc(&c->draw_left_h, 2 * sizeof(int32_t), hipHostMallocDefault) != hipSuccess) return GM_ENOMEM;
+    c->draw_left_h[0] = c->draw_left_h[1] = 0;
     HIPCHECK(hipEventCreateWithFlags(&c->draw_ev, hipEventDisableTiming));
     for (int l = 1; l <= 2; l++) {
       TRY(dalloc(c, &s.plist[l], s.plist_cap[l]));
-      TRY(dalloc(c, &s.plist_cnt[l], 1));
       TRY(dalloc(c, &s.statusl[l], (size_t)s.plist_cap[l] * (l == 1 ? GM_D_MORE : GM_D_LAST)));
     }
     HIPCHECK(ctx_memset(c, s.pending, 0, sizeof(int32_t) * n));
@@ -1021,6 +1025,7 @@ extern "C" int gm_tick(gm_ctx *c) {
 extern "C" int gm_sync(gm_ctx *c) {
   if (!c) return GM_EINVAL;
   TRY(f_settle(c));
+  if (c->cfg.mode == GM_MODE_SCALED) TRY(draw_settle(c));  // a sharded tick's remaining draw rounds
   HIPCHECK(hipStreamSynchronize(c->stream));
   return check_err(c);
 }
@@ -1971,10 +1976,7 @@ extern "C" int gm_shard_loopback_tick(gm_ctx **ctxs, int32_t G) {
     gm_ctx *c = ctxs[g];
     SState &s = c->s;
     const bool drop = c->cfg.drop_pct > 0 && t_send >= c->cfg.drop_from && t_send < c->cfg.drop_to;
-    HIPCHECK(hipMemsetAsync(s.xcnt, 0, xcnt_bytes(s), ls));
-    for (int l = 1; l <= 2; l++) HIPCHECK(hipMemsetAsync(s.plist_cnt[l], 0, sizeof(uint32_t), ls));
-    HIPCHECK(hipMemsetAsync(s.npending, 0, sizeof(int32_t), ls));
-    HIPCHECK(gm_launch_tick_prologue(s, t, ls));
+    HIPCHECK(gm_launch_tick_prologue(s, t, ls, true));  // as tick_sharded: no fills
     for (int ch = 0; ch < s.xk; ch++) {
       const int r0 = ch << s.xlog;
       HIPCHECK(gm_launch_band_rows(s, t, drop ? c->cfg.drop_pct : -1, r0, r0 + xchunk_rows(s, ch), ls));
@@ -2140,20 +2142,20 @@ static int xcnt_allgather(gm_ctx *c, int ch, hipStream_t st) {
   return GM_OK;
 }
 
-// Bounded rounds 1 and 2 (no host round trip) over the rows round 0 left pending: their sorted
-// list (identical on every rank) takes the next 64 S2 outputs, then up to 256 rows the next 256;
-// a row still short sets GM_ERR_DRAWS. Then the device count of rows the rounds could not take is
-// read back without a wait (draw_settle finishes them with host-driven rounds).
-static int bounded_rounds(gm_ctx *c) {
+// Bounded rounds 1 and 2 of tick t over the rows round 0 left pending: their sorted list (identical on
+// every rank) takes the next 64 S2 outputs, then up to 256 rows the next 256; a row still short sets
+// GM_ERR_DRAWS. Rows the rounds could not take are counted in npending (draw_settle finishes them with
+// host-driven rounds).
+static int run_bounded(gm_ctx *c, int t) {
   SState &s = c->s;
   for (int l = 1; l <= 2; l++) {
     const int D = l == 1 ? GM_D_MORE : GM_D_LAST;
     HIPCHECK(gm_launch_plist_sort(s, l, c->stream));
-    HIPCHECK(gm_launch_draw(s, c->t, l, D, l, c->stream));
+    HIPCHECK(gm_launch_draw(s, t, l, D, l, c->stream));
     if (!s.stub)
       NCCLCHECK(ncclAllReduce(s.statusl[l], s.statusl[l], (size_t)s.plist_cap[l] * D, ncclInt32, ncclMax, c->comm,
                               c->stream));
-    HIPCHECK(gm_launch_accept(s, c->t, D, l, l == 1 ? 2 : -1, c->stream));
+    HIPCHECK(gm_launch_accept(s, t, D, l, l == 1 ? 2 : -1, c->stream));
   }
   if (getenv("GM_DEBUG_ROUNDS")) {  // diagnostics: rows left after round 0, error flags
     uint32_t pc1 = 0, pc2 = 0, e = 0;
@@ -2161,11 +2163,24 @@ static int bounded_rounds(gm_ctx *c) {
     HIPCHECK(hipMemcpyAsync(&pc2, s.plist_cnt[2], sizeof pc2, hipMemcpyDeviceToHost, c->stream));
     HIPCHECK(hipMemcpyAsync(&e, s.err, sizeof e, hipMemcpyDeviceToHost, c->stream));
     HIPCHECK(hipStreamSynchronize(c->stream));
-    fprintf(stderr, "[gm] t=%d rows pending after round 0: %u (cap %d), after round 1: %u (cap %d), err 0x%x\n", c->t,
+    fprintf(stderr, "[gm] t=%d rows pending after round 0: %u (cap %d), after round 1: %u (cap %d), err 0x%x\n", t,
             pc1, s.plist_cap[1], pc2, s.plist_cap[2], e);
   }
-  HIPCHECK(hipMemcpyAsync(c->draw_left_h, s.npending, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  return GM_OK;
+}
+
+// The end of a sharded tick's device work: the counts of rows still drawing go to the host without
+// a wait (draw_settle reads them before anything uses the tick). deferred (the pipelined tick):
+// bounded rounds 1, 2 have not run; draw_settle runs them only when round 0 left rows pending -- in
+// the steady state it leaves none, so a tick pays neither their six launches nor their two
+// MAX-allreduces. Every rank takes the same decision (the acceptance is identical on all ranks), so
+// the ranks' RCCL calls stay in step.
+static int end_draws(gm_ctx *c, bool deferred) {
+  SState &s = c->s;
+  if (!deferred) TRY(run_bounded(c, c->t));
+  HIPCHECK(hipMemcpyAsync(c->draw_left_h, s.npending, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
   HIPCHECK(hipEventRecord(c->draw_ev, c->stream));
+  c->draw_rounds = deferred;
   c->t--;  // gm_tick advances globaltime
   c->draw_check = true;  // before end_tick: the msgcount phase waits for draw_settle
   TRY(gm_shard_end_tick(c));
@@ -2198,10 +2213,9 @@ static int tick_sharded(gm_ctx *c) {
     TRY(before_tick_events(c));
     const int t = c->t, t_send = t - 1;
     const bool drop = c->cfg.drop_pct > 0 && t_send >= c->cfg.drop_from && t_send < c->cfg.drop_to;
-    HIPCHECK(hipMemsetAsync(s.xcnt, 0, xcnt_bytes(s), c->stream));
-    for (int l = 1; l <= 2; l++) HIPCHECK(hipMemsetAsync(s.plist_cnt[l], 0, sizeof(uint32_t), c->stream));
-    HIPCHECK(hipMemsetAsync(s.npending, 0, sizeof(int32_t), c->stream));
-    HIPCHECK(gm_launch_tick_prologue(s, t, c->stream));
+    // no fills: gm_s_xrows writes this rank's xcnt slots whole (no join ramp here) and gm_s_mtgen
+    // zeroes the draw rounds' counters
+    HIPCHECK(gm_launch_tick_prologue(s, t, c->stream, true));
     hipEvent_t k0 = nullptr, k1 = nullptr;
     if (c->timing) TRY(timing_slot(c, &k0, &k1));
     if (k0) HIPCHECK(hipEventRecord(k0, c->stream));
@@ -2229,7 +2243,7 @@ static int tick_sharded(gm_ctx *c) {
     }
     HIPCHECK(hipEventRecord(c->p_done, cs));
     HIPCHECK(hipStreamWaitEvent(c->stream, c->p_done, 0));
-    return bounded_rounds(c);
+    return end_draws(c, true);
   }
   TRY(gm_shard_merge(c));
   for (int ch = 0; ch < s.xk; ch++) TRY(xcnt_allgather(c, ch, c->stream));
@@ -2249,7 +2263,7 @@ static int tick_sharded(gm_ctx *c) {
     if (!s.stub)
       NCCLCHECK(ncclAllReduce(s.status, s.status, n * GM_D_FIRST, ncclInt32, ncclMax, c->comm, c->stream));
     HIPCHECK(gm_launch_accept(s, c->t, GM_D_FIRST, 0, 1, c->stream));
-    return bounded_rounds(c);
+    return end_draws(c, false);
   }
   int round = 0, D = GM_D_FIRST;
   for (;;) {
@@ -2282,9 +2296,17 @@ static int draw_settle(gm_ctx *c) {
   if (!c->draw_check) return c->latched;
   c->draw_check = false;
   HIPCHECK(hipEventSynchronize(c->draw_ev));
-  int32_t pend = *c->draw_left_h;
+  int32_t pend = c->draw_left_h[0];
   const int t = c->t - 1;
   const size_t n = (size_t)c->n;
+  if (c->draw_rounds) {  // the pipelined tick's bounded rounds, only if round 0 left rows pending
+    c->draw_rounds = false;
+    if (c->draw_left_h[1] > 0) {
+      TRY(run_bounded(c, t));
+      HIPCHECK(hipMemcpyAsync(&pend, c->s.npending, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+      HIPCHECK(hipStreamSynchronize(c->stream));
+    }
+  }
   for (int round = 0; pend > 0; round++) {
     if (getenv("GM_DEBUG_ROUNDS")) fprintf(stderr, "[gm] t=%d settle round %d: %d rows still drawing\n", t, round, pend);
     if (round >= GM_MAX_ROUNDS) {

@@ -43,10 +43,17 @@ typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 // Also zeroes the tick's counters (no fill launch of their own each tick): the event spill ring's
 // count and the striped event totals (the last tick's records stay readable until here), and the
 // fused draw's fallback-row count (gm_s_pick0 runs after the band kernels). Grid: max(n, 1 + S_EV_STRIPES).
-__global__ __launch_bounds__(256) void gm_s_mtgen(SState s, int t) {
+// zero_draw (the pipelined column-shard tick): also the draw rounds' counters -- the pending lists'
+// append counts and the rows left to the host-driven rounds (three fill launches a tick before)
+__global__ __launch_bounds__(256) void gm_s_mtgen(SState s, int t, int zero_draw) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r < 1 + S_EV_STRIPES) s.ev_spill_cnt[r] = 0;
   if (r == 0 && s.pk_cnt) *s.pk_cnt = 0;
+  if (zero_draw && r == 0) {
+    *s.plist_cnt[1] = 0;
+    *s.plist_cnt[2] = 0;
+    *s.npending = 0;
+  }
   if (r >= s.n) return;
   uint32_t out[S_MT_RAW];
   gm_mt_first16(gm_rd_seed(s.rd_seed, t, r + 1), out);
@@ -2052,7 +2059,9 @@ __global__ __launch_bounds__(256) void gm_s_xrows(SState s, int r0, int r1) {
     f += S_BC_FAIL(z);
   }
   int32_t *x = s.xcnt + S_XC(s, s.shard_rank, r);
-  x[0] = (int32_t)((uint32_t)x[0] & S_XC_SELFAPP) | (int32_t)p;
+  // the join ramp's self-append flag (set by the band kernel, in a slot zeroed before it) is kept;
+  // without the ramp the slot is written whole, so the tick needs no fill of xcnt
+  x[0] = (s.ramp ? (int32_t)((uint32_t)x[0] & S_XC_SELFAPP) : 0) | (int32_t)p;
   x[1] = (int32_t)f;
 }
 
@@ -2522,10 +2531,11 @@ static void launch_band_b(const SState &s, int t, int drop_pct, int r0, int r1, 
 }
 
 // the per-tick work before the band kernels: event counters, the S2 precompute
-hipError_t gm_launch_tick_prologue(const SState &s, int t, hipStream_t st) {
+hipError_t gm_launch_tick_prologue(const SState &s, int t, hipStream_t st, bool zero_draw) {
   // the event records of a tick (per-(row, band) slots + spill ring) stay readable until the next
   // tick: gm_s_mtgen zeroes their counters
-  hipLaunchKernelGGL(gm_s_mtgen, dim3((std::max(s.n, 1 + S_EV_STRIPES) + 255) / 256), dim3(256), 0, st, s, t);
+  hipLaunchKernelGGL(gm_s_mtgen, dim3((std::max(s.n, 1 + S_EV_STRIPES) + 255) / 256), dim3(256), 0, st, s, t,
+                     zero_draw ? 1 : 0);
   return hipGetLastError();
 }
 
@@ -2544,7 +2554,7 @@ hipError_t gm_launch_band_rows(const SState &s, int t, int drop_pct, int r0, int
 template <int B>
 static hipError_t launch_tick_b(const SState &s, int t, int drop_pct, hipStream_t st, hipEvent_t k0,
                                 hipEvent_t k1, bool pick) {
-  (void)gm_launch_tick_prologue(s, t, st);
+  (void)gm_launch_tick_prologue(s, t, st, false);
   if (k0) (void)hipEventRecord(k0, st);
   launch_band_b<B>(s, t, drop_pct, 0, s.n, st);
   if (k1) (void)hipEventRecord(k1, st);
