@@ -1194,21 +1194,31 @@ __device__ __forceinline__ bool unit_fast(const SState &s, int t, const UnitIn<B
       npres += ne;
       nfail += ne;
       const uint32_t col = ent & 0xFFFFu;
-      uint64_t gb = __builtin_amdgcn_ballot_w64(gone);
-      if (gb) {  // TREMOVE ticks: the holding lanes' removal bits, one gone entry per (uniform) step
-        for (; gb; gb &= gb - 1) {
-          const int cg = __builtin_amdgcn_readlane((int)col, __builtin_ctzll(gb));
-          gmask |= li == cg / Q ? 1u << (cg % Q) : 0u;
+      if (__builtin_amdgcn_ballot_w64(gone)) {
+        // TREMOVE ticks: each gone entry's lane sets, in the holding lane's LDS words, its cell's removal
+        // bit and a 0xFF over its byte (one scatter for all of them -- a uniform step per gone entry
+        // cost ~6 VALU each, ~5 per unit at the peak); the holding lanes read their words back. The
+        // wave's LDS is free here: the quick path parks nothing, and stores no escape bytes (em = 0)
+        uint32_t *gw = lds;                    // [64] removal bits per lane (cell order)
+        u32x4 *gbm = (u32x4 *)(lds + 64);      // [64][4] byte masks per lane (cell 4w + b: byte b of word w)
+        gw[li] = 0u;
+        gbm[li] = (u32x4){0u, 0u, 0u, 0u};
+        lds_wave_sync();
+        if (gone) {
+          const uint32_t ol = col / Q, q = col % Q;
+          atomicOr(gw + ol, 1u << q);
+          atomicOr(lds + 64 + 4 * ol + (q >> 2), 0xFFu << (8 * (q & 3)));
         }
+        lds_wave_sync();
+        gmask = gw[li];
+        const u32x4 bm = gbm[li];
+        lds_wave_sync();  // read back before any later use of the wave's LDS
         ngone = __builtin_popcount(gmask);
         npres -= ngone;
-#pragma unroll
-        for (int w = 0; w < 4; w++) {  // the removed cells' bytes to 0 (absent): cell 4w + b is byte b of word w
-          uint32_t x = (gmask >> (4 * w)) & 0xFu;
-          x = (x | (x << 14)) & 0x00030003u;  // bits 2, 3 -> 16, 17
-          x = (x | (x << 7)) & 0x01010101u;   // bits 1, 17 -> 8, 24
-          bw[w] &= ~(x * 0xFFu);
-        }
+        bw[0] &= ~bm.x;  // the removed cells' bytes to 0 (absent)
+        bw[1] &= ~bm.y;
+        bw[2] &= ~bm.z;
+        bw[3] &= ~bm.w;
       }
       sv = ent_lane && !gone;
       sent = col | (c << 16);
