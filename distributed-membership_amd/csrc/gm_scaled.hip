@@ -1822,6 +1822,13 @@ __device__ __forceinline__ int row16_scan(int v) {  // inclusive scan within eac
 }
 // rows in pending list l this tick: its append count, or 0 when the appends overflowed its
 // capacity (gm_s_plist_sort: such a list is void on every rank)
+// gm_shard_stub (diagnostics): a draw landing in a peer's columns resolves to a fresh target spread
+// evenly over the whole cluster -- rank ix of the row's `size` present entries stands for column
+// ix * n / size. (Round 5 took column ix % n: the top ~1 % of the rows never received a list, their
+// cells aged into escapes and removals, and the shard's band kernels grew ~25 % slower tick by tick.)
+__device__ __forceinline__ int32_t stub_target(uint32_t ix, uint32_t size, int n) {
+  return (int32_t)(((uint64_t)ix * (uint32_t)n / max(size, 1u)) << 1) | 1;
+}
 __device__ __forceinline__ int plist_len(const SState &s, int l) {
   const uint32_t c = *s.plist_cnt[l];
   return c > (uint32_t)s.plist_cap[l] ? 0 : (int)c;
@@ -2150,7 +2157,7 @@ __global__ __launch_bounds__(256) void gm_s_draw0(SState s, int t, int r0, int r
   const uint32_t ix = (uint32_t)(prod >> 32);
   const bool mine = ok && ix >= own_lo && ix < own_lo + own_cnt;
   int32_t *st = s.status + (size_t)rc * S_MT_RAW;  // round 0: D = the 16 precomputed outputs
-  if (pend && !mine) st[q] = ok ? (s.stub ? (int32_t)((ix % (uint32_t)s.n) << 1) | 1 : -1) : -2;
+  if (pend && !mine) st[q] = ok ? (s.stub ? stub_target(ix, size, s.n) : -1) : -2;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -2349,7 +2356,7 @@ __global__ __launch_bounds__(256) void gm_s_draw(SState s, int t, int round, int
     const bool ok = lane < cnt && (uint32_t)prod >= thr;
     const uint32_t ix = (uint32_t)(prod >> 32);
     const bool mine = ok && ix >= own_lo && ix < own_lo + own_cnt;
-    int32_t val = ok ? (s.stub ? (int32_t)((ix % (uint32_t)s.n) << 1) | 1 : -1) : -2;
+    int32_t val = ok ? (s.stub ? stub_target(ix, size, s.n) : -1) : -2;
     uint64_t m = __ballot(mine);
     if (m && !have_pre) {
       uint32_t osz, onf;
