@@ -31,6 +31,7 @@
 #define GM_ERR_LAG 64u        // SCALED: an entry heartbeat lag beyond the narrow cell encoding
 #define GM_ERR_ESC 128u       // SCALED: an escape pool (compact wide cells / payload bytes) overflowed
 #define GM_ERR_XCHG 256u      // PARTIAL row shards: a packed exchange block overflowed its capacity
+#define GM_ERR_PARITY 512u    // PARTIAL: an even heartbeat distance (the odd-heartbeat invariant broke)
 
 __device__ __forceinline__ uint32_t gm_pack(uint32_t hb, uint32_t ts) { return (ts << 16) | hb; }
 __device__ __forceinline__ uint32_t gm_hb(uint32_t e) { return e & 0xFFFFu; }

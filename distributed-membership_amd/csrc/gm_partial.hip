@@ -422,32 +422,43 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
     for (int q = 0; q < DS; q++)
       if (q < dm && dw[q]) keep |= (mask_t)1 << q;
   } else {
-    // heartbeat distance from the top (2t-1 = this tick's self heartbeat); alive
-    // entries have age < TREMOVE, i.e. distance <= 40 < 64
+    // heartbeat distance from the top (2t-1 = this tick's self heartbeat); alive entries have
+    // age < TREMOVE, i.e. distance <= 40; every heartbeat is odd (2k - 1, MP1Node.cpp:412-415), so the
+    // distances are even. The cut class (the smallest distance whose cumulative count of candidates
+    // -- self excluded -- reaches V - 1) is found by ballots, class by class: the candidates crowd into
+    // ~4 classes, so a 64-bin LDS histogram took its atomics ~58 lanes to one address at a time
+    // (serialised in the LDS pipe: ~4 ms of the S-C tick, profiles/r06/sc_sections/)
     const int top = 2 * t - 1;
-    hist[lane] = 0;
-    p_wsync();
-#pragma unroll
-    for (int q = 0; q < DS; q++)  // entries that do not count go to a private trash word
-      if (q < dm)
-        atomicAdd((dw[q] && !(dw[q] & P_SELF)) ? &hist[min(max(top - (int)dh[q], 0), 63)] : &tid[H - 64 + lane], 1u);
-    p_wsync();
     const int need = V - 1;  // self is always kept
-    int c = (int)hist[lane];
-    int inc = p_scan(c, lane);
-    const uint64_t over = __ballot(inc >= need);
-    const int dcut = __builtin_ctzll(over);
-    const int before = __builtin_amdgcn_readlane(inc - c, dcut);
-    const int bsz = __builtin_amdgcn_readlane(c, dcut);
+    int dd[DS];              // the slot's distance class, 64 = no candidate (empty, or self)
+    bool odd = false;
+#pragma unroll
+    for (int q = 0; q < DS; q++) {
+      dd[q] = 64;
+      if (q < dm && dw[q] && !(dw[q] & P_SELF)) dd[q] = min(max(top - (int)dh[q], 0), 63);
+      odd |= dd[q] & 1;
+    }
+    if (__ballot(odd) && lane == 0) atomicOr(s.err, GM_ERR_PARITY);  // cannot happen: heartbeats are odd
+    int dcut = 62, before = 0, bsz = 0;
+    for (int d = 0; d <= 62; d += 2) {  // wave-uniform; ends within the populated classes (m - 1 > need)
+      int c = 0;
+#pragma unroll
+      for (int q = 0; q < DS; q++)
+        if (q < dm) c += __builtin_popcountll(__ballot(dd[q] == d));
+      if (before + c >= need) {
+        dcut = d;
+        bsz = c;
+        break;
+      }
+      before += c;
+    }
     const int needb = need - before;  // 1 <= needb <= bsz
     mask_t bucket = 0;
 #pragma unroll
     for (int q = 0; q < DS; q++) {
       if (q >= dm) continue;
-      const int d = min(max(top - (int)dh[q], 0), 63);
-      const mask_t v = dw[q] != 0;
-      keep |= (v & (mask_t)(((dw[q] & P_SELF) != 0) | (d < dcut))) << q;
-      bucket |= (v & (mask_t)(!(dw[q] & P_SELF) && d == dcut)) << q;
+      keep |= (mask_t)(((dw[q] & P_SELF) != 0) | (dd[q] < dcut)) << q;
+      bucket |= (mask_t)(dd[q] == dcut) << q;
     }
     if (needb == bsz) {
       keep |= bucket;
@@ -468,8 +479,8 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
       for (int q = 0; q < DS; q++)
         if (q < dm) atomicAdd(((bucket >> q) & 1) ? &hist[key[q] >> 26] : &tid[H - 64 + lane], 1u);
       p_wsync();
-      c = (int)hist[lane];
-      inc = p_scan(c, lane);
+      const int c = (int)hist[lane];
+      const int inc = p_scan(c, lane);
       const uint64_t over2 = __ballot(inc >= needb);
       const int bcut = __builtin_ctzll(over2);
       const int before2 = __builtin_amdgcn_readlane(inc - c, bcut);

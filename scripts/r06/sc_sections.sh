@@ -10,7 +10,7 @@ T=${1:?tag}
 O=gpurun_out/$T
 mkdir -p $O
 CMD="python3 bench.py --scenario S-C --no-cpu --no-pmc --steps 16 --warmup 1"
-for l in 1 2 3 4 5; do
+for l in ${LEVELS:-1 2 3 4 5}; do
   L=build_dbg/sc_l$l/libgm.so
   GM_AB_BUILD=1 GM_LIBRARY=$L timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $O/trace_l$l -o sc -- \
     $CMD > $O/trace_l$l.log 2>&1 || exit 1
