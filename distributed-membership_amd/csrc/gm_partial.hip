@@ -360,17 +360,22 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
     // (heartbeats start at 2t-1 >= 1; hb < 2^31) and an empty slot holds hb 0, so one compare per
     // slot gives the alive bit; removals = present - alive (rare: tested once per row)
     const uint32_t xa = (uint32_t)max(2 * (t - GM_TREMOVE) + 1, 1);
-    tmask_t alive = 0, rown = 0;
-    int rcount = 0;
+    // the alive count by compares whose results feed carry-ins (v_cmp + v_addc per slot), not by a
+    // per-lane bit mask built and popcounted (~4 VALU per slot); the mask is built only in the rare
+    // removal branch
+    int rcount = 0, na = 0;
 #pragma unroll
-    for (int u = 0; u < TS; u++) {  // branch-free: exec-mask traffic is what this kernel spends SALU on
-      alive |= (tmask_t)((xa - 1u - hh[u]) >> 31) << u;
+    for (int u = 0; u < TS; u++) {
+      na += hh[u] >= xa;
       rcount += (int)min(w[u], 1u);
     }
-    rcount -= __builtin_popcountll(alive);
+    rcount -= na;
     int tot;
     removed = nrem = 0;
     if (__ballot(rcount != 0)) {  // rare: TREMOVE removals in this row
+      tmask_t alive = 0, rown = 0;
+#pragma unroll
+      for (int u = 0; u < TS; u++) alive |= (tmask_t)(hh[u] >= xa) << u;
 #pragma unroll
       for (int u = 0; u < TS; u++) rown |= (tmask_t)((w[u] >> 31) & (uint32_t)!((alive >> u) & 1)) << u;
       (void)p_excl<CB>(rcount, &removed);
@@ -384,7 +389,6 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
     }
     // the alive slots' dense positions: an inclusive DPP scan of the per-lane counts (A/B on one box
     // against p_excl's ballot per count bit: -0.3 %, profiles/r04/sc_sweep/)
-    const int na = __builtin_popcountll(alive);
     const int incl = p_scan(na, lane);
     tot = __builtin_amdgcn_readlane(incl, 63);
     int pos = incl - na;
@@ -393,7 +397,7 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
     // range (m <= (1+KK)V+1 < H-64) and free of bank conflicts
 #pragma unroll
     for (int u = 0; u < TS; u++) {
-      const bool a = (alive >> u) & 1;
+      const bool a = hh[u] >= xa;
       const int at = a ? pos : H - 64 + lane;
       tid[at] = w[u];
       thb[at] = hh[u];
