@@ -118,20 +118,22 @@ __device__ __forceinline__ uint64_t p_readlane64(uint64_t v, int l) {
   return ((uint64_t)hi << 32) | lo;
 }
 
-// claim or find the slot of `id` (idw = id | flags on claim), raise its heartbeat word
+// claim or find the slot of `id`, raise its heartbeat word. The merge claims bare ids (flags are
+// ORed in after it), so one compare finds an id: the loop is 4 VALU + 1 LDS op per probe
 template <int H>
-__device__ __forceinline__ int p_insert(uint32_t *tid, uint32_t *thb, uint32_t id, uint32_t idw, uint32_t hb) {
+__device__ __forceinline__ int p_insert(uint32_t *tid, uint32_t *thb, uint32_t id, uint32_t hb) {
   // slot = low bits of id ^ id >> 9: view ids are uniform node indices, so this spreads them like a
   // multiplicative hash without its quarter-rate 32-bit multiply (the slot never shows in a result:
   // the table is compacted and ranked by id)
-  uint32_t h = (id ^ (id >> 9)) & (H - 1);
+  // (probing steps a byte offset: with the table at LDS address 0 the slot's address is the offset)
+  uint32_t a = ((id ^ (id >> 9)) & (H - 1)) * 4;
   for (;;) {  // claim-or-compare in one LDS op
-    const uint32_t cur = atomicCAS(&tid[h], 0u, idw);
-    if (cur == 0 || (cur & P_IDMASK) == id) break;
-    h = (h + 1) & (H - 1);
+    const uint32_t cur = atomicCAS((uint32_t *)((unsigned char *)tid + a), 0u, id);
+    if (cur == 0 || cur == id) break;
+    a = (a + 4) & (4 * H - 1);
   }
-  atomicMax(&thb[h], hb);
-  return (int)h;
+  atomicMax((uint32_t *)((unsigned char *)thb + a), hb);
+  return (int)(a >> 2);
 }
 
 // owning row shard of node d: contiguous balanced ranges [n*g/G, n*(g+1)/G), boundaries
@@ -296,12 +298,12 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
                                (uint64_t)(uint32_t)i);
   const uint32_t dthr = gm_drop_thresh(s.drop_pct);
   p_wsync();
-  // ---- 2. merge: own entries first (they carry P_OWN), then the delivered lists
+  // ---- 2. merge: own entries first (their slots get P_OWN after the merge), then the delivered lists
   int hslot = -1;
   const uint32_t self_id = (uint32_t)(i + 1);
   if (own != 0) {
     const uint32_t id = (uint32_t)(own >> 32);
-    hslot = p_insert<H>(tid, thb, id, id | P_OWN, (uint32_t)own);
+    hslot = p_insert<H>(tid, thb, id, (uint32_t)own);
   }
   p_wsync();
   {
@@ -317,10 +319,11 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
         const uint32_t pair = (uint32_t)step_val((int)pairv, st);
         take = take && (gm_fmix32(pair ^ (id - 1)) >> 16) >= dthr;
       }
-      if (take) (void)p_insert<H>(tid, thb, id, id, (uint32_t)e);
+      if (take) (void)p_insert<H>(tid, thb, id, (uint32_t)e);
       if (mc) nrecv += __builtin_popcountll(__ballot(take));
     }
   }
+  if (own != 0) atomicOr(&tid[hslot], P_OWN);  // after the merge: its probes compare bare ids
   p_wsync();
   // ---- 3. self bump (heartbeat++; myPos->setheartbeat(heartbeat++)), then sweep + compaction
   {
@@ -332,7 +335,7 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
       hs = 0;
       if (lane == 0) {
         atomicOr(s.err, GM_ERR_SELF);
-        hs = p_insert<H>(tid, thb, self_id, self_id | P_OWN, 1u);
+        hs = p_insert<H>(tid, thb, self_id, 1u);  // self is in no own slot: its id is bare
       }
       hs = __builtin_amdgcn_readfirstlane(hs);
     }
@@ -708,17 +711,20 @@ __device__ __forceinline__ void p_small_node(const PState &s, int t, const PPre 
 // P_NPW consecutive nodes per wave: each node's loads are prefetched during the node before it
 // (p_prefetch), so a node starts with one global round trip (its delivered lists) instead of two.
 // Held to 8 waves per SIMD (64 VGPRs; the loop keeps more live otherwise, and some SGPRs spill to
-// VGPR lanes: ~40 more VALU per node, still faster than one node per wave: 26.1 vs 27.5 ms)
+// VGPR lanes: ~40 more VALU per node, still faster than one node per wave: 26.1 vs 27.5 ms).
+// P_SWG = 1 wave per workgroup: a finished wave releases its LDS slice at once (with 4 waves per
+// workgroup the slice waited for the workgroup's last wave: 23.5 -> 22.8 ms)
 template <bool MC, bool RM, int VF>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void gm_p_tick_small_pf(
+__global__ __launch_bounds__(64 * P_SWG) __attribute__((amdgpu_waves_per_eu(8, 8))) void gm_p_tick_small_pf(
     PState s, int t, const uint32_t *mtraw, int chunk, int r0, int r1, int npw) {
-  extern __shared__ __align__(16) unsigned char p_smem[];
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int l0 = r0 + (blockIdx.x * 4 + wave) * npw;
+  // static LDS: its addresses are compile-time constants (offsets fold into the LDS instructions)
+  __shared__ __align__(16) unsigned char p_smem[P_SWG * (PLds<P_HS>::bytes + P_PF_BYTES)];
+  const int wave = P_SWG == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int l0 = r0 + (blockIdx.x * P_SWG + wave) * npw;
   if (l0 >= r1) return;  // whole wave; no workgroup barrier in this kernel
   unsigned char *base = p_smem + (size_t)wave * PLds<P_HS>::bytes;
   const int l1 = min(r1, l0 + npw);
-  uint32_t *pf = (uint32_t *)(p_smem + 4 * (size_t)PLds<P_HS>::bytes + (size_t)wave * P_PF_BYTES);
+  uint32_t *pf = (uint32_t *)(p_smem + P_SWG * (size_t)PLds<P_HS>::bytes + (size_t)wave * P_PF_BYTES);
   const uint32_t pfa =
       __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(__attribute__((address_space(3))) uint32_t *)pf);
   p_prefetch(s, t, mtraw, l0, lane, pfa);
@@ -972,8 +978,7 @@ hipError_t gm_launch_partial_chunk(const PState &s, int t, const uint32_t *mtraw
     // nodes per wave: P_NPW; a row shard's chunk (a few hundred thousand nodes per launch) takes
     // P_NPW_CHUNK, so the launch's last round of waves is a smaller share of it
     const int npw = s.nchunk > 1 ? P_NPW_CHUNK : P_NPW;
-    hipLaunchKernelGGL(small, dim3((r1 - r0 + 4 * npw - 1) / (4 * npw)), dim3(256),
-                       4 * (PLds<P_HS>::bytes + P_PF_BYTES), st, s, t, mtraw, c, r0, r1, npw);
+    hipLaunchKernelGGL(small, dim3((r1 - r0 + P_SWG * npw - 1) / (P_SWG * npw)), dim3(64 * P_SWG), 0, st, s, t, mtraw, c, r0, r1, npw);
   }
   hipLaunchKernelGGL(mc ? gm_p_tick_big<true> : gm_p_tick_big<false>, dim3(P_BIG_GRID), dim3(256),
                      4 * PLds<P_HB>::bytes, st, s, t, mtraw, c, r0);
