@@ -1454,18 +1454,23 @@ __global__ __launch_bounds__(256) void gm_s_band_listed(SState s, int t, int u0,
 // and payload gathers issue as soon as the first unit's payload words are merged (nxt), so they are
 // in flight under the first unit's sweep and stores -- one dependent round trip per unit instead of
 // two (inbox, then gathers).
+#ifndef GM_FAST_WG
+#define GM_FAST_WG 1  // waves per workgroup of gm_s_band_fast (1: a finished wave frees its LDS slice at once;
+                      // 4: 3.29 ms per S-A tick, 1: 3.22, profiles/r06/ab_fwg/)
+#endif
 template <int B, bool CH, int BPW>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) void gm_s_band_fast(SState s, int t, int u0, int u1) {
+__global__ __launch_bounds__(64 * GM_FAST_WG) __attribute__((amdgpu_waves_per_eu(7, 8))) void gm_s_band_fast(SState s, int t, int u0, int u1) {
   if (!CH) {
     u0 = 0;
     u1 = s.n;
   }
-  const int ub = __builtin_amdgcn_readfirstlane(u0 + (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6));
+  const int wv = GM_FAST_WG == 1 ? 0 : (int)(threadIdx.x >> 6);
+  const int ub = __builtin_amdgcn_readfirstlane(u0 + (int)blockIdx.x * GM_FAST_WG + wv);
   if (ub >= u1) return;  // whole wave (one row per wave)
   // per wave: escape cells by column, the park, the per-lane words of the escaped cells' outcomes
   constexpr int W = 2 * S_LDS_WAVE_WORDS + 192;
-  __shared__ uint32_t lds_all[4 * W];
-  uint32_t *lds = lds_all + (threadIdx.x >> 6) * W;
+  __shared__ uint32_t lds_all[GM_FAST_WG * W];
+  uint32_t *lds = lds_all + wv * W;
   const int b0 = (int)blockIdx.y * BPW;
   const bool two = BPW == 2 && b0 + 1 < s.nb;  // wave-uniform
   UnitIn<B> in, in2;
@@ -2536,11 +2541,13 @@ static void launch_band_b(const SState &s, int t, int drop_pct, int r0, int r1, 
   if (drop_pct >= 0) {
     hipLaunchKernelGGL((gm_s_band<B, true>), dim3(nblk), dim3(256), 0, st, s, t, drop_pct, u0, u1);
   } else if (B == 1024 && !s.ramp && s.fb_list) {  // the fast path, then the units it handed back
-    const dim3 nblk2(nblk.x, (s.nb + GM_FAST_BPW - 1) / GM_FAST_BPW);
+    const dim3 nblk2((u1 - u0 + GM_FAST_WG - 1) / GM_FAST_WG, (s.nb + GM_FAST_BPW - 1) / GM_FAST_BPW);
     if (u0 == 0 && r1 == s.n)
-      hipLaunchKernelGGL((gm_s_band_fast<B == 1024 ? B : 1024, false, GM_FAST_BPW>), nblk2, dim3(256), 0, st, s, t, u0, u1);
+      hipLaunchKernelGGL((gm_s_band_fast<B == 1024 ? B : 1024, false, GM_FAST_BPW>), nblk2, dim3(64 * GM_FAST_WG), 0,
+                         st, s, t, u0, u1);
     else
-      hipLaunchKernelGGL((gm_s_band_fast<B == 1024 ? B : 1024, true, GM_FAST_BPW>), nblk2, dim3(256), 0, st, s, t, u0, u1);
+      hipLaunchKernelGGL((gm_s_band_fast<B == 1024 ? B : 1024, true, GM_FAST_BPW>), nblk2, dim3(64 * GM_FAST_WG), 0,
+                         st, s, t, u0, u1);
     hipLaunchKernelGGL((gm_s_band_listed<B == 1024 ? B : 1024>), dim3(S_FB_BLOCKS), dim3(256), 0, st, s, t, u0, u1);
   } else {
     hipLaunchKernelGGL((gm_s_band<B, false>), dim3(nblk), dim3(256), 0, st, s, t, drop_pct, u0, u1);

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Build libgm.so from the current csrc with patches applied into build_dbg/<name>/ (A/B scratch;
 # the product library is untouched). usage: scripts/r06/build_variant.sh <name> [patch ...]
-# A patch named "w7" sets the S-C node kernel to amdgpu_waves_per_eu(7, 8).
+# EXTRA_FLAGS: more hipcc flags (e.g. -DGM_FAST_WG=1). A patch named "w7" sets the S-C node kernel to amdgpu_waves_per_eu(7, 8).
 set -e
 N=${1:?name}; shift
 cd "$(dirname "$0")/../.."
@@ -15,7 +15,7 @@ for p in "$@"; do
     patch -s -d $W/csrc -p3 < "$p"
   fi
 done
-F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Iinclude -I$W/csrc -Wall -Wno-unused-result -Wno-pass-failed"
+F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Iinclude -I$W/csrc -Wall -Wno-unused-result -Wno-pass-failed ${EXTRA_FLAGS:-}"
 for k in gm_faithful gm_scaled gm_partial gm_host; do /opt/rocm/bin/hipcc $F -c -o $W/obj/$k.o $W/csrc/$k.hip & done
 wait
 mkdir -p build_dbg/$N
