@@ -10,7 +10,9 @@
 #define P_HB 1024        // big kernel: LDS hash slots per wave (>= (1 + P_KP) * P_VMAX / 0.53)
 #define P_HH 4096        // huge kernel: LDS hash slots per wave (>= (1 + P_KMAX) * P_VMAX / 0.51)
 #define P_KMAX 64        // inbox row: count + P_KMAX - 1 = 63 lists queued per receiver per tick; every list is merged
+#ifndef P_NPW
 #define P_NPW 16         // small kernel: consecutive nodes per wave, prefetching (one-box A/Bs: 16 -0.8 % vs 8, 32 -0.25 % vs 16)
+#endif
 #ifndef P_SWG
 #define P_SWG 1          // small kernel: waves per workgroup (1: every wave's LDS starts at address 0)
 #endif
