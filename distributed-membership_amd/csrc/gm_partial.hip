@@ -118,21 +118,29 @@ __device__ __forceinline__ uint64_t p_readlane64(uint64_t v, int l) {
   return ((uint64_t)hi << 32) | lo;
 }
 
-// claim or find the slot of `id`, raise its heartbeat word. The merge claims bare ids (flags are
-// ORed in after it), so one compare finds an id: the loop is 4 VALU + 1 LDS op per probe
+// claim or find the slot of `id`, raise its heartbeat word. Every lane of the wave runs the probe
+// loop (no divergent loop: its exec-mask bookkeeping was ~5 SALU per probe). A lane with nothing to
+// insert (take false) points at its own word of the misc area (hist[lane], 2H words past tid),
+// which holds P_TRASH while the lists merge: its CAS changes nothing and finds "its" id at once, and
+// its max of 0 changes nothing (distinct words: no same-address serialisation). A lane that found
+// its slot repeats an idempotent CAS. The merge claims bare ids (flags are ORed in after it), so one
+// compare finds an id. Returns the slot (>= 2H for a lane that took nothing).
+#define P_TRASH 0xFFFFFFFFu
 template <int H>
-__device__ __forceinline__ int p_insert(uint32_t *tid, uint32_t *thb, uint32_t id, uint32_t hb) {
+__device__ __forceinline__ int p_insert(uint32_t *tid, bool take, uint32_t id, uint32_t hb, int lane) {
   // slot = low bits of id ^ id >> 9: view ids are uniform node indices, so this spreads them like a
   // multiplicative hash without its quarter-rate 32-bit multiply (the slot never shows in a result:
-  // the table is compacted and ranked by id)
-  // (probing steps a byte offset: with the table at LDS address 0 the slot's address is the offset)
-  uint32_t a = ((id ^ (id >> 9)) & (H - 1)) * 4;
+  // the table is compacted and ranked by id). Probing steps a byte offset: with the table at LDS
+  // address 0 the slot's address is the offset
+  const uint32_t idw = take ? id : P_TRASH;
+  uint32_t a = take ? ((id ^ (id >> 9)) & (H - 1)) * 4 : 8 * H + 4 * lane;
   for (;;) {  // claim-or-compare in one LDS op
-    const uint32_t cur = atomicCAS((uint32_t *)((unsigned char *)tid + a), 0u, id);
-    if (cur == 0 || cur == id) break;
-    a = (a + 4) & (4 * H - 1);
+    const uint32_t cur = atomicCAS((uint32_t *)((unsigned char *)tid + a), 0u, idw);
+    const bool more = cur != 0 && cur != idw;
+    if (!__ballot(more)) break;
+    if (more) a = (a + 4) & (4 * H - 1);
   }
-  atomicMax((uint32_t *)((unsigned char *)thb + a), hb);
+  atomicMax((uint32_t *)((unsigned char *)tid + a + (take ? 4 * H : 0)), take ? hb : 0u);
   return (int)(a >> 2);
 }
 
@@ -251,6 +259,7 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
     uint4 *z = (uint4 *)tid;
 #pragma unroll
     for (int q = 0; q < H / 128; q++) z[lane + 64 * q] = make_uint4(0, 0, 0, 0);
+    tid[2 * H + lane] = P_TRASH;  // hist[lane]: the lane's trash word while the lists merge (p_insert)
   }
   const int kk = min(k, KK);
   // lists per load step (per), entry (l) and list slot (jo) of this lane; V = 32 (S-C) takes the
@@ -301,10 +310,7 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
   // ---- 2. merge: own entries first (their slots get P_OWN after the merge), then the delivered lists
   int hslot = -1;
   const uint32_t self_id = (uint32_t)(i + 1);
-  if (own != 0) {
-    const uint32_t id = (uint32_t)(own >> 32);
-    hslot = p_insert<H>(tid, thb, id, (uint32_t)own);
-  }
+  hslot = p_insert<H>(tid, own != 0, (uint32_t)(own >> 32), (uint32_t)own, lane);
   p_wsync();
   {
     const uint32_t tfresh = (uint32_t)max(0, 2 * t - 11);  // hb >= 2t-11 <=> (t-1) - (hb+1)/2 < TFAIL
@@ -314,16 +320,17 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
       const uint64_t e = dv[st];
       bool take = e != 0 && (uint32_t)e >= tfresh;
       const uint32_t id = (uint32_t)(e >> 32);
-      if (dropping && __ballot(take)) {  // per-entry drops keyed by (t_send, src, dst, id-1): lost iff the
-        // top 16 bits of fmix32(pair ^ (id-1)) are below the threshold
+      if (dropping) {  // per-entry drops keyed by (t_send, src, dst, id-1): lost iff the top 16 bits of
+        // fmix32(pair ^ (id-1)) are below the threshold
         const uint32_t pair = (uint32_t)step_val((int)pairv, st);
         take = take && (gm_fmix32(pair ^ (id - 1)) >> 16) >= dthr;
       }
-      if (take) (void)p_insert<H>(tid, thb, id, (uint32_t)e);
+      (void)p_insert<H>(tid, take, id, (uint32_t)e, lane);
       if (mc) nrecv += __builtin_popcountll(__ballot(take));
     }
   }
-  if (own != 0) atomicOr(&tid[hslot], P_OWN);  // after the merge: its probes compare bare ids
+  atomicOr(&tid[hslot], own != 0 ? P_OWN : 0u);  // after the merge: its probes compare bare ids (a lane
+                                                 // with no own entry ORs 0 into its trash word)
   p_wsync();
   // ---- 3. self bump (heartbeat++; myPos->setheartbeat(heartbeat++)), then sweep + compaction
   {
@@ -335,7 +342,7 @@ __device__ __forceinline__ void p_node(const PState &s, int t, const PPre &pre, 
       hs = 0;
       if (lane == 0) {
         atomicOr(s.err, GM_ERR_SELF);
-        hs = p_insert<H>(tid, thb, self_id, 1u);  // self is in no own slot: its id is bare
+        hs = p_insert<H>(tid, true, self_id, 1u, lane);  // self is in no own slot: its id is bare
       }
       hs = __builtin_amdgcn_readfirstlane(hs);
     }
