@@ -66,6 +66,8 @@ struct gm_ctx {
   std::vector<hipEvent_t> tev;            // per-tick band-kernel event pairs (single context)
   double kernel_ms_sum = 0;
   int shard_sync = -1;               // sharded tick draw rounds: 1 host-driven unbounded loop, 0 bounded
+  bool diag_nowait = false;          // diagnostics (GM_DIAG_NOWAIT, timing only): skip the pipelined tick's
+                                     // settle wait, as if round 0 never left rows pending
   int diag_zero_row = -1;            // diagnostics (GM_DIAG_ZERO_ROW, tests): the pipelined column-shard tick
                                      //   clears this row's cells after its band kernels, so its records'
                                      //   counts disagree with the cells and a draw finds no holder
@@ -407,6 +409,7 @@ static int create_scaled(gm_ctx *c) {
   }
   c->shard_sync = getenv("GM_SHARD_SYNC") ? (atoi(getenv("GM_SHARD_SYNC")) ? 1 : 0) : -1;
   if (getenv("GM_DIAG_ZERO_ROW")) c->diag_zero_row = atoi(getenv("GM_DIAG_ZERO_ROW"));
+  c->diag_nowait = getenv("GM_DIAG_NOWAIT") && atoi(getenv("GM_DIAG_NOWAIT"));
   TRY(dalloc(c, &s.msg, cells));        // nibbles: 2 parities x band/2 bytes per (band, row)
   // Escape storage (gm_scaled.h), one set per tick parity: a 16-cell inline slot per (band, row)
   // list (1/32 B per cell at B = 1024) and the pools. The pools are DENSE-equivalent (every
@@ -2175,11 +2178,14 @@ static int run_bounded(gm_ctx *c, int t) {
 // the steady state it leaves none, so a tick pays neither their six launches nor their two
 // MAX-allreduces. Every rank takes the same decision (the acceptance is identical on all ranks), so
 // the ranks' RCCL calls stay in step.
-static int end_draws(gm_ctx *c, bool deferred) {
+// ds: the stream whose work decides the counts (the pipelined tick's comm stream: the copy follows
+// its last acceptance directly instead of behind a cross-stream join)
+static int end_draws(gm_ctx *c, bool deferred, hipStream_t ds = nullptr) {
   SState &s = c->s;
   if (!deferred) TRY(run_bounded(c, c->t));
-  HIPCHECK(hipMemcpyAsync(c->draw_left_h, s.npending, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
-  HIPCHECK(hipEventRecord(c->draw_ev, c->stream));
+  if (!ds) ds = c->stream;
+  HIPCHECK(hipMemcpyAsync(c->draw_left_h, s.npending, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, ds));
+  HIPCHECK(hipEventRecord(c->draw_ev, ds));
   c->draw_rounds = deferred;
   c->t--;  // gm_tick advances globaltime
   c->draw_check = true;  // before end_tick: the msgcount phase waits for draw_settle
@@ -2243,7 +2249,7 @@ static int tick_sharded(gm_ctx *c) {
     }
     HIPCHECK(hipEventRecord(c->p_done, cs));
     HIPCHECK(hipStreamWaitEvent(c->stream, c->p_done, 0));
-    return end_draws(c, true);
+    return end_draws(c, true, cs);
   }
   TRY(gm_shard_merge(c));
   for (int ch = 0; ch < s.xk; ch++) TRY(xcnt_allgather(c, ch, c->stream));
@@ -2295,7 +2301,16 @@ static int tick_sharded(gm_ctx *c) {
 static int draw_settle(gm_ctx *c) {
   if (!c->draw_check) return c->latched;
   c->draw_check = false;
-  HIPCHECK(hipEventSynchronize(c->draw_ev));
+  if (c->diag_nowait && c->draw_rounds) {
+    c->draw_rounds = false;
+    return c->latched;
+  }
+  // the next tick waits on these two counts: spin on the event (a blocking wait let the GPU idle
+  // ~40 us per tick while the host thread woke up: profiles/r06/stub_gap/)
+  hipError_t q;
+  while ((q = hipEventQuery(c->draw_ev)) == hipErrorNotReady) {
+  }
+  HIPCHECK(q);
   int32_t pend = c->draw_left_h[0];
   const int t = c->t - 1;
   const size_t n = (size_t)c->n;

@@ -2171,68 +2171,88 @@ __global__ __launch_bounds__(256) void gm_s_draw0(SState s, int t, int r0, int r
   if (!any) return;
   const int me = r;
   int32_t myst = -1;  // status of this lane's draw (output q), when it lands in this shard's columns
+  // up to DB of the row's draws per pass (a row has ~16/G in this shard's columns): their band
+  // searches, then their band records' loads, then their chunk loads, each batch in flight together
+  constexpr int DB = 4;
   while (__ballot(mm != 0)) {
-    const bool act = mm != 0;
-    const int d = act ? __builtin_ctz(mm) : 0;
-    mm &= mm - 1;
-    const uint32_t x = (uint32_t)row16_bcast((int)ix, g, d) - own_lo;  // rank among this shard's entries
-    // 16-ary search: the band b with bpre[b] <= x < bpre[b + 1]
-    int lo = 0, span = nb;
-    while (__ballot(act && span > 1)) {
-      const int step = (span + 15) >> 4;
-      const int idx = lo + q * step;
-      const bool le = act && q * step < span && bpre[idx] <= x;
-      const int c = __builtin_popcount(row16_bits(__ballot(le), g));
-      if (act && span > 1) {
-        lo += (max(c, 1) - 1) * step;
-        span = min(step, span - (max(c, 1) - 1) * step);
-      }
-    }
-    const int band = lo;
-    uint32_t rem = act ? x - bpre[band] : 0u;  // rank inside the band
-    // the band record's 8 chunk counts, then the chunk (128 cells: 8 bytes per lane of the row)
-    const uint4 rec = act ? s.brec[(size_t)band * s.n + rc] : make_uint4(0u, 0u, 0u, 0u);
-    const uint64_t cc = (uint64_t)rec.x | ((uint64_t)rec.y << 32);
-    int ch = 0;
+    bool act[DB];
+    int dj[DB], band[DB];
+    uint32_t rem[DB];
 #pragma unroll
-    for (int k = 0; k < 7; k++) {
-      const uint32_t c8 = (uint32_t)(cc >> (8 * ch)) & 0xFFu;
-      if (rem >= c8 && ch == k) {
-        rem -= c8;
-        ch++;
-      }
-    }
-    uint2 w = make_uint2(0u, 0u);
-    if (act) w = *(const uint2 *)(s.table + ((size_t)band * s.n + rc) * B + ch * 128 + q * 8);
-    // present (non-zero) bytes of the lane's 8 cells
-    auto nzb = [](uint32_t v) { return (v | (v >> 1) | (v >> 2) | (v >> 3) | (v >> 4) | (v >> 5) | (v >> 6) | (v >> 7)) & 0x01010101u; };
-    const uint32_t m0 = nzb(w.x), m1 = nzb(w.y);
-    const int cnt = __builtin_popcount(m0) + __builtin_popcount(m1);
-    const int incl = row16_scan(cnt);
-    const int excl = incl - cnt;
-    const bool holder = act && (int)rem >= excl && (int)rem < incl;
-    int32_t val = -1;
-    if (holder) {  // the (rem - excl)-th present cell of its 8
-      int need = (int)rem - excl, pos = 0;
-      uint32_t byte = 0;
-#pragma unroll
-      for (int v = 0; v < 8; v++) {
-        const uint32_t bv = ((v < 4 ? w.x : w.y) >> (8 * (v & 3))) & 0xFFu;
-        if (bv != 0) {
-          if (need == 0) { pos = v; byte = bv; }
-          need--;
+    for (int j = 0; j < DB; j++) {
+      act[j] = mm != 0;
+      dj[j] = act[j] ? __builtin_ctz(mm) : 0;
+      mm &= mm - 1;
+      const uint32_t x = (uint32_t)row16_bcast((int)ix, g, dj[j]) - own_lo;  // rank among this shard's entries
+      // 16-ary search: the band b with bpre[b] <= x < bpre[b + 1]
+      int lo = 0, span = nb;
+      while (__ballot(act[j] && span > 1)) {
+        const int step = (span + 15) >> 4;
+        const int idx = lo + q * step;
+        const bool le = act[j] && q * step < span && bpre[idx] <= x;
+        const int c = __builtin_popcount(row16_bits(__ballot(le), g));
+        if (act[j] && span > 1) {
+          lo += (max(c, 1) - 1) * step;
+          span = min(step, span - (max(c, 1) - 1) * step);
         }
       }
-      const int col = band * B + ch * 128 + q * 8 + pos;  // shard-local column
-      const bool fresh = s_is_esc(byte) ? esc_fresh(s, rc, col) : S_AGE(s_widen(byte)) < GM_TFAIL;
-      val = ((s.c0 + col) << 1) | (int32_t)(fresh && s.c0 + col != me);
+      band[j] = lo;
+      rem[j] = act[j] ? x - bpre[lo] : 0u;  // rank inside the band
     }
-    // lane d of the row takes draw d's status from its holder; a draw no lane holds (the record's
-    // counts and the cells disagree) keeps -1, which the acceptance reports as GM_ERR_DRAWS if it
-    // reaches it -- never an older tick's value left in the reused status buffer
-    const uint32_t hm = row16_bits(__ballot(holder), g);
-    const int32_t v = row16_bcast(val, g, hm ? __builtin_ctz(hm) : 0);
-    if (act && q == d) myst = hm ? v : -1;
+    // the band records' 8 chunk counts, then the chunks (128 cells: 8 bytes per lane of the row)
+    uint4 rec[DB];
+#pragma unroll
+    for (int j = 0; j < DB; j++)
+      rec[j] = act[j] ? s.brec[(size_t)band[j] * s.n + rc] : make_uint4(0u, 0u, 0u, 0u);
+    int ch[DB];
+    uint2 w[DB];
+#pragma unroll
+    for (int j = 0; j < DB; j++) {
+      const uint64_t cc = (uint64_t)rec[j].x | ((uint64_t)rec[j].y << 32);
+      ch[j] = 0;
+#pragma unroll
+      for (int k = 0; k < 7; k++) {
+        const uint32_t c8 = (uint32_t)(cc >> (8 * ch[j])) & 0xFFu;
+        if (rem[j] >= c8 && ch[j] == k) {
+          rem[j] -= c8;
+          ch[j]++;
+        }
+      }
+      w[j] = make_uint2(0u, 0u);
+      if (act[j]) w[j] = *(const uint2 *)(s.table + ((size_t)band[j] * s.n + rc) * B + ch[j] * 128 + q * 8);
+    }
+#pragma unroll
+    for (int j = 0; j < DB; j++) {
+      // present (non-zero) bytes of the lane's 8 cells
+      auto nzb = [](uint32_t v) { return (v | (v >> 1) | (v >> 2) | (v >> 3) | (v >> 4) | (v >> 5) | (v >> 6) | (v >> 7)) & 0x01010101u; };
+      const uint32_t m0 = nzb(w[j].x), m1 = nzb(w[j].y);
+      const int cnt = __builtin_popcount(m0) + __builtin_popcount(m1);
+      const int incl = row16_scan(cnt);
+      const int excl = incl - cnt;
+      const bool holder = act[j] && (int)rem[j] >= excl && (int)rem[j] < incl;
+      int32_t val = -1;
+      if (holder) {  // the (rem - excl)-th present cell of its 8
+        int need = (int)rem[j] - excl, pos = 0;
+        uint32_t byte = 0;
+#pragma unroll
+        for (int v = 0; v < 8; v++) {
+          const uint32_t bv = ((v < 4 ? w[j].x : w[j].y) >> (8 * (v & 3))) & 0xFFu;
+          if (bv != 0) {
+            if (need == 0) { pos = v; byte = bv; }
+            need--;
+          }
+        }
+        const int col = band[j] * B + ch[j] * 128 + q * 8 + pos;  // shard-local column
+        const bool fresh = s_is_esc(byte) ? esc_fresh(s, rc, col) : S_AGE(s_widen(byte)) < GM_TFAIL;
+        val = ((s.c0 + col) << 1) | (int32_t)(fresh && s.c0 + col != me);
+      }
+      // lane d of the row takes draw d's status from its holder; a draw no lane holds (the record's
+      // counts and the cells disagree) keeps -1, which the acceptance reports as GM_ERR_DRAWS if it
+      // reaches it -- never an older tick's value left in the reused status buffer
+      const uint32_t hm = row16_bits(__ballot(holder), g);
+      const int32_t v = row16_bcast(val, g, hm ? __builtin_ctz(hm) : 0);
+      if (act[j] && q == dj[j]) myst = hm ? v : -1;
+    }
   }
   if (mine) st[q] = myst;
 }
@@ -2407,27 +2427,50 @@ __global__ __launch_bounds__(256) void gm_s_accept(SState s, int t, int D, int i
   const int r = in_list ? s.plist[in_list][i] : i;
   if (r >= (in_list ? s.n : r1) || !s.pending[r]) return;
   int32_t *acc = s.acc + (size_t)r * 8;
-  int n = acc[0];
-  const int numpot = acc[6];
-  int g[GM_FANOUT];
-  for (int q = 0; q < n; q++) g[q] = acc[1 + q];
+  // the row's accumulator (8 ints) and, in round 0 (D = 16), its 16 statuses by vector loads, all
+  // in flight together: the draw loop below then runs on registers, not one load round trip per
+  // draw (each row's words are its own 32 B / 64 B)
+  const int4 a0 = ((const int4 *)acc)[0], a1 = ((const int4 *)acc)[1];
+  int n = a0.x;
+  const int numpot = a1.z;
+  int g[GM_FANOUT] = {a0.y, a0.z, a0.w, a1.x, a1.y};
+  static_assert(GM_FANOUT == 5, "acc = {n, g[0..4], numpot, size}");
   const int32_t *st = in_list ? s.statusl[in_list] + (size_t)i * D : s.status + (size_t)r * D;
   bool done = n >= GM_FANOUT || n >= numpot;
-  for (int d = 0; d < D && !done; d++) {
-    const int32_t v = st[d];
-    if (v == -2) continue;  // output rejected by Lemire: not a draw
-    if (v < 0) {            // a draw no shard resolved
+  auto take = [&](int32_t v) {  // one draw of MP1Node.cpp:466-489, in draw order
+    if (done || v == -2) return;  // output rejected by Lemire: not a draw
+    if (v < 0) {                  // a draw no shard resolved
       atomicOr(s.err, GM_ERR_DRAWS);
       done = true;
-      break;
+      return;
     }
     const int c = v >> 1;
-    if (c == r) continue;    // "me"
-    if (!(v & 1)) continue;  // age >= TFAIL
+    if (c == r) return;     // "me"
+    if (!(v & 1)) return;   // age >= TFAIL
     bool dup = false;
-    for (int q = 0; q < n; q++) dup |= g[q] == c;
-    if (!dup) g[n++] = c;
+#pragma unroll
+    for (int q = 0; q < GM_FANOUT; q++) dup |= q < n && g[q] == c;
+    if (!dup) {
+#pragma unroll
+      for (int q = 0; q < GM_FANOUT; q++)
+        if (q == n) g[q] = c;
+      n++;
+    }
     done = n >= GM_FANOUT || n >= numpot;
+  };
+  if (D == 16) {
+    int4 v4[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) v4[q] = ((const int4 *)st)[q];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      take(v4[q].x);
+      take(v4[q].y);
+      take(v4[q].z);
+      take(v4[q].w);
+    }
+  } else {
+    for (int d = 0; d < D && !done; d++) take(st[d]);
   }
   for (int q = 0; q < n; q++) acc[1 + q] = g[q];
   acc[0] = n;
