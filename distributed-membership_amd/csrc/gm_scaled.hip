@@ -1459,7 +1459,10 @@ __global__ __launch_bounds__(256) void gm_s_band_listed(SState s, int t, int u0,
                       // 4: 3.29 ms per S-A tick, 1: 3.22, profiles/r06/ab_fwg/)
 #endif
 template <int B, bool CH, int BPW>
-__global__ __launch_bounds__(64 * GM_FAST_WG) __attribute__((amdgpu_waves_per_eu(7, 8))) void gm_s_band_fast(SState s, int t, int u0, int u1) {
+#ifndef GM_FAST_MINW
+#define GM_FAST_MINW 7  // gm_s_band_fast's waves per SIMD (72 VGPRs at 7)
+#endif
+__global__ __launch_bounds__(64 * GM_FAST_WG) __attribute__((amdgpu_waves_per_eu(GM_FAST_MINW, 8))) void gm_s_band_fast(SState s, int t, int u0, int u1) {
   if (!CH) {
     u0 = 0;
     u1 = s.n;
@@ -2574,7 +2577,9 @@ __global__ __launch_bounds__(256) void gm_s_init(SState s, int warm, int t0, uin
 // ------------------------------------------------------------ launch wrappers
 // (template dispatch over the band width; called by gm_host.hip)
 // the band kernels of rows [r0, r1) (r0, r1 multiples of the rows per unit, or r1 = n)
+#ifndef GM_FAST_BPW
 #define GM_FAST_BPW 2  // bands per wave of gm_s_band_fast (profiles/r05/ab4, ab5: 3.38 vs 3.48 ms at one)
+#endif
 template <int B>
 static void launch_band_b(const SState &s, int t, int drop_pct, int r0, int r1, hipStream_t st) {
   constexpr int RPW = 64 / (B / S_COLS_PER_LANE);

@@ -18,6 +18,6 @@ for i in 1 2 3; do
     fi
   done
 done
-for n in "$@"; do for f in $O/${n}_*.json; do python3 -c "
+for n in "$@"; do for f in $O/${n}_[0-9].json; do python3 -c "
 import json; d=json.loads(open('$f').read().strip().splitlines()[-1]); print('$f', round(d['ms_per_step'],3), round(d['roofline']['kernel_ms'],3))"; done; done
 if [ "${STUB:-0}" = 1 ]; then for n in "$@"; do for f in $O/${n}_stub_*.json; do echo "$f $(cut -c1-200 $f)"; done; done; fi
