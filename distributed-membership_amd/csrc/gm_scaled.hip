@@ -1851,19 +1851,22 @@ __device__ __forceinline__ uint32_t row16_bits(uint64_t bal, int g) { return (ui
 // a repeat. Rows the 16 outputs do not finish go to s.pk_list for gm_s_pick (from output 0). Same
 // results as gm_s_pick at a fraction of its instructions.
 template <int B>
-__global__ __launch_bounds__(256) void gm_s_pick0(SState s, int t) {
+#ifndef GM_PICK_WG
+#define GM_PICK_WG 4  // waves per workgroup of gm_s_pick0 (four rows per wave)
+#endif
+__global__ __launch_bounds__(64 * GM_PICK_WG) void gm_s_pick0(SState s, int t) {
   static_assert(B == 1024, "8 rank-select chunks of 128 columns per band");
   extern __shared__ __align__(16) uint32_t p_smem[];
   const int lane = threadIdx.x & 63, g = lane >> 4, q = lane & 15;
-  const int slot = (int)(threadIdx.x >> 4);  // row slot of the workgroup (0..15)
-  const int r = (int)blockIdx.x * 16 + slot;
+  const int slot = (int)(threadIdx.x >> 4);  // row slot of the workgroup (0 .. 4 GM_PICK_WG - 1)
+  const int r = (int)blockIdx.x * (4 * GM_PICK_WG) + slot;
   const bool valid = r < s.n;
   const int rc = valid ? r : s.n - 1;
   const int nb = s.nb, perb = (nb + 15) >> 4, par = t & 1;
   uint32_t *bpre = p_smem + (size_t)slot * (nb + 1);
   // the band records' chunk counts in LDS too (read with the prefix's words, same lines): a draw then
   // waits for one load (its table chunk), not two
-  uint2 *bcc = (uint2 *)(p_smem + 16 * (size_t)(nb + 1)) + (size_t)slot * nb;
+  uint2 *bcc = (uint2 *)(p_smem + 4 * GM_PICK_WG * (size_t)(nb + 1)) + (size_t)slot * nb;
   const int k = s.inbox_cnt[par][rc], failed = s.failed[rc];
   const uint32_t raw = s.mtraw[(size_t)rc * S_MT_RAW + q];
   uint32_t bp = 0, bf = 0;
@@ -2636,8 +2639,9 @@ static hipError_t launch_tick_b(const SState &s, int t, int drop_pct, hipStream_
   }
   const size_t smem = sizeof(uint32_t) * 4 * gm_draw_lds_words(s.wp, s.band);
   if (pick && B == 1024 && s.pk_list && !s.ramp) {  // four rows per wave, then the rows it left (pk_cnt: 0 by gm_s_mtgen)
-    hipLaunchKernelGGL((gm_s_pick0<B == 1024 ? B : 1024>), dim3((s.n + 15) / 16), dim3(256),
-                       sizeof(uint32_t) * 16 * (size_t)(s.nb + 1) + sizeof(uint2) * 16 * (size_t)s.nb, st, s, t);
+    constexpr int R = 4 * GM_PICK_WG;  // rows per workgroup
+    hipLaunchKernelGGL((gm_s_pick0<B == 1024 ? B : 1024>), dim3((s.n + R - 1) / R), dim3(64 * GM_PICK_WG),
+                       sizeof(uint32_t) * R * (size_t)(s.nb + 1) + sizeof(uint2) * R * (size_t)s.nb, st, s, t);
     hipLaunchKernelGGL((gm_s_pick<B>), dim3(256), dim3(256), smem, st, s, t, 1);
   } else if (pick) {
     hipLaunchKernelGGL((gm_s_pick<B>), dim3((s.n + 3) / 4), dim3(256), smem, st, s, t, 0);
