@@ -66,8 +66,6 @@ struct gm_ctx {
   std::vector<hipEvent_t> tev;            // per-tick band-kernel event pairs (single context)
   double kernel_ms_sum = 0;
   int shard_sync = -1;               // sharded tick draw rounds: 1 host-driven unbounded loop, 0 bounded
-  bool diag_nowait = false;          // diagnostics (GM_DIAG_NOWAIT, timing only): skip the pipelined tick's
-                                     // settle wait, as if round 0 never left rows pending
   int diag_zero_row = -1;            // diagnostics (GM_DIAG_ZERO_ROW, tests): the pipelined column-shard tick
                                      //   clears this row's cells after its band kernels, so its records'
                                      //   counts disagree with the cells and a draw finds no holder
@@ -409,7 +407,6 @@ static int create_scaled(gm_ctx *c) {
   }
   c->shard_sync = getenv("GM_SHARD_SYNC") ? (atoi(getenv("GM_SHARD_SYNC")) ? 1 : 0) : -1;
   if (getenv("GM_DIAG_ZERO_ROW")) c->diag_zero_row = atoi(getenv("GM_DIAG_ZERO_ROW"));
-  c->diag_nowait = getenv("GM_DIAG_NOWAIT") && atoi(getenv("GM_DIAG_NOWAIT"));
   TRY(dalloc(c, &s.msg, cells));        // nibbles: 2 parities x band/2 bytes per (band, row)
   // Escape storage (gm_scaled.h), one set per tick parity: a 16-cell inline slot per (band, row)
   // list (1/32 B per cell at B = 1024) and the pools. The pools are DENSE-equivalent (every
@@ -2301,10 +2298,6 @@ static int tick_sharded(gm_ctx *c) {
 static int draw_settle(gm_ctx *c) {
   if (!c->draw_check) return c->latched;
   c->draw_check = false;
-  if (c->diag_nowait && c->draw_rounds) {
-    c->draw_rounds = false;
-    return c->latched;
-  }
   // the next tick waits on these two counts: spin on the event (a blocking wait let the GPU idle
   // ~40 us per tick while the host thread woke up: profiles/r06/stub_gap/)
   hipError_t q;

@@ -1,5 +1,6 @@
 #!/bin/bash
-# Diagnostics: the S-A stub shard tick with and without the host's settle wait (GM_DIAG_NOWAIT=1:
+# Diagnostics (run at round 6 with profiles/r06/stub_tail/diag_nowait.patch applied; the toggle is not in
+# the product): the S-A stub shard tick with and without the host's settle wait (GM_DIAG_NOWAIT=1:
 # timing only), plus a kernel trace of the no-wait run. usage: scripts/r06/stub_nowait.sh <tag>
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
