@@ -2298,8 +2298,9 @@ static int tick_sharded(gm_ctx *c) {
 static int draw_settle(gm_ctx *c) {
   if (!c->draw_check) return c->latched;
   c->draw_check = false;
-  // the next tick waits on these two counts: spin on the event (a blocking wait let the GPU idle
-  // ~40 us per tick while the host thread woke up: profiles/r06/stub_gap/)
+  // the next tick's launches wait on these two counts: spin on the event rather than block (the
+  // wait costs 2-18 us of GPU idle per pipelined tick, profiles/r06/stub_tail/). No work of the
+  // next tick is enqueued before it: its S2 precompute zeroes the counts the copy reads
   hipError_t q;
   while ((q = hipEventQuery(c->draw_ev)) == hipErrorNotReady) {
   }
